@@ -1,0 +1,143 @@
+"""Oracle: CPU restatement of the reference retrieval back end (+ fp32 encoders).
+
+TEST INFRASTRUCTURE ONLY — imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, as the checker or the timed CPU baseline.  The
+product package (multimodal-reid_amd/) never imports it and has no CPU fallback.
+
+Parity status:
+  * eval_func, re_ranking stages R2-R7: pinned bit-exact to fixtures made by the
+    reference itself (tests/golden/make_goldens.py).
+  * euclidean_distance / F.normalize: the reference uses torch CPU BLAS whose
+    accumulation order is not reproducible; pinned within 2e-6 abs.
+  * encoders (oracle/vit_ref.py): fp32 torch restatement pinned to the reference
+    modules' fp32 outputs on synthetic weights.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+_f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+_i64p = np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS")
+_i32p = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+_f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+_u16p = np.ctypeslib.ndpointer(np.uint16, flags="C_CONTIGUOUS")
+_i64 = ctypes.c_int64
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(HERE, "build", "liboracle.so")
+        if not os.path.exists(path):
+            build()
+        L = ctypes.CDLL(path)
+        L.orc_l2norm.argtypes = [_f32p, _f32p, _i64, _i64]
+        L.orc_distmat.argtypes = [_f32p, _f32p, _i64, _i64, _i64, _f32p]
+        L.orc_topk_rows.argtypes = [_f32p, _i64, _i64, _i64, _i32p]
+        L.orc_eval_rows.argtypes = [_f32p, _i64, _i64, _i64p, _i64p, _i64p, _i64p, _i32p, _i64p, _f64p, _i64p]
+        L.orc_rerank_from_dist.argtypes = [_f32p, _i64, _i64, ctypes.c_int, ctypes.c_int, ctypes.c_uint16,
+                                           ctypes.c_float, _f32p, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_void_p]
+        L.orc_np_expf.argtypes = [ctypes.c_float]
+        L.orc_np_expf.restype = ctypes.c_float
+        L.orc_f2h.argtypes = [ctypes.c_float]
+        L.orc_f2h.restype = ctypes.c_uint16
+        L.orc_pairwise_f32.argtypes = [_f32p, _i64]
+        L.orc_pairwise_f32.restype = ctypes.c_float
+        L.orc_pairwise_f64.argtypes = [_f64p, _i64]
+        L.orc_pairwise_f64.restype = ctypes.c_double
+        _LIB = L
+    return _LIB
+
+
+def _c(a, dt):
+    return np.ascontiguousarray(np.asarray(a), dtype=dt)
+
+
+def l2norm(x):
+    x = _c(x, np.float32)
+    y = np.empty_like(x)
+    lib().orc_l2norm(x, y, x.shape[0], x.shape[1])
+    return y
+
+
+def distmat(q, g):
+    q, g = _c(q, np.float32), _c(g, np.float32)
+    out = np.empty((q.shape[0], g.shape[0]), np.float32)
+    lib().orc_distmat(q, g, q.shape[0], g.shape[0], q.shape[1], out)
+    return out
+
+
+def topk_rows(dist, k):
+    dist = _c(dist, np.float32)
+    out = np.empty((dist.shape[0], k), np.int32)
+    lib().orc_topk_rows(dist, dist.shape[0], dist.shape[1], k, out)
+    return out
+
+
+def eval_rows(dist, q_pids, g_pids, q_camids, g_camids):
+    dist = _c(dist, np.float32)
+    Q, G = dist.shape
+    valid = np.empty(Q, np.int32)
+    first = np.empty(Q, np.int64)
+    ap = np.empty(Q, np.float64)
+    nkept = np.empty(Q, np.int64)
+    lib().orc_eval_rows(dist, Q, G, _c(q_pids, np.int64), _c(g_pids, np.int64), _c(q_camids, np.int64),
+                        _c(g_camids, np.int64), valid, first, ap, nkept)
+    return valid, first, ap, nkept
+
+
+def eval_func(distmat_, q_pids, g_pids, q_camids, g_camids, max_rank=50):
+    """evaluate.py:29-88 restated: per-query part in C, the aggregation (82-88) here."""
+    Q, G = distmat_.shape
+    if G < max_rank:
+        max_rank = G
+    valid, first, ap, nkept = eval_rows(distmat_, q_pids, g_pids, q_camids, g_camids)
+    all_cmc, all_ap = [], []
+    for q in range(Q):
+        if not valid[q]:
+            continue
+        cmc = (np.arange(nkept[q]) >= first[q]).astype(np.int32)
+        all_cmc.append(cmc[:max_rank])
+        all_ap.append(ap[q])
+    assert len(all_cmc) > 0, "Error: all query identities do not appear in gallery"
+    all_cmc = np.asarray(all_cmc).astype(np.float32)
+    all_cmc = all_cmc.sum(0) / float(len(all_ap))
+    return all_cmc, np.mean(all_ap)
+
+
+def rerank_from_dist(D, num_query, k1, k2, lambda_value, debug=False):
+    """re_ranking(..., local_distmat=D, only_local=True) restated (reranking.py:29-100)."""
+    D = _c(D, np.float32)
+    N = D.shape[0]
+    Q = num_query
+    final = np.empty((Q, N - Q), np.float32)
+    K = min(max(k1 + 1, k2), N)
+    lam_h = np.float16(1 - lambda_value).view(np.uint16)
+    lam_f = np.float32(lambda_value)
+    if debug:
+        rank = np.empty((N, K), np.int32)
+        vqe = np.empty((N, N), np.uint16)
+        jac = np.empty((Q, N), np.uint16)
+        ptrs = [rank.ctypes.data, vqe.ctypes.data, jac.ctypes.data]
+    else:
+        ptrs = [None, None, None]
+    lib().orc_rerank_from_dist(D, N, Q, k1, k2, int(lam_h), float(lam_f), final, *ptrs)
+    if debug:
+        return final, rank, vqe, jac
+    return final
+
+
+def re_ranking(probFea, galFea, k1, k2, lambda_value):
+    """Full reference path: distance from features (oracle arithmetic) then R2-R7."""
+    feat = np.concatenate([np.asarray(probFea, np.float32), np.asarray(galFea, np.float32)])
+    return rerank_from_dist(distmat(feat, feat), len(probFea), k1, k2, lambda_value)

@@ -1,0 +1,338 @@
+/*
+ * reid_oracle.c — CPU restatement of the CLIP-ReID retrieval back end.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this (as the checker / the timed CPU baseline).  The
+ * product path (libreidmi.so) never links, loads or falls back to it.
+ *
+ * It restates, function by function, the reference numpy/torch back end:
+ *   evaluate.py:7-13   euclidean_distance          -> orc_distmat
+ *   evaluate.py:114    F.normalize(p=2, dim=1)      -> orc_l2norm
+ *   evaluate.py:29-88  eval_func (per-query part)   -> orc_eval_rows
+ *   reranking.py:29-100 re_ranking (R2..R7)         -> orc_rerank_from_dist
+ * Pinned against fixtures produced by the reference itself in this container
+ * (tests/golden/make_goldens.py): eval_func and re_ranking(only_local=True) are
+ * reproduced bit-exactly (ties canonicalised stable-by-index on both sides).
+ *
+ * Arithmetic definitions shared with the HIP kernels (bit-exact contract):
+ *  - dot / squared norm: fmaf chain over k ascending (what v_mfma_f32_32x32x2_f32
+ *    computes); distance = (qq + gg) - 2*dot.
+ *  - numpy float32 exp (AVX512F/AVX2 simd_exp_f32, numpy 2.2.6): Cody-Waite + 5/2
+ *    rational polynomial, constants pinned by probing numpy here (2e6/2e6 match).
+ *  - numpy float32 pairwise sum (PW_BLOCKSIZE 128, 8 accumulators).
+ *  - numpy float16 ufuncs: op in float32 then round-to-nearest-even to half.
+ * Build with -ffp-contract=off (no implicit FMA) — see oracle/Makefile.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ---------------------------------------------------------------- fp16 ---- */
+uint16_t orc_f2h(float f) {
+    uint32_t x; memcpy(&x, &f, 4);
+    uint32_t sign = (x >> 16) & 0x8000u;
+    uint32_t ax = x & 0x7fffffffu;
+    if (ax >= 0x7f800000u) return (uint16_t)(sign | 0x7c00u | (ax > 0x7f800000u ? 0x200u : 0));
+    if (ax >= 0x477ff000u) return (uint16_t)(sign | 0x7c00u); /* rounds to >= 65520 -> inf */
+    if (ax < 0x38800000u) { /* subnormal half (or zero) */
+        if (ax < 0x33000000u) return (uint16_t)sign; /* < 2^-25 -> 0 (tie at 2^-25 -> even 0) */
+        uint32_t e = ax >> 23, m = (ax & 0x7fffffu) | 0x800000u;
+        /* value = m * 2^(e-150); in units of the half subnormal step 2^-24: m >> (126 - e) */
+        uint32_t shift = 126 - e;
+        uint32_t q = m >> shift, r = m & ((1u << shift) - 1), half = 1u << (shift - 1);
+        if (r > half || (r == half && (q & 1))) q++;
+        return (uint16_t)(sign | q);
+    }
+    uint32_t e = (ax >> 23) - 112; /* rebias 127 -> 15 */
+    uint32_t m = ax & 0x7fffffu;
+    uint32_t q = (e << 10) | (m >> 13), r = m & 0x1fffu;
+    if (r > 0x1000u || (r == 0x1000u && (q & 1))) q++;
+    return (uint16_t)(sign | q);
+}
+
+float orc_h2f(uint16_t h) {
+    uint32_t sign = (uint32_t)(h & 0x8000u) << 16, e = (h >> 10) & 0x1fu, m = h & 0x3ffu, x;
+    if (e == 0) {
+        if (m == 0) x = sign;
+        else { float f = (float)m * 5.9604644775390625e-08f; memcpy(&x, &f, 4); x |= sign; }
+    } else if (e == 31) x = sign | 0x7f800000u | (m << 13);
+    else x = sign | ((e + 112) << 23) | (m << 13);
+    float f; memcpy(&f, &x, 4); return f;
+}
+
+/* ------------------------------------------------------- numpy float32 exp */
+float orc_np_expf(float x) {
+    if (x != x) return x;
+    if (x > 88.72283935546875f) return INFINITY;
+    if (x < -103.97208404541015625f) return 0.0f;
+    const float log2e = 1.442695040888963407359924681001892137f;
+    float quad = rintf(x * log2e);
+    float r = fmaf(quad, -6.93145752e-1f, x);
+    r = fmaf(quad, -1.42860677e-6f, r);
+    float num = fmaf(5.082762527590693718096e-04f, r, 6.757896990527504603057e-03f);
+    num = fmaf(num, r, 5.114512081637298353406e-02f);
+    num = fmaf(num, r, 2.473615434895520810817e-01f);
+    num = fmaf(num, r, 7.257664613233124478488e-01f);
+    num = fmaf(num, r, 9.999999999980870924916e-01f);
+    float den = fmaf(2.159509375685829852307e-02f, r, -2.742335390411667452936e-01f);
+    den = fmaf(den, r, 1.0f);
+    return ldexpf(num / den, (int)quad);
+}
+
+/* ---------------------------------------------------- numpy pairwise sums */
+float orc_pairwise_f32(const float* a, int64_t n) {
+    if (n < 8) {
+        float res = 0.0f;
+        for (int64_t i = 0; i < n; i++) res += a[i];
+        return res;
+    } else if (n <= 128) {
+        float r[8];
+        for (int j = 0; j < 8; j++) r[j] = a[j];
+        int64_t i;
+        for (i = 8; i < n - (n % 8); i += 8)
+            for (int j = 0; j < 8; j++) r[j] += a[i + j];
+        float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        for (; i < n; i++) res += a[i];
+        return res;
+    }
+    int64_t n2 = n / 2; n2 -= n2 % 8;
+    return orc_pairwise_f32(a, n2) + orc_pairwise_f32(a + n2, n - n2);
+}
+
+double orc_pairwise_f64(const double* a, int64_t n) {
+    if (n < 8) {
+        double res = 0.0;
+        for (int64_t i = 0; i < n; i++) res += a[i];
+        return res;
+    } else if (n <= 128) {
+        double r[8];
+        for (int j = 0; j < 8; j++) r[j] = a[j];
+        int64_t i;
+        for (i = 8; i < n - (n % 8); i += 8)
+            for (int j = 0; j < 8; j++) r[j] += a[i + j];
+        double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        for (; i < n; i++) res += a[i];
+        return res;
+    }
+    int64_t n2 = n / 2; n2 -= n2 % 8;
+    return orc_pairwise_f64(a, n2) + orc_pairwise_f64(a + n2, n - n2);
+}
+
+/* --------------------------------------------------------- l2 / distmat */
+static float sqnorm(const float* x, int64_t d) {
+    float acc = 0.0f;
+    for (int64_t k = 0; k < d; k++) acc = fmaf(x[k], x[k], acc);
+    return acc;
+}
+
+/* F.normalize(x, p=2, dim=1): x / max(||x||, 1e-12)   (evaluate.py:114) */
+void orc_l2norm(const float* x, float* y, int64_t n, int64_t d) {
+    for (int64_t i = 0; i < n; i++) {
+        float nrm = sqrtf(sqnorm(x + i * d, d));
+        if (nrm < 1e-12f) nrm = 1e-12f;
+        for (int64_t k = 0; k < d; k++) y[i * d + k] = x[i * d + k] / nrm;
+    }
+}
+
+/* ||q||^2 + ||g||^2 - 2 q.g   (evaluate.py:7-13; reranking.py:36-41) */
+void orc_distmat(const float* q, const float* g, int64_t Q, int64_t G, int64_t D, float* out) {
+    float* gg = (float*)malloc(sizeof(float) * (size_t)(G > 0 ? G : 1));
+    for (int64_t j = 0; j < G; j++) gg[j] = sqnorm(g + j * D, D);
+    for (int64_t i = 0; i < Q; i++) {
+        float qq = sqnorm(q + i * D, D);
+        for (int64_t j = 0; j < G; j++) {
+            float acc = 0.0f;
+            const float* a = q + i * D; const float* b = g + j * D;
+            for (int64_t k = 0; k < D; k++) acc = fmaf(a[k], b[k], acc);
+            out[i * G + j] = fmaf(-2.0f, acc, qq + gg[j]);
+        }
+    }
+    free(gg);
+}
+
+/* ---------------------------------------------------- stable argsort (rows) */
+typedef struct { float v; int32_t i; } kv_t;
+static int kv_cmp(const void* a, const void* b) {
+    const kv_t* x = (const kv_t*)a; const kv_t* y = (const kv_t*)b;
+    if (x->v < y->v) return -1;
+    if (y->v < x->v) return 1;
+    return (x->i > y->i) - (x->i < y->i);
+}
+/* argsort of one row; ties broken by index (== np.argsort(kind="stable")) */
+static void argsort_row(const float* row, int64_t n, kv_t* tmp, int32_t* idx) {
+    for (int64_t j = 0; j < n; j++) { tmp[j].v = row[j]; tmp[j].i = (int32_t)j; }
+    qsort(tmp, (size_t)n, sizeof(kv_t), kv_cmp);
+    for (int64_t j = 0; j < n; j++) idx[j] = tmp[j].i;
+}
+
+void orc_topk_rows(const float* dist, int64_t Q, int64_t G, int64_t k, int32_t* out) {
+    kv_t* tmp = (kv_t*)malloc(sizeof(kv_t) * (size_t)G);
+    int32_t* idx = (int32_t*)malloc(sizeof(int32_t) * (size_t)G);
+    for (int64_t i = 0; i < Q; i++) {
+        argsort_row(dist + i * G, G, tmp, idx);
+        memcpy(out + i * k, idx, sizeof(int32_t) * (size_t)k);
+    }
+    free(tmp); free(idx);
+}
+
+/* ------------------------------------------------------------- eval_func */
+/* Per-query part of eval_func (evaluate.py:40-80).  For each query:
+ *   valid[q]  = any positive kept  (evaluate.py:61-63)
+ *   first[q]  = 0-based position of the first match among kept items
+ *   ap[q]     = AP exactly as numpy computes it (cumsum/arange*orig_cmc, pairwise sum / num_rel)
+ *   nkept[q]  = number of kept gallery items (length of orig_cmc)            */
+void orc_eval_rows(const float* dist, int64_t Q, int64_t G, const int64_t* qp, const int64_t* gp,
+                   const int64_t* qc, const int64_t* gc, int32_t* valid, int64_t* first, double* ap,
+                   int64_t* nkept) {
+    kv_t* tmp = (kv_t*)malloc(sizeof(kv_t) * (size_t)G);
+    int32_t* idx = (int32_t*)malloc(sizeof(int32_t) * (size_t)G);
+    double* t = (double*)malloc(sizeof(double) * (size_t)G);
+    for (int64_t q = 0; q < Q; q++) {
+        argsort_row(dist + q * G, G, tmp, idx);
+        int64_t n = 0, hits = 0, f = -1;
+        for (int64_t j = 0; j < G; j++) {
+            int32_t g = idx[j];
+            if (gp[g] == qp[q] && gc[g] == qc[q]) continue; /* remove */
+            int m = gp[g] == qp[q];
+            if (m) { hits++; if (f < 0) f = n; }
+            /* tmp_cmc = cumsum / arange(1..) ; * orig_cmc  (evaluate.py:74-78) */
+            t[n] = m ? (double)hits / (double)(n + 1) : 0.0;
+            n++;
+        }
+        nkept[q] = n;
+        valid[q] = hits > 0;
+        first[q] = f;
+        ap[q] = hits > 0 ? orc_pairwise_f64(t, n) / (double)hits : 0.0;
+    }
+    free(tmp); free(idx); free(t);
+}
+
+/* ------------------------------------------------------------- re_ranking */
+static int cmp_i32(const void* a, const void* b) {
+    int32_t x = *(const int32_t*)a, y = *(const int32_t*)b;
+    return (x > y) - (x < y);
+}
+
+/* k-reciprocal set of row i at depth kk (reranking.py:53-56 / 60-63):
+ * forward = R[i, :kk+1]; keep forward[f] whose row R[forward[f], :kk+1] contains i. */
+static int kreciprocal(const int32_t* R, int64_t ldr, int32_t i, int kk1, int32_t* out) {
+    int n = 0;
+    for (int f = 0; f < kk1; f++) {
+        int32_t c = R[(int64_t)i * ldr + f];
+        for (int b = 0; b < kk1; b++)
+            if (R[(int64_t)c * ldr + b] == i) { out[n++] = c; break; }
+    }
+    return n;
+}
+
+/* re_ranking(..., local_distmat=D, only_local=True) — reranking.py:29-100 with
+ * D the N x N original distance (rows/cols: queries then gallery).
+ * one_minus_lambda_h = np.float16(1 - lambda) bits and lambda_f = np.float32(lambda): the
+ * numpy weak-scalar conversions of reranking.py:95 (the caller makes them with numpy).
+ * final: Q x (N-Q) float32.  Optional debug outputs (may be NULL):
+ * rank_out N x K int32 (K = min(max(k1+1,k2), N)), vqe_out N x N fp16 bits, jac_out Q x N fp16 bits. */
+int orc_rerank_from_dist(const float* D, int64_t N, int64_t Q, int k1, int k2, uint16_t one_minus_lambda_h,
+                         float lambda_f, float* final_out, int32_t* rank_out, uint16_t* vqe_out, uint16_t* jac_out) {
+    int64_t G = N - Q;
+    /* R2: od = transpose(D / max(D, axis=0))  (reranking.py:46) */
+    float* colmax = (float*)malloc(sizeof(float) * (size_t)N);
+    for (int64_t c = 0; c < N; c++) colmax[c] = D[c];
+    for (int64_t r = 1; r < N; r++)
+        for (int64_t c = 0; c < N; c++) if (D[r * N + c] > colmax[c]) colmax[c] = D[r * N + c];
+    float* od = (float*)malloc(sizeof(float) * (size_t)(N * N));
+    for (int64_t i = 0; i < N; i++)
+        for (int64_t j = 0; j < N; j++) od[i * N + j] = D[j * N + i] / colmax[i];
+    /* initial_rank = argsort(od) (stable), first K columns (reranking.py:48) */
+    int64_t K = k1 + 1 > k2 ? k1 + 1 : k2; if (K > N) K = N;
+    int32_t* R = (int32_t*)malloc(sizeof(int32_t) * (size_t)(N * K));
+    orc_topk_rows(od, N, N, K, R);
+    if (rank_out) memcpy(rank_out, R, sizeof(int32_t) * (size_t)(N * K));
+    int kf = (int)(k1 + 1 < N ? k1 + 1 : N);
+    int kh = (int)nearbyint((double)k1 / 2.0); /* int(np.around(k1/2)) (round half even) */
+    int kh1 = kh + 1 < N ? kh + 1 : (int)N;
+    /* R3: V (dense fp16 bits) */
+    uint16_t* V = (uint16_t*)calloc((size_t)(N * N), sizeof(uint16_t));
+    int32_t* kr = (int32_t*)malloc(sizeof(int32_t) * (size_t)kf);
+    int32_t* ckr = (int32_t*)malloc(sizeof(int32_t) * (size_t)kh1);
+    int32_t* exp_idx = (int32_t*)malloc(sizeof(int32_t) * (size_t)(kf + (int64_t)kf * kh1));
+    float* w = (float*)malloc(sizeof(float) * (size_t)(kf + (int64_t)kf * kh1));
+    for (int64_t i = 0; i < N; i++) {
+        int nk = kreciprocal(R, K, (int32_t)i, kf, kr);
+        int ne = 0;
+        for (int a = 0; a < nk; a++) exp_idx[ne++] = kr[a];
+        for (int a = 0; a < nk; a++) {
+            int nc = kreciprocal(R, K, kr[a], kh1, ckr);
+            int inter = 0;
+            for (int b = 0; b < nc; b++)
+                for (int c = 0; c < nk; c++) if (ckr[b] == kr[c]) { inter++; break; }
+            if ((double)inter > 2.0 / 3.0 * (double)nc)
+                for (int b = 0; b < nc; b++) exp_idx[ne++] = ckr[b];
+        }
+        qsort(exp_idx, (size_t)ne, sizeof(int32_t), cmp_i32);
+        int nu = 0;
+        for (int a = 0; a < ne; a++) if (nu == 0 || exp_idx[a] != exp_idx[nu - 1]) exp_idx[nu++] = exp_idx[a];
+        for (int a = 0; a < nu; a++) w[a] = orc_np_expf(-od[i * N + exp_idx[a]]);
+        float s = orc_pairwise_f32(w, nu);
+        for (int a = 0; a < nu; a++) V[i * N + exp_idx[a]] = orc_f2h(w[a] / s);
+    }
+    /* R4: query expansion (reranking.py:73-78) */
+    if (k2 != 1) {
+        uint16_t* Vq = (uint16_t*)malloc(sizeof(uint16_t) * (size_t)(N * N));
+        float* acc = (float*)malloc(sizeof(float) * (size_t)N);
+        for (int64_t i = 0; i < N; i++) {
+            for (int64_t c = 0; c < N; c++) acc[c] = 0.0f;
+            for (int r = 0; r < k2; r++) {
+                const uint16_t* row = V + (int64_t)R[i * K + r] * N;
+                for (int64_t c = 0; c < N; c++) acc[c] += orc_h2f(row[c]);
+            }
+            for (int64_t c = 0; c < N; c++) Vq[i * N + c] = orc_f2h(acc[c] / (float)k2);
+        }
+        free(acc); free(V); V = Vq;
+    }
+    if (vqe_out) memcpy(vqe_out, V, sizeof(uint16_t) * (size_t)(N * N));
+    /* R5: invIndex (reranking.py:80-82) as column lists, rows ascending */
+    int64_t* cnt = (int64_t*)calloc((size_t)N + 1, sizeof(int64_t));
+    for (int64_t r = 0; r < N; r++)
+        for (int64_t c = 0; c < N; c++) if (V[r * N + c] & 0x7fffu) cnt[c + 1]++;
+    for (int64_t c = 0; c < N; c++) cnt[c + 1] += cnt[c];
+    int32_t* inv = (int32_t*)malloc(sizeof(int32_t) * (size_t)(cnt[N] > 0 ? cnt[N] : 1));
+    int64_t* pos = (int64_t*)malloc(sizeof(int64_t) * (size_t)N);
+    for (int64_t c = 0; c < N; c++) pos[c] = cnt[c];
+    for (int64_t r = 0; r < N; r++)
+        for (int64_t c = 0; c < N; c++) if (V[r * N + c] & 0x7fffu) inv[pos[c]++] = (int32_t)r;
+    /* R6: Jaccard (reranking.py:84-93) with fp16 sequential accumulation */
+    uint16_t* tmin = (uint16_t*)malloc(sizeof(uint16_t) * (size_t)N);
+    uint16_t lam16 = one_minus_lambda_h;
+    float lam_f = lambda_f;
+    for (int64_t i = 0; i < Q; i++) {
+        for (int64_t r = 0; r < N; r++) tmin[r] = 0;
+        for (int64_t c = 0; c < N; c++) {
+            uint16_t vi = V[i * N + c];
+            if (!(vi & 0x7fffu)) continue;
+            float fvi = orc_h2f(vi);
+            for (int64_t p = cnt[c]; p < cnt[c + 1]; p++) {
+                int32_t r = inv[p];
+                float fvr = orc_h2f(V[(int64_t)r * N + c]);
+                float mn = fvr < fvi ? fvr : fvi;               /* np.minimum (fp16) */
+                tmin[r] = orc_f2h(orc_h2f(tmin[r]) + mn);        /* fp16 + fp16 -> fp16 */
+            }
+        }
+        for (int64_t r = 0; r < N; r++) {
+            float t = orc_h2f(tmin[r]);
+            uint16_t den = orc_f2h(2.0f - t);                       /* 2 - temp_min   */
+            uint16_t qt = orc_f2h(t / orc_h2f(den));                /* temp_min / (.) */
+            uint16_t jac = orc_f2h(1.0f - orc_h2f(qt));             /* 1 - (.)        */
+            if (jac_out) jac_out[i * N + r] = jac;
+            if (r >= Q) {
+                /* R7: jaccard*(1-lambda) [fp16] + original_dist*lambda [fp32] (reranking.py:95) */
+                float a = orc_h2f(orc_f2h(orc_h2f(jac) * orc_h2f(lam16)));
+                float b = od[i * N + r] * lam_f;
+                final_out[i * G + (r - Q)] = a + b;
+            }
+        }
+    }
+    free(colmax); free(od); free(R); free(V); free(kr); free(ckr); free(exp_idx); free(w);
+    free(cnt); free(inv); free(pos); free(tmin);
+    return 0;
+}
