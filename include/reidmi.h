@@ -1,0 +1,193 @@
+/*
+ * reidmi.h — C ABI of libreidmi.so, the MI355X-native CLIP-ReID inference +
+ * retrieval path.  Plain pointers and sizes only: every pointer argument is a
+ * device pointer (caller-owned, e.g. torch tensor .data_ptr()) unless noted; every
+ * call is stream-ordered on `stream` (a hipStream_t passed as void*) and never
+ * allocates or synchronises, so a caller may capture it into a hipGraph.
+ * Return value: 0 on success, non-zero status with reidmi_last_error() set.
+ *
+ * The reference (SuperbTUM/Multimodal-ReID) is pure Python with no FFI; each entry
+ * point below names the reference function whose semantics it implements.  The
+ * Python binding (ctypes) that re-exports the reference call surface lives in
+ * multimodal-reid_amd/_lib.py; INTEGRATION.md shows how a reference checkout
+ * would bind it.
+ */
+#ifndef REIDMI_H
+#define REIDMI_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define REIDMI_OK 0
+#define REIDMI_EINVAL 1
+#define REIDMI_EHIP 2
+#define REIDMI_ECAP 3
+
+const char* reidmi_last_error(void);
+int reidmi_abi_version(void);
+
+/* ------------------------------------------------------------ retrieval back end */
+
+/* sum_k x[i,k]^2 as an fmaf chain over k ascending (building block of the two below). */
+int reidmi_row_sqnorm_f32(const float* x, int64_t n, int64_t d, int64_t ldx, float* out, void* stream);
+
+/* torch.nn.functional.normalize(feats, dim=1, p=2)  — evaluate.py:114.
+ * ws: n floats. */
+int reidmi_l2norm_f32(const float* x, int64_t n, int64_t d, int64_t ldx, float* y, int64_t ldy, float* ws,
+                      void* stream);
+
+/* euclidean_distance(qf, gf) — evaluate.py:7-13 (also reranking.py:36-41 with q = g = feat).
+ * out[i*ldo+j] = (||q_i||^2 + ||g_j||^2) - 2 q_i.g_j in exact fp32 (v_mfma_f32_32x32x2_f32).
+ * ws: Q+G floats. */
+int reidmi_distmat_f32(const float* q, int64_t Q, int64_t ldq, const float* g, int64_t G, int64_t ldg, int64_t D,
+                       float* out, int64_t ldo, float* ws, void* stream);
+
+/* cosine_similarity(qf, gf) — evaluate.py:16-26: arccos(clip(q.g / (|q||g|), -1+1e-5, 1-1e-5)).
+ * Same tiling as reidmi_distmat_f32; ws: Q+G floats. */
+int reidmi_cosine_f32(const float* q, int64_t Q, int64_t ldq, const float* g, int64_t G, int64_t ldg, int64_t D,
+                      float* out, int64_t ldo, float* ws, void* stream);
+
+/* np.argsort(x, axis=1)[:, :k] with ties in index order (kind="stable") — evaluate.py:40,
+ * reranking.py:48.  row_div (nullable): rows are divided by row_div[row] first
+ * (reranking.py:46 column-max normalisation of a symmetric distance).  k <= 64.
+ * out_val (nullable) receives the selected values. */
+int reidmi_topk_rows_f32(const float* x, int64_t rows, int64_t cols, int64_t ldx, const float* row_div, int k,
+                         int32_t* out_idx, float* out_val, int64_t ldo, void* stream);
+
+/* Per-query part of eval_func — evaluate.py:40-80.  For query q: valid[q] (any match kept),
+ * first[q] (0-based kept-rank of the first match), ap[q] (float64 AP exactly as numpy sums
+ * it), nkept[q] (gallery items left after same-pid-same-cam removal).  overflow: one int32,
+ * set to 1 if some query has > 2048 positives. */
+int reidmi_eval_rows(const float* dist, int64_t Q, int64_t G, int64_t ldd, const int64_t* q_pids,
+                     const int64_t* g_pids, const int64_t* q_cams, const int64_t* g_cams, int32_t* valid,
+                     int64_t* first, double* ap, int64_t* nkept, int32_t* overflow, void* stream);
+
+
+/* ------------------------------------------------------------------ encoders */
+
+/* bf16 GEMM C = A . W^T (+bias) on v_mfma_f32_16x16x32_bf16, fp32 accumulation.
+ * A [M][lda] bf16, W [N][ldw] bf16 (Linear weight layout), N % 128 == 0, K % 64 == 0.
+ * epi: 0 -> out bf16 = acc+bias; 1 -> out bf16 = QuickGELU(acc+bias); 2 -> out fp32 += acc+bias;
+ *      5 -> out fp32 = acc+bias.  (nn.Linear / mlp.c_fc+QuickGELU / residual adds of
+ *      custom_clip_model.py:8-29.)  bias nullable (fp32). */
+int reidmi_gemm_bf16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N,
+                     int64_t K, const float* bias, void* out, int64_t ldc, void* stream);
+
+/* Live timing of the bf16 GEMM launches (HIP events on the launch stream), used by bench.py
+ * for the roofline of the dominant kernel.  collect: epi = GEMM epilogue id (-1 = all);
+ * returns summed device ms, launch count, algorithmic FLOPs (2MNK) and clears the record. */
+int reidmi_prof_enable(int on);
+int reidmi_prof_collect(int epi, double* total_ms, int64_t* count, double* flops);
+
+/* Key padding used for an L-token sequence by the attention kernel (rows of v^T). */
+int reidmi_attn_lpad(int L);
+
+/* softmax(Q K^T / 8 [+causal]) V per (sequence, head): the SDPA of nn.MultiheadAttention
+ * (custom_clip_model.py:22-24; causal text mask maple.py:956-962).  q,k [nseq*H][L][64],
+ * vt [nseq*H][64][reidmi_attn_lpad(L)], o [nseq*L][H*64]; all bf16.  L <= 256. */
+int reidmi_mhsa_bf16(const void* q, const void* k, const void* vt, void* o, int64_t nseq, int L, int H, int causal,
+                     void* stream);
+
+/* LayerNorm over rows of width W in {512,768,1024} (fp32 math, eps) — custom_clip_model.py:43-49.
+ * Row r of the output reads input row row_idx ? row_idx[r] : r.  y32 / y16 (bf16) nullable. */
+int reidmi_layernorm(const float* x, int64_t rows, int64_t ldx, const int32_t* row_idx, int64_t W,
+                     const float* gamma, const float* beta, float eps, float* y32, int64_t ldy32, void* y16,
+                     int64_t ldy16, void* stream);
+
+/* Per-block weights of a CLIP transformer block (ResidualAttentionBlock,
+ * custom_clip_model.py:8-29 / ResidualAttentionBlock_IVLP, maple.py:579-644).
+ * Matrices bf16 in PyTorch [out][in] layout, vectors fp32.  prompt: IVLP VPT_shallow
+ * [n_ctx][W] (fp32) that replaces the prompt rows before this block, or NULL. */
+typedef struct reidmi_block_weights {
+    const float* ln1_w;
+    const float* ln1_b;
+    const void* qkv_w;
+    const float* qkv_b;
+    const void* out_w;
+    const float* out_b;
+    const float* ln2_w;
+    const float* ln2_b;
+    const void* fc1_w;
+    const float* fc1_b;
+    const void* fc2_w;
+    const float* fc2_b;
+    const float* prompt;
+} reidmi_block_weights;
+
+/* Vision tower: custom_clip_model.VisionTransformer (custom_clip_model.py:57-100) and the
+ * IVLP variant maple.VisionTransformer (maple.py:722-785) when n_ctx > 0.
+ * conv_w: conv1.weight [W][3*P*P] flattened (c,ky,kx) and zero-padded to kpad (multiple of
+ * 64), bf16.  proj_t: proj^T [out_dim][W] bf16.  blocks: HOST array of `layers` entries. */
+typedef struct reidmi_vit_weights {
+    int32_t width, layers, heads, patch, stride, out_dim, grid_h, grid_w, n_ctx, kpad;
+    const void* conv_w;
+    const float* class_emb;
+    const float* pos_emb;
+    const float* ln_pre_w;
+    const float* ln_pre_b;
+    const float* ln_post_w;
+    const float* ln_post_b;
+    const void* proj_t;
+    const float* vpt;
+    const reidmi_block_weights* blocks;
+} reidmi_vit_weights;
+
+/* Workspace bytes for reidmi_vit_forward at batch B (full = 0: CLS outputs only). */
+int64_t reidmi_vit_workspace_bytes(const reidmi_vit_weights* w, int64_t B, int full);
+
+/* encode_image: runs resblocks[:11] then resblocks[11] (custom_clip_model.py:91-92, also for
+ * deeper towers), ln_post and proj.  images [B][3][H][Wimg] fp32 (images_bf16 = 0) or bf16,
+ * already normalised.  tta (nullable, device int32 [B][2]): apply the augmented loader's
+ * flip + Pad((10,5)) + crop at (top, left) on the fly (data_prepare.py:263-270).
+ * full = 0: out_x12 [B][W] = ln_post(x12)[:,0], out_proj [B][E] = (x12 @ proj)[:,0],
+ *           out_x11 [B][W] = x11[:,0] (nullable)          (zero_shot_learning.py:84-87)
+ * full = 1: out_x12 [B][L][W], out_proj [B][L][E], out_x11 [B][L][W] (nullable)
+ *           — the (x11, x12, xproj) triple of encode_image. */
+int reidmi_vit_forward(const reidmi_vit_weights* w, const void* images, int images_bf16, int64_t B, int H,
+                       int Wimg, const int32_t* tta, int full, float* out_x12, float* out_proj, float* out_x11,
+                       void* ws, int64_t ws_bytes, void* stream);
+
+/* Text tower: CLIP.encode_text (maple.py:971-984) from token ids, or
+ * text_encoder.TextEncoder.forward (text_encoder.py:14-24) from pre-embedded prompts.
+ * tok_emb [vocab][W] fp32, pos_emb [ctx][W] fp32, proj_t = text_projection^T [E][W] bf16. */
+typedef struct reidmi_text_weights {
+    int32_t width, layers, heads, ctx, vocab, out_dim, n_ctx;
+    const float* tok_emb;
+    const float* pos_emb;
+    const float* ln_final_w;
+    const float* ln_final_b;
+    const void* proj_t;
+    const reidmi_block_weights* blocks;
+} reidmi_text_weights;
+
+int64_t reidmi_text_workspace_bytes(const reidmi_text_weights* w, int64_t N);
+
+/* tokens: device int64 [N][ctx] (always needed: the EOT row is tokens.argmax(-1)).
+ * prompts: device fp32 [N][ctx][W] or NULL (then x = tok_emb[tokens]).  out [N][E] fp32. */
+int reidmi_text_forward(const reidmi_text_weights* w, const int64_t* tokens, const float* prompts, int64_t N,
+                        float* out, void* ws, int64_t ws_bytes, void* stream);
+
+/* -------------------------------------------------------- inference glue (G1) */
+
+/* zeroshot_classifier (zero_shot_learning.py:42-48): out[c] = normalize(mean over rows
+ * [offsets[c], offsets[c+1]) of normalize(feats[row])).  feats [rows][E], offsets device
+ * int64 [ncls+1], out [ncls][E]; all fp32. */
+int reidmi_class_mean_normalize(const float* feats, const int64_t* offsets, int64_t ncls, int64_t E, float* out,
+                                void* stream);
+
+/* zero_shot_learning.py:93,121-126 (non-mm): emb[b] = (cat(x12a,pa) + cat(x12b,pb)) / 2,
+ * fp32 [B][W+E] with row stride lde. */
+int reidmi_feature_tta_avg(const float* x12a, const float* pa, const float* x12b, const float* pb, int64_t B,
+                           int64_t W, int64_t E, float* emb, int64_t lde, void* stream);
+
+/* zero_shot_learning.py:116-122 (mm): emb[b] = cat((x12a+x12b)/2,
+ * softmax((1/0.07) * normalize((pa+pb)/2) @ zs^T)), zs [ncls][E] fp32. */
+int reidmi_feature_tta_mm(const float* x12a, const float* pa, const float* x12b, const float* pb, const float* zs,
+                          int64_t B, int64_t W, int64_t E, int64_t ncls, float* emb, int64_t lde, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* REIDMI_H */

@@ -1,0 +1,87 @@
+"""ctypes binding of libreidmi.so (the C ABI in include/reidmi.h).
+
+This is the product's only route to compute: there is no CPU or PyTorch fallback.
+If the library is missing or no GPU is present, calls raise loudly.
+"""
+import ctypes
+import os
+
+import torch
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, "libreidmi.so")
+
+_vp = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_i32 = ctypes.c_int
+_f32 = ctypes.c_float
+_u16 = ctypes.c_uint16
+
+# name -> argtypes (all return int status)
+SIGNATURES = {
+    "reidmi_row_sqnorm_f32": [_vp, _i64, _i64, _i64, _vp, _vp],
+    "reidmi_l2norm_f32": [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp],
+    "reidmi_distmat_f32": [_vp, _i64, _i64, _vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp],
+    "reidmi_cosine_f32": [_vp, _i64, _i64, _vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp],
+    "reidmi_topk_rows_f32": [_vp, _i64, _i64, _i64, _vp, _i32, _vp, _vp, _i64, _vp],
+    "reidmi_eval_rows": [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "reidmi_gemm_bf16": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _i64, _vp],
+    "reidmi_attn_lpad": [_i32],
+    "reidmi_prof_enable": [_i32],
+    "reidmi_prof_collect": [_i32, _vp, _vp, _vp],
+    "reidmi_mhsa_bf16": [_vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp],
+    "reidmi_layernorm": [_vp, _i64, _i64, _vp, _i64, _vp, _vp, _f32, _vp, _i64, _vp, _i64, _vp],
+    "reidmi_feature_tta_avg": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _i64, _vp],
+    "reidmi_feature_tta_mm": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _vp, _i64, _vp],
+    "reidmi_class_mean_normalize": [_vp, _vp, _i64, _i64, _vp, _vp],
+}
+# entry points with struct arguments are typed in model.py (reidmi_vit_*, reidmi_text_*)
+STRUCT_ENTRY_POINTS = ("reidmi_vit_workspace_bytes", "reidmi_vit_forward", "reidmi_text_workspace_bytes",
+                       "reidmi_text_forward")
+
+_LIB = None
+
+
+class ReidmiError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libreidmi.so (torch's HIP runtime is already loaded by `import torch`, so the
+    library's libamdhip64.so.7 dependency resolves to that same runtime)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise ReidmiError(f"{LIB_PATH} is not built: run `python __graft_entry__.py build` "
+                          "(there is no CPU fallback)")
+    L = ctypes.CDLL(LIB_PATH)
+    L.reidmi_last_error.restype = ctypes.c_char_p
+    L.reidmi_abi_version.restype = _i32
+    for name, args in SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = _i32
+    _LIB = L
+    return L
+
+
+def call(name, *args):
+    L = load()
+    rc = getattr(L, name)(*args)
+    if rc != 0:
+        raise ReidmiError(f"{name} failed ({rc}): {L.reidmi_last_error().decode()}")
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def require_cuda(*tensors):
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise ReidmiError("libreidmi operates on device tensors (got a CPU tensor)")

@@ -1,0 +1,404 @@
+// backend.hip — retrieval back end of the CLIP-ReID eval path on gfx950.
+//
+//   reidmi_l2norm_f32      F.normalize(feats, p=2, dim=1)           evaluate.py:114
+//   reidmi_distmat_f32     ||q||^2 + ||g||^2 - 2 q.g  (exact fp32)  evaluate.py:7-13, reranking.py:36-41
+//   reidmi_topk_rows_f32   first k of np.argsort(row) (stable)      evaluate.py:40, reranking.py:48
+//   reidmi_eval_rows       per-query CMC/AP of eval_func            evaluate.py:40-80
+//
+// Bit-exact contract with oracle/reid_oracle.c: every dot product / squared norm is an
+// fmaf chain over k ascending.  The distance GEMM runs on v_mfma_f32_32x32x2_f32, whose
+// result is bit-for-bit that chain (one rounding per product, k-pairs in order).
+#include "common.h"
+
+namespace reidmi {
+
+// --------------------------------------------------------------------------- norms
+__global__ void row_sqnorm_kernel(const float* __restrict__ x, int64_t n, int64_t d, int64_t ld,
+                                  float* __restrict__ out) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float* r = x + i * ld;
+    float acc = 0.0f;
+    for (int64_t k = 0; k < d; k++) acc = __builtin_fmaf(r[k], r[k], acc);
+    out[i] = acc;
+}
+
+// y = x / max(sqrt(ss), 1e-12): one workgroup per row, coalesced.
+__global__ void row_scale_kernel(const float* __restrict__ x, const float* __restrict__ ss, int64_t d,
+                                 int64_t ldx, float* __restrict__ y, int64_t ldy) {
+    int64_t i = blockIdx.x;
+    float nrm = __builtin_sqrtf(ss[i]);
+    nrm = nrm < 1e-12f ? 1e-12f : nrm;
+    for (int64_t k = threadIdx.x; k < d; k += blockDim.x) y[i * ldy + k] = x[i * ldx + k] / nrm;
+}
+
+// ------------------------------------------------------------------- distance GEMM
+// 128x128 output tile per 256-thread workgroup (2x2 waves, 64x64 per wave as 2x2
+// 32x32 MFMA tiles).  Operands staged k-major in LDS so each MFMA operand read is 32
+// consecutive floats per half-wave.
+constexpr int DM_BM = 128, DM_BN = 128, DM_BK = 16, DM_PAD = 4;
+
+template <bool COSINE>
+__global__ __launch_bounds__(256) void distmat_f32_kernel(
+    const float* __restrict__ q, const float* __restrict__ g, const float* __restrict__ qq,
+    const float* __restrict__ gg, int64_t Q, int64_t G, int64_t D, int64_t ldq, int64_t ldg,
+    float* __restrict__ out, int64_t ldo) {
+    __shared__ float sA[DM_BK][DM_BM + DM_PAD];
+    __shared__ float sB[DM_BK][DM_BN + DM_PAD];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid >> 1, wn = wid & 1;
+    const int64_t bm = (int64_t)blockIdx.y * DM_BM, bn = (int64_t)blockIdx.x * DM_BN;
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++) acc[a][b] = f32x16{};
+    for (int64_t k0 = 0; k0 < D; k0 += DM_BK) {
+        // stage: 128 rows x 16 k per operand, 8 elements per thread, 16 threads per row
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            int e = tid + 256 * u;
+            int r = e >> 4, kk = e & 15;
+            int64_t gk = k0 + kk;
+            int64_t qi = bm + r, gj = bn + r;
+            sA[kk][r] = (qi < Q && gk < D) ? q[qi * ldq + gk] : 0.0f;
+            sB[kk][r] = (gj < G && gk < D) ? g[gj * ldg + gk] : 0.0f;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < DM_BK / 2; s++) {
+            const int kr = 2 * s + (lane >> 5);
+            float a0 = sA[kr][wm * 64 + (lane & 31)];
+            float a1 = sA[kr][wm * 64 + 32 + (lane & 31)];
+            float b0 = sB[kr][wn * 64 + (lane & 31)];
+            float b1 = sB[kr][wn * 64 + 32 + (lane & 31)];
+            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+        for (int nt = 0; nt < 2; nt++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                int64_t i = bm + wm * 64 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                int64_t j = bn + wn * 64 + nt * 32 + (lane & 31);
+                if (i < Q && j < G) {
+                    if constexpr (COSINE) {
+                        // evaluate.py:16-26: arccos(clip(q.g * (1/(|q||g|)), -1+1e-5, 1-1e-5))
+                        const float c = acc[mt][nt][r] * (1.0f / (__builtin_sqrtf(qq[i]) * __builtin_sqrtf(gg[j])));
+                        out[i * ldo + j] = acosf(fminf(fmaxf(c, -1.0f + 1e-5f), 1.0f - 1e-5f));
+                    } else {
+                        out[i * ldo + j] = __builtin_fmaf(-2.0f, acc[mt][nt][r], qq[i] + gg[j]);
+                    }
+                }
+            }
+}
+
+// ---------------------------------------------------------------- key helpers
+__device__ __forceinline__ bool key_less(float av, int ai, float bv, int bi) {
+    return av < bv || (av == bv && ai < bi);
+}
+
+// In-LDS bitonic sort of (v,i) pairs, ascending by (v, i); P a power of two.
+__device__ void bitonic_sort_kv(float* sv, int* si, int P) {
+    for (int k = 2; k <= P; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int t = threadIdx.x; t < P; t += blockDim.x) {
+                int o = t ^ j;
+                if (o > t) {
+                    bool up = (t & k) == 0;
+                    float av = sv[t], bv = sv[o];
+                    int ai = si[t], bi = si[o];
+                    bool gt = key_less(bv, bi, av, ai);
+                    if (gt == up) { sv[t] = bv; sv[o] = av; si[t] = bi; si[o] = ai; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+__device__ __forceinline__ int pow2_ceil(int n) {
+    int p = 1;
+    while (p < n) p <<= 1;
+    return p;
+}
+
+// --------------------------------------------------------------------- top-k
+// Per row: k smallest (value, index) pairs in ascending order == np.argsort(kind="stable")[:k].
+// Streams the row once; a candidate buffer in LDS collects elements under the running
+// k-th key and is merged (bitonic) into the selection when it fills.  Optional per-row
+// divisor implements reranking.py:46 (od[i,:] = D[i,:] / colmax[i] for symmetric D).
+constexpr int TK_CAP = 2048, TK_CHUNK = 1024;
+
+__global__ __launch_bounds__(256) void topk_rows_kernel(const float* __restrict__ x, int64_t cols, int64_t ld,
+                                                        const float* __restrict__ row_div, int K,
+                                                        int32_t* __restrict__ out_idx, float* __restrict__ out_val,
+                                                        int64_t ldo) {
+    __shared__ float sv[TK_CAP];
+    __shared__ int si[TK_CAP];
+    __shared__ int s_cnt, s_nsel;
+    __shared__ float s_tv;
+    __shared__ int s_ti;
+    const int64_t row = blockIdx.x;
+    const float* base = x + row * ld;
+    const bool has_div = row_div != nullptr;
+    const float dv = has_div ? row_div[row] : 1.0f;
+    if (threadIdx.x == 0) { s_cnt = 0; s_nsel = 0; s_tv = __builtin_inff(); s_ti = 0x7fffffff; }
+    __syncthreads();
+    for (int64_t c0 = 0; c0 < cols; c0 += TK_CHUNK) {
+        const float tv = s_tv;
+        const int ti = s_ti, nsel = s_nsel;
+#pragma unroll
+        for (int u = 0; u < TK_CHUNK / 256; u++) {
+            int64_t j = c0 + u * 256 + threadIdx.x;
+            if (j < cols) {
+                float v = base[j];
+                if (has_div) v = v / dv;
+                if (key_less(v, (int)j, tv, ti)) {
+                    int p = atomicAdd(&s_cnt, 1);
+                    sv[nsel + p] = v;
+                    si[nsel + p] = (int)j;
+                }
+            }
+        }
+        __syncthreads();
+        const bool last = c0 + TK_CHUNK >= cols;
+        const int n = s_nsel + s_cnt;
+        __syncthreads();  // every thread has read s_cnt before anyone appends again
+        if (last || n > TK_CAP - TK_CHUNK) {
+            const int P = pow2_ceil(n < 2 ? 2 : n);
+            for (int t = n + threadIdx.x; t < P; t += blockDim.x) { sv[t] = __builtin_inff(); si[t] = 0x7fffffff; }
+            __syncthreads();
+            bitonic_sort_kv(sv, si, P);
+            if (threadIdx.x == 0) {
+                int ns = n < K ? n : K;
+                s_nsel = ns;
+                s_cnt = 0;
+                if (ns == K) { s_tv = sv[K - 1]; s_ti = si[K - 1]; }
+            }
+            __syncthreads();
+        }
+    }
+    for (int r = threadIdx.x; r < K; r += blockDim.x) {
+        out_idx[row * ldo + r] = si[r];
+        if (out_val) out_val[row * ldo + r] = sv[r];
+    }
+}
+
+// ------------------------------------------------------------------- eval rows
+// numpy pairwise sum (PW_BLOCKSIZE 128, 8 accumulators) of an n-long float64 vector that
+// is zero except at sorted positions pos[0..m) with values val[]: adding +0.0 is exact,
+// so only the tree structure over the nonzeros matters.  Iterative post-order walk.
+__device__ double leaf_sum(const int64_t* pos, const double* val, int lo, int hi, int64_t off, int64_t n) {
+    if (n < 8) {
+        double res = 0.0;
+        for (int t = lo; t < hi; t++) res += val[t];
+        return res;
+    }
+    double r[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int64_t main_end = n - (n % 8);
+    int t = lo;
+    for (; t < hi && pos[t] - off < main_end; t++) {
+        int64_t p = pos[t] - off;
+        r[p & 7] += val[t];
+    }
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; t < hi; t++) res += val[t];
+    return res;
+}
+
+__device__ int lower_pos(const int64_t* pos, int lo, int hi, int64_t x) {
+    while (lo < hi) {
+        int mid = (lo + hi) >> 1;
+        if (pos[mid] < x) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+__device__ double pairwise_sparse(const int64_t* pos, const double* val, int m, int64_t n) {
+    struct Frame { int64_t off, n, n2; int lo, hi, mid, stage; double left; };
+    Frame st[48];
+    int sp = 0;
+    st[sp++] = Frame{0, n, 0, 0, m, 0, 0, 0.0};
+    double ret = 0.0;
+    while (sp > 0) {
+        Frame& f = st[sp - 1];
+        if (f.stage == 0) {
+            if (f.lo == f.hi) { ret = 0.0; sp--; continue; }
+            if (f.n <= 128) { ret = leaf_sum(pos, val, f.lo, f.hi, f.off, f.n); sp--; continue; }
+            int64_t n2 = f.n / 2;
+            n2 -= n2 % 8;
+            f.n2 = n2;
+            f.mid = lower_pos(pos, f.lo, f.hi, f.off + n2);
+            f.stage = 1;
+            Frame c{f.off, n2, 0, f.lo, f.mid, 0, 0, 0.0};
+            st[sp++] = c;
+        } else if (f.stage == 1) {
+            f.left = ret;
+            f.stage = 2;
+            Frame c{f.off + f.n2, f.n - f.n2, 0, f.mid, f.hi, 0, 0, 0.0};
+            st[sp++] = c;
+        } else {
+            ret = f.left + ret;
+            sp--;
+        }
+    }
+    return ret;
+}
+
+constexpr int EV_MAXP = 2048;
+
+// One workgroup per query row.  Positives (same pid, other camera) are collected and
+// sorted; every other kept gallery item is binned by how many positives precede it
+// (binary search), so rank(positive k) = k + #kept negatives before it.  Junk (same pid
+// and camera) is removed exactly as evaluate.py:55-56.
+__global__ __launch_bounds__(256) void eval_rows_kernel(
+    const float* __restrict__ dist, int64_t G, int64_t ld, const int64_t* __restrict__ qp,
+    const int64_t* __restrict__ gp, const int64_t* __restrict__ qc, const int64_t* __restrict__ gc,
+    int32_t* __restrict__ valid, int64_t* __restrict__ first, double* __restrict__ ap,
+    int64_t* __restrict__ nkept, int32_t* __restrict__ overflow) {
+    __shared__ float pv[EV_MAXP];
+    __shared__ int pi[EV_MAXP];
+    __shared__ int hist[EV_MAXP + 1];
+    __shared__ int64_t rk[EV_MAXP];
+    __shared__ double rv[EV_MAXP];
+    __shared__ int s_m, s_junk;
+    const int64_t q = blockIdx.x;
+    const float* row = dist + q * ld;
+    const int64_t qpid = qp[q], qcam = qc[q];
+    if (threadIdx.x == 0) { s_m = 0; s_junk = 0; }
+    __syncthreads();
+    for (int64_t j = threadIdx.x; j < G; j += blockDim.x) {
+        if (gp[j] == qpid) {
+            if (gc[j] == qcam) atomicAdd(&s_junk, 1);
+            else {
+                int p = atomicAdd(&s_m, 1);
+                if (p < EV_MAXP) { pv[p] = row[j]; pi[p] = (int)j; }
+            }
+        }
+    }
+    __syncthreads();
+    const int m = s_m;
+    if (m > EV_MAXP) {
+        if (threadIdx.x == 0) { atomicExch(overflow, 1); valid[q] = 0; first[q] = -1; ap[q] = 0.0; nkept[q] = G - s_junk; }
+        return;
+    }
+    const int P = pow2_ceil(m < 2 ? 2 : m);
+    for (int t = m + threadIdx.x; t < P; t += blockDim.x) { pv[t] = __builtin_inff(); pi[t] = 0x7fffffff; }
+    for (int t = threadIdx.x; t <= m; t += blockDim.x) hist[t] = 0;
+    __syncthreads();
+    bitonic_sort_kv(pv, pi, P);
+    if (m > 0) {
+        for (int64_t j = threadIdx.x; j < G; j += blockDim.x) {
+            if (gp[j] == qpid) continue;  // positives counted separately, junk removed
+            const float v = row[j];
+            int lo = 0, hi = m;
+            while (lo < hi) {
+                int mid = (lo + hi) >> 1;
+                if (key_less(pv[mid], pi[mid], v, (int)j)) lo = mid + 1; else hi = mid;
+            }
+            if (lo < m) atomicAdd(&hist[lo], 1);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int64_t n = G - s_junk;
+        nkept[q] = n;
+        valid[q] = m > 0;
+        if (m == 0) { first[q] = -1; ap[q] = 0.0; return; }
+        int64_t cum = 0;
+        for (int k = 0; k < m; k++) {
+            cum += hist[k];
+            rk[k] = k + cum;
+            rv[k] = (double)(k + 1) / (double)(rk[k] + 1);
+        }
+        first[q] = rk[0];
+        ap[q] = pairwise_sparse(rk, rv, m, n) / (double)m;
+    }
+}
+
+}  // namespace reidmi
+
+using namespace reidmi;
+
+REIDMI_API int reidmi_row_sqnorm_f32(const float* x, int64_t n, int64_t d, int64_t ldx, float* out, void* stream) {
+    RM_REQUIRE(n >= 0 && d >= 0 && ldx >= d, "row_sqnorm: bad shape");
+    if (n == 0) return OK;
+    hipLaunchKernelGGL(row_sqnorm_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, (hipStream_t)stream, x, n, d, ldx, out);
+    RM_LAUNCHED();
+    return OK;
+}
+
+REIDMI_API int reidmi_l2norm_f32(const float* x, int64_t n, int64_t d, int64_t ldx, float* y, int64_t ldy,
+                                 float* ws, void* stream) {
+    RM_REQUIRE(n >= 0 && d > 0 && ldx >= d && ldy >= d && ws != nullptr, "l2norm: bad shape or workspace");
+    if (n == 0) return OK;
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(row_sqnorm_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, s, x, n, d, ldx, ws);
+    RM_LAUNCHED();
+    hipLaunchKernelGGL(row_scale_kernel, dim3((unsigned)n), dim3(256), 0, s, x, ws, d, ldx, y, ldy);
+    RM_LAUNCHED();
+    return OK;
+}
+
+static int distmat_impl(bool cosine, const float* q, int64_t Q, int64_t ldq, const float* g, int64_t G,
+                        int64_t ldg, int64_t D, float* out, int64_t ldo, float* ws, void* stream) {
+    RM_REQUIRE(Q >= 0 && G >= 0 && D > 0 && ldq >= D && ldg >= D && ldo >= G, "distmat: bad shape");
+    RM_REQUIRE(ws != nullptr, "distmat: workspace (Q+G floats) required");
+    if (Q == 0 || G == 0) return OK;
+    hipStream_t s = (hipStream_t)stream;
+    float* qq = ws;
+    float* gg = ws + Q;
+    hipLaunchKernelGGL(row_sqnorm_kernel, dim3(ceil_div(Q, 256)), dim3(256), 0, s, q, Q, D, ldq, qq);
+    RM_LAUNCHED();
+    hipLaunchKernelGGL(row_sqnorm_kernel, dim3(ceil_div(G, 256)), dim3(256), 0, s, g, G, D, ldg, gg);
+    RM_LAUNCHED();
+    dim3 grid(ceil_div(G, DM_BN), ceil_div(Q, DM_BM));
+    RM_REQUIRE(grid.y <= 65535, "distmat: too many query rows for one launch");
+    if (cosine)
+        hipLaunchKernelGGL(distmat_f32_kernel<true>, grid, dim3(256), 0, s, q, g, qq, gg, Q, G, D, ldq, ldg, out, ldo);
+    else
+        hipLaunchKernelGGL(distmat_f32_kernel<false>, grid, dim3(256), 0, s, q, g, qq, gg, Q, G, D, ldq, ldg, out, ldo);
+    RM_LAUNCHED();
+    return OK;
+}
+
+REIDMI_API int reidmi_distmat_f32(const float* q, int64_t Q, int64_t ldq, const float* g, int64_t G, int64_t ldg,
+                                  int64_t D, float* out, int64_t ldo, float* ws, void* stream) {
+    return distmat_impl(false, q, Q, ldq, g, G, ldg, D, out, ldo, ws, stream);
+}
+
+REIDMI_API int reidmi_cosine_f32(const float* q, int64_t Q, int64_t ldq, const float* g, int64_t G, int64_t ldg,
+                                 int64_t D, float* out, int64_t ldo, float* ws, void* stream) {
+    return distmat_impl(true, q, Q, ldq, g, G, ldg, D, out, ldo, ws, stream);
+}
+
+REIDMI_API int reidmi_topk_rows_f32(const float* x, int64_t rows, int64_t cols, int64_t ldx, const float* row_div,
+                                    int k, int32_t* out_idx, float* out_val, int64_t ldo, void* stream) {
+    RM_REQUIRE(rows >= 0 && cols > 0 && ldx >= cols && k > 0 && k <= 64 && k <= cols && ldo >= k,
+               "topk_rows: need 0 < k <= min(64, cols)");
+    RM_REQUIRE(cols < 0x7fffffff, "topk_rows: cols must fit int32");
+    if (rows == 0) return OK;
+    hipLaunchKernelGGL(topk_rows_kernel, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream, x, cols, ldx,
+                       row_div, k, out_idx, out_val, ldo);
+    RM_LAUNCHED();
+    return OK;
+}
+
+REIDMI_API int reidmi_eval_rows(const float* dist, int64_t Q, int64_t G, int64_t ldd, const int64_t* q_pids,
+                                const int64_t* g_pids, const int64_t* q_cams, const int64_t* g_cams, int32_t* valid,
+                                int64_t* first, double* ap, int64_t* nkept, int32_t* overflow, void* stream) {
+    RM_REQUIRE(Q >= 0 && G > 0 && ldd >= G && G < 0x7fffffff, "eval_rows: bad shape");
+    RM_REQUIRE(overflow != nullptr, "eval_rows: overflow flag pointer required");
+    if (Q == 0) return OK;
+    hipLaunchKernelGGL(eval_rows_kernel, dim3((unsigned)Q), dim3(256), 0, (hipStream_t)stream, dist, G, ldd, q_pids,
+                       g_pids, q_cams, g_cams, valid, first, ap, nkept, overflow);
+    RM_LAUNCHED();
+    return OK;
+}

@@ -1,0 +1,392 @@
+// encoder.hip — CLIP vision / text towers of the CLIP-ReID eval path (gfx950).
+//
+// Elementwise/normalisation kernels (LayerNorm, on-the-fly TTA im2col, CLS/prompt rows,
+// token embedding, EOT gather) and the host-side orchestration of one forward:
+//   vision: custom_clip_model.VisionTransformer.forward (custom_clip_model.py:77-100),
+//           IVLP maple.VisionTransformer.forward (maple.py:754-785, blocks maple.py:617-644)
+//   text:   CLIP.encode_text (maple.py:971-984) / TextEncoder.forward (text_encoder.py:14-24)
+// Per block: LN1 -> QKV GEMM (head-split epilogue) -> fused MHSA -> out_proj GEMM (+residual)
+//            -> LN2 -> c_fc GEMM (+QuickGELU) -> c_proj GEMM (+residual).
+// The residual stream stays fp32 in HBM; GEMM operands are bf16.
+#include "gemm.h"
+
+namespace reidmi {
+
+int mhsa(const void* q, const void* k, const void* vt, void* o, int64_t nseq, int L, int H, bool causal,
+         hipStream_t s);
+int attn_lpad(int L);
+
+// ------------------------------------------------------------------- LayerNorm
+// One wave per row; W = NV*256 floats, each lane holds NV float4.  Two-pass mean/var in
+// registers, eps inside the sqrt (torch.nn.LayerNorm).
+template <int NV>
+__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, int64_t rows, int64_t ldx,
+                                                        const int32_t* __restrict__ row_idx,
+                                                        const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta, float eps,
+                                                        float* __restrict__ y32, int64_t ldy32,
+                                                        __bf16* __restrict__ y16, int64_t ldy16) {
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= rows) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t src = row_idx ? (int64_t)row_idx[r] : r;
+    const float4* xr = (const float4*)(x + src * ldx);
+    float4 v[NV];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; i++) {
+        v[i] = xr[lane + 64 * i];
+        s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+    }
+    constexpr float invW = 1.0f / (NV * 256);
+    const float mean = wave_sum(s) * invW;
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; i++) {
+        const float a = v[i].x - mean, b = v[i].y - mean, c = v[i].z - mean, d = v[i].w - mean;
+        ss += (a * a + b * b) + (c * c + d * d);
+    }
+    const float rstd = __builtin_amdgcn_rsqf(wave_sum(ss) * invW + eps);
+#pragma unroll
+    for (int i = 0; i < NV; i++) {
+        const int f = lane + 64 * i;
+        const float4 g = ((const float4*)gamma)[f], b = ((const float4*)beta)[f];
+        float4 o;
+        o.x = (v[i].x - mean) * rstd * g.x + b.x;
+        o.y = (v[i].y - mean) * rstd * g.y + b.y;
+        o.z = (v[i].z - mean) * rstd * g.z + b.z;
+        o.w = (v[i].w - mean) * rstd * g.w + b.w;
+        if (y32) ((float4*)(y32 + r * ldy32))[f] = o;
+        if (y16) {
+            bf16x4 h = {(__bf16)o.x, (__bf16)o.y, (__bf16)o.z, (__bf16)o.w};
+            ((bf16x4*)(y16 + r * ldy16))[f] = h;
+        }
+    }
+}
+
+int layernorm(const float* x, int64_t rows, int64_t ldx, const int32_t* row_idx, int64_t W, const float* g,
+              const float* b, float eps, float* y32, int64_t ldy32, __bf16* y16, int64_t ldy16, hipStream_t s) {
+    if (rows == 0) return OK;
+    RM_REQUIRE(ldx % 4 == 0 && (!y32 || ldy32 % 4 == 0) && (!y16 || ldy16 % 4 == 0), "layernorm: strides");
+    dim3 grid(ceil_div(rows, 4));
+    switch (W) {
+        case 512:
+            hipLaunchKernelGGL(layernorm_kernel<2>, grid, dim3(256), 0, s, x, rows, ldx, row_idx, g, b, eps, y32,
+                               ldy32, y16, ldy16);
+            break;
+        case 768:
+            hipLaunchKernelGGL(layernorm_kernel<3>, grid, dim3(256), 0, s, x, rows, ldx, row_idx, g, b, eps, y32,
+                               ldy32, y16, ldy16);
+            break;
+        case 1024:
+            hipLaunchKernelGGL(layernorm_kernel<4>, grid, dim3(256), 0, s, x, rows, ldx, row_idx, g, b, eps, y32,
+                               ldy32, y16, ldy16);
+            break;
+        default:
+            return fail(EINVAL_, "layernorm: width must be 512, 768 or 1024");
+    }
+    RM_LAUNCHED();
+    return OK;
+}
+
+// ---------------------------------------------------------- patch embed im2col
+// col[b*NP + p][k], k = c*P*P + ky*P + kx (conv1.weight flattening), zero for k >= 3P^2.
+// Optional TTA (data_prepare.py:263-270 on a normalised crop): flip, Pad((10,5)) with
+// value -1 (= 0 before Normalize(0.5,0.5)), crop at (top i, left j).
+template <typename TI>
+__global__ void im2col_kernel(const TI* __restrict__ img, int64_t B, int H, int Wd, int P, int S, int gw, int NP,
+                              int kpad, const int32_t* __restrict__ tta, __bf16* __restrict__ col) {
+    const int64_t chunks = B * NP * (kpad / 8);
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= chunks) return;
+    const int kc = (int)(e % (kpad / 8));
+    const int64_t bp = e / (kpad / 8);
+    const int64_t b = bp / NP;
+    const int p = (int)(bp % NP);
+    const int py = p / gw, px = p % gw;
+    int ti = 0, tj = 0;
+    const bool aug = tta != nullptr;
+    if (aug) { ti = tta[2 * b]; tj = tta[2 * b + 1]; }
+    const TI* im = img + b * 3 * (int64_t)H * Wd;
+    bf16x8 out;
+    const int PP = P * P;
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+        const int k = kc * 8 + u;
+        float v = 0.f;
+        if (k < 3 * PP) {
+            const int c = k / PP, rem = k % PP, ky = rem / P, kx = rem % P;
+            int y = py * S + ky, x = px * S + kx;
+            bool inb = true;
+            if (aug) {
+                y = y + ti - 5;
+                x = x + tj - 10;
+                inb = y >= 0 && y < H && x >= 0 && x < Wd;
+                x = Wd - 1 - x;
+            }
+            v = inb ? (float)im[((int64_t)c * H + y) * Wd + x] : -1.0f;
+        }
+        out[u] = (__bf16)v;
+    }
+    *(bf16x8*)(col + bp * kpad + kc * 8) = out;
+}
+
+// x[b*L+0] = class_emb + pos[0]; IVLP: x[b*L+1+NP+i] = half(vpt[i]) (maple.py:765-767).
+__global__ void cls_rows_kernel(float* __restrict__ x, int64_t B, int L, int W, const float* __restrict__ cls,
+                                const float* __restrict__ pos, int NP, int n_ctx, const float* __restrict__ vpt) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int rows = 1 + n_ctx;
+    if (e >= B * rows * W) return;
+    const int n = (int)(e % W);
+    const int64_t br = e / W;
+    const int64_t b = br / rows;
+    const int r = (int)(br % rows);
+    if (r == 0) x[(b * L) * W + n] = cls[n] + pos[n];
+    else x[(b * L + 1 + NP + (r - 1)) * W + n] = (float)(_Float16)vpt[(r - 1) * W + n];
+}
+
+// IVLP per-block prompt: rows [row0, row0+n_ctx) of every sequence <- half(prompt)
+// (vision row0 = L-n_ctx, maple.py:620-629; text row0 = 1, maple.py:630-640).
+__global__ void prompt_rows_kernel(float* __restrict__ x, int64_t nseq, int L, int W, int row0, int n_ctx,
+                                   const float* __restrict__ prompt) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= nseq * n_ctx * W) return;
+    const int n = (int)(e % W);
+    const int64_t br = e / W;
+    const int64_t b = br / n_ctx;
+    const int r = (int)(br % n_ctx);
+    x[(b * L + row0 + r) * W + n] = (float)(_Float16)prompt[r * W + n];
+}
+
+// x[n*L+t] = (prompts ? prompts[n,t] : tok_emb[tokens[n,t]]) + pos[t]   (maple.py:972-974)
+__global__ void text_embed_kernel(float* __restrict__ x, const int64_t* __restrict__ tokens,
+                                  const float* __restrict__ prompts, const float* __restrict__ tok_emb,
+                                  const float* __restrict__ pos, int64_t N, int L, int W, int64_t vocab) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= N * L * (W / 4)) return;
+    const int c4 = (int)(e % (W / 4));
+    const int64_t nt = e / (W / 4);
+    const int t = (int)(nt % L);
+    float4 v;
+    if (prompts) v = ((const float4*)(prompts + nt * W))[c4];
+    else {
+        int64_t id = tokens[nt];
+        id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
+        v = ((const float4*)(tok_emb + id * W))[c4];
+    }
+    const float4 p = ((const float4*)(pos + (int64_t)t * W))[c4];
+    v.x += p.x; v.y += p.y; v.z += p.z; v.w += p.w;
+    ((float4*)(x + nt * W))[c4] = v;
+}
+
+// row index of tokens[n].argmax() (first maximum, torch semantics) in the [N*L] row space
+__global__ void eot_rows_kernel(const int64_t* __restrict__ tokens, int64_t N, int L, int32_t* __restrict__ rows) {
+    const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= N) return;
+    const int64_t* t = tokens + n * L;
+    int best = 0;
+    int64_t bv = t[0];
+    for (int i = 1; i < L; i++)
+        if (t[i] > bv) { bv = t[i]; best = i; }
+    rows[n] = (int32_t)(n * L + best);
+}
+
+// --------------------------------------------------------------- workspace plan
+struct Plan {
+    int64_t x, h, q, k, vt, o, u, rows, total;
+};
+
+static int64_t al(int64_t v) { return (v + 255) & ~(int64_t)255; }
+
+static Plan plan(int64_t nseq, int L, int W, int lp, int64_t extra_rows) {
+    Plan p{};
+    const int64_t M = nseq * L;
+    int64_t off = 0;
+    p.x = off; off = al(off + M * W * 4);
+    p.h = off; off = al(off + M * W * 2);
+    p.q = off; off = al(off + M * W * 2);
+    p.k = off; off = al(off + M * W * 2);
+    p.vt = off; off = al(off + nseq * W * (int64_t)lp * 2);
+    p.o = off; off = al(off + M * W * 2);
+    p.u = off; off = al(off + M * 4 * W * 2);
+    p.rows = off; off = al(off + extra_rows * 4);
+    p.total = off;
+    return p;
+}
+
+// One ResidualAttentionBlock on the fp32 residual stream x [nseq*L][W].
+static int run_block(const reidmi_block_weights& bw, char* ws, const Plan& P, int64_t nseq, int L, int W, int H,
+                     bool causal, hipStream_t s) {
+    const int64_t M = nseq * L;
+    float* x = (float*)(ws + P.x);
+    __bf16* h = (__bf16*)(ws + P.h);
+    __bf16* o = (__bf16*)(ws + P.o);
+    __bf16* u = (__bf16*)(ws + P.u);
+    int rc;
+    if ((rc = layernorm(x, M, W, nullptr, W, bw.ln1_w, bw.ln1_b, 1e-5f, nullptr, 0, h, W, s))) return rc;
+    EpiArgs ea{};
+    ea.bias = bw.qkv_b;
+    ea.q = ws + P.q;
+    ea.k = ws + P.k;
+    ea.vt = ws + P.vt;
+    ea.seq = L;
+    ea.heads = H;
+    ea.lpad = attn_lpad(L);
+    if ((rc = gemm_bf16(EPI_QKV, h, W, bw.qkv_w, W, M, 3 * W, W, ea, s))) return rc;
+    if ((rc = mhsa(ws + P.q, ws + P.k, ws + P.vt, o, nseq, L, H, causal, s))) return rc;
+    EpiArgs er{};
+    er.out = x;
+    er.ldc = W;
+    er.bias = bw.out_b;
+    if ((rc = gemm_bf16(EPI_RESID_F32, o, W, bw.out_w, W, M, W, W, er, s))) return rc;
+    if ((rc = layernorm(x, M, W, nullptr, W, bw.ln2_w, bw.ln2_b, 1e-5f, nullptr, 0, h, W, s))) return rc;
+    EpiArgs eg{};
+    eg.out = u;
+    eg.ldc = 4 * W;
+    eg.bias = bw.fc1_b;
+    if ((rc = gemm_bf16(EPI_GELU_BF16, h, W, bw.fc1_w, W, M, 4 * W, W, eg, s))) return rc;
+    EpiArgs e2{};
+    e2.out = x;
+    e2.ldc = W;
+    e2.bias = bw.fc2_b;
+    if ((rc = gemm_bf16(EPI_RESID_F32, u, 4 * W, bw.fc2_w, 4 * W, M, W, 4 * W, e2, s))) return rc;
+    return OK;
+}
+
+static int vit_check(const reidmi_vit_weights* w) {
+    RM_REQUIRE(w && w->blocks, "vit: null weights");
+    RM_REQUIRE(w->layers >= 12, "vit: the reference forward runs resblocks[:11] + resblocks[11]; needs >= 12 layers");
+    RM_REQUIRE(w->width == w->heads * 64, "vit: head dim must be 64");
+    RM_REQUIRE(w->kpad % 64 == 0 && w->kpad >= 3 * w->patch * w->patch, "vit: kpad");
+    RM_REQUIRE(w->out_dim % 128 == 0 && w->width % 128 == 0, "vit: width/out_dim must be multiples of 128");
+    return OK;
+}
+
+}  // namespace reidmi
+
+using namespace reidmi;
+
+REIDMI_API int reidmi_layernorm(const float* x, int64_t rows, int64_t ldx, const int32_t* row_idx, int64_t W,
+                                const float* gamma, const float* beta, float eps, float* y32, int64_t ldy32, void* y16,
+                                int64_t ldy16, void* stream) {
+    return layernorm(x, rows, ldx, row_idx, W, gamma, beta, eps, y32, ldy32, (__bf16*)y16, ldy16,
+                     (hipStream_t)stream);
+}
+
+REIDMI_API int64_t reidmi_vit_workspace_bytes(const reidmi_vit_weights* w, int64_t B, int full) {
+    if (vit_check(w)) return -1;
+    const int L = 1 + w->grid_h * w->grid_w + w->n_ctx;
+    return plan(B, L, w->width, attn_lpad(L), 0).total;
+}
+
+REIDMI_API int reidmi_vit_forward(const reidmi_vit_weights* w, const void* images, int images_bf16, int64_t B, int H,
+                                  int Wimg, const int32_t* tta, int full, float* out_x12, float* out_proj,
+                                  float* out_x11, void* ws_, int64_t ws_bytes, void* stream) {
+    int rc;
+    if ((rc = vit_check(w))) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    const int W = w->width, NP = w->grid_h * w->grid_w, L = 1 + NP + w->n_ctx, E = w->out_dim;
+    RM_REQUIRE((H - w->patch) / w->stride + 1 == w->grid_h && (Wimg - w->patch) / w->stride + 1 == w->grid_w,
+               "vit: image size does not match the positional-embedding grid");
+    RM_REQUIRE(attn_lpad(L) > 0, "vit: too many tokens (max 256)");
+    const Plan P = plan(B, L, W, attn_lpad(L), 0);
+    RM_REQUIRE(ws_bytes >= P.total, "vit: workspace too small");
+    RM_REQUIRE(out_x12 && out_proj, "vit: outputs required");
+    if (B == 0) return OK;
+    char* ws = (char*)ws_;
+    float* x = (float*)(ws + P.x);
+    __bf16* h = (__bf16*)(ws + P.h);
+    __bf16* col = (__bf16*)(ws + P.u);
+    const int64_t M = B * L;
+    // patch embed (+pos), CLS/VPT rows, ln_pre
+    const int64_t chunks = B * NP * (w->kpad / 8);
+    if (images_bf16)
+        hipLaunchKernelGGL(im2col_kernel<__bf16>, dim3(ceil_div(chunks, 256)), dim3(256), 0, s,
+                           (const __bf16*)images, B, H, Wimg, w->patch, w->stride, w->grid_w, NP, w->kpad, tta, col);
+    else
+        hipLaunchKernelGGL(im2col_kernel<float>, dim3(ceil_div(chunks, 256)), dim3(256), 0, s,
+                           (const float*)images, B, H, Wimg, w->patch, w->stride, w->grid_w, NP, w->kpad, tta, col);
+    RM_LAUNCHED();
+    EpiArgs ep{};
+    ep.out = x;
+    ep.ldc = W;
+    ep.pos = w->pos_emb;
+    ep.npatch = NP;
+    ep.seq = L;
+    if ((rc = gemm_bf16(EPI_PATCH, col, w->kpad, w->conv_w, w->kpad, B * NP, W, w->kpad, ep, s))) return rc;
+    RM_REQUIRE(w->n_ctx == 0 || w->vpt != nullptr, "vit: n_ctx > 0 needs vpt");
+    const int64_t ce = B * (1 + w->n_ctx) * W;
+    hipLaunchKernelGGL(cls_rows_kernel, dim3(ceil_div(ce, 256)), dim3(256), 0, s, x, B, L, W, w->class_emb,
+                       w->pos_emb, NP, w->n_ctx, w->vpt);
+    RM_LAUNCHED();
+    if ((rc = layernorm(x, M, W, nullptr, W, w->ln_pre_w, w->ln_pre_b, 1e-5f, x, W, nullptr, 0, s))) return rc;
+    // resblocks[:11] then resblocks[11] (custom_clip_model.py:91-92)
+    for (int i = 0; i < 12; i++) {
+        const reidmi_block_weights& bw = w->blocks[i];
+        if (i > 0 && bw.prompt && w->n_ctx > 0) {
+            const int64_t pe = B * w->n_ctx * W;
+            hipLaunchKernelGGL(prompt_rows_kernel, dim3(ceil_div(pe, 256)), dim3(256), 0, s, x, B, L, W,
+                               L - w->n_ctx, w->n_ctx, bw.prompt);
+            RM_LAUNCHED();
+        }
+        if ((rc = run_block(bw, ws, P, B, L, W, w->heads, false, s))) return rc;
+        if (i == 10 && out_x11) {
+            if (full) RM_CHECK_HIP(hipMemcpyAsync(out_x11, x, M * W * 4, hipMemcpyDeviceToDevice, s));
+            else
+                RM_CHECK_HIP(hipMemcpy2DAsync(out_x11, W * 4, x, (size_t)L * W * 4, W * 4, B,
+                                              hipMemcpyDeviceToDevice, s));
+        }
+    }
+    // ln_post, then @ proj (custom_clip_model.py:96-98)
+    const int64_t rows = full ? M : B;
+    const int64_t ldx = full ? W : (int64_t)L * W;
+    if ((rc = layernorm(x, rows, ldx, nullptr, W, w->ln_post_w, w->ln_post_b, 1e-5f, out_x12, W, h, W, s))) return rc;
+    EpiArgs eo{};
+    eo.out = out_proj;
+    eo.ldc = E;
+    if ((rc = gemm_bf16(EPI_F32, h, W, w->proj_t, W, rows, E, W, eo, s))) return rc;
+    return OK;
+}
+
+REIDMI_API int64_t reidmi_text_workspace_bytes(const reidmi_text_weights* w, int64_t N) {
+    if (!w || attn_lpad(w->ctx) < 0) return -1;
+    return plan(N, w->ctx, w->width, attn_lpad(w->ctx), N).total;
+}
+
+REIDMI_API int reidmi_text_forward(const reidmi_text_weights* w, const int64_t* tokens, const float* prompts,
+                                   int64_t N, float* out, void* ws_, int64_t ws_bytes, void* stream) {
+    RM_REQUIRE(w && w->blocks && tokens && out, "text: null argument");
+    RM_REQUIRE(w->width == w->heads * 64 && w->width % 256 == 0, "text: width");
+    hipStream_t s = (hipStream_t)stream;
+    const int W = w->width, L = w->ctx, E = w->out_dim;
+    RM_REQUIRE(attn_lpad(L) > 0, "text: context too long");
+    const Plan P = plan(N, L, W, attn_lpad(L), N);
+    RM_REQUIRE(ws_bytes >= P.total, "text: workspace too small");
+    if (N == 0) return OK;
+    char* ws = (char*)ws_;
+    float* x = (float*)(ws + P.x);
+    __bf16* h = (__bf16*)(ws + P.h);
+    int32_t* rows = (int32_t*)(ws + P.rows);
+    const int64_t te = N * L * (W / 4);
+    hipLaunchKernelGGL(text_embed_kernel, dim3(ceil_div(te, 256)), dim3(256), 0, s, x, tokens, prompts, w->tok_emb,
+                       w->pos_emb, N, L, W, (int64_t)w->vocab);
+    RM_LAUNCHED();
+    int rc;
+    for (int i = 0; i < w->layers; i++) {
+        const reidmi_block_weights& bw = w->blocks[i];
+        if (i > 0 && bw.prompt && w->n_ctx > 0) {
+            const int64_t pe = N * w->n_ctx * W;
+            hipLaunchKernelGGL(prompt_rows_kernel, dim3(ceil_div(pe, 256)), dim3(256), 0, s, x, N, L, W, 1,
+                               w->n_ctx, bw.prompt);
+            RM_LAUNCHED();
+        }
+        if ((rc = run_block(bw, ws, P, N, L, W, w->heads, true, s))) return rc;
+    }
+    hipLaunchKernelGGL(eot_rows_kernel, dim3(ceil_div(N, 256)), dim3(256), 0, s, tokens, N, L, rows);
+    RM_LAUNCHED();
+    if ((rc = layernorm(x, N, W, rows, W, w->ln_final_w, w->ln_final_b, 1e-5f, nullptr, 0, h, W, s))) return rc;
+    EpiArgs eo{};
+    eo.out = out;
+    eo.ldc = E;
+    return gemm_bf16(EPI_F32, h, W, w->proj_t, W, N, E, W, eo, s);
+}

@@ -1,0 +1,41 @@
+// gemm.h — bf16 MFMA GEMM with fused epilogues for the CLIP encoders (gfx950).
+//
+// C[M,N] = A[M,K] . W[N,K]^T (+ bias[N]), A row-major bf16 (activations), W row-major bf16
+// (PyTorch Linear / conv weight layout [out, in]), fp32 accumulation on
+// v_mfma_f32_16x16x32_bf16.  Epilogues implement the ops that follow each GEMM in
+// custom_clip_model.py:8-29 / maple.py:617-644 so no elementwise pass touches HBM:
+//   EPI_BF16      out bf16 = acc + bias                       (generic)
+//   EPI_GELU_BF16 out bf16 = QuickGELU(acc + bias)            (mlp.c_fc + gelu, :14-16,52-54)
+//   EPI_RESID_F32 x fp32 += acc + bias                        (out_proj / c_proj + residual, :27-28)
+//   EPI_QKV       q,k -> [B,H,L,64] bf16, v -> [B,H,64,Lp]    (attn.in_proj + head split)
+//   EPI_PATCH     x[b*L+1+p] = acc + pos[1+p]  fp32           (conv1 + pos-embed, :78-86)
+//   EPI_F32       out fp32 = acc + bias                       (proj / text_projection)
+#pragma once
+#include "common.h"
+
+namespace reidmi {
+
+enum Epi : int { EPI_BF16 = 0, EPI_GELU_BF16 = 1, EPI_RESID_F32 = 2, EPI_QKV = 3, EPI_PATCH = 4, EPI_F32 = 5 };
+
+struct EpiArgs {
+    void* out;          // bf16 / fp32 output (or residual x for RESID, x for PATCH)
+    int64_t ldc;        // row stride of out (elements)
+    const float* bias;  // [N] or null
+    // QKV head split
+    void* q;
+    void* k;
+    void* vt;
+    int seq;    // L (tokens per sequence)
+    int heads;  // H
+    int lpad;   // Lp (row length of vt)
+    // PATCH
+    const float* pos;  // [1+NP][N]
+    int npatch;        // NP
+};
+
+// Launch C = A . W^T with epilogue `epi`.  Requires N % 128 == 0, K % 64 == 0,
+// lda/ldw multiples of 8 (16-byte rows); M arbitrary.
+int gemm_bf16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N, int64_t K,
+              const EpiArgs& ea, hipStream_t stream);
+
+}  // namespace reidmi

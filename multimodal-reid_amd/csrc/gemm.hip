@@ -1,0 +1,277 @@
+// gemm.hip — bf16 MFMA GEMM (C = A . W^T) with fused epilogues; see gemm.h.
+//
+// Tiling (MI355X / gfx950): 128x128x64 block tile, 256 threads = 4 waves as 2x2, each
+// wave owns 64x64 = 4x4 tiles of v_mfma_f32_16x16x32_bf16.  Operand tiles are staged
+// global -> registers -> LDS (double-buffered, one barrier per K-step: the loads for
+// tile k+1 are in flight while tile k is multiplied).  LDS rows are 128 B; 16-byte
+// chunks are XOR-swizzled with (row>>1)&7 so the fragment reads (16 rows x 4 chunks per
+// ds_read_b128 lane group) are bank-conflict free.  Operands are swapped in the MFMA
+// (W fragment as A, activation fragment as B) so each lane ends up holding one output
+// row and 4 consecutive output columns: epilogue loads/stores are 8-16 B per lane.
+// Block ids are remapped XCD-contiguously (consecutive tiles of one A row panel share
+// an XCD's L2).
+#include "gemm.h"
+
+#include <mutex>
+#include <vector>
+
+namespace reidmi {
+
+// ----------------------------------------------------------- live GEMM timing
+// bench.py measures the roofline of the dominant kernel with HIP events recorded on the
+// launch stream around each GEMM of the timed region (reidmi_prof_*).  Off by default.
+namespace prof {
+struct Rec {
+    hipEvent_t a, b;
+    double flops;
+    int epi;
+};
+static bool enabled = false;
+static std::mutex mu;
+static std::vector<Rec> recs;
+static std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
+static size_t used = 0;
+}  // namespace prof
+
+constexpr int GB_M = 128, GB_N = 128, GB_K = 64;
+
+__device__ __forceinline__ int swz(int r, int kc) { return r * GB_K + ((kc ^ ((r >> 1) & 7)) << 3); }
+
+__device__ __forceinline__ uint2 pack_bf16x4(float a, float b, float c, float d) {
+    bf16x4 v = {(__bf16)a, (__bf16)b, (__bf16)c, (__bf16)d};
+    return __builtin_bit_cast(uint2, v);
+}
+
+__device__ __forceinline__ float quick_gelu(float x) {
+    // x * sigmoid(1.702 x)   (custom_clip_model.py:52-54)
+    return x * __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * x));
+}
+
+template <int EPI>
+__global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(const __bf16* __restrict__ A, int64_t lda,
+                                                           const __bf16* __restrict__ W, int64_t ldw, int64_t M,
+                                                           int N, int K, EpiArgs ea, int tiles_n, int nwg) {
+    __shared__ __attribute__((aligned(16))) __bf16 smem[2][2][GB_M * GB_K];
+    const int bid = blockIdx.x;
+    const int xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
+    const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+    const int tm = wg / tiles_n, tn = wg % tiles_n;
+    const int64_t m0 = (int64_t)tm * GB_M;
+    const int n0 = tn * GB_N;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid >> 1, wn = wid & 1;
+
+    // per-thread staging slots: 4 x 16 B of A and of W per K-step
+    const __bf16* gA[4];
+    const __bf16* gW[4];
+    int soff[4];
+    bool aval[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const int c = tid + 256 * u, row = c >> 3, kc = c & 7;
+        aval[u] = m0 + row < M;
+        gA[u] = A + (aval[u] ? (m0 + row) : 0) * lda + kc * 8;
+        gW[u] = W + (int64_t)(n0 + row) * ldw + kc * 8;
+        soff[u] = swz(row, kc);
+    }
+    uint4 ra0, ra1, ra2, ra3, rw0, rw1, rw2, rw3;
+#define GLOAD(k0)                                                                  \
+    do {                                                                           \
+        ra0 = aval[0] ? *(const uint4*)(gA[0] + (k0)) : make_uint4(0, 0, 0, 0);   \
+        ra1 = aval[1] ? *(const uint4*)(gA[1] + (k0)) : make_uint4(0, 0, 0, 0);   \
+        ra2 = aval[2] ? *(const uint4*)(gA[2] + (k0)) : make_uint4(0, 0, 0, 0);   \
+        ra3 = aval[3] ? *(const uint4*)(gA[3] + (k0)) : make_uint4(0, 0, 0, 0);   \
+        rw0 = *(const uint4*)(gW[0] + (k0));                                       \
+        rw1 = *(const uint4*)(gW[1] + (k0));                                       \
+        rw2 = *(const uint4*)(gW[2] + (k0));                                       \
+        rw3 = *(const uint4*)(gW[3] + (k0));                                       \
+    } while (0)
+#define LSTORE(buf)                                                                \
+    do {                                                                           \
+        *(uint4*)(&smem[buf][0][soff[0]]) = ra0;                                   \
+        *(uint4*)(&smem[buf][0][soff[1]]) = ra1;                                   \
+        *(uint4*)(&smem[buf][0][soff[2]]) = ra2;                                   \
+        *(uint4*)(&smem[buf][0][soff[3]]) = ra3;                                   \
+        *(uint4*)(&smem[buf][1][soff[0]]) = rw0;                                   \
+        *(uint4*)(&smem[buf][1][soff[1]]) = rw1;                                   \
+        *(uint4*)(&smem[buf][1][soff[2]]) = rw2;                                   \
+        *(uint4*)(&smem[buf][1][soff[3]]) = rw3;                                   \
+    } while (0)
+
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    GLOAD(0);
+    LSTORE(0);
+    __syncthreads();
+    const int nk = K / GB_K;
+    for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        if (kt + 1 < nk) GLOAD((kt + 1) * GB_K);
+        const __bf16* sA = smem[cur][0];
+        const __bf16* sW = smem[cur][1];
+#pragma unroll
+        for (int ks = 0; ks < 2; ks++) {
+            bf16x8 af[4], wf[4];
+            const int kc = ks * 4 + (lane >> 4);
+#pragma unroll
+            for (int i = 0; i < 4; i++) af[i] = *(const bf16x8*)(sA + swz(wm * 64 + i * 16 + (lane & 15), kc));
+#pragma unroll
+            for (int j = 0; j < 4; j++) wf[j] = *(const bf16x8*)(sW + swz(wn * 64 + j * 16 + (lane & 15), kc));
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af[i], acc[i][j], 0, 0, 0);
+        }
+        if (kt + 1 < nk) LSTORE(cur ^ 1);
+        __syncthreads();
+    }
+
+    // ------------------------------------------------------------------ epilogue
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int64_t m = m0 + wm * 64 + i * 16 + (lane & 15);
+        if (m >= M) continue;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int nb = n0 + wn * 64 + j * 16 + (lane >> 4) * 4;
+            f32x4 v = acc[i][j];
+            if (EPI != EPI_PATCH && ea.bias != nullptr) {
+                const float4 b = *(const float4*)(ea.bias + nb);
+                v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+            }
+            if constexpr (EPI == EPI_BF16) {
+                *(uint2*)((__bf16*)ea.out + m * ea.ldc + nb) = pack_bf16x4(v[0], v[1], v[2], v[3]);
+            } else if constexpr (EPI == EPI_GELU_BF16) {
+                *(uint2*)((__bf16*)ea.out + m * ea.ldc + nb) =
+                    pack_bf16x4(quick_gelu(v[0]), quick_gelu(v[1]), quick_gelu(v[2]), quick_gelu(v[3]));
+            } else if constexpr (EPI == EPI_RESID_F32) {
+                float4* p = (float4*)((float*)ea.out + m * ea.ldc + nb);
+                float4 x = *p;
+                x.x += v[0]; x.y += v[1]; x.z += v[2]; x.w += v[3];
+                *p = x;
+            } else if constexpr (EPI == EPI_F32) {
+                *(float4*)((float*)ea.out + m * ea.ldc + nb) = make_float4(v[0], v[1], v[2], v[3]);
+            } else if constexpr (EPI == EPI_PATCH) {
+                const int64_t b = m / ea.npatch, p = m % ea.npatch;
+                const int64_t row = b * ea.seq + 1 + p;
+                const float4 pe = *(const float4*)(ea.pos + (1 + p) * (int64_t)N + nb);
+                *(float4*)((float*)ea.out + row * ea.ldc + nb) =
+                    make_float4(v[0] + pe.x, v[1] + pe.y, v[2] + pe.z, v[3] + pe.w);
+            } else if constexpr (EPI == EPI_QKV) {
+                const int wd = ea.heads * 64;
+                const int which = nb / wd, h = (nb % wd) >> 6, d = nb & 63;
+                const int64_t b = m / ea.seq, t = m % ea.seq;
+                const int64_t bh = b * ea.heads + h;
+                if (which < 2) {
+                    __bf16* dst = (__bf16*)(which == 0 ? ea.q : ea.k) + (bh * ea.seq + t) * 64 + d;
+                    *(uint2*)dst = pack_bf16x4(v[0], v[1], v[2], v[3]);
+                } else {
+                    __bf16* dst = (__bf16*)ea.vt + (bh * 64 + d) * (int64_t)ea.lpad + t;
+                    dst[0] = (__bf16)v[0];
+                    dst[ea.lpad] = (__bf16)v[1];
+                    dst[2 * (int64_t)ea.lpad] = (__bf16)v[2];
+                    dst[3 * (int64_t)ea.lpad] = (__bf16)v[3];
+                }
+            }
+        }
+    }
+#undef GLOAD
+#undef LSTORE
+}
+
+template <int EPI>
+static int launch(const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N, int64_t K,
+                  const EpiArgs& ea, hipStream_t s) {
+    const int tiles_m = ceil_div(M, GB_M), tiles_n = (int)(N / GB_N);
+    const int64_t nwg = (int64_t)tiles_m * tiles_n;
+    RM_REQUIRE(nwg < (1ll << 31), "gemm: grid too large");
+    hipLaunchKernelGGL(gemm_bf16_kernel<EPI>, dim3((unsigned)nwg), dim3(256), 0, s, (const __bf16*)A, lda,
+                       (const __bf16*)W, ldw, M, (int)N, (int)K, ea, tiles_n, (int)nwg);
+    RM_LAUNCHED();
+    return OK;
+}
+
+int gemm_bf16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N, int64_t K,
+              const EpiArgs& ea, hipStream_t s) {
+    RM_REQUIRE(M >= 0 && N > 0 && K > 0, "gemm: bad shape");
+    RM_REQUIRE(N % GB_N == 0 && K % GB_K == 0, "gemm: needs N % 128 == 0 and K % 64 == 0");
+    RM_REQUIRE(lda % 8 == 0 && ldw % 8 == 0 && lda >= K && ldw >= K, "gemm: lda/ldw must be >= K and 16-byte rows");
+    if (M == 0) return OK;
+    hipEvent_t ev_b = nullptr;
+    if (prof::enabled) {
+        std::lock_guard<std::mutex> g(prof::mu);
+        if (prof::used == prof::pool.size()) {
+            hipEvent_t a, b;
+            RM_CHECK_HIP(hipEventCreate(&a));
+            RM_CHECK_HIP(hipEventCreate(&b));
+            prof::pool.push_back({a, b});
+        }
+        auto pr = prof::pool[prof::used++];
+        prof::recs.push_back({pr.first, pr.second, 2.0 * (double)M * (double)N * (double)K, epi});
+        RM_CHECK_HIP(hipEventRecord(pr.first, s));
+        ev_b = pr.second;
+    }
+    int rc;
+    switch (epi) {
+        case EPI_BF16: rc = launch<EPI_BF16>(A, lda, W, ldw, M, N, K, ea, s); break;
+        case EPI_GELU_BF16: rc = launch<EPI_GELU_BF16>(A, lda, W, ldw, M, N, K, ea, s); break;
+        case EPI_RESID_F32: rc = launch<EPI_RESID_F32>(A, lda, W, ldw, M, N, K, ea, s); break;
+        case EPI_QKV: rc = launch<EPI_QKV>(A, lda, W, ldw, M, N, K, ea, s); break;
+        case EPI_PATCH: rc = launch<EPI_PATCH>(A, lda, W, ldw, M, N, K, ea, s); break;
+        case EPI_F32: rc = launch<EPI_F32>(A, lda, W, ldw, M, N, K, ea, s); break;
+        default: return fail(EINVAL_, "gemm: unknown epilogue");
+    }
+    if (ev_b) RM_CHECK_HIP(hipEventRecord(ev_b, s));
+    return rc;
+}
+
+}  // namespace reidmi
+
+using namespace reidmi;
+
+REIDMI_API int reidmi_prof_enable(int on) {
+    std::lock_guard<std::mutex> g(prof::mu);
+    prof::enabled = on != 0;
+    prof::recs.clear();
+    prof::used = 0;
+    return OK;
+}
+
+// Sum of device time (ms), launch count and algorithmic FLOPs of the recorded GEMM launches
+// with epilogue `epi` (-1: all).  Waits for the recorded events; then clears the record.
+REIDMI_API int reidmi_prof_collect(int epi, double* total_ms, int64_t* count, double* flops) {
+    std::lock_guard<std::mutex> g(prof::mu);
+    double t = 0, f = 0;
+    int64_t n = 0;
+    for (auto& r : prof::recs) {
+        if (epi >= 0 && r.epi != epi) continue;
+        RM_CHECK_HIP(hipEventSynchronize(r.b));
+        float ms = 0;
+        RM_CHECK_HIP(hipEventElapsedTime(&ms, r.a, r.b));
+        t += ms;
+        f += r.flops;
+        n++;
+    }
+    if (total_ms) *total_ms = t;
+    if (count) *count = n;
+    if (flops) *flops = f;
+    prof::recs.clear();
+    prof::used = 0;
+    return OK;
+}
+
+REIDMI_API int reidmi_gemm_bf16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N,
+                                int64_t K, const float* bias, void* out, int64_t ldc, void* stream) {
+    RM_REQUIRE(epi == EPI_BF16 || epi == EPI_GELU_BF16 || epi == EPI_RESID_F32 || epi == EPI_F32,
+               "reidmi_gemm_bf16: epi must be 0 (bf16), 1 (gelu bf16), 2 (residual f32) or 5 (f32)");
+    EpiArgs ea{};
+    ea.out = out;
+    ea.ldc = ldc;
+    ea.bias = bias;
+    return gemm_bf16(epi, A, lda, W, ldw, M, N, K, ea, (hipStream_t)stream);
+}

@@ -1,0 +1,308 @@
+"""Host side of the CLIP-ReID encoders: weight packing into the libreidmi C structs
+and the reference's model duck types.
+
+    VisionTransformer.encode_image(img) -> (x11, x12, xproj)   custom_clip_model.py:77-100
+                                                               maple.py:754-785 (IVLP, n_ctx>0)
+    VisionTransformer.encode_cls(img, tta=None) -> (x12[:,0], xproj[:,0])  (inference fast path)
+    TextTransformer.encode_text(tokens) -> (N, E)              maple.py:971-984
+    TextEncoder(text)(prompts, tokenized_prompts) -> (N, E)    text_encoder.py:14-24
+    CLIP(visual, text): encode_image / encode_text / dtype      maple.py:964-984
+
+Weights come from a state dict with the reference's key layout (numpy or torch, fp32/fp16):
+the vision keys of custom_clip_model.VisionTransformer (``conv1.weight``,
+``transformer.resblocks.{i}.attn.in_proj_weight``, ... ``proj``; plus ``VPT`` /
+``VPT_shallow`` for IVLP) and the text keys of CLIP (``token_embedding.weight``,
+``transformer.resblocks.{i}...``, ``ln_final.*``, ``text_projection``).  Matrices are
+stored bf16 in HBM, vectors fp32.  All compute runs in libreidmi.so.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+
+_vp = ctypes.c_void_p
+_i32 = ctypes.c_int32
+
+
+class BlockWeights(ctypes.Structure):
+    _fields_ = [(n, _vp) for n in ("ln1_w", "ln1_b", "qkv_w", "qkv_b", "out_w", "out_b", "ln2_w", "ln2_b",
+                                   "fc1_w", "fc1_b", "fc2_w", "fc2_b", "prompt")]
+
+
+class VitWeights(ctypes.Structure):
+    _fields_ = [(n, _i32) for n in ("width", "layers", "heads", "patch", "stride", "out_dim", "grid_h", "grid_w",
+                                    "n_ctx", "kpad")] + \
+               [(n, _vp) for n in ("conv_w", "class_emb", "pos_emb", "ln_pre_w", "ln_pre_b", "ln_post_w",
+                                   "ln_post_b", "proj_t", "vpt")] + [("blocks", ctypes.POINTER(BlockWeights))]
+
+
+class TextWeights(ctypes.Structure):
+    _fields_ = [(n, _i32) for n in ("width", "layers", "heads", "ctx", "vocab", "out_dim", "n_ctx")] + \
+               [(n, _vp) for n in ("tok_emb", "pos_emb", "ln_final_w", "ln_final_b", "proj_t")] + \
+               [("blocks", ctypes.POINTER(BlockWeights))]
+
+
+_SIG = {
+    "reidmi_vit_workspace_bytes": ([ctypes.POINTER(VitWeights), ctypes.c_int64, ctypes.c_int], ctypes.c_int64),
+    "reidmi_vit_forward": ([ctypes.POINTER(VitWeights), _vp, ctypes.c_int, ctypes.c_int64, ctypes.c_int,
+                            ctypes.c_int, _vp, ctypes.c_int, _vp, _vp, _vp, _vp, ctypes.c_int64, _vp], ctypes.c_int),
+    "reidmi_text_workspace_bytes": ([ctypes.POINTER(TextWeights), ctypes.c_int64], ctypes.c_int64),
+    "reidmi_text_forward": ([ctypes.POINTER(TextWeights), _vp, _vp, ctypes.c_int64, _vp, _vp, ctypes.c_int64, _vp],
+                            ctypes.c_int),
+}
+
+
+def _fn(name):
+    L = _lib.load()
+    f = getattr(L, name)
+    if name in _SIG and getattr(f, "_reidmi_typed", None) is None:
+        f.argtypes, f.restype = _SIG[name]
+        f._reidmi_typed = True
+    return f
+
+
+def _t(a):
+    if isinstance(a, torch.Tensor):
+        return a.detach().float().cpu()
+    return torch.from_numpy(np.asarray(a, dtype=np.float32))
+
+
+class _Packer:
+    """Moves tensors to the device once and keeps them alive."""
+
+    def __init__(self, device):
+        self.device = device
+        self.keep = []
+
+    def f32(self, a):
+        t = _t(a).contiguous().to(self.device)
+        self.keep.append(t)
+        return t
+
+    def bf16(self, a):
+        t = _t(a).contiguous().to(torch.bfloat16).to(self.device)
+        self.keep.append(t)
+        return t
+
+
+def _pack_blocks(sd, prefix, layers, pk):
+    arr = (BlockWeights * layers)()
+    for i in range(layers):
+        p = f"{prefix}transformer.resblocks.{i}."
+        b = arr[i]
+        b.ln1_w = pk.f32(sd[p + "ln_1.weight"]).data_ptr()
+        b.ln1_b = pk.f32(sd[p + "ln_1.bias"]).data_ptr()
+        b.qkv_w = pk.bf16(sd[p + "attn.in_proj_weight"]).data_ptr()
+        b.qkv_b = pk.f32(sd[p + "attn.in_proj_bias"]).data_ptr()
+        b.out_w = pk.bf16(sd[p + "attn.out_proj.weight"]).data_ptr()
+        b.out_b = pk.f32(sd[p + "attn.out_proj.bias"]).data_ptr()
+        b.ln2_w = pk.f32(sd[p + "ln_2.weight"]).data_ptr()
+        b.ln2_b = pk.f32(sd[p + "ln_2.bias"]).data_ptr()
+        b.fc1_w = pk.bf16(sd[p + "mlp.c_fc.weight"]).data_ptr()
+        b.fc1_b = pk.f32(sd[p + "mlp.c_fc.bias"]).data_ptr()
+        b.fc2_w = pk.bf16(sd[p + "mlp.c_proj.weight"]).data_ptr()
+        b.fc2_b = pk.f32(sd[p + "mlp.c_proj.bias"]).data_ptr()
+        b.prompt = pk.f32(sd[p + "VPT_shallow"]).data_ptr() if (p + "VPT_shallow") in sd else None
+    return arr
+
+
+def resize_pos_embed(posemb, gh, gw):
+    """utils.py:111-125 / maple.py:1027-1041: bicubic resize of the square grid of a
+    pretrained positional embedding to (gh, gw) (load time, host side)."""
+    posemb = _t(posemb)
+    tok, grid = posemb[:1], posemb[1:]
+    gs = int(round(len(grid) ** 0.5))
+    grid = grid.reshape(1, gs, gs, -1).permute(0, 3, 1, 2)
+    grid = torch.nn.functional.interpolate(grid, size=(gh, gw), mode="bicubic")
+    grid = grid.permute(0, 2, 3, 1).reshape(gh * gw, -1)
+    return torch.cat([tok, grid], 0)
+
+
+class VisionTransformer:
+    """libreidmi vision tower.  ``stride`` defaults to the CLIP-ReID value 12
+    (utils.py:169).  ``height``/``width`` are the input crop size (256x128)."""
+
+    def __init__(self, state_dict, height=256, width=128, stride=12, device=None, prefix=""):
+        sd = {k[len(prefix):]: v for k, v in state_dict.items() if k.startswith(prefix)}
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        conv = _t(sd["conv1.weight"])
+        W, _, P, _ = conv.shape
+        layers = len([k for k in sd if k.endswith(".attn.in_proj_weight")])
+        self.width, self.layers, self.heads, self.patch, self.stride = W, layers, W // 64, P, stride
+        self.out_dim = _t(sd["proj"]).shape[1]
+        self.height, self.img_width = height, width
+        gh, gw = (height - P) // stride + 1, (width - P) // stride + 1
+        self.grid = (gh, gw)
+        self.n_ctx = int(_t(sd["VPT"]).shape[0]) if "VPT" in sd else 0
+        self.seq_len = 1 + gh * gw + self.n_ctx
+        pos = _t(sd["positional_embedding"])
+        if pos.shape[0] != 1 + gh * gw:
+            pos = resize_pos_embed(pos, gh, gw)
+        kpad = (3 * P * P + 63) // 64 * 64
+        convp = torch.zeros(W, kpad)
+        convp[:, :3 * P * P] = conv.reshape(W, -1)
+        pk = self._pk = _Packer(self.device)
+        w = self.weights = VitWeights()
+        w.width, w.layers, w.heads, w.patch, w.stride = W, layers, W // 64, P, stride
+        w.out_dim, w.grid_h, w.grid_w, w.n_ctx, w.kpad = self.out_dim, gh, gw, self.n_ctx, kpad
+        w.conv_w = pk.bf16(convp).data_ptr()
+        w.class_emb = pk.f32(sd["class_embedding"]).data_ptr()
+        w.pos_emb = pk.f32(pos).data_ptr()
+        w.ln_pre_w = pk.f32(sd["ln_pre.weight"]).data_ptr()
+        w.ln_pre_b = pk.f32(sd["ln_pre.bias"]).data_ptr()
+        w.ln_post_w = pk.f32(sd["ln_post.weight"]).data_ptr()
+        w.ln_post_b = pk.f32(sd["ln_post.bias"]).data_ptr()
+        w.proj_t = pk.bf16(_t(sd["proj"]).t()).data_ptr()
+        w.vpt = pk.f32(sd["VPT"]).data_ptr() if self.n_ctx else None
+        self._blocks = _pack_blocks(sd, "", layers, pk)
+        w.blocks = self._blocks
+        self._ws = {}
+
+    @property
+    def dtype(self):
+        return torch.float32
+
+    def _workspace(self, B, full):
+        nbytes = _fn("reidmi_vit_workspace_bytes")(ctypes.byref(self.weights), B, int(full))
+        if nbytes < 0:
+            raise _lib.ReidmiError(_lib.load().reidmi_last_error().decode())
+        ws = self._ws.get("buf")
+        if ws is None or ws.numel() < nbytes:
+            ws = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+            self._ws["buf"] = ws
+        return ws, nbytes
+
+    def _images(self, img):
+        if not isinstance(img, torch.Tensor):
+            img = torch.from_numpy(np.asarray(img))
+        img = img.to(self.device)
+        if img.dtype not in (torch.float32, torch.bfloat16):
+            img = img.float()
+        return img.contiguous()
+
+    def _run(self, img, tta, full, x12, proj, x11):
+        img = self._images(img)
+        B, C, H, Wd = img.shape
+        if C != 3:
+            raise ValueError("expected (B,3,H,W) images")
+        ws, nbytes = self._workspace(B, full)
+        if tta is not None:
+            tta = torch.as_tensor(tta, dtype=torch.int32).to(self.device).contiguous()
+        rc = _fn("reidmi_vit_forward")(ctypes.byref(self.weights), img.data_ptr(), int(img.dtype == torch.bfloat16),
+                                       B, H, Wd, None if tta is None else tta.data_ptr(), int(full),
+                                       x12.data_ptr(), proj.data_ptr(), None if x11 is None else x11.data_ptr(),
+                                       ws.data_ptr(), nbytes, _lib.stream(self.device))
+        if rc != 0:
+            raise _lib.ReidmiError(f"reidmi_vit_forward: {_lib.load().reidmi_last_error().decode()}")
+
+    def encode_image(self, img):
+        """(x11, x12, xproj), each [B, L, *] fp32 — custom_clip_model.py:100."""
+        B = img.shape[0]
+        L, W, E = self.seq_len, self.width, self.out_dim
+        kw = dict(device=self.device, dtype=torch.float32)
+        x11, x12, xp = torch.empty(B, L, W, **kw), torch.empty(B, L, W, **kw), torch.empty(B, L, E, **kw)
+        self._run(img, None, True, x12, xp, x11)
+        return x11, x12, xp
+
+    __call__ = encode_image
+
+    def encode_cls(self, img, tta=None, out_x12=None, out_proj=None):
+        """(x12[:,0], xproj[:,0]) of encode_image(img) (or of the augmented view when
+        ``tta`` [B,2] crop offsets are given) — what zero_shot_learning.py:85-87 consumes."""
+        B = img.shape[0]
+        kw = dict(device=self.device, dtype=torch.float32)
+        x12 = out_x12 if out_x12 is not None else torch.empty(B, self.width, **kw)
+        xp = out_proj if out_proj is not None else torch.empty(B, self.out_dim, **kw)
+        self._run(img, tta, False, x12, xp, None)
+        return x12, xp
+
+
+class TextTransformer:
+    """libreidmi text tower (CLIP.encode_text, maple.py:971-984; TextEncoder,
+    text_encoder.py:14-24)."""
+
+    def __init__(self, state_dict, device=None, prefix=""):
+        sd = {k[len(prefix):]: v for k, v in state_dict.items() if k.startswith(prefix)}
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        tok = _t(sd["token_embedding.weight"])
+        pos = _t(sd["positional_embedding"])
+        W = tok.shape[1]
+        layers = len([k for k in sd if k.startswith("transformer.") and k.endswith(".attn.in_proj_weight")])
+        self.width, self.layers, self.heads, self.ctx, self.vocab = W, layers, W // 64, pos.shape[0], tok.shape[0]
+        self.out_dim = _t(sd["text_projection"]).shape[1]
+        vp = [k for k in sd if k.endswith("VPT_shallow")]
+        self.n_ctx = int(_t(sd[vp[0]]).shape[0]) if vp else 0
+        pk = self._pk = _Packer(self.device)
+        w = self.weights = TextWeights()
+        w.width, w.layers, w.heads, w.ctx, w.vocab, w.out_dim, w.n_ctx = (W, layers, W // 64, pos.shape[0],
+                                                                          tok.shape[0], self.out_dim, self.n_ctx)
+        self.token_embedding_weight = pk.f32(tok)
+        w.tok_emb = self.token_embedding_weight.data_ptr()
+        self.positional_embedding = pk.f32(pos)
+        w.pos_emb = self.positional_embedding.data_ptr()
+        w.ln_final_w = pk.f32(sd["ln_final.weight"]).data_ptr()
+        w.ln_final_b = pk.f32(sd["ln_final.bias"]).data_ptr()
+        w.proj_t = pk.bf16(_t(sd["text_projection"]).t()).data_ptr()
+        self._blocks = _pack_blocks(sd, "", layers, pk)
+        w.blocks = self._blocks
+        self._ws = None
+
+    def token_embedding(self, tokens):
+        """nn.Embedding lookup (device) — used by prompt learners to build prompts."""
+        return self.token_embedding_weight[torch.as_tensor(tokens, device=self.device).long()]
+
+    def _forward(self, tokens, prompts):
+        tokens = torch.as_tensor(tokens).to(self.device, torch.int64).contiguous()
+        N = tokens.shape[0]
+        nbytes = _fn("reidmi_text_workspace_bytes")(ctypes.byref(self.weights), N)
+        if self._ws is None or self._ws.numel() < nbytes:
+            self._ws = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+        out = torch.empty(N, self.out_dim, device=self.device, dtype=torch.float32)
+        if prompts is not None:
+            prompts = prompts.to(self.device, torch.float32).contiguous()
+        rc = _fn("reidmi_text_forward")(ctypes.byref(self.weights), tokens.data_ptr(),
+                                        None if prompts is None else prompts.data_ptr(), N, out.data_ptr(),
+                                        self._ws.data_ptr(), nbytes, _lib.stream(self.device))
+        if rc != 0:
+            raise _lib.ReidmiError(f"reidmi_text_forward: {_lib.load().reidmi_last_error().decode()}")
+        return out
+
+    def encode_text(self, text):
+        return self._forward(text, None)
+
+
+class TextEncoder:
+    """text_encoder.TextEncoder over a TextTransformer: forward(prompts, tokenized_prompts)."""
+
+    def __init__(self, text_model):
+        self.text = text_model
+        self.positional_embedding = text_model.positional_embedding
+        self.dtype = torch.float32
+
+    def __call__(self, prompts, tokenized_prompts):
+        return self.text._forward(tokenized_prompts, prompts)
+
+    forward = __call__
+
+
+class CLIP:
+    """Minimal CLIP container with the reference's encode_image / encode_text."""
+
+    def __init__(self, visual=None, text=None):
+        self.visual = visual
+        self.text = text
+
+    @property
+    def dtype(self):
+        return torch.float32
+
+    def encode_image(self, image):
+        return self.visual.encode_image(image)
+
+    def encode_text(self, text):
+        return self.text.encode_text(text)
+
+    def eval(self):
+        return self

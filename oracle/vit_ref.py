@@ -1,0 +1,113 @@
+"""Floating-point oracle for the encoders: a plain-torch fp32 restatement of
+  custom_clip_model.VisionTransformer.forward (custom_clip_model.py:57-100),
+  maple.VisionTransformer IVLP prompts (maple.py:617-644, 754-785),
+  CLIP.encode_text / TextEncoder.forward (maple.py:971-984, text_encoder.py:14-24),
+over the same state-dict layout libreidmi packs.
+
+TEST INFRASTRUCTURE ONLY (tests/, smoke(), bench.py cpu_baseline leg).
+
+``bf16=True`` rounds to bfloat16 exactly where the HIP kernels do (GEMM operands, q/k/v,
+softmax probabilities before P.V, attention output), so tests can separate kernel bugs
+from the precision the MI355X path runs at.  With bf16=False it is the reference's fp32
+math, pinned to tests/golden/vit_b16.npz and text.npz (made by the reference modules).
+"""
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+
+def _t(a):
+    return a.detach().float() if isinstance(a, torch.Tensor) else torch.from_numpy(np.asarray(a, np.float32))
+
+
+def _r(x, on):
+    return x.to(torch.bfloat16).float() if on else x
+
+
+def _ln(x, w, b):
+    return F.layer_norm(x, (x.shape[-1],), _t(w), _t(b), 1e-5)
+
+
+def block(x, sd, p, heads, causal=False, bf16=False):
+    """ResidualAttentionBlock.forward (custom_clip_model.py:26-29) on x [B, L, W]."""
+    B, L, W = x.shape
+    h = _r(_ln(x, sd[p + "ln_1.weight"], sd[p + "ln_1.bias"]), bf16)
+    qkv = h @ _r(_t(sd[p + "attn.in_proj_weight"]), bf16).t() + _t(sd[p + "attn.in_proj_bias"])
+    qkv = _r(qkv, bf16).reshape(B, L, 3, heads, 64).permute(2, 0, 3, 1, 4)
+    q, k, v = qkv[0], qkv[1], qkv[2]
+    s = (q @ k.transpose(-1, -2)) * 0.125
+    if causal:
+        s = s + torch.full((L, L), float("-inf")).triu(1)
+    m = s.amax(-1, keepdim=True)
+    e = torch.exp(s - m)
+    den = e.sum(-1, keepdim=True)
+    o = (_r(e, bf16) @ v) / den
+    o = _r(o.permute(0, 2, 1, 3).reshape(B, L, W), bf16)
+    x = x + (o @ _r(_t(sd[p + "attn.out_proj.weight"]), bf16).t() + _t(sd[p + "attn.out_proj.bias"]))
+    h = _r(_ln(x, sd[p + "ln_2.weight"], sd[p + "ln_2.bias"]), bf16)
+    u = h @ _r(_t(sd[p + "mlp.c_fc.weight"]), bf16).t() + _t(sd[p + "mlp.c_fc.bias"])
+    u = _r(u * torch.sigmoid(1.702 * u), bf16)
+    return x + (u @ _r(_t(sd[p + "mlp.c_proj.weight"]), bf16).t() + _t(sd[p + "mlp.c_proj.bias"]))
+
+
+def tta_view(img, offs):
+    """data_prepare.py:263-270 on a normalised crop: flip, Pad((10,5)) (-1 fill), crop."""
+    B, C, H, W = img.shape
+    padded = torch.full((B, C, H + 10, W + 20), -1.0)
+    padded[:, :, 5:5 + H, 10:10 + W] = img.flip(-1)
+    return torch.stack([padded[b, :, int(offs[b][0]):int(offs[b][0]) + H, int(offs[b][1]):int(offs[b][1]) + W]
+                        for b in range(B)])
+
+
+def vit_forward(sd, img, stride=12, bf16=False, tta=None):
+    """(x11, x12, xproj) of the vision tower; img [B,3,H,W] fp32."""
+    img = _t(img)
+    if tta is not None:
+        img = tta_view(img, tta)
+    conv = _t(sd["conv1.weight"])
+    W, _, P, _ = conv.shape
+    B, _, H, Wd = img.shape
+    gh, gw = (H - P) // stride + 1, (Wd - P) // stride + 1
+    heads = W // 64
+    cols = F.unfold(_r(img, bf16), P, stride=stride).transpose(1, 2)  # [B, NP, 3PP] (c,ky,kx)
+    x = cols @ _r(conv.reshape(W, -1), bf16).t()
+    pos = _t(sd["positional_embedding"])
+    cls = (_t(sd["class_embedding"]) + pos[0]).expand(B, 1, W)
+    x = torch.cat([cls, x + pos[1:1 + gh * gw]], 1)
+    n_ctx = 0
+    if "VPT" in sd:
+        vpt = _t(sd["VPT"]).half().float()
+        n_ctx = vpt.shape[0]
+        x = torch.cat([x, vpt.expand(B, -1, -1)], 1)
+    x = _ln(x, sd["ln_pre.weight"], sd["ln_pre.bias"])
+    L = x.shape[1]
+    x11 = None
+    for i in range(12):
+        p = f"transformer.resblocks.{i}."
+        if i > 0 and (p + "VPT_shallow") in sd:
+            x = torch.cat([x[:, :L - n_ctx], _t(sd[p + "VPT_shallow"]).half().float().expand(B, -1, -1)], 1)
+        x = block(x, sd, p, heads, False, bf16)
+        if i == 10:
+            x11 = x
+    x12 = _ln(x, sd["ln_post.weight"], sd["ln_post.bias"])
+    xp = _r(x12, bf16) @ _r(_t(sd["proj"]), bf16)
+    return x11, x12, xp
+
+
+def text_forward(sd, tokens, prompts=None, bf16=False):
+    """CLIP.encode_text(tokens) or TextEncoder(prompts, tokens): [N, E]."""
+    tokens = torch.as_tensor(np.asarray(tokens)).long()
+    W = _t(sd["ln_final.weight"]).shape[0]
+    heads = W // 64
+    x = _t(sd["token_embedding.weight"])[tokens] if prompts is None else _t(prompts)
+    x = x + _t(sd["positional_embedding"])
+    N, L, _ = x.shape
+    layers = len([k for k in sd if k.startswith("transformer.") and k.endswith(".attn.in_proj_weight")])
+    for i in range(layers):
+        p = f"transformer.resblocks.{i}."
+        if i > 0 and (p + "VPT_shallow") in sd:
+            ctx = _t(sd[p + "VPT_shallow"]).half().float()
+            x = torch.cat([x[:, :1], ctx.expand(N, -1, -1), x[:, 1 + ctx.shape[0]:]], 1)
+        x = block(x, sd, p, heads, True, bf16)
+    x = _ln(x[torch.arange(N), tokens.argmax(-1)], sd["ln_final.weight"], sd["ln_final.bias"])
+    return _r(x, bf16) @ _r(_t(sd["text_projection"]), bf16)

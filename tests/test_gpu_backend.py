@@ -1,0 +1,137 @@
+"""GPU parity of the retrieval back end (libreidmi) against the oracle and the
+reference-generated fixtures.  Integer/index outputs and exact-fp32 distances are
+compared bit-for-bit."""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from multimodal_reid_amd import synthetic as syn
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _ev():
+    from multimodal_reid_amd import evaluate
+    return evaluate
+
+
+def _inputs(seed=1, Q=100, G=500, D=1280, junk=0.04):
+    qp, gp, qc, gc = syn.labels(Q, G, num_ids=60, num_cams=6, seed=seed, distractor_frac=0.1, junk_frac=junk)
+    qf, gf = syn.features(qp, gp, dim=D, seed=seed, noise=4.0)
+    return qf, gf, qp, gp, qc, gc
+
+
+def test_l2norm_bitexact(gpu):
+    qf, gf, *_ = _inputs()
+    x = np.concatenate([qf, gf])
+    y = _ev().l2_normalize_device(torch.from_numpy(x)).cpu().numpy()
+    assert np.array_equal(y.view(np.uint32), oracle.l2norm(x).view(np.uint32))
+
+
+@pytest.mark.parametrize("Q,G,D", [(100, 500, 1280), (37, 259, 768), (1, 1, 2), (130, 129, 1792), (5, 300, 513)])
+def test_distmat_bitexact(gpu, Q, G, D):
+    r = np.random.default_rng(Q * 7 + G)
+    q = r.standard_normal((Q, D)).astype(np.float32)
+    g = r.standard_normal((G, D)).astype(np.float32)
+    d = _ev().euclidean_distance(torch.from_numpy(q), torch.from_numpy(g))
+    assert isinstance(d, np.ndarray) and d.dtype == np.float32
+    assert np.array_equal(d.view(np.uint32), oracle.distmat(q, g).view(np.uint32))
+
+
+def test_distmat_matches_reference_fixture(gpu):
+    g = golden("backend_small.npz")
+    qf, gf, *_ = _inputs()
+    feats = torch.nn.functional.normalize(torch.from_numpy(np.concatenate([qf, gf])), dim=1, p=2)
+    d = _ev().euclidean_distance(feats[:100], feats[100:])
+    assert np.abs(d - g["distmat"]).max() < 1e-5
+
+
+@pytest.mark.parametrize("name,k", [("backend_small.npz", 50), ("backend_ties.npz", 20)])
+def test_topk_rank_lists_bitexact(gpu, name, k):
+    g = golden(name)
+    idx = _ev().topk_rows_device(torch.from_numpy(g["distmat"]), k).cpu().numpy()
+    assert np.array_equal(idx, g[f"rank{k}_stable"])
+
+
+def test_topk_long_rows_and_divisor(gpu):
+    r = np.random.default_rng(5)
+    x = np.round(r.random((40, 20000)) * 512).astype(np.float32)  # heavy ties
+    div = (1 + r.random(40)).astype(np.float32)
+    idx, val = _ev().topk_rows_device(torch.from_numpy(x), 51, row_div=torch.from_numpy(div).cuda(),
+                                      with_values=True)
+    ref = oracle.topk_rows(x / div[:, None], 51)
+    assert np.array_equal(idx.cpu().numpy(), ref)
+
+
+def _eval_rows_np(dist, qp, gp, qc, gc):
+    v, f, a, n, o = _ev().eval_rows_device(torch.from_numpy(dist), qp, gp, qc, gc)
+    return v.cpu().numpy(), f.cpu().numpy(), a.cpu().numpy(), n.cpu().numpy()
+
+
+@pytest.mark.parametrize("name,max_rank", [("backend_small.npz", 50), ("backend_ties.npz", 20)])
+def test_eval_bitexact(gpu, name, max_rank):
+    g = golden(name)
+    args = (g["q_pids"], g["g_pids"], g["q_cams"], g["g_cams"])
+    rows = _eval_rows_np(g["distmat"], *args)
+    ref = oracle.eval_rows(g["distmat"], *args)
+    for a, b in zip(rows, ref):
+        assert np.array_equal(a.astype(b.dtype), b)
+    cmc, mAP = _ev().eval_func(g["distmat"], *args, max_rank=max_rank)
+    assert np.array_equal(cmc, g["cmc_stable"]) and cmc.dtype == np.float32
+    assert mAP == g["map_stable"]
+
+
+def test_r1_map_eval_end_to_end(gpu):
+    g = golden("backend_small.npz")
+    qf, gf, qp, gp, qc, gc = _inputs()
+    ev = _ev().R1_mAP_eval(100, max_rank=50, feat_norm=True)
+    ev.reset()
+    ev.update((torch.from_numpy(np.concatenate([qf, gf])), np.concatenate([qp, gp]), np.concatenate([qc, gc])))
+    cmc, mAP = ev.compute()
+    assert abs(mAP - g["map_r1map"]) < 1e-6
+    assert np.abs(cmc - g["cmc_r1map"]).max() <= 1.0 / 100 + 1e-7  # at most one query flips on a near-tie
+
+
+def test_eval_market_scale_rows_vs_oracle(gpu):
+    sp = syn.DATASET_SPLITS["market1501"]
+    qp, gp, qc, gc = syn.labels(sp["num_query"], sp["num_gallery"], sp["num_ids"], sp["num_cams"], seed=7,
+                                junk_frac=0.02)
+    r = np.random.default_rng(7)
+    dev = torch.device("cuda")
+    q = torch.from_numpy(r.standard_normal((sp["num_query"], 256)).astype(np.float32)).to(dev)
+    gf = torch.from_numpy(r.standard_normal((sp["num_gallery"], 256)).astype(np.float32)).to(dev)
+    ev = _ev()
+    dist = ev.euclidean_distance_device(q, gf)
+    v, f, a, n, o = ev.eval_rows_device(dist, qp, gp, qc, gc)
+    sel = np.arange(0, sp["num_query"], 97)
+    dsub = dist[sel].cpu().numpy()
+    assert np.array_equal(dsub.view(np.uint32), oracle.distmat(q[sel].cpu().numpy(), gf.cpu().numpy()).view(np.uint32))
+    ref = oracle.eval_rows(dsub, qp[sel], gp, qc[sel], gc)
+    for a_, b_ in zip((v, f, a, n), ref):
+        assert np.array_equal(a_.cpu().numpy()[sel].astype(b_.dtype), b_)
+    idx = ev.topk_rows_device(dist[sel], 50).cpu().numpy()
+    assert np.array_equal(idx, oracle.topk_rows(dsub, 50))
+
+
+def test_eval_edge_cases(gpu):
+    ev = _ev()
+    r = np.random.default_rng(3)
+    # gallery smaller than max_rank: max_rank shrinks to num_g (evaluate.py:37-39)
+    dist = r.random((4, 10)).astype(np.float32)
+    qp = np.array([1, 2, 3, 9]); gp = np.array([1, 1, 2, 2, 3, 3, 4, 4, 5, 5])
+    qc = np.zeros(4, np.int64); gc = np.ones(10, np.int64)
+    cmc, mAP = ev.eval_func(dist, qp, gp, qc, gc, max_rank=50)
+    ocmc, omap = oracle.eval_func(dist, qp, gp, qc, gc, max_rank=50)
+    assert cmc.shape == (10,) and np.array_equal(cmc, ocmc) and mAP == omap
+    # no query identity in the gallery -> AssertionError (evaluate.py:82)
+    with pytest.raises(AssertionError):
+        ev.eval_func(dist, np.array([7, 8, 9, 9]), gp, qc, gc)
+    # ragged kept lengths below max_rank -> ValueError like np.asarray(all_cmc) (evaluate.py:84)
+    gp2 = np.array([1, 1, 1, 2, 2, 3, 3, 4, 4, 5])
+    gc2 = np.array([0, 0, 1, 0, 1, 0, 1, 0, 1, 0])
+    with pytest.raises(ValueError):
+        oracle.eval_func(dist, qp, gp2, qc, gc2, max_rank=50)
+    with pytest.raises(ValueError):
+        ev.eval_func(dist, qp, gp2, qc, gc2, max_rank=50)
