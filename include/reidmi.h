@@ -65,6 +65,23 @@ int reidmi_eval_rows(const float* dist, int64_t Q, int64_t G, int64_t ldd, const
                      int64_t* first, double* ap, int64_t* nkept, int32_t* overflow, void* stream);
 
 
+/* k-reciprocal re-ranking — re_ranking(probFea, galFea, k1, k2, lambda_value) (reranking.py:29-100),
+ * bit-exact with the reference's numpy arithmetic given the same distances (stable ties).
+ * feat [Q+G][ldf] fp32 = cat(probFea, galFea).  final_dist [Q][ldo] fp32 = re-ranked q x g
+ * distances.  one_minus_lambda_h = np.float16(1 - lambda) bits, lambda_f = np.float32(lambda)
+ * (numpy's weak-scalar conversions, reranking.py:95).  1 <= k1 <= 50, 1 <= k2 <= 32.
+ * flags: device int32, OR-ed with 1/2/4 when a row exceeds the V / V_qe / staging capacity. */
+int64_t reidmi_rerank_workspace_bytes(int64_t Q, int64_t G, int k1, int k2, int from_dist, int need_transpose);
+int reidmi_rerank(const float* feat, int64_t Q, int64_t G, int64_t D, int64_t ldf, int k1, int k2,
+                  uint16_t one_minus_lambda_h, float lambda_f, float* final_dist, int64_t ldo, void* ws,
+                  int64_t ws_bytes, int32_t* flags, void* stream);
+/* From a given (Q+G) x (Q+G) distance (reranking.py:33-35 only_local / local_distmat paths):
+ * original_dist = dist (+ add, nullable); symmetric = 1 promises original_dist == its
+ * transpose (then no transpose pass is made). */
+int reidmi_rerank_from_dist(const float* dist, const float* add, int64_t Q, int64_t G, int symmetric, int k1,
+                            int k2, uint16_t one_minus_lambda_h, float lambda_f, float* final_dist, int64_t ldo,
+                            void* ws, int64_t ws_bytes, int32_t* flags, void* stream);
+
 /* ------------------------------------------------------------------ encoders */
 
 /* bf16 GEMM C = A . W^T (+bias) on v_mfma_f32_16x16x32_bf16, fp32 accumulation.

@@ -26,6 +26,10 @@ SIGNATURES = {
     "reidmi_topk_rows_f32": [_vp, _i64, _i64, _i64, _vp, _i32, _vp, _vp, _i64, _vp],
     "reidmi_eval_rows": [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "reidmi_gemm_bf16": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _i64, _vp],
+    "reidmi_rerank_workspace_bytes": [_i64, _i64, _i32, _i32, _i32, _i32],
+    "reidmi_rerank": [_vp, _i64, _i64, _i64, _i64, _i32, _i32, _u16, _f32, _vp, _i64, _vp, _i64, _vp, _vp],
+    "reidmi_rerank_from_dist": [_vp, _vp, _i64, _i64, _i32, _i32, _i32, _u16, _f32, _vp, _i64, _vp, _i64, _vp,
+                                _vp],
     "reidmi_attn_lpad": [_i32],
     "reidmi_prof_enable": [_i32],
     "reidmi_prof_collect": [_i32, _vp, _vp, _vp],
@@ -61,7 +65,7 @@ def load():
     for name, args in SIGNATURES.items():
         fn = getattr(L, name)
         fn.argtypes = args
-        fn.restype = _i32
+        fn.restype = _i64 if name.endswith("_bytes") else _i32
     _LIB = L
     return L
 

@@ -323,6 +323,26 @@ __global__ __launch_bounds__(256) void eval_rows_kernel(
     }
 }
 
+int topk_launch(const float* x, int64_t rows, int64_t cols, int64_t ldx, const float* row_div, int K,
+                int32_t* out_idx, float* out_val, int64_t ldo, hipStream_t s) {
+    RM_REQUIRE(rows >= 0 && cols > 0 && ldx >= cols && K > 0 && K <= 64 && K <= cols && ldo >= K,
+               "topk_rows: need 0 < k <= min(64, cols)");
+    RM_REQUIRE(cols < 0x7fffffff, "topk_rows: cols must fit int32");
+    if (rows == 0) return OK;
+    hipLaunchKernelGGL(topk_rows_kernel, dim3((unsigned)rows), dim3(256), 0, s, x, cols, ldx, row_div, K, out_idx,
+                       out_val, ldo);
+    RM_LAUNCHED();
+    return OK;
+}
+
+int distmat_impl(bool cosine, const float* q, int64_t Q, int64_t ldq, const float* g, int64_t G, int64_t ldg,
+                 int64_t D, float* out, int64_t ldo, float* ws, void* stream);
+
+int distmat_launch(const float* q, int64_t Q, int64_t ldq, const float* g, int64_t G, int64_t ldg, int64_t D,
+                   float* out, int64_t ldo, float* ws, hipStream_t s) {
+    return distmat_impl(false, q, Q, ldq, g, G, ldg, D, out, ldo, ws, s);
+}
+
 }  // namespace reidmi
 
 using namespace reidmi;
@@ -347,7 +367,7 @@ REIDMI_API int reidmi_l2norm_f32(const float* x, int64_t n, int64_t d, int64_t l
     return OK;
 }
 
-static int distmat_impl(bool cosine, const float* q, int64_t Q, int64_t ldq, const float* g, int64_t G,
+int reidmi::distmat_impl(bool cosine, const float* q, int64_t Q, int64_t ldq, const float* g, int64_t G,
                         int64_t ldg, int64_t D, float* out, int64_t ldo, float* ws, void* stream) {
     RM_REQUIRE(Q >= 0 && G >= 0 && D > 0 && ldq >= D && ldg >= D && ldo >= G, "distmat: bad shape");
     RM_REQUIRE(ws != nullptr, "distmat: workspace (Q+G floats) required");
@@ -381,14 +401,7 @@ REIDMI_API int reidmi_cosine_f32(const float* q, int64_t Q, int64_t ldq, const f
 
 REIDMI_API int reidmi_topk_rows_f32(const float* x, int64_t rows, int64_t cols, int64_t ldx, const float* row_div,
                                     int k, int32_t* out_idx, float* out_val, int64_t ldo, void* stream) {
-    RM_REQUIRE(rows >= 0 && cols > 0 && ldx >= cols && k > 0 && k <= 64 && k <= cols && ldo >= k,
-               "topk_rows: need 0 < k <= min(64, cols)");
-    RM_REQUIRE(cols < 0x7fffffff, "topk_rows: cols must fit int32");
-    if (rows == 0) return OK;
-    hipLaunchKernelGGL(topk_rows_kernel, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream, x, cols, ldx,
-                       row_div, k, out_idx, out_val, ldo);
-    RM_LAUNCHED();
-    return OK;
+    return topk_launch(x, rows, cols, ldx, row_div, k, out_idx, out_val, ldo, (hipStream_t)stream);
 }
 
 REIDMI_API int reidmi_eval_rows(const float* dist, int64_t Q, int64_t G, int64_t ldd, const int64_t* q_pids,

@@ -167,7 +167,7 @@ def test_text_encoder_vs_reference(gpu):
     assert _cos(out, g["text_feat"]).min() >= 0.9999
     with torch.no_grad():
         ref = vit_ref.text_forward(sd, g["tokens"], bf16=True).numpy()
-    assert _cos(out, ref).min() >= 0.99999
+    assert _cos(out, ref).min() >= 0.99995  # 12 causal blocks: bf16 rounding flips compound
     # TextEncoder(prompts, tokenized) == encode_text when prompts = token_embedding(tokens)
     te = TextEncoder(tm)
     prompts = tm.token_embedding(g["tokens"])
