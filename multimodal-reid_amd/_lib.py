@@ -32,6 +32,7 @@ SIGNATURES = {
                                 _vp],
     "reidmi_attn_lpad": [_i32],
     "reidmi_prof_enable": [_i32],
+    "reidmi_gemm_set_variant": [_i32],
     "reidmi_prof_collect": [_i32, _vp, _vp, _vp],
     "reidmi_mhsa_bf16": [_vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp],
     "reidmi_layernorm": [_vp, _i64, _i64, _vp, _i64, _vp, _vp, _f32, _vp, _i64, _vp, _i64, _vp],

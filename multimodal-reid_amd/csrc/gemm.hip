@@ -12,6 +12,7 @@
 // an XCD's L2).
 #include "gemm.h"
 
+#include <cstdlib>
 #include <mutex>
 #include <vector>
 
@@ -33,6 +34,18 @@ static std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
 static size_t used = 0;
 }  // namespace prof
 
+// Tile selection: 0 = auto (v2 when it fills the chip), 1 = force v1 (128x128), 2 = force v2
+// (256x256).  Set by reidmi_gemm_set_variant (tests / A-B timing in one process); the
+// REIDMI_GEMM_VARIANT environment variable gives the initial value.
+static int g_variant = -1;
+static int variant() {
+    if (g_variant < 0) {
+        const char* e = getenv("REIDMI_GEMM_VARIANT");
+        g_variant = e ? atoi(e) : 0;
+    }
+    return g_variant;
+}
+
 constexpr int GB_M = 128, GB_N = 128, GB_K = 64;
 
 __device__ __forceinline__ int swz(int r, int kc) { return r * GB_K + ((kc ^ ((r >> 1) & 7)) << 3); }
@@ -45,6 +58,48 @@ __device__ __forceinline__ uint2 pack_bf16x4(float a, float b, float c, float d)
 __device__ __forceinline__ float quick_gelu(float x) {
     // x * sigmoid(1.702 x)   (custom_clip_model.py:52-54)
     return x * __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * x));
+}
+
+// Epilogue of one lane's 4 consecutive outputs C[m][nb..nb+3] (see gemm.h for the modes).
+template <int EPI>
+__device__ __forceinline__ void epilogue(const EpiArgs& ea, f32x4 v, int64_t m, int nb, int N) {
+    if (EPI != EPI_PATCH && ea.bias != nullptr) {
+        const float4 b = *(const float4*)(ea.bias + nb);
+        v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+    }
+    if constexpr (EPI == EPI_BF16) {
+        *(uint2*)((__bf16*)ea.out + m * ea.ldc + nb) = pack_bf16x4(v[0], v[1], v[2], v[3]);
+    } else if constexpr (EPI == EPI_GELU_BF16) {
+        *(uint2*)((__bf16*)ea.out + m * ea.ldc + nb) =
+            pack_bf16x4(quick_gelu(v[0]), quick_gelu(v[1]), quick_gelu(v[2]), quick_gelu(v[3]));
+    } else if constexpr (EPI == EPI_RESID_F32) {
+        float4* p = (float4*)((float*)ea.out + m * ea.ldc + nb);
+        float4 x = *p;
+        x.x += v[0]; x.y += v[1]; x.z += v[2]; x.w += v[3];
+        *p = x;
+    } else if constexpr (EPI == EPI_F32) {
+        *(float4*)((float*)ea.out + m * ea.ldc + nb) = make_float4(v[0], v[1], v[2], v[3]);
+    } else if constexpr (EPI == EPI_PATCH) {
+        const int64_t b = m / ea.npatch, p = m % ea.npatch;
+        const int64_t row = b * ea.seq + 1 + p;
+        const float4 pe = *(const float4*)(ea.pos + (1 + p) * (int64_t)N + nb);
+        *(float4*)((float*)ea.out + row * ea.ldc + nb) = make_float4(v[0] + pe.x, v[1] + pe.y, v[2] + pe.z, v[3] + pe.w);
+    } else if constexpr (EPI == EPI_QKV) {
+        const int wd = ea.heads * 64;
+        const int which = nb / wd, h = (nb % wd) >> 6, d = nb & 63;
+        const int64_t b = m / ea.seq, t = m % ea.seq;
+        const int64_t bh = b * ea.heads + h;
+        if (which < 2) {
+            __bf16* dst = (__bf16*)(which == 0 ? ea.q : ea.k) + (bh * ea.seq + t) * 64 + d;
+            *(uint2*)dst = pack_bf16x4(v[0], v[1], v[2], v[3]);
+        } else {
+            __bf16* dst = (__bf16*)ea.vt + (bh * 64 + d) * (int64_t)ea.lpad + t;
+            dst[0] = (__bf16)v[0];
+            dst[ea.lpad] = (__bf16)v[1];
+            dst[2 * (int64_t)ea.lpad] = (__bf16)v[2];
+            dst[3 * (int64_t)ea.lpad] = (__bf16)v[3];
+        }
+    }
 }
 
 template <int EPI>
@@ -137,56 +192,132 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(const __bf16* __restr
         const int64_t m = m0 + wm * 64 + i * 16 + (lane & 15);
         if (m >= M) continue;
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int nb = n0 + wn * 64 + j * 16 + (lane >> 4) * 4;
-            f32x4 v = acc[i][j];
-            if (EPI != EPI_PATCH && ea.bias != nullptr) {
-                const float4 b = *(const float4*)(ea.bias + nb);
-                v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
-            }
-            if constexpr (EPI == EPI_BF16) {
-                *(uint2*)((__bf16*)ea.out + m * ea.ldc + nb) = pack_bf16x4(v[0], v[1], v[2], v[3]);
-            } else if constexpr (EPI == EPI_GELU_BF16) {
-                *(uint2*)((__bf16*)ea.out + m * ea.ldc + nb) =
-                    pack_bf16x4(quick_gelu(v[0]), quick_gelu(v[1]), quick_gelu(v[2]), quick_gelu(v[3]));
-            } else if constexpr (EPI == EPI_RESID_F32) {
-                float4* p = (float4*)((float*)ea.out + m * ea.ldc + nb);
-                float4 x = *p;
-                x.x += v[0]; x.y += v[1]; x.z += v[2]; x.w += v[3];
-                *p = x;
-            } else if constexpr (EPI == EPI_F32) {
-                *(float4*)((float*)ea.out + m * ea.ldc + nb) = make_float4(v[0], v[1], v[2], v[3]);
-            } else if constexpr (EPI == EPI_PATCH) {
-                const int64_t b = m / ea.npatch, p = m % ea.npatch;
-                const int64_t row = b * ea.seq + 1 + p;
-                const float4 pe = *(const float4*)(ea.pos + (1 + p) * (int64_t)N + nb);
-                *(float4*)((float*)ea.out + row * ea.ldc + nb) =
-                    make_float4(v[0] + pe.x, v[1] + pe.y, v[2] + pe.z, v[3] + pe.w);
-            } else if constexpr (EPI == EPI_QKV) {
-                const int wd = ea.heads * 64;
-                const int which = nb / wd, h = (nb % wd) >> 6, d = nb & 63;
-                const int64_t b = m / ea.seq, t = m % ea.seq;
-                const int64_t bh = b * ea.heads + h;
-                if (which < 2) {
-                    __bf16* dst = (__bf16*)(which == 0 ? ea.q : ea.k) + (bh * ea.seq + t) * 64 + d;
-                    *(uint2*)dst = pack_bf16x4(v[0], v[1], v[2], v[3]);
-                } else {
-                    __bf16* dst = (__bf16*)ea.vt + (bh * 64 + d) * (int64_t)ea.lpad + t;
-                    dst[0] = (__bf16)v[0];
-                    dst[ea.lpad] = (__bf16)v[1];
-                    dst[2 * (int64_t)ea.lpad] = (__bf16)v[2];
-                    dst[3 * (int64_t)ea.lpad] = (__bf16)v[3];
-                }
-            }
-        }
+        for (int j = 0; j < 4; j++) epilogue<EPI>(ea, acc[i][j], m, n0 + wn * 64 + j * 16 + (lane >> 4) * 4, N);
     }
 #undef GLOAD
 #undef LSTORE
 }
 
+
+// ===================================================================== v2 tile
+// 256x256x64 block tile, 512 threads = 8 waves as 2 (M) x 4 (N), 128x64 per wave
+// (8x4 tiles of 16x16x32): half the LDS bytes per FLOP of the 64x64-per-wave v1 tile.
+// Operands go HBM -> LDS by global_load_lds_dwordx4 (no VGPR staging): one wave-instruction
+// fills 1 KiB = 8 LDS rows of 128 B, lane l -> row 8j + l/8, physical 16-B chunk l%8.  The
+// (row>>1)&7 XOR swizzle is applied on the per-lane SOURCE address (logical chunk
+// kc = physical ^ swz(row)), and the same XOR on the ds_read side, so LDS stays lane-linear
+// and fragment reads stay conflict-free.  Two LDS stages (2 x 64 KiB): tile t+1 streams in
+// while tile t is multiplied; one vmcnt(0) + barrier per K-step.  All LDS is one dynamic
+// array (a second __shared__ object makes hipcc drain vmcnt before every ds_read).
+constexpr int G2_M = 256, G2_N = 256;
+constexpr int G2_STAGE = (G2_M + G2_N) * GB_K;  // bf16 elements per stage
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+template <int EPI>
+__global__ __launch_bounds__(512, 2) void gemm2_bf16_kernel(const __bf16* __restrict__ A, int64_t lda,
+                                                            const __bf16* __restrict__ W, int64_t ldw, int64_t M,
+                                                            int N, int K, EpiArgs ea, int tiles_n, int nwg) {
+    extern __shared__ __attribute__((aligned(16))) __bf16 lds2[];
+    const int bid = blockIdx.x;
+    const int xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
+    const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+    const int tm = wg / tiles_n, tn = wg % tiles_n;
+    const int64_t m0 = (int64_t)tm * G2_M;
+    const int n0 = tn * G2_N;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wid >> 2, wn = wid & 3;
+
+    // glds sources: wave wid fills 1-KiB pieces j = 4*wid + u (u < 4) of A and of W
+    const __bf16* srcA[4];
+    const __bf16* srcW[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const int j = wid * 4 + u;
+        const int r = 8 * j + (lane >> 3);
+        const int kc = (lane & 7) ^ ((r >> 1) & 7);
+        int64_t gm = m0 + r;
+        gm = gm < M ? gm : M - 1;  // rows past M read a valid row; their outputs are dropped
+        srcA[u] = A + gm * lda + kc * 8;
+        srcW[u] = W + (int64_t)(n0 + r) * ldw + kc * 8;
+    }
+#define G2_ISSUE(stage, k0)                                                                              \
+    do {                                                                                                 \
+        __bf16* base_ = lds2 + (stage) * G2_STAGE;                                                       \
+        _Pragma("unroll") for (int u = 0; u < 4; u++) {                                                  \
+            const int j = wid * 4 + u;                                                                   \
+            __builtin_amdgcn_global_load_lds(srcA[u] + (k0), (lds_ptr_t)(base_ + j * 512), 16, 0, 0);    \
+            __builtin_amdgcn_global_load_lds(srcW[u] + (k0), (lds_ptr_t)(base_ + G2_M * GB_K + j * 512), \
+                                             16, 0, 0);                                                  \
+        }                                                                                                \
+    } while (0)
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    G2_ISSUE(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int nk = K / GB_K;
+    for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        if (kt + 1 < nk) G2_ISSUE(cur ^ 1, (kt + 1) * GB_K);
+        const __bf16* sA = lds2 + cur * G2_STAGE;
+        const __bf16* sW = sA + G2_M * GB_K;
+#pragma unroll
+        for (int ks = 0; ks < 2; ks++) {
+            const int kc = ks * 4 + (lane >> 4);
+            bf16x8 wf[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) wf[j] = *(const bf16x8*)(sW + swz(wn * 64 + j * 16 + (lane & 15), kc));
+            bf16x8 af[8];
+#pragma unroll
+            for (int i = 0; i < 8; i++) af[i] = *(const bf16x8*)(sA + swz(wm * 128 + i * 16 + (lane & 15), kc));
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af[i], acc[i][j], 0, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+#undef G2_ISSUE
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const int64_t m = m0 + wm * 128 + i * 16 + (lane & 15);
+        if (m >= M) continue;
+#pragma unroll
+        for (int j = 0; j < 4; j++) epilogue<EPI>(ea, acc[i][j], m, n0 + wn * 64 + j * 16 + (lane >> 4) * 4, N);
+    }
+}
+
 template <int EPI>
 static int launch(const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N, int64_t K,
                   const EpiArgs& ea, hipStream_t s) {
+    const int var = variant();
+    if (N % G2_N == 0 && var != 1 && (var == 2 || (int64_t)ceil_div(M, G2_M) * (N / G2_N) >= 512)) {
+        const int tiles_m = ceil_div(M, G2_M), tiles_n = (int)(N / G2_N);
+        const int64_t nwg = (int64_t)tiles_m * tiles_n;
+        RM_REQUIRE(nwg < (1ll << 31), "gemm: grid too large");
+        const size_t lds = 2 * (size_t)G2_STAGE * 2;
+        static bool attr = false;
+        if (!attr) {
+            RM_CHECK_HIP(hipFuncSetAttribute((const void*)gemm2_bf16_kernel<EPI>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            attr = true;
+        }
+        hipLaunchKernelGGL(gemm2_bf16_kernel<EPI>, dim3((unsigned)nwg), dim3(512), lds, s, (const __bf16*)A, lda,
+                           (const __bf16*)W, ldw, M, (int)N, (int)K, ea, tiles_n, (int)nwg);
+        RM_LAUNCHED();
+        return OK;
+    }
     const int tiles_m = ceil_div(M, GB_M), tiles_n = (int)(N / GB_N);
     const int64_t nwg = (int64_t)tiles_m * tiles_n;
     RM_REQUIRE(nwg < (1ll << 31), "gemm: grid too large");
@@ -233,6 +364,12 @@ int gemm_bf16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, i
 }  // namespace reidmi
 
 using namespace reidmi;
+
+REIDMI_API int reidmi_gemm_set_variant(int v) {
+    RM_REQUIRE(v >= 0 && v <= 2, "gemm variant must be 0 (auto), 1 (128x128) or 2 (256x256)");
+    g_variant = v;
+    return OK;
+}
 
 REIDMI_API int reidmi_prof_enable(int on) {
     std::lock_guard<std::mutex> g(prof::mu);

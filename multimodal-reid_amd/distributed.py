@@ -1,0 +1,77 @@
+"""Data-parallel evaluation over one node: one process per GPU, torch.distributed with the
+"nccl" backend (= RCCL over xGMI on MI355X); "gloo" for CPU tests.
+
+The reference is single-GPU (no collective call sites).  The one exchange
+step this path needs:
+  1. rank r embeds its contiguous shard of query and gallery images (no communication);
+  2. all-gather of the (L2-normalised) gallery feature blocks — every rank needs the
+     whole gallery to rank its queries;
+  3. each rank scores its query shard (distmat + eval rows) locally;
+  4. all-gather of the per-query results (valid, first-match rank, AP, n_kept: 32 B/query),
+     then every rank reduces them in global query order with numpy's own arithmetic, so the
+     CMC/mAP are bit-identical for any world size.
+Re-ranking needs every row of the N x N neighbourhood structure; it runs replicated after
+an all-gather of query and gallery features (the rerank stage itself is not sharded yet).
+"""
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def world():
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+def shard(n, rank, world_size):
+    """Contiguous [lo, hi) slice of n items for `rank` (sizes differ by at most one)."""
+    return n * rank // world_size, n * (rank + 1) // world_size
+
+
+def gather_rows(x, n_total):
+    """All-gather row shards produced by `shard(n_total, r, W)` into one [n_total, ...] tensor
+    (same device as x).  RCCL path: one padded all_gather_into_tensor."""
+    rank, W = world()
+    if W == 1:
+        return x
+    sizes = [shard(n_total, r, W)[1] - shard(n_total, r, W)[0] for r in range(W)]
+    mx = max(sizes)
+    pad = torch.zeros((mx,) + tuple(x.shape[1:]), device=x.device, dtype=x.dtype)
+    pad[:x.shape[0]] = x
+    if dist.get_backend() == "nccl":
+        out = torch.empty((W * mx,) + tuple(x.shape[1:]), device=x.device, dtype=x.dtype)
+        dist.all_gather_into_tensor(out, pad)
+        parts = [out[r * mx:r * mx + sizes[r]] for r in range(W)]
+    else:
+        bufs = [torch.empty_like(pad) for _ in range(W)]
+        dist.all_gather(bufs, pad)
+        parts = [bufs[r][:sizes[r]] for r in range(W)]
+    return torch.cat(parts)
+
+
+def pack_rows(valid, first, ap, nkept):
+    """Per-query results as one float64 [Q_local, 4] block (indices < 2^53 are exact)."""
+    return torch.stack([torch.as_tensor(valid).double(), torch.as_tensor(first).double(),
+                        torch.as_tensor(ap).double(), torch.as_tensor(nkept).double()], 1)
+
+
+def unpack_rows(rows):
+    rows = rows.cpu().numpy() if isinstance(rows, torch.Tensor) else rows
+    return rows[:, 0] > 0, rows[:, 1].astype(np.int64), rows[:, 2], rows[:, 3].astype(np.int64)
+
+
+def sharded_eval(q_feat, g_feat, q_pids, g_pids, q_camids, g_camids, num_query, num_gallery, rows_fn, max_rank=50,
+                 aggregate=None):
+    """Steps 2-4 above.  q_feat / g_feat: this rank's normalised shards; pids/cams: full
+    arrays; rows_fn(q, g, qp, gp, qc, gc) -> (valid, first, ap, nkept) computes this rank's
+    query rows (libreidmi kernels in the product).  Returns (cmc, mAP) on every rank."""
+    from .evaluate import aggregate_cmc_map
+    rank, W = world()
+    g_all = gather_rows(g_feat, num_gallery)
+    qlo, qhi = shard(num_query, rank, W)
+    v, f, a, n = rows_fn(q_feat, g_all, q_pids[qlo:qhi], g_pids, q_camids[qlo:qhi], g_camids)
+    rows = pack_rows(v, f, a, n).to(g_feat.device)
+    rows = gather_rows(rows, num_query)
+    agg = aggregate or aggregate_cmc_map
+    return agg(*unpack_rows(rows), num_gallery, max_rank)
