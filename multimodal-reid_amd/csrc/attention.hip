@@ -4,163 +4,228 @@
 // nn.MultiheadAttention dispatches in custom_clip_model.py:12,22-24 (vision: L = 211/213,
 // no mask) and maple.py:956-962,976 (text: L = 77, additive -inf causal mask).
 //
-// One workgroup (4 waves) per (sequence, head).  K [Lp][64] and V^T [64][Lp] of the head
-// live in LDS for the whole sweep (L <= 256 fits: one key sweep, no online rescaling).
-// Each wave takes 16-query blocks:
-//   S^T = K Q^T with v_mfma_f32_16x16x32_bf16 (K fragment as A) so each lane holds the
-//     scores of ONE query for 4 keys per 16-key block -> row max / row sum are in-lane
-//     plus two xor-shuffles across the 4 lane groups;
-//   O^T = V^T P^T: the probabilities are already in the B-operand layout (the k order
-//     inside each 32-key step is permuted identically on both operands), V^T rows are
-//     read as 2 x 8 B from LDS.  O comes out one query per lane, 4 consecutive dims.
+// One workgroup per (sequence, head), one wave per 32-query block.  K [Lp][64] and V^T
+// [64][Lp] of the head live in LDS for the whole sweep (L <= 256 fits: one key sweep, no
+// online rescaling).  Row max / row sum are in-lane plus one xor-shuffle (lane ^ 32).
 // Inputs from the QKV GEMM epilogue: q,k [B*H][L][64] bf16, vt [B*H][64][Lp] bf16.
 // Output o [B*L][H*64] bf16 (token-major: the A operand of out_proj).
 #include "common.h"
 
 namespace reidmi {
 
+int attn_lpad(int L);
+
 __device__ __forceinline__ int kswz(int r, int kc) { return r * 64 + ((kc ^ ((r >> 1) & 7)) << 3); }
 
+// One workgroup per (sequence, head) with one wave per 32-query block (ceil(L/32) waves).
+// NKB = number of 32-key blocks (Lp = 32 * NKB).  v_mfma_f32_32x32x16_bf16 throughout:
+//   S^T[key][q] = K Q^T: K fragment (A) from LDS, Q fragment (B) from HBM once per wave;
+//     lane (q = lane&31, h = lane>>5) holds keys kb*32 + (r&3) + 8(r>>2) + 4h in s[kb][r];
+//   P stays in those registers: registers 8s'..8s'+7 of block kb ARE the B fragment of
+//     key-step s' of O^T = V^T P^T (the accumulator-as-operand identity), so V^T rows are
+//     read with the matching key permutation (two 8-byte reads per fragment);
+//   O^T[d][q] comes out as 4 runs of 4 consecutive d per lane -> 8-byte stores.
 template <int NKB, bool CAUSAL>
-__global__ __launch_bounds__(256) void mhsa_kernel(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
+__global__ __launch_bounds__(512) void mhsa_kernel(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
                                                    const __bf16* __restrict__ vt, __bf16* __restrict__ o, int L,
                                                    int H, int lpad_g, int vstride, float scale_log2) {
-    constexpr int LP = NKB * 16;
+    constexpr int LP = NKB * 32;
     extern __shared__ __attribute__((aligned(16))) __bf16 lds[];
-    __bf16* sK = lds;                 // [LP][64], swizzled 16-byte chunks
-    __bf16* sV = lds + LP * 64;       // [64][vstride]
+    __bf16* sK = lds;            // [LP][64], swizzled 16-byte chunks
+    __bf16* sV = lds + LP * 64;  // [64][vstride]; vstride = 2 dwords mod 64 dwords
     const int bh = blockIdx.x;
-    const int b = bh / H, h = bh % H;
+    const int b = bh / H, hd = bh % H;
     const __bf16* qh = q + (int64_t)bh * L * 64;
     const __bf16* kh = k + (int64_t)bh * L * 64;
     const __bf16* vh = vt + (int64_t)bh * 64 * lpad_g;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nthr = blockDim.x;
 
-    // stage K (rows >= L zero) and V^T (16-byte chunks; columns >= L zeroed below)
-    for (int c = tid; c < LP * 8; c += 256) {
+    for (int c = tid; c < LP * 8; c += nthr) {
         const int r = c >> 3, kc = c & 7;
         uint4 v = make_uint4(0, 0, 0, 0);
         if (r < L) v = *(const uint4*)(kh + (int64_t)r * 64 + kc * 8);
         *(uint4*)(sK + kswz(r, kc)) = v;
     }
-    const int vchunks = LP / 8;
-    for (int c = tid; c < 64 * vchunks; c += 256) {
-        const int d = c / vchunks, kc = c % vchunks;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (kc * 8 < lpad_g) v = *(const uint4*)(vh + (int64_t)d * lpad_g + kc * 8);
-        *(uint4*)(sV + d * vstride + kc * 8) = v;
+    const int vq = LP / 4;  // 8-byte pieces per V^T row
+    for (int c = tid; c < 64 * vq; c += nthr) {
+        const int d = c / vq, kq = c % vq;
+        uint2 v = make_uint2(0, 0);
+        if (kq * 4 < L) v = *(const uint2*)(vh + (int64_t)d * lpad_g + kq * 4);
+        *(uint2*)(sV + d * vstride + kq * 4) = v;
     }
     __syncthreads();
-    for (int c = tid; c < 64 * (LP - L); c += 256) {
+    for (int c = tid; c < 64 * (LP - L); c += nthr) {
         const int d = c / (LP - L), t = L + c % (LP - L);
         sV[d * vstride + t] = (__bf16)0.0f;
     }
     __syncthreads();
 
-    const int nqb = (L + 15) / 16;
-    const int g = lane >> 4, ql = lane & 15;
-    for (int qb = wid; qb < nqb; qb += 4) {
-        const int qi = qb * 16 + ql;  // this lane's query row
-        bf16x8 qf0, qf1;
-        if (qi < L) {
-            qf0 = *(const bf16x8*)(qh + (int64_t)qi * 64 + g * 8);
-            qf1 = *(const bf16x8*)(qh + (int64_t)qi * 64 + 32 + g * 8);
-        } else {
-            qf0 = bf16x8{};
-            qf1 = bf16x8{};
+    const int hh = lane >> 5, ql = lane & 31;
+    const int qi = wid * 32 + ql;
+    if (wid * 32 >= L) return;
+    bf16x8 qf[4];
+#pragma unroll
+    for (int ks = 0; ks < 4; ks++)
+        qf[ks] = qi < L ? *(const bf16x8*)(qh + (int64_t)qi * 64 + ks * 16 + hh * 8) : bf16x8{};
+    f32x16 s[NKB];
+#pragma unroll
+    for (int kb = 0; kb < NKB; kb++) {
+        f32x16 a = f32x16{};
+#pragma unroll
+        for (int ks = 0; ks < 4; ks++) {
+            const bf16x8 kf = *(const bf16x8*)(sK + kswz(kb * 32 + ql, 2 * ks + hh));
+            a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], a, 0, 0, 0);
         }
-        f32x4 s[NKB];
+        s[kb] = a;
+    }
+    float mx = -__builtin_inff();
 #pragma unroll
-        for (int kb = 0; kb < NKB; kb++) {
-            const int kr = kb * 16 + ql;
-            const bf16x8 k0 = *(const bf16x8*)(sK + kswz(kr, g));
-            const bf16x8 k1 = *(const bf16x8*)(sK + kswz(kr, 4 + g));
-            f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
-            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k0, qf0, a, 0, 0, 0);
-            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k1, qf1, a, 0, 0, 0);
-            s[kb] = a;  // s[kb][r] = S[query qi][key kb*16 + 4g + r]
+    for (int kb = 0; kb < NKB; kb++)
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            const int key = kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            const bool ok = key < L && (!CAUSAL || key <= qi);
+            s[kb][r] = ok ? s[kb][r] * scale_log2 : -__builtin_inff();
+            mx = fmaxf(mx, s[kb][r]);
         }
-        // masked row max
-        float mx = -__builtin_inff();
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float sum = 0.f;
 #pragma unroll
-        for (int kb = 0; kb < NKB; kb++)
+    for (int kb = 0; kb < NKB; kb++)
 #pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const int key = kb * 16 + 4 * g + r;
-                const bool ok = key < L && (!CAUSAL || key <= qi);
-                s[kb][r] = ok ? s[kb][r] : -__builtin_inff();
-                mx = fmaxf(mx, s[kb][r]);
-            }
-        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-        const float mb = mx * scale_log2;
-        float sum = 0.f;
+        for (int r = 0; r < 16; r++) {
+            const float p = __builtin_amdgcn_exp2f(s[kb][r] - mx);
+            s[kb][r] = p;
+            sum += p;
+        }
+    sum += __shfl_xor(sum, 32, 64);
+    const float inv = 1.0f / sum;
+    f32x16 oacc[2] = {f32x16{}, f32x16{}};
 #pragma unroll
-        for (int kb = 0; kb < NKB; kb++)
+    for (int kb = 0; kb < NKB; kb++)
 #pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const float p = exp2f(s[kb][r] * scale_log2 - mb);
-                s[kb][r] = p;
-                sum += p;
-            }
-        sum += __shfl_xor(sum, 16, 64);
-        sum += __shfl_xor(sum, 32, 64);
-        const float inv = 1.0f / sum;
-        // O^T[d][q] = sum_key V^T[d][key] P^T[key][q]; k-slot 8g+t <-> key 32s+4g+t (t<4),
-        // 32s+16+4g+(t-4) (t>=4) on both operands.
-        f32x4 oacc[4];
-#pragma unroll
-        for (int db = 0; db < 4; db++) oacc[db] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int st = 0; st < NKB / 2; st++) {
+        for (int sp = 0; sp < 2; sp++) {
             bf16x8 pf;
 #pragma unroll
-            for (int t = 0; t < 4; t++) {
-                pf[t] = (__bf16)s[2 * st][t];
-                pf[4 + t] = (__bf16)s[2 * st + 1][t];
-            }
+            for (int j = 0; j < 8; j++) pf[j] = (__bf16)s[kb][8 * sp + j];
 #pragma unroll
-            for (int db = 0; db < 4; db++) {
-                const __bf16* vr = sV + (db * 16 + ql) * vstride + 32 * st + 4 * g;
+            for (int db = 0; db < 2; db++) {
+                const __bf16* vr = sV + (db * 32 + ql) * vstride + kb * 32 + 16 * sp + 4 * hh;
                 const bf16x4 v0 = *(const bf16x4*)(vr);
-                const bf16x4 v1 = *(const bf16x4*)(vr + 16);
+                const bf16x4 v1 = *(const bf16x4*)(vr + 8);
                 const bf16x8 vf = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-                oacc[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, oacc[db], 0, 0, 0);
+                oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, oacc[db], 0, 0, 0);
             }
         }
-        if (qi < L) {
-            __bf16* orow = o + ((int64_t)b * L + qi) * (H * 64) + h * 64;
+    if (qi < L) {
+        __bf16* orow = o + ((int64_t)b * L + qi) * (H * 64) + hd * 64;
 #pragma unroll
-            for (int db = 0; db < 4; db++) {
-                bf16x4 w = {(__bf16)(oacc[db][0] * inv), (__bf16)(oacc[db][1] * inv), (__bf16)(oacc[db][2] * inv),
-                            (__bf16)(oacc[db][3] * inv)};
-                *(bf16x4*)(orow + db * 16 + 4 * g) = w;
+        for (int db = 0; db < 2; db++)
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                bf16x4 w = {(__bf16)(oacc[db][4 * g] * inv), (__bf16)(oacc[db][4 * g + 1] * inv),
+                            (__bf16)(oacc[db][4 * g + 2] * inv), (__bf16)(oacc[db][4 * g + 3] * inv)};
+                *(bf16x4*)(orow + db * 32 + 8 * g + 4 * hh) = w;
             }
-        }
     }
 }
 
-// V^T LDS row stride (elements): >= LP and == 4 dwords mod 64 dwords, so the 16 rows x 2
-// lane groups of one ds_read_b64 land on distinct banks.
+// V^T LDS row stride (elements): >= LP and == 2 dwords mod 64 dwords, so the 32 rows of one
+// half-wave ds_read_b64 cover all 64 banks exactly once.
 static int vt_stride(int lp) {
     int dw = lp / 2;
-    int pad = ((4 - dw) % 64 + 64) % 64;
+    int pad = ((2 - dw) % 64 + 64) % 64;
     return (dw + pad) * 2;
 }
 
 template <int NKB, bool CAUSAL>
 static int launch_mhsa(const void* q, const void* k, const void* vt, void* o, int64_t nseq, int L, int H,
                        int lpad_g, hipStream_t s) {
-    constexpr int LP = NKB * 16;
+    constexpr int LP = NKB * 32;
     const int vs = vt_stride(LP);
     const size_t lds = (size_t)LP * 64 * 2 + (size_t)64 * vs * 2;
     const float scale_log2 = 0.125f * 1.4426950408889634f;  // 1/sqrt(64) * log2(e)
-    if (lds > 64 * 1024)
+    static bool attr = false;
+    if (!attr && lds > 64 * 1024) {
         RM_CHECK_HIP(hipFuncSetAttribute((const void*)mhsa_kernel<NKB, CAUSAL>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL((mhsa_kernel<NKB, CAUSAL>), dim3((unsigned)(nseq * H)), dim3(256), lds, s,
+        attr = true;
+    }
+    const int waves = (L + 31) / 32;
+    hipLaunchKernelGGL((mhsa_kernel<NKB, CAUSAL>), dim3((unsigned)(nseq * H)), dim3(64 * waves), lds, s,
                        (const __bf16*)q, (const __bf16*)k, (const __bf16*)vt, (__bf16*)o, L, H, lpad_g, vs,
                        scale_log2);
+    RM_LAUNCHED();
+    return OK;
+}
+
+// CLS query only (the last block of the inference path): one wave per (sequence, head).
+// q [nseq*H][64] (the CLS rows), k [nseq*H][L][64], vt [nseq*H][64][lpad] -> o [nseq][H*64].
+// Lane t-strided scores, wave-reduced softmax, probabilities through LDS, lane d sums
+// p_t * V^T[d][t] over its contiguous row.
+__global__ __launch_bounds__(256) void mhsa_cls_kernel(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
+                                                       const __bf16* __restrict__ vt, __bf16* __restrict__ o,
+                                                       int64_t nbh, int L, int H, int lpad, float scale_log2) {
+    __shared__ float sp[4][256];
+    __shared__ float sq[4][64];
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t bh = (int64_t)blockIdx.x * 4 + wid;
+    if (bh >= nbh) return;
+    sq[wid][lane] = (float)q[bh * 64 + lane];
+    __builtin_amdgcn_wave_barrier();
+    const __bf16* kh = k + bh * (int64_t)L * 64;
+    float sv[4];
+    float mx = -__builtin_inff();
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int t = lane + 64 * j;
+        float a = -__builtin_inff();
+        if (t < L) {
+            a = 0.f;
+            const bf16x8* kr = (const bf16x8*)(kh + (int64_t)t * 64);
+#pragma unroll
+            for (int c = 0; c < 8; c++) {
+                const bf16x8 kv = kr[c];
+#pragma unroll
+                for (int e = 0; e < 8; e++) a += sq[wid][c * 8 + e] * (float)kv[e];
+            }
+            a *= scale_log2;
+        }
+        sv[j] = a;
+        mx = fmaxf(mx, a);
+    }
+    mx = wave_max(mx);
+    float sum = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int t = lane + 64 * j;
+        const float p = t < L ? __builtin_amdgcn_exp2f(sv[j] - mx) : 0.f;
+        // bf16-rounded probabilities, as the blocked kernel feeds its P.V MFMAs
+        sp[wid][t] = (float)(__bf16)p;
+        sum += p;
+    }
+    sum = wave_sum(sum);
+    __builtin_amdgcn_wave_barrier();
+    const __bf16* vr = vt + (bh * 64 + lane) * (int64_t)lpad;
+    float acc = 0.f;
+    for (int t0 = 0; t0 < L; t0 += 8) {
+        const bf16x8 v = *(const bf16x8*)(vr + t0);
+#pragma unroll
+        for (int e = 0; e < 8; e++)
+            if (t0 + e < L) acc += sp[wid][t0 + e] * (float)v[e];
+    }
+    const int64_t b = bh / H, h = bh % H;
+    o[b * (int64_t)H * 64 + h * 64 + lane] = (__bf16)(acc / sum);
+}
+
+int mhsa_cls(const void* q, const void* k, const void* vt, void* o, int64_t nseq, int L, int H, hipStream_t s) {
+    const int lp = attn_lpad(L);
+    RM_REQUIRE(lp > 0, "mhsa_cls: sequence length must be <= 256");
+    const int64_t nbh = nseq * H;
+    hipLaunchKernelGGL(mhsa_cls_kernel, dim3(ceil_div(nbh, 4)), dim3(256), 0, s, (const __bf16*)q, (const __bf16*)k,
+                       (const __bf16*)vt, (__bf16*)o, nbh, L, H, lp, 0.125f * 1.4426950408889634f);
     RM_LAUNCHED();
     return OK;
 }
@@ -168,11 +233,8 @@ static int launch_mhsa(const void* q, const void* k, const void* vt, void* o, in
 // Smallest instantiated key-padding >= L.  Lp must also equal the vt row length the
 // QKV epilogue wrote (attn_lpad()).
 int attn_lpad(int L) {
-    if (L <= 96) return 96;
-    if (L <= 128) return 128;
-    if (L <= 224) return 224;
-    if (L <= 256) return 256;
-    return -1;
+    if (L < 1 || L > 256) return -1;
+    return (L + 31) / 32 * 32;
 }
 
 int mhsa(const void* q, const void* k, const void* vt, void* o, int64_t nseq, int L, int H, bool causal,
@@ -180,20 +242,22 @@ int mhsa(const void* q, const void* k, const void* vt, void* o, int64_t nseq, in
     const int lp = attn_lpad(L);
     RM_REQUIRE(lp > 0, "mhsa: sequence length must be <= 256");
     RM_REQUIRE(nseq * H < (1ll << 31), "mhsa: too many (sequence, head) pairs");
-    if (causal) {
-        switch (lp) {
-            case 96: return launch_mhsa<6, true>(q, k, vt, o, nseq, L, H, lp, s);
-            case 128: return launch_mhsa<8, true>(q, k, vt, o, nseq, L, H, lp, s);
-            case 224: return launch_mhsa<14, true>(q, k, vt, o, nseq, L, H, lp, s);
-            default: return launch_mhsa<16, true>(q, k, vt, o, nseq, L, H, lp, s);
-        }
+#define RM_MHSA_CASE(n)                                                                                  \
+    case n:                                                                                              \
+        return causal ? launch_mhsa<n, true>(q, k, vt, o, nseq, L, H, lp, s)                            \
+                      : launch_mhsa<n, false>(q, k, vt, o, nseq, L, H, lp, s);
+    switch (lp / 32) {
+        RM_MHSA_CASE(1)
+        RM_MHSA_CASE(2)
+        RM_MHSA_CASE(3)
+        RM_MHSA_CASE(4)
+        RM_MHSA_CASE(5)
+        RM_MHSA_CASE(6)
+        RM_MHSA_CASE(7)
+        RM_MHSA_CASE(8)
     }
-    switch (lp) {
-        case 96: return launch_mhsa<6, false>(q, k, vt, o, nseq, L, H, lp, s);
-        case 128: return launch_mhsa<8, false>(q, k, vt, o, nseq, L, H, lp, s);
-        case 224: return launch_mhsa<14, false>(q, k, vt, o, nseq, L, H, lp, s);
-        default: return launch_mhsa<16, false>(q, k, vt, o, nseq, L, H, lp, s);
-    }
+#undef RM_MHSA_CASE
+    return fail(EINVAL_, "mhsa: unsupported length");
 }
 
 }  // namespace reidmi

@@ -15,6 +15,7 @@ namespace reidmi {
 int mhsa(const void* q, const void* k, const void* vt, void* o, int64_t nseq, int L, int H, bool causal,
          hipStream_t s);
 int attn_lpad(int L);
+int mhsa_cls(const void* q, const void* k, const void* vt, void* o, int64_t nseq, int L, int H, hipStream_t s);
 
 // ------------------------------------------------------------------- LayerNorm
 // One wave per row; W = NV*256 floats, each lane holds NV float4.  Two-pass mean/var in
@@ -253,6 +254,56 @@ static int run_block(const reidmi_block_weights& bw, char* ws, const Plan& P, in
     return OK;
 }
 
+// The last block when only the CLS row of its output is consumed (inference path,
+// zero_shot_learning.py:85-87 reads x12[:,0] / xproj[:,0]): K and V for every token, then
+// Q, attention, out_proj, LN2 and the MLP for the CLS rows only.  Every CLS-row value is
+// computed by the same kernels in the same order as in run_block, so the result is
+// bit-identical to the full block's row 0 (tests/test_gpu_encoder.py checks equality).
+static int run_block_cls(const reidmi_block_weights& bw, char* ws, const Plan& P, int64_t nseq, int L, int W, int H,
+                         hipStream_t s) {
+    const int64_t M = nseq * L;
+    float* x = (float*)(ws + P.x);
+    __bf16* h = (__bf16*)(ws + P.h);
+    __bf16* o = (__bf16*)(ws + P.o);
+    __bf16* u = (__bf16*)(ws + P.u);
+    int rc;
+    if ((rc = layernorm(x, M, W, nullptr, W, bw.ln1_w, bw.ln1_b, 1e-5f, nullptr, 0, h, W, s))) return rc;
+    EpiArgs kv{};
+    kv.bias = bw.qkv_b + W;
+    kv.k = ws + P.k;
+    kv.vt = ws + P.vt;
+    kv.seq = L;
+    kv.heads = H;
+    kv.lpad = attn_lpad(L);
+    kv.n_off = W;
+    if ((rc = gemm_bf16(EPI_QKV, h, W, (const __bf16*)bw.qkv_w + (int64_t)W * W, W, M, 2 * W, W, kv, s))) return rc;
+    EpiArgs qa{};
+    qa.bias = bw.qkv_b;
+    qa.q = ws + P.q;
+    qa.seq = 1;  // one (CLS) row per sequence: q [nseq*H][1][64]
+    qa.heads = H;
+    qa.lpad = 1;
+    if ((rc = gemm_bf16(EPI_QKV, h, (int64_t)L * W, bw.qkv_w, W, nseq, W, W, qa, s))) return rc;
+    if ((rc = mhsa_cls(ws + P.q, ws + P.k, ws + P.vt, o, nseq, L, H, s))) return rc;
+    EpiArgs er{};
+    er.out = x;
+    er.ldc = (int64_t)L * W;
+    er.bias = bw.out_b;
+    if ((rc = gemm_bf16(EPI_RESID_F32, o, W, bw.out_w, W, nseq, W, W, er, s))) return rc;
+    if ((rc = layernorm(x, nseq, (int64_t)L * W, nullptr, W, bw.ln2_w, bw.ln2_b, 1e-5f, nullptr, 0, h, W, s)))
+        return rc;
+    EpiArgs eg{};
+    eg.out = u;
+    eg.ldc = 4 * W;
+    eg.bias = bw.fc1_b;
+    if ((rc = gemm_bf16(EPI_GELU_BF16, h, W, bw.fc1_w, W, nseq, 4 * W, W, eg, s))) return rc;
+    EpiArgs e2{};
+    e2.out = x;
+    e2.ldc = (int64_t)L * W;
+    e2.bias = bw.fc2_b;
+    return gemm_bf16(EPI_RESID_F32, u, 4 * W, bw.fc2_w, 4 * W, nseq, W, 4 * W, e2, s);
+}
+
 static int vit_check(const reidmi_vit_weights* w) {
     RM_REQUIRE(w && w->blocks, "vit: null weights");
     RM_REQUIRE(w->layers >= 12, "vit: the reference forward runs resblocks[:11] + resblocks[11]; needs >= 12 layers");
@@ -329,7 +380,9 @@ REIDMI_API int reidmi_vit_forward(const reidmi_vit_weights* w, const void* image
                                L - w->n_ctx, w->n_ctx, bw.prompt);
             RM_LAUNCHED();
         }
-        if ((rc = run_block(bw, ws, P, B, L, W, w->heads, false, s))) return rc;
+        if (i == 11 && !full) rc = run_block_cls(bw, ws, P, B, L, W, w->heads, s);
+        else rc = run_block(bw, ws, P, B, L, W, w->heads, false, s);
+        if (rc) return rc;
         if (i == 10 && out_x11) {
             if (full) RM_CHECK_HIP(hipMemcpyAsync(out_x11, x, M * W * 4, hipMemcpyDeviceToDevice, s));
             else

@@ -28,6 +28,7 @@ struct EpiArgs {
     int seq;    // L (tokens per sequence)
     int heads;  // H
     int lpad;   // Lp (row length of vt)
+    int n_off;  // QKV: column offset of this GEMM inside [q | k | v] (a GEMM may produce k,v only)
     // PATCH
     const float* pos;  // [1+NP][N]
     int npatch;        // NP

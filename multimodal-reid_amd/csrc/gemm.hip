@@ -86,7 +86,8 @@ __device__ __forceinline__ void epilogue(const EpiArgs& ea, f32x4 v, int64_t m, 
         *(float4*)((float*)ea.out + row * ea.ldc + nb) = make_float4(v[0] + pe.x, v[1] + pe.y, v[2] + pe.z, v[3] + pe.w);
     } else if constexpr (EPI == EPI_QKV) {
         const int wd = ea.heads * 64;
-        const int which = nb / wd, h = (nb % wd) >> 6, d = nb & 63;
+        const int nq = nb + ea.n_off;
+        const int which = nq / wd, h = (nq % wd) >> 6, d = nq & 63;
         const int64_t b = m / ea.seq, t = m % ea.seq;
         const int64_t bh = b * ea.heads + h;
         if (which < 2) {

@@ -1,0 +1,82 @@
+"""Weight-format boundary of the drop-in (load time, host side; not timed).
+
+    model_adaptor(model, height, width, weights=None, model_type="vit", training_mode="coop",
+                  vision_stride_size=12) -> (model, bottleneck, bottleneck_proj)   utils.py:169-262
+    load_clip(state_dict, height, width, ...) -> model.CLIP                       maple.py:1044-1098
+    resize_pos_embed                                                              utils.py:111-125
+
+CLIP-ReID checkpoints store the towers under ``image_encoder.*`` / ``text_encoder.*``
+(utils.py:211-214, zero_shot_learning.py:31-34); OpenAI CLIP state dicts under
+``visual.*`` and top-level text keys.  Checkpoints are read with
+``torch.load(weights_only=True)`` (no pickle code execution); the reference's
+``torch.jit.load`` archives are tried first, as utils.py:171-175 does.
+BNNeck (utils.py:128-142) is constructed and loaded but, as in the reference's eval
+(zero_shot_learning.py:91-92), never applied.
+"""
+import torch
+
+from .model import CLIP, TextTransformer, VisionTransformer, resize_pos_embed  # noqa: F401
+
+
+def load_checkpoint(path):
+    try:
+        m = torch.jit.load(path, map_location="cpu")
+        return {k: v for k, v in m.state_dict().items()}
+    except Exception:
+        sd = torch.load(path, map_location="cpu", weights_only=True)
+        if isinstance(sd, dict) and "state_dict" in sd:
+            sd = sd["state_dict"]
+        return {k[7:] if k.startswith("module.") else k: v for k, v in sd.items()}
+
+
+class BNNeck:
+    """utils.py:128-142 (BatchNorm1d, eval mode): y = (x - mean) / sqrt(var + eps) * w + b."""
+
+    def __init__(self, width, proj):
+        self.proj = proj
+        self.width = width
+        self.params = None
+
+    def load_state_dict(self, sd, strict=False):
+        key = "bottleneck_proj" if self.proj else "bottleneck"
+        p = {k.split(".")[-1]: v for k, v in sd.items() if k.split(".")[0] == key}
+        self.params = p or None
+
+    def eval(self):
+        return self
+
+
+def model_adaptor(model, height, width, weights=None, model_type="vit", training_mode="coop",
+                  vision_stride_size=12, device=None):
+    """Build the libreidmi vision tower from a CLIP-ReID checkpoint (``image_encoder.*``
+    keys) exactly as utils.py:169-262 re-shapes the model: stride-12 patches, grid
+    height//12 x width//12, positional embedding bicubic-resized when its grid differs.
+    ``model`` may be None or a model.CLIP whose text tower is kept."""
+    if model_type != "vit":
+        raise NotImplementedError("libreidmi implements the ViT towers (north-star path)")
+    sd = load_checkpoint(weights) if isinstance(weights, str) else weights
+    if sd is None:
+        raise ValueError("model_adaptor: a checkpoint (path or state dict) is required")
+    vis = {k[len("image_encoder."):]: v for k, v in sd.items() if k.startswith("image_encoder.")}
+    if not vis:
+        vis = {k[len("visual."):]: v for k, v in sd.items() if k.startswith("visual.")}
+    visual = VisionTransformer(vis, height=height, width=width, stride=vision_stride_size, device=device)
+    bottleneck = BNNeck(visual.width, False)
+    bottleneck_proj = BNNeck(visual.out_dim, True)
+    bneck = {k: v for k, v in sd.items() if "bottleneck" in k}
+    if bneck:
+        bottleneck.load_state_dict(bneck)
+        bottleneck_proj.load_state_dict(bneck)
+    text = getattr(model, "text", None)
+    return CLIP(visual, text), bottleneck, bottleneck_proj
+
+
+def load_clip(state_dict, height=256, width=128, stride=12, device=None, text=True):
+    """CLIP from an OpenAI-layout state dict (``visual.*`` + text keys), maple.build_model style."""
+    vis = {k[len("visual."):]: v for k, v in state_dict.items() if k.startswith("visual.")}
+    visual = VisionTransformer(vis, height=height, width=width, stride=stride, device=device) if vis else None
+    tx = None
+    if text and "token_embedding.weight" in state_dict:
+        txt = {k: v for k, v in state_dict.items() if not k.startswith("visual.")}
+        tx = TextTransformer(txt, device=device)
+    return CLIP(visual, tx)
