@@ -13,6 +13,7 @@
 #include "gemm.h"
 
 #include <cstdlib>
+#include <type_traits>
 #include <mutex>
 #include <vector>
 
@@ -299,10 +300,288 @@ __global__ __launch_bounds__(512, 2) void gemm2_bf16_kernel(const __bf16* __rest
     }
 }
 
+
+// ===================================================================== v3 tile
+// v2's 256x256x64 tile and LDS-DMA staging, made persistent and software-pipelined:
+//  * grid = min(#tiles, 256) workgroups (one per CU); each XCD group (bid % 8) walks a
+//    contiguous range of tiles (consecutive tiles share the A row panel in that XCD's L2);
+//  * during the last K-step of a tile the first K-step of the workgroup's next tile is
+//    already streaming into the free LDS stage, so a tile's prologue latency is hidden;
+//  * inside a K-step the fragments of k-step 1 are read while the MFMAs of k-step 0 run.
+// Same MFMA sequence per output element as v1/v2 -> bit-identical results.
+template <int EPI>
+__global__ __launch_bounds__(512, 2) void gemm3_bf16_kernel(const __bf16* __restrict__ A, int64_t lda,
+                                                            const __bf16* __restrict__ W, int64_t ldw, int64_t M,
+                                                            int N, int K, EpiArgs ea, int tiles_n, int ntiles) {
+    extern __shared__ __attribute__((aligned(16))) __bf16 lds3[];
+    const int G = gridDim.x;
+    const int bid = blockIdx.x;
+    // XCD group x = bid % ng owns tiles [lo_x, hi_x); its members j = bid / ng stride by its size
+    const int ng = G < 8 ? G : 8;
+    const int x = bid % ng, gx = G / ng + ((G % ng) > x ? 1 : 0);
+    const int j = bid / ng;
+    const int lo = (int)((int64_t)ntiles * x / ng), hi = (int)((int64_t)ntiles * (x + 1) / ng);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wid >> 2, wn = wid & 3;
+    const int nk = K / GB_K;
+
+    // glds piece jj = 4*wid + u covers LDS rows 8jj..8jj+7; lane -> row 8jj + lane/8
+    const int lrow = lane >> 3, lchunk = lane & 7;
+    auto issue = [&](int tile, int k0, int stage) {
+        const int64_t m0 = (int64_t)(tile / tiles_n) * G2_M;
+        const int n0 = (tile % tiles_n) * G2_N;
+        __bf16* base = lds3 + stage * G2_STAGE;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int jj = wid * 4 + u;
+            const int r = 8 * jj + lrow;
+            const int kc = (lchunk ^ ((r >> 1) & 7)) * 8;
+            int64_t gm = m0 + r;
+            gm = gm < M ? gm : M - 1;
+            __builtin_amdgcn_global_load_lds(A + gm * lda + k0 + kc, (lds_ptr_t)(base + jj * 512), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(W + (int64_t)(n0 + r) * ldw + k0 + kc,
+                                             (lds_ptr_t)(base + G2_M * GB_K + jj * 512), 16, 0, 0);
+        }
+    };
+
+    int tile = lo + j;
+    if (tile >= hi) return;
+    int stage = 0;
+    issue(tile, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (; tile < hi; tile += gx) {
+        const int next = tile + gx;
+        f32x4 acc[8][4];
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+#pragma unroll
+            for (int jn = 0; jn < 4; jn++) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int kt = 0; kt < nk; ++kt) {
+            if (kt + 1 < nk) issue(tile, (kt + 1) * GB_K, stage ^ 1);
+            else if (next < hi) issue(next, 0, stage ^ 1);
+            const __bf16* sA = lds3 + stage * G2_STAGE;
+            const __bf16* sW = sA + G2_M * GB_K;
+            const int kc0 = lane >> 4, kc1 = 4 + (lane >> 4);
+            bf16x8 wf0[4], wf1[4], a0[8], a1[8];
+#pragma unroll
+            for (int jn = 0; jn < 4; jn++) wf0[jn] = *(const bf16x8*)(sW + swz(wn * 64 + jn * 16 + (lane & 15), kc0));
+#pragma unroll
+            for (int i = 0; i < 8; i++) a0[i] = *(const bf16x8*)(sA + swz(wm * 128 + i * 16 + (lane & 15), kc0));
+#pragma unroll
+            for (int jn = 0; jn < 4; jn++) wf1[jn] = *(const bf16x8*)(sW + swz(wn * 64 + jn * 16 + (lane & 15), kc1));
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                // k-step 1 fragment of row block i streams in behind k-step 0's MFMAs
+                a1[i] = *(const bf16x8*)(sA + swz(wm * 128 + i * 16 + (lane & 15), kc1));
+#pragma unroll
+                for (int jn = 0; jn < 4; jn++)
+                    acc[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf0[jn], a0[i], acc[i][jn], 0, 0, 0);
+            }
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+#pragma unroll
+                for (int jn = 0; jn < 4; jn++)
+                    acc[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf1[jn], a1[i], acc[i][jn], 0, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            stage ^= 1;
+        }
+        const int64_t m0 = (int64_t)(tile / tiles_n) * G2_M;
+        const int n0 = (tile % tiles_n) * G2_N;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int64_t m = m0 + wm * 128 + i * 16 + (lane & 15);
+            if (m >= M) continue;
+#pragma unroll
+            for (int jn = 0; jn < 4; jn++)
+                epilogue<EPI>(ea, acc[i][jn], m, n0 + wn * 64 + jn * 16 + (lane >> 4) * 4, N);
+        }
+    }
+}
+
+
+// ===================================================================== v4 tile
+// 256x256x64, 8 waves, LDS-DMA staging as v2, with a ping-pong section schedule: every
+// K-tile is 4 LOAD sections (ds_read fragments of one 64x32 output quadrant, issue a share
+// of the next K-tile's LDS-DMA, lgkmcnt(0)) interleaved with 4 COMPUTE sections (16
+// register-only MFMAs), one workgroup barrier after each section.  Waves 4-7 start one
+// barrier late, so on each SIMD (waves w and w+4) one wave's LOAD runs beside the other's
+// COMPUTE.  Quadrant order (0,0),(0,1),(1,1),(1,0) reuses A or B fragments between
+// sections (12+4+8+4 reads per K-tile).  Hazards (slot = barrier interval, group B = one
+// slot behind): next-tile DMA is issued in LOAD 0/1 of tile t into the buffer last read in
+// LOAD 3 of tile t-1 (retired by lgkmcnt(0) before its barrier); every wave drains its DMA
+// with vmcnt(0) at the end of LOAD 3, a barrier before any wave's LOAD 0 of tile t+1.
+// Same MFMA sequence per output element as v1-v3 -> bit-identical results.
+template <int EPI>
+__global__ __launch_bounds__(512, 2) void gemm4_bf16_kernel(const __bf16* __restrict__ A, int64_t lda,
+                                                            const __bf16* __restrict__ W, int64_t ldw, int64_t M,
+                                                            int N, int K, EpiArgs ea, int tiles_n, int nwg) {
+    extern __shared__ __attribute__((aligned(16))) __bf16 lds4[];
+    const int bid = blockIdx.x;
+    const int xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
+    const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+    const int tm = wg / tiles_n, tn = wg % tiles_n;
+    const int64_t m0 = (int64_t)tm * G2_M;
+    const int n0 = tn * G2_N;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = wid >> 2, wc = wid & 3;
+
+    const __bf16* srcA[4];
+    const __bf16* srcW[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const int j = wid * 4 + u;
+        const int r = 8 * j + (lane >> 3);
+        const int kc = (lane & 7) ^ ((r >> 1) & 7);
+        int64_t gm = m0 + r;
+        gm = gm < M ? gm : M - 1;
+        srcA[u] = A + gm * lda + kc * 8;
+        srcW[u] = W + (int64_t)(n0 + r) * ldw + kc * 8;
+    }
+#define G4_ISSUE_A(stage, k0)                                                                                   \
+    _Pragma("unroll") for (int u = 0; u < 4; u++) __builtin_amdgcn_global_load_lds(                             \
+        srcA[u] + (k0), (lds_ptr_t)(lds4 + (stage) * G2_STAGE + (wid * 4 + u) * 512), 16, 0, 0)
+#define G4_ISSUE_W(stage, k0)                                                                                   \
+    _Pragma("unroll") for (int u = 0; u < 4; u++) __builtin_amdgcn_global_load_lds(                             \
+        srcW[u] + (k0), (lds_ptr_t)(lds4 + (stage) * G2_STAGE + G2_M * GB_K + (wid * 4 + u) * 512), 16, 0, 0)
+#define G4_BARRIER()                              \
+    do {                                          \
+        __builtin_amdgcn_sched_barrier(0);        \
+        __builtin_amdgcn_s_barrier();             \
+        __builtin_amdgcn_sched_barrier(0);        \
+    } while (0)
+#define G4_LDS_DONE() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+
+    bf16x8 fa[4][2], fb[2][2];
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    auto load_a = [&](const __bf16* sA, int qm) {
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int ks = 0; ks < 2; ks++)
+                fa[i][ks] = *(const bf16x8*)(sA + swz(wr * 128 + qm * 64 + i * 16 + (lane & 15), ks * 4 + (lane >> 4)));
+    };
+    auto load_b = [&](const __bf16* sW, int qn) {
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+#pragma unroll
+            for (int ks = 0; ks < 2; ks++)
+                fb[j][ks] = *(const bf16x8*)(sW + swz(wc * 64 + qn * 32 + j * 16 + (lane & 15), ks * 4 + (lane >> 4)));
+    };
+    auto compute = [&](int qm, int qn) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ks++)
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int j = 0; j < 2; j++)
+                    acc[qm * 4 + i][qn * 2 + j] =
+                        __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][ks], fa[i][ks], acc[qm * 4 + i][qn * 2 + j], 0, 0, 0);
+    };
+
+    G4_ISSUE_A(0, 0);
+    G4_ISSUE_W(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (wr == 1) G4_BARRIER();
+    const int nk = K / GB_K;
+    auto kstep = [&](int kt, auto more_tag) {
+        constexpr bool MORE = decltype(more_tag)::value;
+        const int buf = kt & 1;
+        const __bf16* sA = lds4 + buf * G2_STAGE;
+        const __bf16* sW = sA + G2_M * GB_K;
+        // LOAD 0 / COMPUTE (0,0)
+        load_a(sA, 0);
+        load_b(sW, 0);
+        if constexpr (MORE) { G4_ISSUE_A(buf ^ 1, (kt + 1) * GB_K); }
+        G4_LDS_DONE();
+        G4_BARRIER();
+        compute(0, 0);
+        G4_BARRIER();
+        // LOAD 1 / COMPUTE (0,1)
+        load_b(sW, 1);
+        if constexpr (MORE) { G4_ISSUE_W(buf ^ 1, (kt + 1) * GB_K); }
+        G4_LDS_DONE();
+        G4_BARRIER();
+        compute(0, 1);
+        G4_BARRIER();
+        // LOAD 2 / COMPUTE (1,1)
+        load_a(sA, 1);
+        G4_LDS_DONE();
+        G4_BARRIER();
+        compute(1, 1);
+        G4_BARRIER();
+        // LOAD 3 / COMPUTE (1,0): drain this wave's DMA for tile kt+1
+        load_b(sW, 0);
+        G4_LDS_DONE();
+        if constexpr (MORE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        G4_BARRIER();
+        compute(1, 0);
+        G4_BARRIER();
+    };
+    for (int kt = 0; kt + 1 < nk; ++kt) kstep(kt, std::integral_constant<bool, true>{});
+    kstep(nk - 1, std::integral_constant<bool, false>{});
+    if (wr == 0) G4_BARRIER();
+#undef G4_ISSUE_A
+#undef G4_ISSUE_W
+#undef G4_BARRIER
+#undef G4_LDS_DONE
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const int64_t m = m0 + wr * 128 + i * 16 + (lane & 15);
+        if (m >= M) continue;
+#pragma unroll
+        for (int j = 0; j < 4; j++) epilogue<EPI>(ea, acc[i][j], m, n0 + wc * 64 + j * 16 + (lane >> 4) * 4, N);
+    }
+}
+
 template <int EPI>
 static int launch(const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N, int64_t K,
                   const EpiArgs& ea, hipStream_t s) {
     const int var = variant();
+    if (N % G2_N == 0 && var == 4) {
+        const int tiles_m = ceil_div(M, G2_M), tiles_n = (int)(N / G2_N);
+        const int64_t nwg = (int64_t)tiles_m * tiles_n;
+        RM_REQUIRE(nwg < (1ll << 31), "gemm: grid too large");
+        const size_t lds = 2 * (size_t)G2_STAGE * 2;
+        static bool attr4 = false;
+        if (!attr4) {
+            RM_CHECK_HIP(hipFuncSetAttribute((const void*)gemm4_bf16_kernel<EPI>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            attr4 = true;
+        }
+        hipLaunchKernelGGL(gemm4_bf16_kernel<EPI>, dim3((unsigned)nwg), dim3(512), lds, s, (const __bf16*)A, lda,
+                           (const __bf16*)W, ldw, M, (int)N, (int)K, ea, tiles_n, (int)nwg);
+        RM_LAUNCHED();
+        return OK;
+    }
+    if (N % G2_N == 0 && (var == 3 || (var == 0 && (int64_t)ceil_div(M, G2_M) * (N / G2_N) >= 512))) {
+        const int tiles_m = ceil_div(M, G2_M), tiles_n = (int)(N / G2_N);
+        const int64_t ntiles = (int64_t)tiles_m * tiles_n;
+        RM_REQUIRE(ntiles < (1ll << 31), "gemm: grid too large");
+        const size_t lds = 2 * (size_t)G2_STAGE * 2;
+        static bool attr3 = false;
+        if (!attr3) {
+            RM_CHECK_HIP(hipFuncSetAttribute((const void*)gemm3_bf16_kernel<EPI>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            attr3 = true;
+        }
+        const int grid = (int)(ntiles < 256 ? ntiles : 256);
+        hipLaunchKernelGGL(gemm3_bf16_kernel<EPI>, dim3((unsigned)grid), dim3(512), lds, s, (const __bf16*)A, lda,
+                           (const __bf16*)W, ldw, M, (int)N, (int)K, ea, tiles_n, (int)ntiles);
+        RM_LAUNCHED();
+        return OK;
+    }
     if (N % G2_N == 0 && var != 1 && (var == 2 || (int64_t)ceil_div(M, G2_M) * (N / G2_N) >= 512)) {
         const int tiles_m = ceil_div(M, G2_M), tiles_n = (int)(N / G2_N);
         const int64_t nwg = (int64_t)tiles_m * tiles_n;
@@ -367,7 +646,7 @@ int gemm_bf16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, i
 using namespace reidmi;
 
 REIDMI_API int reidmi_gemm_set_variant(int v) {
-    RM_REQUIRE(v >= 0 && v <= 2, "gemm variant must be 0 (auto), 1 (128x128) or 2 (256x256)");
+    RM_REQUIRE(v >= 0 && v <= 4, "gemm variant: 0 auto, 1 128x128, 2 256x256, 3 256x256 persistent, 4 ping-pong");
     g_variant = v;
     return OK;
 }

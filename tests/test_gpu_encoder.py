@@ -58,7 +58,8 @@ def test_gemm_epilogues(gpu, epi, M, N, K):
 @pytest.mark.parametrize("epi", [0, 1, 2, 5])
 @pytest.mark.parametrize("M,N,K", [(54016, 768, 768), (1000, 2304, 768), (700, 512, 3072)])
 def test_gemm_v2_tile_bitexact_vs_v1(gpu, epi, M, N, K):
-    """The 256x256 LDS-DMA tile and the 128x128 register-staged tile run the same MFMA
+    """The 256x256 LDS-DMA tile (plain and persistent/prefetching) and the 128x128
+    register-staged tile run the same MFMA
     sequence per output element (k-steps ascending), so they agree bit for bit; rows
     past M (clamped source rows) must not leak into the result."""
     L = _lib()
@@ -67,7 +68,7 @@ def test_gemm_v2_tile_bitexact_vs_v1(gpu, epi, M, N, K):
     W = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16).cuda()
     bias = torch.randn(N, generator=g).cuda()
     outs = []
-    for v in (1, 2):
+    for v in (1, 2, 3, 4):
         L.call("reidmi_gemm_set_variant", v)
         if epi in (0, 1):
             out = torch.zeros(M, N, dtype=torch.bfloat16, device="cuda")
@@ -76,7 +77,8 @@ def test_gemm_v2_tile_bitexact_vs_v1(gpu, epi, M, N, K):
         L.call("reidmi_gemm_bf16", epi, L.ptr(A), K, L.ptr(W), K, M, N, K, L.ptr(bias), L.ptr(out), N, L.stream())
         outs.append(out)
     L.call("reidmi_gemm_set_variant", 0)
-    assert torch.equal(outs[0], outs[1])
+    for o in outs[1:]:
+        assert torch.equal(outs[0], o)
     rows = torch.arange(0, M, max(1, M // 97), device="cuda")
     ref = A[rows].float() @ W.float().t() + bias
     if epi == 1:
