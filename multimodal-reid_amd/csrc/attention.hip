@@ -17,127 +17,181 @@ int attn_lpad(int L);
 
 __device__ __forceinline__ int kswz(int r, int kc) { return r * 64 + ((kc ^ ((r >> 1) & 7)) << 3); }
 
-// One workgroup per (sequence, head) with one wave per 32-query block (ceil(L/32) waves).
-// NKB = number of 32-key blocks (Lp = 32 * NKB).  v_mfma_f32_32x32x16_bf16 throughout:
-//   S^T[key][q] = K Q^T: K fragment (A) from LDS, Q fragment (B) from HBM once per wave;
-//     lane (q = lane&31, h = lane>>5) holds keys kb*32 + (r&3) + 8(r>>2) + 4h in s[kb][r];
-//   P stays in those registers: registers 8s'..8s'+7 of block kb ARE the B fragment of
-//     key-step s' of O^T = V^T P^T (the accumulator-as-operand identity), so V^T rows are
-//     read with the matching key permutation (two 8-byte reads per fragment);
+// Persistent: gridDim.x workgroups (one per CU) walk the (sequence, head) pairs; one wave
+// per 32-query block (ceil(L/32) waves).  NKB = number of 32-key blocks (Lp = 32 * NKB).
+// K of the next head is copied into the other LDS stage by global_load_lds (8 rows per 1-KiB
+// piece, XOR swizzle applied on the source address) and V^T of the next head as one
+// contiguous blob (its HBM row stride == its LDS row stride, see attn_lpad), both while
+// the current head is being computed; Q of the next head is prefetched into registers.
+//   S^T[key][q] = K Q^T on v_mfma_f32_32x32x16_bf16; lane (q = lane&31, h = lane>>5) holds
+//     keys kb*32 + (r&3) + 8(r>>2) + 4h in s[kb][r];
+//   P stays in registers: registers 8s'..8s'+7 of block kb are the B fragment of key-step s'
+//     of O^T = V^T P^T (accumulator-as-operand), V^T read with the same key permutation;
 //   O^T[d][q] comes out as 4 runs of 4 consecutive d per lane -> 8-byte stores.
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
 template <int NKB, bool CAUSAL>
 __global__ __launch_bounds__(512) void mhsa_kernel(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
                                                    const __bf16* __restrict__ vt, __bf16* __restrict__ o, int L,
-                                                   int H, int lpad_g, int vstride, float scale_log2) {
+                                                   int H, int vstride, int64_t nbh, float scale_log2) {
     constexpr int LP = NKB * 32;
     extern __shared__ __attribute__((aligned(16))) __bf16 lds[];
-    __bf16* sK = lds;            // [LP][64], swizzled 16-byte chunks
-    __bf16* sV = lds + LP * 64;  // [64][vstride]; vstride = 2 dwords mod 64 dwords
-    const int bh = blockIdx.x;
-    const int b = bh / H, hd = bh % H;
-    const __bf16* qh = q + (int64_t)bh * L * 64;
-    const __bf16* kh = k + (int64_t)bh * L * 64;
-    const __bf16* vh = vt + (int64_t)bh * 64 * lpad_g;
+    const int stage_elems = LP * 64 + 64 * vstride;  // K [LP][64] then V^T [64][vstride]
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int nthr = blockDim.x;
-
-    for (int c = tid; c < LP * 8; c += nthr) {
-        const int r = c >> 3, kc = c & 7;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (r < L) v = *(const uint4*)(kh + (int64_t)r * 64 + kc * 8);
-        *(uint4*)(sK + kswz(r, kc)) = v;
-    }
-    const int vq = LP / 4;  // 8-byte pieces per V^T row
-    for (int c = tid; c < 64 * vq; c += nthr) {
-        const int d = c / vq, kq = c % vq;
-        uint2 v = make_uint2(0, 0);
-        if (kq * 4 < L) v = *(const uint2*)(vh + (int64_t)d * lpad_g + kq * 4);
-        *(uint2*)(sV + d * vstride + kq * 4) = v;
-    }
-    __syncthreads();
-    for (int c = tid; c < 64 * (LP - L); c += nthr) {
-        const int d = c / (LP - L), t = L + c % (LP - L);
-        sV[d * vstride + t] = (__bf16)0.0f;
-    }
-    __syncthreads();
-
+    const int nw = blockDim.x >> 6;
     const int hh = lane >> 5, ql = lane & 31;
     const int qi = wid * 32 + ql;
-    if (wid * 32 >= L) return;
+    const int kpieces = LP / 8;                           // 1-KiB pieces of K
+    const int vbytes = 64 * vstride * 2;                   // V^T blob (a multiple of 512 B)
+    const int vpieces = (vbytes + 1023) / 1024;             // 1-KiB pieces; last may be half
+    const int vlast_lanes = (vbytes - (vpieces - 1) * 1024) / 16;
+
+    auto issue = [&](int64_t bh, int stage) {
+        __bf16* sK = lds + stage * stage_elems;
+        __bf16* sV = sK + LP * 64;
+        const __bf16* kh = k + bh * L * 64;
+        const __bf16* vh = vt + bh * 64 * (int64_t)vstride;
+        for (int pc = wid; pc < kpieces; pc += nw) {
+            int r = 8 * pc + (lane >> 3);
+            const int kc = (lane & 7) ^ ((r >> 1) & 7);
+            r = r < L ? r : L - 1;  // rows >= L: any finite key (masked to -inf below)
+            __builtin_amdgcn_global_load_lds(kh + (int64_t)r * 64 + kc * 8, (lds_ptr_t)(sK + pc * 512), 16, 0, 0);
+        }
+        for (int pc = wid; pc < vpieces; pc += nw)
+            if (pc + 1 < vpieces || lane < vlast_lanes)  // never read or write past the blob
+                __builtin_amdgcn_global_load_lds(vh + pc * 512 + lane * 8, (lds_ptr_t)(sV + pc * 512), 16, 0, 0);
+    };
+    auto load_q = [&](int64_t bh, bf16x8* qf) {
+        const __bf16* qh = q + bh * L * 64;
+#pragma unroll
+        for (int ks = 0; ks < 4; ks++)
+            qf[ks] = qi < L ? *(const bf16x8*)(qh + (int64_t)qi * 64 + ks * 16 + hh * 8) : bf16x8{};
+    };
+    auto zero_pad = [&](int stage) {  // V^T key columns [L, LP) were DMA'd from padding
+        __bf16* sV = lds + stage * stage_elems + LP * 64;
+        for (int c = tid; c < 64 * (LP - L); c += blockDim.x) {
+            const int d = c / (LP - L), t = L + c % (LP - L);
+            sV[d * vstride + t] = (__bf16)0.0f;
+        }
+    };
+
+    int64_t bh = blockIdx.x;
+    if (bh >= nbh) return;
+    int stage = 0;
+    issue(bh, 0);
     bf16x8 qf[4];
-#pragma unroll
-    for (int ks = 0; ks < 4; ks++)
-        qf[ks] = qi < L ? *(const bf16x8*)(qh + (int64_t)qi * 64 + ks * 16 + hh * 8) : bf16x8{};
-    f32x16 s[NKB];
-#pragma unroll
-    for (int kb = 0; kb < NKB; kb++) {
-        f32x16 a = f32x16{};
-#pragma unroll
-        for (int ks = 0; ks < 4; ks++) {
-            const bf16x8 kf = *(const bf16x8*)(sK + kswz(kb * 32 + ql, 2 * ks + hh));
-            a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], a, 0, 0, 0);
+    load_q(bh, qf);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    zero_pad(0);
+    __syncthreads();
+    for (; bh < nbh; bh += gridDim.x) {
+        const int64_t nxt = bh + gridDim.x;
+        bf16x8 qn[4];
+        if (nxt < nbh) {
+            issue(nxt, stage ^ 1);
+            load_q(nxt, qn);
         }
-        s[kb] = a;
-    }
-    float mx = -__builtin_inff();
+        const __bf16* sK = lds + stage * stage_elems;
+        const __bf16* sV = sK + LP * 64;
+        if (wid * 32 < L) {
+            f32x16 s[NKB];
 #pragma unroll
-    for (int kb = 0; kb < NKB; kb++)
+            for (int kb = 0; kb < NKB; kb++) {
+                f32x16 a = f32x16{};
 #pragma unroll
-        for (int r = 0; r < 16; r++) {
-            const int key = kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-            const bool ok = key < L && (!CAUSAL || key <= qi);
-            s[kb][r] = ok ? s[kb][r] * scale_log2 : -__builtin_inff();
-            mx = fmaxf(mx, s[kb][r]);
-        }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    float sum = 0.f;
+                for (int ks = 0; ks < 4; ks++) {
+                    const bf16x8 kf = *(const bf16x8*)(sK + kswz(kb * 32 + ql, 2 * ks + hh));
+                    a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], a, 0, 0, 0);
+                }
+                s[kb] = a;
+            }
+            float mx = -__builtin_inff();
 #pragma unroll
-    for (int kb = 0; kb < NKB; kb++)
+            for (int kb = 0; kb < NKB; kb++)
 #pragma unroll
-        for (int r = 0; r < 16; r++) {
-            const float p = __builtin_amdgcn_exp2f(s[kb][r] - mx);
-            s[kb][r] = p;
-            sum += p;
-        }
-    sum += __shfl_xor(sum, 32, 64);
-    const float inv = 1.0f / sum;
-    f32x16 oacc[2] = {f32x16{}, f32x16{}};
+                for (int r = 0; r < 16; r++) {
+                    if (CAUSAL || kb == NKB - 1) {
+                        const int key = kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+                        const bool ok = key < L && (!CAUSAL || key <= qi);
+                        s[kb][r] = ok ? s[kb][r] : -__builtin_inff();
+                    }
+                    mx = fmaxf(mx, s[kb][r]);
+                }
+            mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+            const float mb = -mx * scale_log2;
+            float sum = 0.f;
 #pragma unroll
-    for (int kb = 0; kb < NKB; kb++)
+            for (int kb = 0; kb < NKB; kb++)
 #pragma unroll
-        for (int sp = 0; sp < 2; sp++) {
-            bf16x8 pf;
+                for (int r = 0; r < 16; r++) {
+                    const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kb][r], scale_log2, mb));
+                    s[kb][r] = p;
+                    sum += p;
+                }
+            sum += __shfl_xor(sum, 32, 64);
+            const float inv = 1.0f / sum;
+            f32x16 oacc[2] = {f32x16{}, f32x16{}};
 #pragma unroll
-            for (int j = 0; j < 8; j++) pf[j] = (__bf16)s[kb][8 * sp + j];
+            for (int kb = 0; kb < NKB; kb++)
 #pragma unroll
-            for (int db = 0; db < 2; db++) {
-                const __bf16* vr = sV + (db * 32 + ql) * vstride + kb * 32 + 16 * sp + 4 * hh;
-                const bf16x4 v0 = *(const bf16x4*)(vr);
-                const bf16x4 v1 = *(const bf16x4*)(vr + 8);
-                const bf16x8 vf = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-                oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, oacc[db], 0, 0, 0);
+                for (int sp = 0; sp < 2; sp++) {
+                    bf16x8 pf;
+#pragma unroll
+                    for (int j = 0; j < 8; j++) pf[j] = (__bf16)s[kb][8 * sp + j];
+#pragma unroll
+                    for (int db = 0; db < 2; db++) {
+                        const __bf16* vr = sV + (db * 32 + ql) * vstride + kb * 32 + 16 * sp + 4 * hh;
+                        const bf16x4 v0 = *(const bf16x4*)(vr);
+                        const bf16x4 v1 = *(const bf16x4*)(vr + 8);
+                        const bf16x8 vf = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+                        oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, oacc[db], 0, 0, 0);
+                    }
+                }
+            if (qi < L) {
+                const int64_t b = bh / H, hd = bh % H;
+                __bf16* orow = o + (b * L + qi) * (int64_t)(H * 64) + hd * 64;
+#pragma unroll
+                for (int db = 0; db < 2; db++)
+#pragma unroll
+                    for (int g = 0; g < 4; g++) {
+                        bf16x4 w = {(__bf16)(oacc[db][4 * g] * inv), (__bf16)(oacc[db][4 * g + 1] * inv),
+                                    (__bf16)(oacc[db][4 * g + 2] * inv), (__bf16)(oacc[db][4 * g + 3] * inv)};
+                        *(bf16x4*)(orow + db * 32 + 8 * g + 4 * hh) = w;
+                    }
             }
         }
-    if (qi < L) {
-        __bf16* orow = o + ((int64_t)b * L + qi) * (H * 64) + hd * 64;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (nxt < nbh) {
+            zero_pad(stage ^ 1);
 #pragma unroll
-        for (int db = 0; db < 2; db++)
-#pragma unroll
-            for (int g = 0; g < 4; g++) {
-                bf16x4 w = {(__bf16)(oacc[db][4 * g] * inv), (__bf16)(oacc[db][4 * g + 1] * inv),
-                            (__bf16)(oacc[db][4 * g + 2] * inv), (__bf16)(oacc[db][4 * g + 3] * inv)};
-                *(bf16x4*)(orow + db * 32 + 8 * g + 4 * hh) = w;
-            }
+            for (int ks = 0; ks < 4; ks++) qf[ks] = qn[ks];
+        }
+        __syncthreads();
+        stage ^= 1;
     }
 }
 
-// V^T LDS row stride (elements): >= LP and == 2 dwords mod 64 dwords, so the 32 rows of one
-// half-wave ds_read_b64 cover all 64 banks exactly once.
+// V^T row stride (elements): >= LP, == 2 dwords mod 64 dwords, so the 32 rows of one
+// half-wave ds_read_b64 cover all 64 banks exactly once.  The QKV epilogue writes V^T with
+// this same stride in HBM, so one head's V^T is a contiguous blob for the LDS-DMA copy.
 static int vt_stride(int lp) {
     int dw = lp / 2;
     int pad = ((2 - dw) % 64 + 64) % 64;
     return (dw + pad) * 2;
+}
+
+static int g_num_cu = 0;
+static int num_cu() {
+    if (!g_num_cu) {
+        int dev = 0;
+        hipGetDevice(&dev);
+        hipDeviceGetAttribute(&g_num_cu, hipDeviceAttributeMultiprocessorCount, dev);
+        if (g_num_cu <= 0) g_num_cu = 256;
+    }
+    return g_num_cu;
 }
 
 template <int NKB, bool CAUSAL>
@@ -145,17 +199,21 @@ static int launch_mhsa(const void* q, const void* k, const void* vt, void* o, in
                        int lpad_g, hipStream_t s) {
     constexpr int LP = NKB * 32;
     const int vs = vt_stride(LP);
-    const size_t lds = (size_t)LP * 64 * 2 + (size_t)64 * vs * 2;
+    RM_REQUIRE(lpad_g == vs, "mhsa: v^T row stride must be reidmi_attn_lpad(L)");
+    const size_t stage = (size_t)LP * 64 * 2 + (size_t)64 * vs * 2;
+    const size_t lds = 2 * stage;
     const float scale_log2 = 0.125f * 1.4426950408889634f;  // 1/sqrt(64) * log2(e)
     static bool attr = false;
-    if (!attr && lds > 64 * 1024) {
+    if (!attr) {
         RM_CHECK_HIP(hipFuncSetAttribute((const void*)mhsa_kernel<NKB, CAUSAL>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         attr = true;
     }
+    const int64_t nbh = nseq * H;
     const int waves = (L + 31) / 32;
-    hipLaunchKernelGGL((mhsa_kernel<NKB, CAUSAL>), dim3((unsigned)(nseq * H)), dim3(64 * waves), lds, s,
-                       (const __bf16*)q, (const __bf16*)k, (const __bf16*)vt, (__bf16*)o, L, H, lpad_g, vs,
+    const int64_t grid = nbh < num_cu() ? nbh : num_cu();
+    hipLaunchKernelGGL((mhsa_kernel<NKB, CAUSAL>), dim3((unsigned)grid), dim3(64 * waves), lds, s,
+                       (const __bf16*)q, (const __bf16*)k, (const __bf16*)vt, (__bf16*)o, L, H, vs, nbh,
                        scale_log2);
     RM_LAUNCHED();
     return OK;
@@ -234,7 +292,7 @@ int mhsa_cls(const void* q, const void* k, const void* vt, void* o, int64_t nseq
 // QKV epilogue wrote (attn_lpad()).
 int attn_lpad(int L) {
     if (L < 1 || L > 256) return -1;
-    return (L + 31) / 32 * 32;
+    return vt_stride((L + 31) / 32 * 32);  // row stride of V^T (elements), >= L
 }
 
 int mhsa(const void* q, const void* k, const void* vt, void* o, int64_t nseq, int L, int H, bool causal,
@@ -246,7 +304,7 @@ int mhsa(const void* q, const void* k, const void* vt, void* o, int64_t nseq, in
     case n:                                                                                              \
         return causal ? launch_mhsa<n, true>(q, k, vt, o, nseq, L, H, lp, s)                            \
                       : launch_mhsa<n, false>(q, k, vt, o, nseq, L, H, lp, s);
-    switch (lp / 32) {
+    switch ((L + 31) / 32) {
         RM_MHSA_CASE(1)
         RM_MHSA_CASE(2)
         RM_MHSA_CASE(3)

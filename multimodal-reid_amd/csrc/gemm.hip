@@ -431,24 +431,35 @@ __global__ __launch_bounds__(512, 2) void gemm4_bf16_kernel(const __bf16* __rest
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wr = wid >> 2, wc = wid & 3;
 
-    const __bf16* srcA[4];
-    const __bf16* srcW[4];
+    // Region DMA: each operand stage is 4 regions of 128 LDS rows (16 pieces of 8 rows):
+    //   A0 = rows {0..63, 128..191} (quadrant qm=0 of both wave rows), A1 = the other 128;
+    //   B0 = W rows {wc*64 + 0..31}, B1 = W rows {wc*64 + 32..63}.
+    // Wave w moves pieces 2w, 2w+1 of a region.  Piece p of region (half h) covers rows
+    // A: 128*(p>>3) + 64*h + 8*(p&7) + lane/8;  B: 64*(p>>2) + 32*h + 8*(p&3) + lane/8.
+    const __bf16* srcA[2][2];
+    const __bf16* srcW[2][2];
+    int offA[2][2], offW[2][2];
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
-        const int j = wid * 4 + u;
-        const int r = 8 * j + (lane >> 3);
-        const int kc = (lane & 7) ^ ((r >> 1) & 7);
-        int64_t gm = m0 + r;
-        gm = gm < M ? gm : M - 1;
-        srcA[u] = A + gm * lda + kc * 8;
-        srcW[u] = W + (int64_t)(n0 + r) * ldw + kc * 8;
-    }
-#define G4_ISSUE_A(stage, k0)                                                                                   \
-    _Pragma("unroll") for (int u = 0; u < 4; u++) __builtin_amdgcn_global_load_lds(                             \
-        srcA[u] + (k0), (lds_ptr_t)(lds4 + (stage) * G2_STAGE + (wid * 4 + u) * 512), 16, 0, 0)
-#define G4_ISSUE_W(stage, k0)                                                                                   \
-    _Pragma("unroll") for (int u = 0; u < 4; u++) __builtin_amdgcn_global_load_lds(                             \
-        srcW[u] + (k0), (lds_ptr_t)(lds4 + (stage) * G2_STAGE + G2_M * GB_K + (wid * 4 + u) * 512), 16, 0, 0)
+    for (int h = 0; h < 2; h++)
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const int pc = 2 * wid + u;
+            const int ra = 128 * (pc >> 3) + 64 * h + 8 * (pc & 7);
+            const int rb = 64 * (pc >> 2) + 32 * h + 8 * (pc & 3);
+            const int r1 = ra + (lane >> 3), r2 = rb + (lane >> 3);
+            int64_t gm = m0 + r1;
+            gm = gm < M ? gm : M - 1;
+            srcA[h][u] = A + gm * lda + ((lane & 7) ^ ((r1 >> 1) & 7)) * 8;
+            srcW[h][u] = W + (int64_t)(n0 + r2) * ldw + ((lane & 7) ^ ((r2 >> 1) & 7)) * 8;
+            offA[h][u] = ra * GB_K;
+            offW[h][u] = G2_M * GB_K + rb * GB_K;
+        }
+#define G4_ISSUE_A(stage, h, k0)                                                                             \
+    _Pragma("unroll") for (int u = 0; u < 2; u++) __builtin_amdgcn_global_load_lds(                          \
+        srcA[h][u] + (k0), (lds_ptr_t)(lds4 + (stage) * G2_STAGE + offA[h][u]), 16, 0, 0)
+#define G4_ISSUE_W(stage, h, k0)                                                                             \
+    _Pragma("unroll") for (int u = 0; u < 2; u++) __builtin_amdgcn_global_load_lds(                          \
+        srcW[h][u] + (k0), (lds_ptr_t)(lds4 + (stage) * G2_STAGE + offW[h][u]), 16, 0, 0)
 #define G4_BARRIER()                              \
     do {                                          \
         __builtin_amdgcn_sched_barrier(0);        \
@@ -489,48 +500,72 @@ __global__ __launch_bounds__(512, 2) void gemm4_bf16_kernel(const __bf16* __rest
                         __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][ks], fa[i][ks], acc[qm * 4 + i][qn * 2 + j], 0, 0, 0);
     };
 
-    G4_ISSUE_A(0, 0);
-    G4_ISSUE_W(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int nk = K / GB_K;
+    // prologue: tile 0 whole, tile 1 without B0 (B0 of tile t+1 goes out in LOAD 0 of tile t)
+    G4_ISSUE_A(0, 0, 0);
+    G4_ISSUE_A(0, 1, 0);
+    G4_ISSUE_W(0, 0, 0);
+    G4_ISSUE_W(0, 1, 0);
+    if (nk > 1) {
+        G4_ISSUE_A(1, 0, GB_K);
+        G4_ISSUE_W(1, 1, GB_K);
+        G4_ISSUE_A(1, 1, GB_K);
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __syncthreads();
     if (wr == 1) G4_BARRIER();
-    const int nk = K / GB_K;
-    auto kstep = [&](int kt, auto more_tag) {
-        constexpr bool MORE = decltype(more_tag)::value;
+    // K-tile t reads stage t&1; region R of stage t&1 is refilled with tile t+2 right after
+    // its last read (LOAD 0: A0, B0; LOAD 1: B1; LOAD 2: A1; LOAD 3: B0 again):
+    //   LOAD 0 issues B0(t+1)  [stage t+1's B0 last read in LOAD 3 of tile t-1]
+    //   LOAD 1 issues A0(t+2), LOAD 2 issues B1(t+2), LOAD 3 issues A1(t+2)
+    // At the end of LOAD 3 everything of tile t+1 must have landed: only the 3 regions of
+    // tile t+2 (6 pieces per wave) may still be in flight -> vmcnt(6).
+    auto kstep = [&](int kt, auto n1_tag, auto n2_tag) {
+        constexpr bool N1 = decltype(n1_tag)::value;  // tile kt+1 exists
+        constexpr bool N2 = decltype(n2_tag)::value;  // tile kt+2 exists
         const int buf = kt & 1;
         const __bf16* sA = lds4 + buf * G2_STAGE;
         const __bf16* sW = sA + G2_M * GB_K;
         // LOAD 0 / COMPUTE (0,0)
         load_a(sA, 0);
         load_b(sW, 0);
-        if constexpr (MORE) { G4_ISSUE_A(buf ^ 1, (kt + 1) * GB_K); }
+        if constexpr (N1) { G4_ISSUE_W(buf ^ 1, 0, (kt + 1) * GB_K); }
         G4_LDS_DONE();
         G4_BARRIER();
         compute(0, 0);
         G4_BARRIER();
         // LOAD 1 / COMPUTE (0,1)
         load_b(sW, 1);
-        if constexpr (MORE) { G4_ISSUE_W(buf ^ 1, (kt + 1) * GB_K); }
+        if constexpr (N2) { G4_ISSUE_A(buf, 0, (kt + 2) * GB_K); }
         G4_LDS_DONE();
         G4_BARRIER();
         compute(0, 1);
         G4_BARRIER();
         // LOAD 2 / COMPUTE (1,1)
         load_a(sA, 1);
+        if constexpr (N2) { G4_ISSUE_W(buf, 1, (kt + 2) * GB_K); }
         G4_LDS_DONE();
         G4_BARRIER();
         compute(1, 1);
         G4_BARRIER();
-        // LOAD 3 / COMPUTE (1,0): drain this wave's DMA for tile kt+1
+        // LOAD 3 / COMPUTE (1,0)
         load_b(sW, 0);
+        if constexpr (N2) { G4_ISSUE_A(buf, 1, (kt + 2) * GB_K); }
         G4_LDS_DONE();
-        if constexpr (MORE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (N2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else if constexpr (N1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         G4_BARRIER();
         compute(1, 0);
         G4_BARRIER();
     };
-    for (int kt = 0; kt + 1 < nk; ++kt) kstep(kt, std::integral_constant<bool, true>{});
-    kstep(nk - 1, std::integral_constant<bool, false>{});
+    using T_ = std::integral_constant<bool, true>;
+    using F_ = std::integral_constant<bool, false>;
+    int kt = 0;
+    for (; kt + 2 < nk; ++kt) kstep(kt, T_{}, T_{});
+    if (kt + 1 < nk) { kstep(kt, T_{}, F_{}); ++kt; }
+    kstep(kt, F_{}, F_{});
     if (wr == 0) G4_BARRIER();
 #undef G4_ISSUE_A
 #undef G4_ISSUE_W
