@@ -99,7 +99,9 @@ int reidmi_prof_enable(int on);
 int reidmi_prof_collect(int epi, double* total_ms, int64_t* count, double* flops);
 
 /* GEMM tile selection: 0 = auto, 1 = 128x128x64 (4 waves), 2 = 256x256x64 (8 waves, LDS-DMA),
- * 3 = variant 2 persistent (one workgroup per CU, cross-tile prefetch). */
+ * 3 = variant 2 persistent (one workgroup per CU, cross-tile prefetch), 4 = 256x256 ping-pong
+ * section schedule with region-level DMA, 5 = variant 4 persistent (the auto choice for
+ * >= 256 tiles).  All variants are bit-identical. */
 int reidmi_gemm_set_variant(int v);
 
 /* Key padding used for an L-token sequence by the attention kernel (rows of v^T). */

@@ -35,8 +35,8 @@ static std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
 static size_t used = 0;
 }  // namespace prof
 
-// Tile selection: 0 = auto (v2 when it fills the chip), 1 = force v1 (128x128), 2 = force v2
-// (256x256).  Set by reidmi_gemm_set_variant (tests / A-B timing in one process); the
+// Tile selection: 0 = auto (>= 256 tiles of 256x256: v5, or v4 when K >= 2048; else v1), 1..5 force
+// v1 (128x128), v2 (256x256), v3 (persistent), v4 (ping-pong), v5 (persistent ping-pong).  Set by reidmi_gemm_set_variant (tests / A-B timing in one process); the
 // REIDMI_GEMM_VARIANT environment variable gives the initial value.
 static int g_variant = -1;
 static int variant() {
@@ -61,45 +61,115 @@ __device__ __forceinline__ float quick_gelu(float x) {
     return x * __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * x));
 }
 
-// Epilogue of one lane's 4 consecutive outputs C[m][nb..nb+3] (see gemm.h for the modes).
-template <int EPI>
-__device__ __forceinline__ void epilogue(const EpiArgs& ea, f32x4 v, int64_t m, int nb, int N) {
-    if (EPI != EPI_PATCH && ea.bias != nullptr) {
-        const float4 b = *(const float4*)(ea.bias + nb);
-        v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+// Epilogue of one wave's output block: NI row groups x 4 column groups of 16x16, lane
+// holding C[m][nb..nb+3] with m = mrow + i*16 + (lane&15), nb = ncol + j*16 + (lane>>4)*4
+// (see gemm.h for the modes).  All loads are hoisted ahead of the stores they feed: bias
+// once per tile, residual / pos-embed rows in batches of NB row groups — otherwise the
+// compiler (which cannot prove `out` does not alias `bias`/`pos`) serialises one memory
+// round trip per fragment.
+template <int EPI, int NI, bool BIAS_DONE = false>
+__device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI][4], int64_t mrow, int ncol,
+                                              int64_t M, int N) {
+    const int lane = threadIdx.x & 63;
+    const int cq = (lane >> 4) * 4;
+    if (!BIAS_DONE && EPI != EPI_PATCH && ea.bias != nullptr) {
+        float4 b[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) b[j] = *(const float4*)(ea.bias + ncol + j * 16 + cq);
+#pragma unroll
+        for (int i = 0; i < NI; i++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                acc[i][j][0] += b[j].x;
+                acc[i][j][1] += b[j].y;
+                acc[i][j][2] += b[j].z;
+                acc[i][j][3] += b[j].w;
+            }
     }
-    if constexpr (EPI == EPI_BF16) {
-        *(uint2*)((__bf16*)ea.out + m * ea.ldc + nb) = pack_bf16x4(v[0], v[1], v[2], v[3]);
-    } else if constexpr (EPI == EPI_GELU_BF16) {
-        *(uint2*)((__bf16*)ea.out + m * ea.ldc + nb) =
-            pack_bf16x4(quick_gelu(v[0]), quick_gelu(v[1]), quick_gelu(v[2]), quick_gelu(v[3]));
-    } else if constexpr (EPI == EPI_RESID_F32) {
-        float4* p = (float4*)((float*)ea.out + m * ea.ldc + nb);
-        float4 x = *p;
-        x.x += v[0]; x.y += v[1]; x.z += v[2]; x.w += v[3];
-        *p = x;
-    } else if constexpr (EPI == EPI_F32) {
-        *(float4*)((float*)ea.out + m * ea.ldc + nb) = make_float4(v[0], v[1], v[2], v[3]);
-    } else if constexpr (EPI == EPI_PATCH) {
-        const int64_t b = m / ea.npatch, p = m % ea.npatch;
-        const int64_t row = b * ea.seq + 1 + p;
-        const float4 pe = *(const float4*)(ea.pos + (1 + p) * (int64_t)N + nb);
-        *(float4*)((float*)ea.out + row * ea.ldc + nb) = make_float4(v[0] + pe.x, v[1] + pe.y, v[2] + pe.z, v[3] + pe.w);
-    } else if constexpr (EPI == EPI_QKV) {
-        const int wd = ea.heads * 64;
-        const int nq = nb + ea.n_off;
-        const int which = nq / wd, h = (nq % wd) >> 6, d = nq & 63;
-        const int64_t b = m / ea.seq, t = m % ea.seq;
-        const int64_t bh = b * ea.heads + h;
-        if (which < 2) {
-            __bf16* dst = (__bf16*)(which == 0 ? ea.q : ea.k) + (bh * ea.seq + t) * 64 + d;
-            *(uint2*)dst = pack_bf16x4(v[0], v[1], v[2], v[3]);
-        } else {
-            __bf16* dst = (__bf16*)ea.vt + (bh * 64 + d) * (int64_t)ea.lpad + t;
-            dst[0] = (__bf16)v[0];
-            dst[ea.lpad] = (__bf16)v[1];
-            dst[2 * (int64_t)ea.lpad] = (__bf16)v[2];
-            dst[3 * (int64_t)ea.lpad] = (__bf16)v[3];
+    if constexpr (EPI == EPI_RESID_F32 || EPI == EPI_PATCH) {
+        // software-pipelined: the loads of batch n+1 are issued before the stores of batch n,
+        // so no wait ever covers a store (vmcnt retires in issue order).
+        constexpr int NB = 2;  // row groups per batch: 8 float4 loads in flight per lane
+        auto row_of = [&](int i) {
+            const int64_t m = mrow + i * 16 + (lane & 15);
+            return m < M ? m : M - 1;  // clamped rows are loaded but not stored
+        };
+        auto dst_row = [&](int64_t m) -> float* {
+            if constexpr (EPI == EPI_RESID_F32) return (float*)ea.out + m * ea.ldc + ncol + cq;
+            else return (float*)ea.out + ((m / ea.npatch) * ea.seq + 1 + m % ea.npatch) * ea.ldc + ncol + cq;
+        };
+        auto src_row = [&](int64_t m) -> const float* {
+            if constexpr (EPI == EPI_RESID_F32) return (const float*)ea.out + m * ea.ldc + ncol + cq;
+            else return ea.pos + (1 + m % ea.npatch) * (int64_t)N + ncol + cq;
+        };
+        auto store_batch = [&](int i0) {
+#pragma unroll
+            for (int ii = 0; ii < NB; ii++) {
+                const int64_t m = mrow + (i0 + ii) * 16 + (lane & 15);
+                if (m >= M) continue;
+                float* d = dst_row(m);
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const f32x4 v = acc[i0 + ii][j];
+                    *(float4*)(d + j * 16) = make_float4(v[0], v[1], v[2], v[3]);
+                }
+            }
+        };
+#pragma unroll
+        for (int i0 = 0; i0 < NI; i0 += NB) {
+            float4 x[NB][4];
+#pragma unroll
+            for (int ii = 0; ii < NB; ii++) {
+                const float* sp = src_row(row_of(i0 + ii));
+#pragma unroll
+                for (int j = 0; j < 4; j++) x[ii][j] = *(const float4*)(sp + j * 16);
+            }
+            if (i0 > 0) store_batch(i0 - NB);
+#pragma unroll
+            for (int ii = 0; ii < NB; ii++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    acc[i0 + ii][j][0] += x[ii][j].x;
+                    acc[i0 + ii][j][1] += x[ii][j].y;
+                    acc[i0 + ii][j][2] += x[ii][j].z;
+                    acc[i0 + ii][j][3] += x[ii][j].w;
+                }
+        }
+        store_batch(NI - NB);
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < NI; i++) {
+        const int64_t m = mrow + i * 16 + (lane & 15);
+        if (m >= M) continue;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const f32x4 v = acc[i][j];
+            const int nb = ncol + j * 16 + cq;
+            if constexpr (EPI == EPI_BF16) {
+                *(uint2*)((__bf16*)ea.out + m * ea.ldc + nb) = pack_bf16x4(v[0], v[1], v[2], v[3]);
+            } else if constexpr (EPI == EPI_GELU_BF16) {
+                *(uint2*)((__bf16*)ea.out + m * ea.ldc + nb) =
+                    pack_bf16x4(quick_gelu(v[0]), quick_gelu(v[1]), quick_gelu(v[2]), quick_gelu(v[3]));
+            } else if constexpr (EPI == EPI_F32) {
+                *(float4*)((float*)ea.out + m * ea.ldc + nb) = make_float4(v[0], v[1], v[2], v[3]);
+            } else if constexpr (EPI == EPI_QKV) {
+                const int wd = ea.heads * 64;
+                const int nq = nb + ea.n_off;
+                const int which = nq / wd, h = (nq % wd) >> 6, d = nq & 63;
+                const int64_t b = m / ea.seq, t = m % ea.seq;
+                const int64_t bh = b * ea.heads + h;
+                if (which < 2) {
+                    __bf16* dst = (__bf16*)(which == 0 ? ea.q : ea.k) + (bh * ea.seq + t) * 64 + d;
+                    *(uint2*)dst = pack_bf16x4(v[0], v[1], v[2], v[3]);
+                } else {
+                    __bf16* dst = (__bf16*)ea.vt + (bh * 64 + d) * (int64_t)ea.lpad + t;
+                    dst[0] = (__bf16)v[0];
+                    dst[ea.lpad] = (__bf16)v[1];
+                    dst[2 * (int64_t)ea.lpad] = (__bf16)v[2];
+                    dst[3 * (int64_t)ea.lpad] = (__bf16)v[3];
+                }
+            }
         }
     }
 }
@@ -189,13 +259,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(const __bf16* __restr
     }
 
     // ------------------------------------------------------------------ epilogue
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const int64_t m = m0 + wm * 64 + i * 16 + (lane & 15);
-        if (m >= M) continue;
-#pragma unroll
-        for (int j = 0; j < 4; j++) epilogue<EPI>(ea, acc[i][j], m, n0 + wn * 64 + j * 16 + (lane >> 4) * 4, N);
-    }
+    epilogue_tile<EPI, 4>(ea, acc, m0 + wm * 64, n0 + wn * 64, M, N);
 #undef GLOAD
 #undef LSTORE
 }
@@ -291,13 +355,7 @@ __global__ __launch_bounds__(512, 2) void gemm2_bf16_kernel(const __bf16* __rest
         __syncthreads();
     }
 #undef G2_ISSUE
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-        const int64_t m = m0 + wm * 128 + i * 16 + (lane & 15);
-        if (m >= M) continue;
-#pragma unroll
-        for (int j = 0; j < 4; j++) epilogue<EPI>(ea, acc[i][j], m, n0 + wn * 64 + j * 16 + (lane >> 4) * 4, N);
-    }
+    epilogue_tile<EPI, 8>(ea, acc, m0 + wm * 128, n0 + wn * 64, M, N);
 }
 
 
@@ -392,14 +450,7 @@ __global__ __launch_bounds__(512, 2) void gemm3_bf16_kernel(const __bf16* __rest
         }
         const int64_t m0 = (int64_t)(tile / tiles_n) * G2_M;
         const int n0 = (tile % tiles_n) * G2_N;
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-            const int64_t m = m0 + wm * 128 + i * 16 + (lane & 15);
-            if (m >= M) continue;
-#pragma unroll
-            for (int jn = 0; jn < 4; jn++)
-                epilogue<EPI>(ea, acc[i][jn], m, n0 + wn * 64 + jn * 16 + (lane >> 4) * 4, N);
-        }
+        epilogue_tile<EPI, 8>(ea, acc, m0 + wm * 128, n0 + wn * 64, M, N);
     }
 }
 
@@ -571,20 +622,241 @@ __global__ __launch_bounds__(512, 2) void gemm4_bf16_kernel(const __bf16* __rest
 #undef G4_ISSUE_W
 #undef G4_BARRIER
 #undef G4_LDS_DONE
+    epilogue_tile<EPI, 8>(ea, acc, m0 + wr * 128, n0 + wc * 64, M, N);
+}
+
+// ===================================================================== v5 tile
+// v4's region-DMA ping-pong schedule made persistent (grid = min(#tiles, 256), tile walk
+// as v3).  The two DMA streams — "+1" (region B0 of the next K-step) and "+2" (A0, B1, A1
+// of the K-step after) — run over the workgroup's concatenated (tile, K-step) sequence, so
+// while a tile's epilogue runs, the next tile's first two K-steps are already landing.
+// The epilogue needs no barrier: group A runs it in the slot where group B computes the
+// tile's last quadrant.  Same MFMA sequence per output as v1-v4 -> bit-identical.
+template <int EPI>
+__global__ __launch_bounds__(512, 2) void gemm5_bf16_kernel(const __bf16* __restrict__ A, int64_t lda,
+                                                            const __bf16* __restrict__ W, int64_t ldw, int64_t M,
+                                                            int N, int K, EpiArgs ea, int tiles_n, int ntiles) {
+    extern __shared__ __attribute__((aligned(16))) __bf16 lds5[];
+    const int G = gridDim.x;
+    const int bid = blockIdx.x;
+    const int ng = G < 8 ? G : 8;
+    const int xg = bid % ng, gx = G / ng + ((G % ng) > xg ? 1 : 0);
+    const int lo = (int)((int64_t)ntiles * xg / ng), hi = (int)((int64_t)ntiles * (xg + 1) / ng);
+    const int first = lo + bid / ng;
+    if (first >= hi) return;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = wid >> 2, wc = wid & 3;
+    const int nk = K / GB_K;
+
+    // per-lane DMA geometry (see v4): piece pc = 2*wid + u of region half h
+    int rowA[2][2], offAg[2][2], kcA[2][2], offWg[2][2], offA[2][2], offW[2][2];
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-        const int64_t m = m0 + wr * 128 + i * 16 + (lane & 15);
-        if (m >= M) continue;
+    for (int h = 0; h < 2; h++)
 #pragma unroll
-        for (int j = 0; j < 4; j++) epilogue<EPI>(ea, acc[i][j], m, n0 + wc * 64 + j * 16 + (lane >> 4) * 4, N);
+        for (int u = 0; u < 2; u++) {
+            const int pc = 2 * wid + u;
+            const int ra = 128 * (pc >> 3) + 64 * h + 8 * (pc & 7);
+            const int rb = 64 * (pc >> 2) + 32 * h + 8 * (pc & 3);
+            const int r1 = ra + (lane >> 3), r2 = rb + (lane >> 3);
+            rowA[h][u] = r1;
+            kcA[h][u] = ((lane & 7) ^ ((r1 >> 1) & 7)) * 8;
+            offAg[h][u] = r1 * (int)lda + kcA[h][u];
+            offWg[h][u] = r2 * (int)ldw + ((lane & 7) ^ ((r2 >> 1) & 7)) * 8;
+            offA[h][u] = ra * GB_K;
+            offW[h][u] = G2_M * GB_K + rb * GB_K;
+        }
+    // a DMA stream position: tile (m0, n0) and K offset
+    struct Pos {
+        int tile, kt;
+        int64_t m0;
+        int n0;
+    };
+    auto set_tile = [&](Pos& p, int tile) {
+        p.tile = tile;
+        p.kt = 0;
+        p.m0 = (int64_t)(tile / tiles_n) * G2_M;
+        p.n0 = (tile % tiles_n) * G2_N;
+    };
+    auto advance = [&](Pos& p) {
+        if (++p.kt == nk) set_tile(p, p.tile + gx);
+    };
+    auto issue_a = [&](int stage, int h, const Pos& p) {
+        const int lim = (int)(M - p.m0 < G2_M ? M - p.m0 : G2_M);  // rows of this tile inside A
+        const __bf16* base = A + p.m0 * lda + p.kt * GB_K;
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const int off = rowA[h][u] < lim ? offAg[h][u] : (lim - 1) * (int)lda + kcA[h][u];
+            __builtin_amdgcn_global_load_lds(base + off, (lds_ptr_t)(lds5 + stage * G2_STAGE + offA[h][u]), 16, 0, 0);
+        }
+    };
+    auto issue_w = [&](int stage, int h, const Pos& p) {
+        const __bf16* base = W + (int64_t)p.n0 * ldw + p.kt * GB_K;
+#pragma unroll
+        for (int u = 0; u < 2; u++)
+            __builtin_amdgcn_global_load_lds(base + offWg[h][u], (lds_ptr_t)(lds5 + stage * G2_STAGE + offW[h][u]), 16,
+                                             0, 0);
+    };
+#define G5_BARRIER()                              \
+    do {                                          \
+        __builtin_amdgcn_sched_barrier(0);        \
+        __builtin_amdgcn_s_barrier();             \
+        __builtin_amdgcn_sched_barrier(0);        \
+    } while (0)
+#define G5_LDS_DONE() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+
+    bf16x8 fa[4][2], fb[2][2];
+    f32x4 acc[8][4];
+    auto load_a = [&](const __bf16* sA, int qm) {
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int ks = 0; ks < 2; ks++)
+                fa[i][ks] = *(const bf16x8*)(sA + swz(wr * 128 + qm * 64 + i * 16 + (lane & 15), ks * 4 + (lane >> 4)));
+    };
+    auto load_b = [&](const __bf16* sW, int qn) {
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+#pragma unroll
+            for (int ks = 0; ks < 2; ks++)
+                fb[j][ks] = *(const bf16x8*)(sW + swz(wc * 64 + qn * 32 + j * 16 + (lane & 15), ks * 4 + (lane >> 4)));
+    };
+    auto compute = [&](int qm, int qn) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ks++)
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int j = 0; j < 2; j++)
+                    acc[qm * 4 + i][qn * 2 + j] =
+                        __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][ks], fa[i][ks], acc[qm * 4 + i][qn * 2 + j], 0, 0, 0);
+    };
+
+    // Bias of the current tile: one LDS-DMA per wave at the tile's first K-step into the
+    // wave's own 1 KB slot (lane l -> bias[n0 + 4l .. 4l+3]); issued before that step's
+    // B0 DMA, so the step's vmcnt(6) retires it.  The epilogue reads it with ds_read.
+    const bool has_bias = EPI != EPI_PATCH && ea.bias != nullptr;
+    float* bias_slot = (float*)(lds5 + 2 * G2_STAGE) + wid * 256;
+    // streams: p1 = step s+1 (region B0), p2 = step s+2 (A0, B1, A1); requires nk >= 2
+    Pos p1, p2;
+    {
+        Pos p0;
+        set_tile(p0, first);
+        issue_a(0, 0, p0);
+        issue_a(0, 1, p0);
+        issue_w(0, 0, p0);
+        issue_w(0, 1, p0);
+        p1 = p0;
+        advance(p1);  // step 1: always inside the first tile (nk >= 2)
+        issue_a(1, 0, p1);
+        issue_w(1, 1, p1);
+        issue_a(1, 1, p1);
+        p2 = p1;
+        advance(p2);
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     }
+    __syncthreads();
+    if (wr == 1) G5_BARRIER();
+    int buf = 0;
+    for (int tile = first; tile < hi; tile += gx) {
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int kt = 0; kt < nk; ++kt) {
+            const bool has1 = p1.tile < hi, has2 = p2.tile < hi;
+            const __bf16* sA = lds5 + buf * G2_STAGE;
+            const __bf16* sW = sA + G2_M * GB_K;
+            // LOAD 0 / COMPUTE (0,0)
+            load_a(sA, 0);
+            load_b(sW, 0);
+            if (kt == 0 && has_bias)
+                __builtin_amdgcn_global_load_lds(ea.bias + (tile % tiles_n) * G2_N + lane * 4, (lds_ptr_t)bias_slot,
+                                                 16, 0, 0);
+            if (has1) issue_w(buf ^ 1, 0, p1);
+            G5_LDS_DONE();
+            G5_BARRIER();
+            compute(0, 0);
+            G5_BARRIER();
+            // LOAD 1 / COMPUTE (0,1)
+            load_b(sW, 1);
+            if (has2) issue_a(buf, 0, p2);
+            G5_LDS_DONE();
+            G5_BARRIER();
+            compute(0, 1);
+            G5_BARRIER();
+            // LOAD 2 / COMPUTE (1,1)
+            load_a(sA, 1);
+            if (has2) issue_w(buf, 1, p2);
+            G5_LDS_DONE();
+            G5_BARRIER();
+            compute(1, 1);
+            G5_BARRIER();
+            // LOAD 3 / COMPUTE (1,0)
+            load_b(sW, 0);
+            if (has2) {
+                issue_a(buf, 1, p2);
+                G5_LDS_DONE();
+                asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+            } else {
+                G5_LDS_DONE();
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            G5_BARRIER();
+            compute(1, 0);
+            G5_BARRIER();
+            advance(p1);
+            advance(p2);
+            buf ^= 1;
+        }
+        const int64_t m0 = (int64_t)(tile / tiles_n) * G2_M;
+        const int n0 = (tile % tiles_n) * G2_N;
+        if (has_bias) {
+            float4 b[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) b[j] = *(const float4*)(bias_slot + wc * 64 + j * 16 + (lane >> 4) * 4);
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    acc[i][j][0] += b[j].x;
+                    acc[i][j][1] += b[j].y;
+                    acc[i][j][2] += b[j].z;
+                    acc[i][j][3] += b[j].w;
+                }
+        }
+        epilogue_tile<EPI, 8, true>(ea, acc, m0 + wr * 128, n0 + wc * 64, M, N);
+    }
+    if (wr == 0) G5_BARRIER();
+#undef G5_BARRIER
+#undef G5_LDS_DONE
 }
 
 template <int EPI>
 static int launch(const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N, int64_t K,
                   const EpiArgs& ea, hipStream_t s) {
     const int var = variant();
-    if (N % G2_N == 0 && var == 4) {
+    const int64_t tiles256 = (int64_t)ceil_div(M, G2_M) * (N / G2_N);
+    if (N % G2_N == 0 && K >= 2 * GB_K && lda * G2_M < (1ll << 31) && ldw * G2_N < (1ll << 31) &&
+        (var == 5 || (var == 0 && tiles256 >= 256 && K < 2048))) {
+        const int tiles_m = ceil_div(M, G2_M), tiles_n = (int)(N / G2_N);
+        const int64_t ntiles = (int64_t)tiles_m * tiles_n;
+        RM_REQUIRE(ntiles < (1ll << 31), "gemm: grid too large");
+        const size_t lds = 2 * (size_t)G2_STAGE * 2 + 8 * 256 * sizeof(float);
+        static bool attr5 = false;
+        if (!attr5) {
+            RM_CHECK_HIP(hipFuncSetAttribute((const void*)gemm5_bf16_kernel<EPI>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            attr5 = true;
+        }
+        const int grid = (int)(ntiles < 256 ? ntiles : 256);
+        hipLaunchKernelGGL(gemm5_bf16_kernel<EPI>, dim3((unsigned)grid), dim3(512), lds, s, (const __bf16*)A, lda,
+                           (const __bf16*)W, ldw, M, (int)N, (int)K, ea, tiles_n, (int)ntiles);
+        RM_LAUNCHED();
+        return OK;
+    }
+    // long K: the non-persistent v4 (workgroups in K-lockstep share the W K-slices in L2)
+    if (N % G2_N == 0 && (var == 4 || (var == 0 && tiles256 >= 256))) {
         const int tiles_m = ceil_div(M, G2_M), tiles_n = (int)(N / G2_N);
         const int64_t nwg = (int64_t)tiles_m * tiles_n;
         RM_REQUIRE(nwg < (1ll << 31), "gemm: grid too large");
@@ -600,7 +872,7 @@ static int launch(const void* A, int64_t lda, const void* W, int64_t ldw, int64_
         RM_LAUNCHED();
         return OK;
     }
-    if (N % G2_N == 0 && (var == 3 || (var == 0 && (int64_t)ceil_div(M, G2_M) * (N / G2_N) >= 512))) {
+    if (N % G2_N == 0 && var == 3) {
         const int tiles_m = ceil_div(M, G2_M), tiles_n = (int)(N / G2_N);
         const int64_t ntiles = (int64_t)tiles_m * tiles_n;
         RM_REQUIRE(ntiles < (1ll << 31), "gemm: grid too large");
@@ -681,7 +953,7 @@ int gemm_bf16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, i
 using namespace reidmi;
 
 REIDMI_API int reidmi_gemm_set_variant(int v) {
-    RM_REQUIRE(v >= 0 && v <= 4, "gemm variant: 0 auto, 1 128x128, 2 256x256, 3 256x256 persistent, 4 ping-pong");
+    RM_REQUIRE(v >= 0 && v <= 5, "gemm variant: 0 auto, 1 128x128, 2 256x256, 3 256x256 persistent, 4 ping-pong, 5 persistent ping-pong");
     g_variant = v;
     return OK;
 }
