@@ -104,6 +104,51 @@ class Workload:
         return cmc, mAP, t1 - t0, t2 - t1
 
 
+def rerank_leg(dev, cpu_n=1000, cpu=True):
+    """configs[2]'s back end: DukeMTMC-size k-reciprocal re-rank (k1=50, k2=15, lambda=0.3;
+    reranking.py:29-100, evaluate.py:124-132) + CMC/mAP on identity-clustered synthetic
+    features, timed on its own after the Market steps (not part of `value`)."""
+    from multimodal_reid_amd import reranking
+    sp = syn.DATASET_SPLITS["dukemtmc"]
+    Q, G = sp["num_query"], sp["num_gallery"]
+    qp, gp, qc, gc = syn.labels(Q, G, sp["num_ids"], sp["num_cams"], seed=0, distractor_frac=0.1, junk_frac=0.02)
+    qf, gf = syn.features(qp, gp)
+    qf = evaluate.l2_normalize_device(torch.from_numpy(qf).to(dev))
+    gf = evaluate.l2_normalize_device(torch.from_numpy(gf).to(dev))
+
+    def run():
+        d = reranking.re_ranking_device(qf, gf, 50, 15, 0.3)
+        valid, first, ap, nkept, ovf = evaluate.eval_rows_device(d, qp, gp, qc, gc)
+        torch.cuda.synchronize()
+        return evaluate.aggregate_cmc_map(valid.cpu().numpy(), first.cpu().numpy(), ap.cpu().numpy(),
+                                          nkept.cpu().numpy(), G, 50, ovf.cpu().numpy())
+
+    run()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    cmc, mAP = run()
+    wall = time.perf_counter() - t
+    N = Q + G
+    out = {"config": f"DukeMTMC {Q}q x {G}g (N={N}) synthetic features D=1280, k1=50 k2=15 lambda=0.3, "
+                     "distance + re-rank + CMC/mAP on 1 GPU",
+           "wall_s": round(wall, 4), "mAP": round(float(mAP), 6),
+           "algorithmic_bytes": 4 * N * N + 4 * Q * G,
+           "reference_cpu_s_survey": 122.0}
+    if cpu:
+        import oracle
+        q = int(cpu_n * Q / N)
+        sqp, sgp = qp[:q], gp[:cpu_n - q]
+        sqf, sgf = syn.features(sqp, sgp, seed=5)
+        t = time.perf_counter()
+        oracle.re_ranking(sqf, sgf, 50, 15, 0.3)
+        tc = time.perf_counter() - t
+        out["cpu_port"] = {"sample": f"oracle C re-rank, {q}q x {cpu_n - q}g, 1 thread", "sample_s": round(tc, 3),
+                           "extrapolated_s": round(tc * (N / cpu_n) ** 2, 1), "kind": "port",
+                           "note": "quadratic extrapolation; the dense C restatement is slower than the "
+                                   "reference's numpy (SURVEY.md §6: 122 s for this config on 8 cores)"}
+    return out
+
+
 def cpu_baseline(wl, n_img=12, n_q=48):
     """The oracle ("port") on this host: fp32 torch restatement of the encoder on a
     bounded image sample (both TTA passes) + C restatement of distmat/eval on a query
@@ -142,6 +187,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-rerank", action="store_true")
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -207,10 +253,13 @@ def main():
                          "traffic": None, "avg_launch_ms": round(avg_ms, 4), "launches": cnt.value,
                          "flops_per_launch": fl.value / max(cnt.value, 1)},
         }
+        if not a.no_rerank:
+            line["rerank"] = rerank_leg(dev, cpu=not a.no_cpu_baseline)
         if not a.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(wl)
         print(json.dumps(line))
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
 
 

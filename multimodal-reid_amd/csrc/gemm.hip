@@ -51,14 +51,20 @@ constexpr int GB_M = 128, GB_N = 128, GB_K = 64;
 
 __device__ __forceinline__ int swz(int r, int kc) { return r * GB_K + ((kc ^ ((r >> 1) & 7)) << 3); }
 
+// one v_cvt_pk_bf16_f32 (RNE, NaN-preserving) per pair
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
+    uint32_t r;
+    asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 __device__ __forceinline__ uint2 pack_bf16x4(float a, float b, float c, float d) {
-    bf16x4 v = {(__bf16)a, (__bf16)b, (__bf16)c, (__bf16)d};
-    return __builtin_bit_cast(uint2, v);
+    return make_uint2(cvt_pk_bf16(a, b), cvt_pk_bf16(c, d));
 }
 
 __device__ __forceinline__ float quick_gelu(float x) {
-    // x * sigmoid(1.702 x)   (custom_clip_model.py:52-54)
-    return x * __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * x));
+    // x * sigmoid(1.702 x) = x / (1 + 2^(-1.702 log2(e) x))   (custom_clip_model.py:52-54)
+    return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -2.4554669595930157f));
 }
 
 // Epilogue of one wave's output block: NI row groups x 4 column groups of 16x16, lane
