@@ -182,6 +182,25 @@ def vit_fixtures(out):
     print("vit fixtures ok")
 
 
+def vitl_fixtures(out):
+    """ViT-L/14 (configs[4]) as the reference executes it: resblocks[:11] + resblocks[11]
+    (custom_clip_model.py:91-92), so a 12-layer state dict covers the executed path."""
+    torch.manual_seed(0)
+    sd = syn.vit_state_dict("ViT-L/14", seed=0, layers=12)
+    spec = syn.VIT_SPECS["ViT-L/14"]
+    gh, gw = syn.vit_grid(256, 128, 12, spec["patch"])
+    m = ref_ccm.VisionTransformer(gh, gw, spec["patch"], 12, spec["width"], 12, spec["width"] // 64,
+                                  spec["out_dim"])
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    m.eval()
+    imgs = syn.images(2, seed=4)
+    with torch.no_grad():
+        x11, x12, xp = m(torch.from_numpy(imgs))
+    np.savez_compressed(os.path.join(out, "vit_l14.npz"), x11cls=x11[:, 0].numpy(), x12cls=x12[:, 0].numpy(),
+                        projcls=xp[:, 0].numpy(), x12_tok=x12[1, 200:204].numpy())
+    print("vit-l fixtures ok")
+
+
 class _FakeClip:
     """Holder with the attributes text_encoder.TextEncoder reads (text_encoder.py:6-12)."""
 
@@ -216,6 +235,6 @@ if __name__ == "__main__":
     ap.add_argument("--out", default=HERE)
     ap.add_argument("--only", default="")
     a = ap.parse_args()
-    todo = a.only.split(",") if a.only else ["backend", "rerank", "vit", "text"]
+    todo = a.only.split(",") if a.only else ["backend", "rerank", "vit", "vitl", "text"]
     for t in todo:
         globals()[f"{t}_fixtures"](a.out)

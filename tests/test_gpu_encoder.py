@@ -153,6 +153,29 @@ def test_vit_b16_encode_image_vs_reference(vit_b16):
     assert _cos(xp[:, 0], bp[:, 0].numpy()).min() >= 0.99999
 
 
+def test_vit_l14_encode_image_vs_reference(gpu):
+    """ViT-L/14 (configs[4]): width 1024, 16 heads, patch 14 (im2col K 588 -> 640), the 12
+    blocks the reference executes; same tolerances as ViT-B/16."""
+    from multimodal_reid_amd.model import VisionTransformer
+    g = golden("vit_l14.npz")
+    sd = syn.vit_state_dict("ViT-L/14", seed=0, layers=12)
+    m = VisionTransformer(sd)
+    assert m.seq_len == 211 and m.width == 1024 and m.heads == 16
+    imgs = syn.images(2, seed=4)
+    x11, x12, xp = (t.cpu().numpy() for t in m.encode_image(torch.from_numpy(imgs)))
+    for got, ref in ((x12[:, 0], g["x12cls"]), (xp[:, 0], g["projcls"]), (x11[:, 0], g["x11cls"]),
+                     (x12[1, 200:204], g["x12_tok"])):
+        assert _cos(got, ref).min() >= 0.9999
+        assert np.abs(got - ref).max() <= 0.05
+    c12, cp = m.encode_cls(torch.from_numpy(imgs))
+    assert _cos(c12.cpu().numpy(), g["x12cls"]).min() >= 0.9999
+    assert _cos(cp.cpu().numpy(), g["projcls"]).min() >= 0.9999
+    with torch.no_grad():
+        _, b12, bp = vit_ref.vit_forward(sd, imgs, bf16=True)
+    assert _cos(x12[:, 0], b12[:, 0].numpy()).min() >= 0.99999
+    assert _cos(xp[:, 0], bp[:, 0].numpy()).min() >= 0.99999
+
+
 def test_vit_cls_path_and_tta(vit_b16):
     sd, m = vit_b16
     g = golden("vit_b16.npz")

@@ -100,3 +100,61 @@ def test_rerank_full_path_close(k1, k2):
     assert np.abs(final - ref).max() < 5e-3
     args = (g["q_pids"], g["g_pids"], g["q_cams"], g["g_cams"], 50)
     assert abs(oracle.eval_func(final, *args)[1] - oracle.eval_func(ref, *args)[1]) <= 1e-3
+
+
+# ------------------------------------------------------------------ encoders (fp32 restatement)
+def _cos(a, b):
+    a = np.asarray(a, np.float64).reshape(len(a), -1)
+    b = np.asarray(b, np.float64).reshape(len(b), -1)
+    return (a * b).sum(1) / np.linalg.norm(a, axis=1) / np.linalg.norm(b, axis=1)
+
+
+def test_vit_b16_oracle_vs_reference():
+    """oracle/vit_ref.py (fp32) vs the reference VisionTransformer's outputs
+    (custom_clip_model.py:77-100) on the same seeded weights/images, plain and TTA view."""
+    from oracle import vit_ref
+    g = golden("vit_b16.npz")
+    sd = syn.vit_state_dict("ViT-B/16", seed=0)
+    imgs = syn.images(3, seed=0)
+    with torch.no_grad():
+        x11, x12, xp = vit_ref.vit_forward(sd, imgs)
+        _, t12, tp = vit_ref.vit_forward(sd, imgs, tta=g["tta_offsets"])
+    for got, ref in ((x12[:, 0], g["x12cls"]), (xp[:, 0], g["projcls"]), (x11[:, 0], g["x11cls"]),
+                     (x12[0, :8], g["x12_tok"]), (xp[0, 100:104], g["proj_tok"]),
+                     (t12[:, 0], g["tta_x12cls"]), (tp[:, 0], g["tta_projcls"])):
+        assert np.abs(got.numpy() - ref).max() < 2e-5
+
+
+def test_vit_l14_oracle_vs_reference():
+    """ViT-L/14 (configs[4]) as the reference executes it (resblocks[:11] + [11])."""
+    from oracle import vit_ref
+    g = golden("vit_l14.npz")
+    sd = syn.vit_state_dict("ViT-L/14", seed=0, layers=12)
+    imgs = syn.images(2, seed=4)
+    with torch.no_grad():
+        x11, x12, xp = vit_ref.vit_forward(sd, imgs)
+    for got, ref in ((x12[:, 0], g["x12cls"]), (xp[:, 0], g["projcls"]), (x11[:, 0], g["x11cls"]),
+                     (x12[1, 200:204], g["x12_tok"])):
+        assert np.abs(got.numpy() - ref).max() < 2e-5
+        assert _cos(got.numpy(), ref).min() > 0.999999
+
+
+def test_tta_view_matches_augmented_images():
+    """The flip + pad + crop view the kernels build from offsets equals the host restatement
+    of the augmented loader's transform (data_prepare.py:263-270)."""
+    from oracle import vit_ref
+    imgs = syn.images(4, seed=9)
+    offs = syn.tta_offsets(4, seed=9)
+    a = vit_ref.tta_view(torch.from_numpy(imgs), offs).numpy()
+    b = syn.tta_images_np(imgs, offs)
+    assert np.array_equal(a, b)
+
+
+def test_text_oracle_vs_reference():
+    """oracle text tower vs text_encoder.TextEncoder (text_encoder.py:14-24) outputs."""
+    from oracle import vit_ref
+    g = golden("text.npz")
+    sd = syn.text_state_dict(seed=0)
+    with torch.no_grad():
+        f = vit_ref.text_forward(sd, g["tokens"])
+    assert np.abs(f.numpy() - g["text_feat"]).max() < 2e-5
