@@ -144,37 +144,75 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
         store_batch(NI - NB);
         return;
     }
+    if constexpr (EPI == EPI_F32) {
 #pragma unroll
-    for (int i = 0; i < NI; i++) {
-        const int64_t m = mrow + i * 16 + (lane & 15);
-        if (m >= M) continue;
+        for (int i = 0; i < NI; i++) {
+            const int64_t m = mrow + i * 16 + (lane & 15);
+            if (m >= M) continue;
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const f32x4 v = acc[i][j];
-            const int nb = ncol + j * 16 + cq;
-            if constexpr (EPI == EPI_BF16) {
-                *(uint2*)((__bf16*)ea.out + m * ea.ldc + nb) = pack_bf16x4(v[0], v[1], v[2], v[3]);
-            } else if constexpr (EPI == EPI_GELU_BF16) {
-                *(uint2*)((__bf16*)ea.out + m * ea.ldc + nb) =
-                    pack_bf16x4(quick_gelu(v[0]), quick_gelu(v[1]), quick_gelu(v[2]), quick_gelu(v[3]));
-            } else if constexpr (EPI == EPI_F32) {
-                *(float4*)((float*)ea.out + m * ea.ldc + nb) = make_float4(v[0], v[1], v[2], v[3]);
-            } else if constexpr (EPI == EPI_QKV) {
-                const int wd = ea.heads * 64;
-                const int nq = nb + ea.n_off;
-                const int which = nq / wd, h = (nq % wd) >> 6, d = nq & 63;
+            for (int j = 0; j < 4; j++) {
+                const f32x4 v = acc[i][j];
+                *(float4*)((float*)ea.out + m * ea.ldc + ncol + j * 16 + cq) = make_float4(v[0], v[1], v[2], v[3]);
+            }
+        }
+        return;
+    }
+    // bf16 outputs.  v^T tiles of the head split keep the scattered 2-byte stores.
+    if constexpr (EPI == EPI_QKV) {
+        const int wd = ea.heads * 64;
+        if ((ncol + ea.n_off) / wd == 2) {  // uniform per tile (wd % tile width == 0)
+#pragma unroll
+            for (int i = 0; i < NI; i++) {
+                const int64_t m = mrow + i * 16 + (lane & 15);
+                if (m >= M) continue;
                 const int64_t b = m / ea.seq, t = m % ea.seq;
-                const int64_t bh = b * ea.heads + h;
-                if (which < 2) {
-                    __bf16* dst = (__bf16*)(which == 0 ? ea.q : ea.k) + (bh * ea.seq + t) * 64 + d;
-                    *(uint2*)dst = pack_bf16x4(v[0], v[1], v[2], v[3]);
-                } else {
-                    __bf16* dst = (__bf16*)ea.vt + (bh * 64 + d) * (int64_t)ea.lpad + t;
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const f32x4 v = acc[i][j];
+                    const int nq = ncol + j * 16 + cq + ea.n_off;
+                    const int h = (nq % wd) >> 6, d = nq & 63;
+                    __bf16* dst = (__bf16*)ea.vt + ((b * ea.heads + h) * 64 + d) * (int64_t)ea.lpad + t;
                     dst[0] = (__bf16)v[0];
                     dst[ea.lpad] = (__bf16)v[1];
                     dst[2 * (int64_t)ea.lpad] = (__bf16)v[2];
                     dst[3 * (int64_t)ea.lpad] = (__bf16)v[3];
                 }
+            }
+            return;
+        }
+    }
+    // Row-per-lane store widening (cdna_hip_programming.md T21, 16-lane form): lane group
+    // q = lane>>4 holds columns 4q..4q+3 of fragments j and j+1; one v_permlane16_swap per
+    // packed dword leaves groups 0/2 with 8 consecutive columns of fragment j and groups
+    // 1/3 with 8 of fragment j+1 -> one 16-byte store per lane per fragment pair.
+    const int q = lane >> 4;
+#pragma unroll
+    for (int i = 0; i < NI; i++) {
+        const int64_t m = mrow + i * 16 + (lane & 15);
+#pragma unroll
+        for (int jp = 0; jp < 2; jp++) {
+            f32x4 a = acc[i][2 * jp], c = acc[i][2 * jp + 1];
+            if constexpr (EPI == EPI_GELU_BF16) {
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    a[e] = quick_gelu(a[e]);
+                    c[e] = quick_gelu(c[e]);
+                }
+            }
+            const auto lo = __builtin_amdgcn_permlane16_swap(cvt_pk_bf16(a[0], a[1]), cvt_pk_bf16(c[0], c[1]), false, false);
+            const auto hi = __builtin_amdgcn_permlane16_swap(cvt_pk_bf16(a[2], a[3]), cvt_pk_bf16(c[2], c[3]), false, false);
+            const uint4 v = make_uint4(lo[0], hi[0], lo[1], hi[1]);
+            const int col = ncol + (2 * jp + (q & 1)) * 16 + (q >> 1) * 8;
+            if (m >= M) continue;
+            if constexpr (EPI == EPI_QKV) {
+                const int wd = ea.heads * 64;
+                const int nq = col + ea.n_off;
+                const int h = (nq % wd) >> 6, d = nq & 63;
+                const int64_t b = m / ea.seq, t = m % ea.seq;
+                __bf16* dst = (__bf16*)(nq < wd ? ea.q : ea.k) + ((b * ea.heads + h) * ea.seq + t) * 64 + d;
+                *(uint4*)dst = v;
+            } else {
+                *(uint4*)((__bf16*)ea.out + m * ea.ldc + col) = v;
             }
         }
     }
@@ -656,7 +694,8 @@ __global__ __launch_bounds__(512, 2) void gemm5_bf16_kernel(const __bf16* __rest
     const int nk = K / GB_K;
 
     // per-lane DMA geometry (see v4): piece pc = 2*wid + u of region half h
-    int rowA[2][2], offAg[2][2], kcA[2][2], offWg[2][2], offA[2][2], offW[2][2];
+    int rowA[2][2], kcA[2][2], offA[2][2], offW[2][2];
+    uint32_t offAb[2][2], offWb[2][2];  // byte offsets from the tile's (row 0, k0) element
 #pragma unroll
     for (int h = 0; h < 2; h++)
 #pragma unroll
@@ -667,41 +706,52 @@ __global__ __launch_bounds__(512, 2) void gemm5_bf16_kernel(const __bf16* __rest
             const int r1 = ra + (lane >> 3), r2 = rb + (lane >> 3);
             rowA[h][u] = r1;
             kcA[h][u] = ((lane & 7) ^ ((r1 >> 1) & 7)) * 8;
-            offAg[h][u] = r1 * (int)lda + kcA[h][u];
-            offWg[h][u] = r2 * (int)ldw + ((lane & 7) ^ ((r2 >> 1) & 7)) * 8;
+            offAb[h][u] = (uint32_t)(r1 * (int)lda + kcA[h][u]) * 2u;
+            offWb[h][u] = (uint32_t)(r2 * (int)ldw + ((lane & 7) ^ ((r2 >> 1) & 7)) * 8) * 2u;
             offA[h][u] = ra * GB_K;
             offW[h][u] = G2_M * GB_K + rb * GB_K;
         }
-    // a DMA stream position: tile (m0, n0) and K offset
+    // a DMA stream position: tile (m0, n0), K-step, and whether all 256 A rows exist
     struct Pos {
         int tile, kt;
         int64_t m0;
         int n0;
+        bool full;
     };
     auto set_tile = [&](Pos& p, int tile) {
         p.tile = tile;
         p.kt = 0;
         p.m0 = (int64_t)(tile / tiles_n) * G2_M;
         p.n0 = (tile % tiles_n) * G2_N;
+        p.full = p.m0 + G2_M <= M;
     };
     auto advance = [&](Pos& p) {
         if (++p.kt == nk) set_tile(p, p.tile + gx);
     };
+    // uniform tile base + per-lane 32-bit element offset (SGPR base + VGPR offset form)
     auto issue_a = [&](int stage, int h, const Pos& p) {
-        const int lim = (int)(M - p.m0 < G2_M ? M - p.m0 : G2_M);  // rows of this tile inside A
         const __bf16* base = A + p.m0 * lda + p.kt * GB_K;
+        if (p.full) {
 #pragma unroll
-        for (int u = 0; u < 2; u++) {
-            const int off = rowA[h][u] < lim ? offAg[h][u] : (lim - 1) * (int)lda + kcA[h][u];
-            __builtin_amdgcn_global_load_lds(base + off, (lds_ptr_t)(lds5 + stage * G2_STAGE + offA[h][u]), 16, 0, 0);
+            for (int u = 0; u < 2; u++)
+                __builtin_amdgcn_global_load_lds((const char*)base + offAb[h][u],
+                                                 (lds_ptr_t)(lds5 + stage * G2_STAGE + offA[h][u]), 16, 0, 0);
+        } else {  // partial last row tile: rows >= M read row M-1 (never stored)
+            const int lim = (int)(M - p.m0);
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const int r = rowA[h][u] < lim ? rowA[h][u] : lim - 1;
+                __builtin_amdgcn_global_load_lds((const char*)base + (uint32_t)(r * (int)lda + kcA[h][u]) * 2u,
+                                                 (lds_ptr_t)(lds5 + stage * G2_STAGE + offA[h][u]), 16, 0, 0);
+            }
         }
     };
     auto issue_w = [&](int stage, int h, const Pos& p) {
         const __bf16* base = W + (int64_t)p.n0 * ldw + p.kt * GB_K;
 #pragma unroll
         for (int u = 0; u < 2; u++)
-            __builtin_amdgcn_global_load_lds(base + offWg[h][u], (lds_ptr_t)(lds5 + stage * G2_STAGE + offW[h][u]), 16,
-                                             0, 0);
+            __builtin_amdgcn_global_load_lds((const char*)base + offWb[h][u],
+                                             (lds_ptr_t)(lds5 + stage * G2_STAGE + offW[h][u]), 16, 0, 0);
     };
 #define G5_BARRIER()                              \
     do {                                          \
@@ -925,6 +975,8 @@ int gemm_bf16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, i
     RM_REQUIRE(M >= 0 && N > 0 && K > 0, "gemm: bad shape");
     RM_REQUIRE(N % GB_N == 0 && K % GB_K == 0, "gemm: needs N % 128 == 0 and K % 64 == 0");
     RM_REQUIRE(lda % 8 == 0 && ldw % 8 == 0 && lda >= K && ldw >= K, "gemm: lda/ldw must be >= K and 16-byte rows");
+    RM_REQUIRE((epi != EPI_BF16 && epi != EPI_GELU_BF16) || (ea.ldc % 8 == 0 && ((uintptr_t)ea.out & 15) == 0),
+               "gemm: bf16 output needs ldc % 8 == 0 and a 16-byte aligned base");
     if (M == 0) return OK;
     hipEvent_t ev_b = nullptr;
     if (prof::enabled) {
