@@ -35,7 +35,7 @@ static std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
 static size_t used = 0;
 }  // namespace prof
 
-// Tile selection: 0 = auto (>= 256 tiles of 256x256: v5, or v4 when K >= 2048; else v1), 1..5 force
+// Tile selection: 0 = auto (>= 256 tiles of 256x256: v5; else v1), 1..5 force
 // v1 (128x128), v2 (256x256), v3 (persistent), v4 (ping-pong), v5 (persistent ping-pong).  Set by reidmi_gemm_set_variant (tests / A-B timing in one process); the
 // REIDMI_GEMM_VARIANT environment variable gives the initial value.
 static int g_variant = -1;
@@ -894,7 +894,7 @@ static int launch(const void* A, int64_t lda, const void* W, int64_t ldw, int64_
     const int var = variant();
     const int64_t tiles256 = (int64_t)ceil_div(M, G2_M) * (N / G2_N);
     if (N % G2_N == 0 && K >= 2 * GB_K && lda * G2_M < (1ll << 31) && ldw * G2_N < (1ll << 31) &&
-        (var == 5 || (var == 0 && tiles256 >= 256 && K < 2048))) {
+        (var == 5 || (var == 0 && tiles256 >= 256))) {
         const int tiles_m = ceil_div(M, G2_M), tiles_n = (int)(N / G2_N);
         const int64_t ntiles = (int64_t)tiles_m * tiles_n;
         RM_REQUIRE(ntiles < (1ll << 31), "gemm: grid too large");
@@ -911,8 +911,7 @@ static int launch(const void* A, int64_t lda, const void* W, int64_t ldw, int64_
         RM_LAUNCHED();
         return OK;
     }
-    // long K: the non-persistent v4 (workgroups in K-lockstep share the W K-slices in L2)
-    if (N % G2_N == 0 && (var == 4 || (var == 0 && tiles256 >= 256))) {
+    if (N % G2_N == 0 && var == 4) {
         const int tiles_m = ceil_div(M, G2_M), tiles_n = (int)(N / G2_N);
         const int64_t nwg = (int64_t)tiles_m * tiles_n;
         RM_REQUIRE(nwg < (1ll << 31), "gemm: grid too large");
