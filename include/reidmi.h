@@ -87,8 +87,10 @@ int reidmi_rerank_from_dist(const float* dist, const float* add, int64_t Q, int6
 /* bf16 GEMM C = A . W^T (+bias) on v_mfma_f32_16x16x32_bf16, fp32 accumulation.
  * A [M][lda] bf16, W [N][ldw] bf16 (Linear weight layout), N % 128 == 0, K % 64 == 0.
  * epi: 0 -> out bf16 = acc+bias; 1 -> out bf16 = QuickGELU(acc+bias); 2 -> out fp32 += acc+bias;
- *      5 -> out fp32 = acc+bias.  (nn.Linear / mlp.c_fc+QuickGELU / residual adds of
- *      custom_clip_model.py:8-29.)  bias nullable (fp32). */
+ *      5 -> out fp32 = acc+bias; 6 -> out fp16 += acc+bias (sum in fp32, one rounding: the
+ *      encoders' fp16 residual stream).  (nn.Linear / mlp.c_fc+QuickGELU / residual adds of
+ *      custom_clip_model.py:8-29.)  bias nullable (fp32).  bf16/fp16 outputs: ldc % 8 == 0,
+ *      16-byte aligned out. */
 int reidmi_gemm_bf16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N,
                      int64_t K, const float* bias, void* out, int64_t ldc, void* stream);
 

@@ -7,7 +7,9 @@
 //   text:   CLIP.encode_text (maple.py:971-984) / TextEncoder.forward (text_encoder.py:14-24)
 // Per block: LN1 -> QKV GEMM (head-split epilogue) -> fused MHSA -> out_proj GEMM (+residual)
 //            -> LN2 -> c_fc GEMM (+QuickGELU) -> c_proj GEMM (+residual).
-// The residual stream stays fp32 in HBM; GEMM operands are bf16.
+// The residual stream x is fp16 in HBM (the reference's GPU dtype, utils.py:145-166; every
+// residual add is computed in fp32 and rounded once); GEMM operands are bf16; LayerNorm
+// statistics are fp32.
 #include "gemm.h"
 
 namespace reidmi {
@@ -18,25 +20,37 @@ int attn_lpad(int L);
 int mhsa_cls(const void* q, const void* k, const void* vt, void* o, int64_t nseq, int L, int H, hipStream_t s);
 
 // ------------------------------------------------------------------- LayerNorm
-// One wave per row; W = NV*256 floats, each lane holds NV float4.  Two-pass mean/var in
-// registers, eps inside the sqrt (torch.nn.LayerNorm).
-template <int NV>
-__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, int64_t rows, int64_t ldx,
+// One wave per row; W = NV*256, each lane holds NV groups of 4 consecutive elements.
+// Two-pass mean/var in fp32 registers, eps inside the sqrt (torch.nn.LayerNorm).
+// TX = float (public entry point) or _Float16 (the encoders' residual stream).
+template <typename TX>
+__device__ __forceinline__ float4 load4(const TX* p) {
+    if constexpr (sizeof(TX) == 4) {
+        return *(const float4*)p;
+    } else {
+        const f16x4 h = *(const f16x4*)p;
+        return make_float4((float)h[0], (float)h[1], (float)h[2], (float)h[3]);
+    }
+}
+
+template <int NV, typename TX>
+__global__ __launch_bounds__(256) void layernorm_kernel(const TX* x, int64_t rows, int64_t ldx,
                                                         const int32_t* __restrict__ row_idx,
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, float eps,
                                                         float* __restrict__ y32, int64_t ldy32,
-                                                        __bf16* __restrict__ y16, int64_t ldy16) {
+                                                        __bf16* __restrict__ y16, int64_t ldy16,
+                                                        _Float16* yh, int64_t ldyh) {
     const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= rows) return;
     const int lane = threadIdx.x & 63;
     const int64_t src = row_idx ? (int64_t)row_idx[r] : r;
-    const float4* xr = (const float4*)(x + src * ldx);
+    const TX* xr = x + src * ldx;
     float4 v[NV];
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < NV; i++) {
-        v[i] = xr[lane + 64 * i];
+        v[i] = load4(xr + 4 * (lane + 64 * i));
         s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
     }
     constexpr float invW = 1.0f / (NV * 256);
@@ -62,32 +76,49 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
             bf16x4 h = {(__bf16)o.x, (__bf16)o.y, (__bf16)o.z, (__bf16)o.w};
             ((bf16x4*)(y16 + r * ldy16))[f] = h;
         }
+        if (yh) {  // may alias x (in-place ln_pre): the whole row is in registers already
+            f16x4 h = {(_Float16)o.x, (_Float16)o.y, (_Float16)o.z, (_Float16)o.w};
+            ((f16x4*)(yh + r * ldyh))[f] = h;
+        }
     }
 }
 
-int layernorm(const float* x, int64_t rows, int64_t ldx, const int32_t* row_idx, int64_t W, const float* g,
-              const float* b, float eps, float* y32, int64_t ldy32, __bf16* y16, int64_t ldy16, hipStream_t s) {
+template <typename TX>
+int layernorm(const TX* x, int64_t rows, int64_t ldx, const int32_t* row_idx, int64_t W, const float* g,
+              const float* b, float eps, float* y32, int64_t ldy32, __bf16* y16, int64_t ldy16, hipStream_t s,
+              _Float16* yh = nullptr, int64_t ldyh = 0) {
     if (rows == 0) return OK;
-    RM_REQUIRE(ldx % 4 == 0 && (!y32 || ldy32 % 4 == 0) && (!y16 || ldy16 % 4 == 0), "layernorm: strides");
+    RM_REQUIRE(ldx % 4 == 0 && (!y32 || ldy32 % 4 == 0) && (!y16 || ldy16 % 4 == 0) && (!yh || ldyh % 4 == 0),
+               "layernorm: strides");
     dim3 grid(ceil_div(rows, 4));
     switch (W) {
         case 512:
-            hipLaunchKernelGGL(layernorm_kernel<2>, grid, dim3(256), 0, s, x, rows, ldx, row_idx, g, b, eps, y32,
-                               ldy32, y16, ldy16);
+            hipLaunchKernelGGL((layernorm_kernel<2, TX>), grid, dim3(256), 0, s, x, rows, ldx, row_idx, g, b, eps, y32,
+                               ldy32, y16, ldy16, yh, ldyh);
             break;
         case 768:
-            hipLaunchKernelGGL(layernorm_kernel<3>, grid, dim3(256), 0, s, x, rows, ldx, row_idx, g, b, eps, y32,
-                               ldy32, y16, ldy16);
+            hipLaunchKernelGGL((layernorm_kernel<3, TX>), grid, dim3(256), 0, s, x, rows, ldx, row_idx, g, b, eps, y32,
+                               ldy32, y16, ldy16, yh, ldyh);
             break;
         case 1024:
-            hipLaunchKernelGGL(layernorm_kernel<4>, grid, dim3(256), 0, s, x, rows, ldx, row_idx, g, b, eps, y32,
-                               ldy32, y16, ldy16);
+            hipLaunchKernelGGL((layernorm_kernel<4, TX>), grid, dim3(256), 0, s, x, rows, ldx, row_idx, g, b, eps, y32,
+                               ldy32, y16, ldy16, yh, ldyh);
             break;
         default:
             return fail(EINVAL_, "layernorm: width must be 512, 768 or 1024");
     }
     RM_LAUNCHED();
     return OK;
+}
+
+// fp16 residual rows -> fp32 output rows (x11 of encode_image / encode_cls)
+__global__ void rows_f16_to_f32_kernel(const _Float16* __restrict__ x, int64_t rows, int64_t ldx, int W,
+                                       float* __restrict__ y) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= rows * (W / 4)) return;
+    const int64_t r = e / (W / 4);
+    const int c = (int)(e % (W / 4)) * 4;
+    *(float4*)(y + r * W + c) = load4(x + r * ldx + c);
 }
 
 // ---------------------------------------------------------- patch embed im2col
@@ -133,7 +164,7 @@ __global__ void im2col_kernel(const TI* __restrict__ img, int64_t B, int H, int 
 }
 
 // x[b*L+0] = class_emb + pos[0]; IVLP: x[b*L+1+NP+i] = half(vpt[i]) (maple.py:765-767).
-__global__ void cls_rows_kernel(float* __restrict__ x, int64_t B, int L, int W, const float* __restrict__ cls,
+__global__ void cls_rows_kernel(_Float16* __restrict__ x, int64_t B, int L, int W, const float* __restrict__ cls,
                                 const float* __restrict__ pos, int NP, int n_ctx, const float* __restrict__ vpt) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int rows = 1 + n_ctx;
@@ -142,13 +173,13 @@ __global__ void cls_rows_kernel(float* __restrict__ x, int64_t B, int L, int W, 
     const int64_t br = e / W;
     const int64_t b = br / rows;
     const int r = (int)(br % rows);
-    if (r == 0) x[(b * L) * W + n] = cls[n] + pos[n];
-    else x[(b * L + 1 + NP + (r - 1)) * W + n] = (float)(_Float16)vpt[(r - 1) * W + n];
+    if (r == 0) x[(b * L) * W + n] = (_Float16)(cls[n] + pos[n]);
+    else x[(b * L + 1 + NP + (r - 1)) * W + n] = (_Float16)vpt[(r - 1) * W + n];
 }
 
 // IVLP per-block prompt: rows [row0, row0+n_ctx) of every sequence <- half(prompt)
 // (vision row0 = L-n_ctx, maple.py:620-629; text row0 = 1, maple.py:630-640).
-__global__ void prompt_rows_kernel(float* __restrict__ x, int64_t nseq, int L, int W, int row0, int n_ctx,
+__global__ void prompt_rows_kernel(_Float16* __restrict__ x, int64_t nseq, int L, int W, int row0, int n_ctx,
                                    const float* __restrict__ prompt) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= nseq * n_ctx * W) return;
@@ -156,11 +187,11 @@ __global__ void prompt_rows_kernel(float* __restrict__ x, int64_t nseq, int L, i
     const int64_t br = e / W;
     const int64_t b = br / n_ctx;
     const int r = (int)(br % n_ctx);
-    x[(b * L + row0 + r) * W + n] = (float)(_Float16)prompt[r * W + n];
+    x[(b * L + row0 + r) * W + n] = (_Float16)prompt[r * W + n];
 }
 
 // x[n*L+t] = (prompts ? prompts[n,t] : tok_emb[tokens[n,t]]) + pos[t]   (maple.py:972-974)
-__global__ void text_embed_kernel(float* __restrict__ x, const int64_t* __restrict__ tokens,
+__global__ void text_embed_kernel(_Float16* __restrict__ x, const int64_t* __restrict__ tokens,
                                   const float* __restrict__ prompts, const float* __restrict__ tok_emb,
                                   const float* __restrict__ pos, int64_t N, int L, int W, int64_t vocab) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -176,8 +207,8 @@ __global__ void text_embed_kernel(float* __restrict__ x, const int64_t* __restri
         v = ((const float4*)(tok_emb + id * W))[c4];
     }
     const float4 p = ((const float4*)(pos + (int64_t)t * W))[c4];
-    v.x += p.x; v.y += p.y; v.z += p.z; v.w += p.w;
-    ((float4*)(x + nt * W))[c4] = v;
+    const f16x4 h = {(_Float16)(v.x + p.x), (_Float16)(v.y + p.y), (_Float16)(v.z + p.z), (_Float16)(v.w + p.w)};
+    ((f16x4*)(x + nt * W))[c4] = h;
 }
 
 // row index of tokens[n].argmax() (first maximum, torch semantics) in the [N*L] row space
@@ -203,7 +234,7 @@ static Plan plan(int64_t nseq, int L, int W, int lp, int64_t extra_rows) {
     Plan p{};
     const int64_t M = nseq * L;
     int64_t off = 0;
-    p.x = off; off = al(off + M * W * 4);
+    p.x = off; off = al(off + M * W * 2);  // fp16 residual stream
     p.h = off; off = al(off + M * W * 2);
     p.q = off; off = al(off + M * W * 2);
     p.k = off; off = al(off + M * W * 2);
@@ -215,11 +246,11 @@ static Plan plan(int64_t nseq, int L, int W, int lp, int64_t extra_rows) {
     return p;
 }
 
-// One ResidualAttentionBlock on the fp32 residual stream x [nseq*L][W].
+// One ResidualAttentionBlock on the fp16 residual stream x [nseq*L][W].
 static int run_block(const reidmi_block_weights& bw, char* ws, const Plan& P, int64_t nseq, int L, int W, int H,
                      bool causal, hipStream_t s) {
     const int64_t M = nseq * L;
-    float* x = (float*)(ws + P.x);
+    _Float16* x = (_Float16*)(ws + P.x);
     __bf16* h = (__bf16*)(ws + P.h);
     __bf16* o = (__bf16*)(ws + P.o);
     __bf16* u = (__bf16*)(ws + P.u);
@@ -239,7 +270,7 @@ static int run_block(const reidmi_block_weights& bw, char* ws, const Plan& P, in
     er.out = x;
     er.ldc = W;
     er.bias = bw.out_b;
-    if ((rc = gemm_bf16(EPI_RESID_F32, o, W, bw.out_w, W, M, W, W, er, s))) return rc;
+    if ((rc = gemm_bf16(EPI_RESID_F16, o, W, bw.out_w, W, M, W, W, er, s))) return rc;
     if ((rc = layernorm(x, M, W, nullptr, W, bw.ln2_w, bw.ln2_b, 1e-5f, nullptr, 0, h, W, s))) return rc;
     EpiArgs eg{};
     eg.out = u;
@@ -250,7 +281,7 @@ static int run_block(const reidmi_block_weights& bw, char* ws, const Plan& P, in
     e2.out = x;
     e2.ldc = W;
     e2.bias = bw.fc2_b;
-    if ((rc = gemm_bf16(EPI_RESID_F32, u, 4 * W, bw.fc2_w, 4 * W, M, W, 4 * W, e2, s))) return rc;
+    if ((rc = gemm_bf16(EPI_RESID_F16, u, 4 * W, bw.fc2_w, 4 * W, M, W, 4 * W, e2, s))) return rc;
     return OK;
 }
 
@@ -262,7 +293,7 @@ static int run_block(const reidmi_block_weights& bw, char* ws, const Plan& P, in
 static int run_block_cls(const reidmi_block_weights& bw, char* ws, const Plan& P, int64_t nseq, int L, int W, int H,
                          hipStream_t s) {
     const int64_t M = nseq * L;
-    float* x = (float*)(ws + P.x);
+    _Float16* x = (_Float16*)(ws + P.x);
     __bf16* h = (__bf16*)(ws + P.h);
     __bf16* o = (__bf16*)(ws + P.o);
     __bf16* u = (__bf16*)(ws + P.u);
@@ -289,7 +320,7 @@ static int run_block_cls(const reidmi_block_weights& bw, char* ws, const Plan& P
     er.out = x;
     er.ldc = (int64_t)L * W;
     er.bias = bw.out_b;
-    if ((rc = gemm_bf16(EPI_RESID_F32, o, W, bw.out_w, W, nseq, W, W, er, s))) return rc;
+    if ((rc = gemm_bf16(EPI_RESID_F16, o, W, bw.out_w, W, nseq, W, W, er, s))) return rc;
     if ((rc = layernorm(x, nseq, (int64_t)L * W, nullptr, W, bw.ln2_w, bw.ln2_b, 1e-5f, nullptr, 0, h, W, s)))
         return rc;
     EpiArgs eg{};
@@ -301,7 +332,7 @@ static int run_block_cls(const reidmi_block_weights& bw, char* ws, const Plan& P
     e2.out = x;
     e2.ldc = (int64_t)L * W;
     e2.bias = bw.fc2_b;
-    return gemm_bf16(EPI_RESID_F32, u, 4 * W, bw.fc2_w, 4 * W, nseq, W, 4 * W, e2, s);
+    return gemm_bf16(EPI_RESID_F16, u, 4 * W, bw.fc2_w, 4 * W, nseq, W, 4 * W, e2, s);
 }
 
 static int vit_check(const reidmi_vit_weights* w) {
@@ -345,7 +376,7 @@ REIDMI_API int reidmi_vit_forward(const reidmi_vit_weights* w, const void* image
     RM_REQUIRE(out_x12 && out_proj, "vit: outputs required");
     if (B == 0) return OK;
     char* ws = (char*)ws_;
-    float* x = (float*)(ws + P.x);
+    _Float16* x = (_Float16*)(ws + P.x);
     __bf16* h = (__bf16*)(ws + P.h);
     __bf16* col = (__bf16*)(ws + P.u);
     const int64_t M = B * L;
@@ -370,7 +401,8 @@ REIDMI_API int reidmi_vit_forward(const reidmi_vit_weights* w, const void* image
     hipLaunchKernelGGL(cls_rows_kernel, dim3(ceil_div(ce, 256)), dim3(256), 0, s, x, B, L, W, w->class_emb,
                        w->pos_emb, NP, w->n_ctx, w->vpt);
     RM_LAUNCHED();
-    if ((rc = layernorm(x, M, W, nullptr, W, w->ln_pre_w, w->ln_pre_b, 1e-5f, x, W, nullptr, 0, s))) return rc;
+    if ((rc = layernorm(x, M, W, nullptr, W, w->ln_pre_w, w->ln_pre_b, 1e-5f, nullptr, 0, nullptr, 0, s, x, W)))
+        return rc;
     // resblocks[:11] then resblocks[11] (custom_clip_model.py:91-92)
     for (int i = 0; i < 12; i++) {
         const reidmi_block_weights& bw = w->blocks[i];
@@ -383,11 +415,11 @@ REIDMI_API int reidmi_vit_forward(const reidmi_vit_weights* w, const void* image
         if (i == 11 && !full) rc = run_block_cls(bw, ws, P, B, L, W, w->heads, s);
         else rc = run_block(bw, ws, P, B, L, W, w->heads, false, s);
         if (rc) return rc;
-        if (i == 10 && out_x11) {
-            if (full) RM_CHECK_HIP(hipMemcpyAsync(out_x11, x, M * W * 4, hipMemcpyDeviceToDevice, s));
-            else
-                RM_CHECK_HIP(hipMemcpy2DAsync(out_x11, W * 4, x, (size_t)L * W * 4, W * 4, B,
-                                              hipMemcpyDeviceToDevice, s));
+        if (i == 10 && out_x11) {  // resblocks[:11] output (fp16 stream -> fp32)
+            const int64_t r11 = full ? M : B;
+            hipLaunchKernelGGL(rows_f16_to_f32_kernel, dim3(ceil_div(r11 * (W / 4), 256)), dim3(256), 0, s, x, r11,
+                               full ? (int64_t)W : (int64_t)L * W, W, out_x11);
+            RM_LAUNCHED();
         }
     }
     // ln_post, then @ proj (custom_clip_model.py:96-98)
@@ -417,7 +449,7 @@ REIDMI_API int reidmi_text_forward(const reidmi_text_weights* w, const int64_t* 
     RM_REQUIRE(ws_bytes >= P.total, "text: workspace too small");
     if (N == 0) return OK;
     char* ws = (char*)ws_;
-    float* x = (float*)(ws + P.x);
+    _Float16* x = (_Float16*)(ws + P.x);
     __bf16* h = (__bf16*)(ws + P.h);
     int32_t* rows = (int32_t*)(ws + P.rows);
     const int64_t te = N * L * (W / 4);

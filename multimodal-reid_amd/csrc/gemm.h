@@ -8,14 +8,23 @@
 //   EPI_GELU_BF16 out bf16 = QuickGELU(acc + bias)            (mlp.c_fc + gelu, :14-16,52-54)
 //   EPI_RESID_F32 x fp32 += acc + bias                        (out_proj / c_proj + residual, :27-28)
 //   EPI_QKV       q,k -> [B,H,L,64] bf16, v -> [B,H,64,Lp]    (attn.in_proj + head split)
-//   EPI_PATCH     x[b*L+1+p] = acc + pos[1+p]  fp32           (conv1 + pos-embed, :78-86)
+//   EPI_PATCH     x[b*L+1+p] = acc + pos[1+p]  fp16           (conv1 + pos-embed, :78-86)
 //   EPI_F32       out fp32 = acc + bias                       (proj / text_projection)
+//   EPI_RESID_F16 x fp16 += acc + bias (fp32 sum, one rounding) (the encoders' residual stream)
 #pragma once
 #include "common.h"
 
 namespace reidmi {
 
-enum Epi : int { EPI_BF16 = 0, EPI_GELU_BF16 = 1, EPI_RESID_F32 = 2, EPI_QKV = 3, EPI_PATCH = 4, EPI_F32 = 5 };
+enum Epi : int {
+    EPI_BF16 = 0,
+    EPI_GELU_BF16 = 1,
+    EPI_RESID_F32 = 2,
+    EPI_QKV = 3,
+    EPI_PATCH = 4,
+    EPI_F32 = 5,
+    EPI_RESID_F16 = 6
+};
 
 struct EpiArgs {
     void* out;          // bf16 / fp32 output (or residual x for RESID, x for PATCH)

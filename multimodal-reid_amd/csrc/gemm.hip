@@ -92,6 +92,67 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
                 acc[i][j][3] += b[j].w;
             }
     }
+    if constexpr (EPI == EPI_RESID_F16) {
+        // Pair the fp32 accumulators first (v_permlane16_swap, see the bf16 path below; swap
+        // whole uint4 images — per-element f32x4 read-modify-write around the builtin was
+        // mis-lowered by hipcc 7.2, duplicating element 0 into elements 1..3):
+        // afterwards lane group q holds columns colp(jp) .. +7 of its row in acc[i][2jp]
+        // (first 4) and acc[i][2jp+1] (next 4) -> 16-byte fp16 loads and stores.
+        const int q = lane >> 4;
+#pragma unroll
+        for (int i = 0; i < NI; i++)
+#pragma unroll
+            for (int jp = 0; jp < 2; jp++) {
+                const uint4 a = __builtin_bit_cast(uint4, acc[i][2 * jp]);
+                const uint4 c = __builtin_bit_cast(uint4, acc[i][2 * jp + 1]);
+                const auto s0 = __builtin_amdgcn_permlane16_swap(a.x, c.x, false, false);
+                const auto s1 = __builtin_amdgcn_permlane16_swap(a.y, c.y, false, false);
+                const auto s2 = __builtin_amdgcn_permlane16_swap(a.z, c.z, false, false);
+                const auto s3 = __builtin_amdgcn_permlane16_swap(a.w, c.w, false, false);
+                acc[i][2 * jp] = __builtin_bit_cast(f32x4, make_uint4(s0[0], s1[0], s2[0], s3[0]));
+                acc[i][2 * jp + 1] = __builtin_bit_cast(f32x4, make_uint4(s0[1], s1[1], s2[1], s3[1]));
+            }
+        _Float16* xo = (_Float16*)ea.out;
+        auto colp = [&](int jp) { return ncol + (2 * jp + (q & 1)) * 16 + (q >> 1) * 8; };
+        constexpr int NB = 2;  // row groups per batch: 4 x 16-byte loads in flight per lane
+        auto store_batch = [&](int i0) {
+#pragma unroll
+            for (int ii = 0; ii < NB; ii++) {
+                const int64_t m = mrow + (i0 + ii) * 16 + (lane & 15);
+                if (m >= M) continue;
+#pragma unroll
+                for (int jp = 0; jp < 2; jp++) {
+                    const f32x4 a = acc[i0 + ii][2 * jp], b = acc[i0 + ii][2 * jp + 1];
+                    const f16x8 h = {(_Float16)a[0], (_Float16)a[1], (_Float16)a[2], (_Float16)a[3],
+                                     (_Float16)b[0], (_Float16)b[1], (_Float16)b[2], (_Float16)b[3]};
+                    *(f16x8*)(xo + m * ea.ldc + colp(jp)) = h;
+                }
+            }
+        };
+#pragma unroll
+        for (int i0 = 0; i0 < NI; i0 += NB) {
+            f16x8 xv[NB][2];
+#pragma unroll
+            for (int ii = 0; ii < NB; ii++) {
+                int64_t m = mrow + (i0 + ii) * 16 + (lane & 15);
+                m = m < M ? m : M - 1;  // clamped rows are loaded but not stored
+#pragma unroll
+                for (int jp = 0; jp < 2; jp++) xv[ii][jp] = *(const f16x8*)(xo + m * ea.ldc + colp(jp));
+            }
+            if (i0 > 0) store_batch(i0 - NB);
+#pragma unroll
+            for (int ii = 0; ii < NB; ii++)
+#pragma unroll
+                for (int jp = 0; jp < 2; jp++)
+#pragma unroll
+                    for (int e = 0; e < 4; e++) {
+                        acc[i0 + ii][2 * jp][e] += (float)xv[ii][jp][e];
+                        acc[i0 + ii][2 * jp + 1][e] += (float)xv[ii][jp][4 + e];
+                    }
+        }
+        store_batch(NI - NB);
+        return;
+    }
     if constexpr (EPI == EPI_RESID_F32 || EPI == EPI_PATCH) {
         // software-pipelined: the loads of batch n+1 are issued before the stores of batch n,
         // so no wait ever covers a store (vmcnt retires in issue order).
@@ -99,10 +160,6 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
         auto row_of = [&](int i) {
             const int64_t m = mrow + i * 16 + (lane & 15);
             return m < M ? m : M - 1;  // clamped rows are loaded but not stored
-        };
-        auto dst_row = [&](int64_t m) -> float* {
-            if constexpr (EPI == EPI_RESID_F32) return (float*)ea.out + m * ea.ldc + ncol + cq;
-            else return (float*)ea.out + ((m / ea.npatch) * ea.seq + 1 + m % ea.npatch) * ea.ldc + ncol + cq;
         };
         auto src_row = [&](int64_t m) -> const float* {
             if constexpr (EPI == EPI_RESID_F32) return (const float*)ea.out + m * ea.ldc + ncol + cq;
@@ -113,11 +170,20 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
             for (int ii = 0; ii < NB; ii++) {
                 const int64_t m = mrow + (i0 + ii) * 16 + (lane & 15);
                 if (m >= M) continue;
-                float* d = dst_row(m);
+                if constexpr (EPI == EPI_RESID_F32) {
+                    float* d = (float*)ea.out + m * ea.ldc + ncol + cq;
 #pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const f32x4 v = acc[i0 + ii][j];
-                    *(float4*)(d + j * 16) = make_float4(v[0], v[1], v[2], v[3]);
+                    for (int j = 0; j < 4; j++) {
+                        const f32x4 v = acc[i0 + ii][j];
+                        *(float4*)(d + j * 16) = make_float4(v[0], v[1], v[2], v[3]);
+                    }
+                } else {  // patch rows of the fp16 residual stream
+                    _Float16* d = (_Float16*)ea.out + ((m / ea.npatch) * ea.seq + 1 + m % ea.npatch) * ea.ldc + ncol + cq;
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const f32x4 v = acc[i0 + ii][j];
+                        *(f16x4*)(d + j * 16) = f16x4{(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
+                    }
                 }
             }
         };
@@ -974,8 +1040,9 @@ int gemm_bf16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, i
     RM_REQUIRE(M >= 0 && N > 0 && K > 0, "gemm: bad shape");
     RM_REQUIRE(N % GB_N == 0 && K % GB_K == 0, "gemm: needs N % 128 == 0 and K % 64 == 0");
     RM_REQUIRE(lda % 8 == 0 && ldw % 8 == 0 && lda >= K && ldw >= K, "gemm: lda/ldw must be >= K and 16-byte rows");
-    RM_REQUIRE((epi != EPI_BF16 && epi != EPI_GELU_BF16) || (ea.ldc % 8 == 0 && ((uintptr_t)ea.out & 15) == 0),
-               "gemm: bf16 output needs ldc % 8 == 0 and a 16-byte aligned base");
+    RM_REQUIRE((epi != EPI_BF16 && epi != EPI_GELU_BF16 && epi != EPI_RESID_F16) ||
+                   (ea.ldc % 8 == 0 && ((uintptr_t)ea.out & 15) == 0),
+               "gemm: bf16/fp16 output needs ldc % 8 == 0 and a 16-byte aligned base");
     if (M == 0) return OK;
     hipEvent_t ev_b = nullptr;
     if (prof::enabled) {
@@ -999,6 +1066,7 @@ int gemm_bf16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, i
         case EPI_QKV: rc = launch<EPI_QKV>(A, lda, W, ldw, M, N, K, ea, s); break;
         case EPI_PATCH: rc = launch<EPI_PATCH>(A, lda, W, ldw, M, N, K, ea, s); break;
         case EPI_F32: rc = launch<EPI_F32>(A, lda, W, ldw, M, N, K, ea, s); break;
+        case EPI_RESID_F16: rc = launch<EPI_RESID_F16>(A, lda, W, ldw, M, N, K, ea, s); break;
         default: return fail(EINVAL_, "gemm: unknown epilogue");
     }
     if (ev_b) RM_CHECK_HIP(hipEventRecord(ev_b, s));
@@ -1048,8 +1116,8 @@ REIDMI_API int reidmi_prof_collect(int epi, double* total_ms, int64_t* count, do
 
 REIDMI_API int reidmi_gemm_bf16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N,
                                 int64_t K, const float* bias, void* out, int64_t ldc, void* stream) {
-    RM_REQUIRE(epi == EPI_BF16 || epi == EPI_GELU_BF16 || epi == EPI_RESID_F32 || epi == EPI_F32,
-               "reidmi_gemm_bf16: epi must be 0 (bf16), 1 (gelu bf16), 2 (residual f32) or 5 (f32)");
+    RM_REQUIRE(epi == EPI_BF16 || epi == EPI_GELU_BF16 || epi == EPI_RESID_F32 || epi == EPI_F32 || epi == EPI_RESID_F16,
+               "reidmi_gemm_bf16: epi must be 0 (bf16), 1 (gelu bf16), 2 (residual f32), 5 (f32) or 6 (residual f16)");
     EpiArgs ea{};
     ea.out = out;
     ea.ldc = ldc;

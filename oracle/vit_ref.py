@@ -6,9 +6,10 @@ over the same state-dict layout libreidmi packs.
 
 TEST INFRASTRUCTURE ONLY (tests/, smoke(), bench.py cpu_baseline leg).
 
-``bf16=True`` rounds to bfloat16 exactly where the HIP kernels do (GEMM operands, q/k/v,
-softmax probabilities before P.V, attention output), so tests can separate kernel bugs
-from the precision the MI355X path runs at.  With bf16=False it is the reference's fp32
+``bf16=True`` rounds exactly where the HIP kernels do — to bfloat16 for GEMM operands,
+q/k/v, softmax probabilities before P.V and the attention output, and to float16 for the
+residual stream x (patch/CLS rows, ln_pre output, every residual add: the reference's own
+GPU dtype) — so tests can separate kernel bugs from the precision the MI355X path runs at.  With bf16=False it is the reference's fp32
 math, pinned to tests/golden/vit_b16.npz and text.npz (made by the reference modules).
 """
 import numpy as np
@@ -22,6 +23,10 @@ def _t(a):
 
 def _r(x, on):
     return x.to(torch.bfloat16).float() if on else x
+
+
+def _h(x, on):
+    return x.half().float() if on else x
 
 
 def _ln(x, w, b):
@@ -43,11 +48,11 @@ def block(x, sd, p, heads, causal=False, bf16=False):
     den = e.sum(-1, keepdim=True)
     o = (_r(e, bf16) @ v) / den
     o = _r(o.permute(0, 2, 1, 3).reshape(B, L, W), bf16)
-    x = x + (o @ _r(_t(sd[p + "attn.out_proj.weight"]), bf16).t() + _t(sd[p + "attn.out_proj.bias"]))
+    x = _h(x + (o @ _r(_t(sd[p + "attn.out_proj.weight"]), bf16).t() + _t(sd[p + "attn.out_proj.bias"])), bf16)
     h = _r(_ln(x, sd[p + "ln_2.weight"], sd[p + "ln_2.bias"]), bf16)
     u = h @ _r(_t(sd[p + "mlp.c_fc.weight"]), bf16).t() + _t(sd[p + "mlp.c_fc.bias"])
     u = _r(u * torch.sigmoid(1.702 * u), bf16)
-    return x + (u @ _r(_t(sd[p + "mlp.c_proj.weight"]), bf16).t() + _t(sd[p + "mlp.c_proj.bias"]))
+    return _h(x + (u @ _r(_t(sd[p + "mlp.c_proj.weight"]), bf16).t() + _t(sd[p + "mlp.c_proj.bias"])), bf16)
 
 
 def tta_view(img, offs):
@@ -73,13 +78,13 @@ def vit_forward(sd, img, stride=12, bf16=False, tta=None):
     x = cols @ _r(conv.reshape(W, -1), bf16).t()
     pos = _t(sd["positional_embedding"])
     cls = (_t(sd["class_embedding"]) + pos[0]).expand(B, 1, W)
-    x = torch.cat([cls, x + pos[1:1 + gh * gw]], 1)
+    x = _h(torch.cat([cls, x + pos[1:1 + gh * gw]], 1), bf16)
     n_ctx = 0
     if "VPT" in sd:
         vpt = _t(sd["VPT"]).half().float()
         n_ctx = vpt.shape[0]
         x = torch.cat([x, vpt.expand(B, -1, -1)], 1)
-    x = _ln(x, sd["ln_pre.weight"], sd["ln_pre.bias"])
+    x = _h(_ln(x, sd["ln_pre.weight"], sd["ln_pre.bias"]), bf16)
     L = x.shape[1]
     x11 = None
     for i in range(12):
@@ -100,7 +105,7 @@ def text_forward(sd, tokens, prompts=None, bf16=False):
     W = _t(sd["ln_final.weight"]).shape[0]
     heads = W // 64
     x = _t(sd["token_embedding.weight"])[tokens] if prompts is None else _t(prompts)
-    x = x + _t(sd["positional_embedding"])
+    x = _h(x + _t(sd["positional_embedding"]), bf16)
     N, L, _ = x.shape
     layers = len([k for k in sd if k.startswith("transformer.") and k.endswith(".attn.in_proj_weight")])
     for i in range(layers):

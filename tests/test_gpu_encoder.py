@@ -30,7 +30,7 @@ def _cos(a, b):
     return (a * b).sum(1) / np.linalg.norm(a, axis=1) / np.linalg.norm(b, axis=1)
 
 
-@pytest.mark.parametrize("epi", [0, 1, 2, 5])
+@pytest.mark.parametrize("epi", [0, 1, 2, 5, 6])
 @pytest.mark.parametrize("M,N,K", [(300, 256, 192), (1, 128, 64), (1000, 768, 768)])
 def test_gemm_epilogues(gpu, epi, M, N, K):
     L = _lib()
@@ -44,18 +44,20 @@ def test_gemm_epilogues(gpu, epi, M, N, K):
         out = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
     else:
         base = torch.randn(M, N, generator=g)
-        out = base.clone().cuda() if epi == 2 else torch.empty(M, N, device="cuda")
+        if epi == 6:
+            base = base.half()
+        out = base.clone().cuda() if epi in (2, 6) else torch.empty(M, N, device="cuda")
     L.call("reidmi_gemm_bf16", epi, L.ptr(dA), K, L.ptr(dW), K, M, N, K, L.ptr(db), L.ptr(out), N, L.stream())
     got = out.float().cpu()
     if epi == 1:
         ref = ref * torch.sigmoid(1.702 * ref)
-    if epi == 2:
-        ref = ref + base
-    tol = 1e-2 if epi in (0, 1) else 2e-3  # bf16 outputs carry their own rounding
+    if epi in (2, 6):
+        ref = ref + base.float()
+    tol = 1e-2 if epi in (0, 1) else (2e-3 if epi == 6 else 2e-3)  # bf16/fp16 outputs carry their own rounding
     assert (got - ref).abs().max() <= tol * (ref.abs().max() + 1)
 
 
-@pytest.mark.parametrize("epi", [0, 1, 2, 5])
+@pytest.mark.parametrize("epi", [0, 1, 2, 5, 6])
 @pytest.mark.parametrize("M,N,K", [(54016, 768, 768), (1000, 2304, 768), (700, 512, 3072), (70000, 256, 192)])
 def test_gemm_v2_tile_bitexact_vs_v1(gpu, epi, M, N, K):
     """The 256x256 LDS-DMA tiles (v2 plain, v3 persistent, v4 ping-pong, v5 persistent
@@ -73,6 +75,8 @@ def test_gemm_v2_tile_bitexact_vs_v1(gpu, epi, M, N, K):
         L.call("reidmi_gemm_set_variant", v)
         if epi in (0, 1):
             out = torch.zeros(M, N, dtype=torch.bfloat16, device="cuda")
+        elif epi == 6:
+            out = torch.ones(M, N, dtype=torch.float16, device="cuda")
         else:
             out = torch.ones(M, N, device="cuda")
         L.call("reidmi_gemm_bf16", epi, L.ptr(A), K, L.ptr(W), K, M, N, K, L.ptr(bias), L.ptr(out), N, L.stream())
@@ -84,7 +88,7 @@ def test_gemm_v2_tile_bitexact_vs_v1(gpu, epi, M, N, K):
     ref = A[rows].float() @ W.float().t() + bias
     if epi == 1:
         ref = ref * torch.sigmoid(1.702 * ref)
-    if epi == 2:
+    if epi in (2, 6):
         ref = ref + 1
     assert (outs[1][rows].float() - ref).abs().max() <= 1e-2 * (ref.abs().max() + 1)
 
