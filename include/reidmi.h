@@ -82,6 +82,44 @@ int reidmi_rerank_from_dist(const float* dist, const float* add, int64_t Q, int6
                             int k2, uint16_t one_minus_lambda_h, float lambda_f, float* final_dist, int64_t ldo,
                             void* ws, int64_t ws_bytes, int32_t* flags, void* stream);
 
+/* Staged re-ranking: R1-R7 of re_ranking (reranking.py:29-100) as row-range stages over
+ * caller-allocated, exactly sized buffers, bit-identical to reidmi_rerank.  The N x N distance
+ * is never materialised (chunk_rows x N row blocks are), and every stage takes a row range,
+ * so ranks can each own [lo, hi) and all-gather R / V / V_qe between stages.
+ * feat [N][ldf] fp32 = cat(probFea, galFea); sqn[N] = squared row norms (reidmi_row_sqnorm_f32).
+ * K = max(k1 + 1, k2) columns of initial_rank.  ELL outputs have vcap / qcap entries per row;
+ * CSR inputs are (off[N+1] int64, col int32, fp16 bits), columns ascending per row. */
+int reidmi_rr_caps(int* vcap, int* qcap);
+/* R1+R2 (reranking.py:36-48): rank_out[hi-lo][K] = stable argsort prefix of od rows lo..hi,
+ * rowmax_out[hi-lo] = the od divisors (column maxima of the symmetric distance). */
+int reidmi_rr_rank_rows(const float* feat, int64_t N, int64_t D, int64_t ldf, const float* sqn, int64_t lo, int64_t hi,
+                        int K, int32_t* rank_out, float* rowmax_out, float* chunk, int64_t chunk_rows, void* stream);
+/* R3 (reranking.py:51-71): V rows lo..hi (ELL [hi-lo][vcap]) from the full rank[N][K] and
+ * rowmax[N]; distance entries recomputed from feat with the distance kernel's arithmetic. */
+int reidmi_rr_v_rows(const float* feat, int64_t N, int64_t D, int64_t ldf, const float* sqn, const float* rowmax,
+                     const int32_t* rank, int K, int64_t lo, int64_t hi, int k1, int32_t* vcol, uint16_t* vval,
+                     int32_t* vnnz, int32_t* flags, void* stream);
+/* off[0..rows] = exclusive scan of nnz[0..rows) (off[rows] = total). */
+int reidmi_rr_row_offsets(const int32_t* nnz, int64_t rows, int64_t* off, void* stream);
+/* ELL rows -> CSR storage at off[]. */
+int reidmi_rr_pack(const int32_t* ell_col, const uint16_t* ell_val, const int32_t* nnz, int64_t rows, int64_t cap,
+                   const int64_t* off, int32_t* col, uint16_t* val, void* stream);
+/* R4 (reranking.py:73-78): V_qe rows lo..hi (ELL [hi-lo][qcap]) from the full V (CSR). */
+int reidmi_rr_qe_rows(const int32_t* rank, int K, int k2, int64_t lo, int64_t hi, const int64_t* voff,
+                      const int32_t* vcol, const uint16_t* vval, int32_t* qcol, uint16_t* qval, int32_t* qnnz,
+                      int32_t* flags, void* stream);
+/* R5 (reranking.py:80-82): inverted index of the full V_qe (CSR, nnz entries) as CSC with
+ * rows ascending per column: coff[N+1], irow[nnz], ival[nnz]. */
+int64_t reidmi_rr_csc_workspace_bytes(int64_t N, int64_t nnz);
+int reidmi_rr_csc(int64_t N, const int64_t* qoff, const int32_t* qcol, const uint16_t* qval, int64_t nnz, int64_t* coff,
+                  int32_t* irow, uint16_t* ival, void* ws, int64_t ws_bytes, void* stream);
+/* R6+R7 (reranking.py:84-100): final rows for queries qlo..qhi: out[qhi-qlo][ldo] (G columns). */
+int reidmi_rr_jaccard_rows(const float* feat, int64_t N, int64_t D, int64_t ldf, const float* sqn,
+                           const float* rowmax, int64_t Q, int64_t qlo, int64_t qhi, const int64_t* qoff,
+                           const int32_t* qcol, const uint16_t* qval, const int64_t* coff, const int32_t* irow,
+                           const uint16_t* ival, uint16_t one_minus_lambda_h, float lambda_f, float* out, int64_t ldo,
+                           float* chunk, int64_t chunk_rows, void* stream);
+
 /* ------------------------------------------------------------------ encoders */
 
 /* bf16 GEMM C = A . W^T (+bias) on v_mfma_f32_16x16x32_bf16, fp32 accumulation.

@@ -30,6 +30,16 @@ SIGNATURES = {
     "reidmi_rerank": [_vp, _i64, _i64, _i64, _i64, _i32, _i32, _u16, _f32, _vp, _i64, _vp, _i64, _vp, _vp],
     "reidmi_rerank_from_dist": [_vp, _vp, _i64, _i64, _i32, _i32, _i32, _u16, _f32, _vp, _i64, _vp, _i64, _vp,
                                 _vp],
+    "reidmi_rr_caps": [_vp, _vp],
+    "reidmi_rr_rank_rows": [_vp, _i64, _i64, _i64, _vp, _i64, _i64, _i32, _vp, _vp, _vp, _i64, _vp],
+    "reidmi_rr_v_rows": [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _i32, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp],
+    "reidmi_rr_row_offsets": [_vp, _i64, _vp, _vp],
+    "reidmi_rr_pack": [_vp, _vp, _vp, _i64, _i64, _vp, _vp, _vp, _vp],
+    "reidmi_rr_qe_rows": [_vp, _i32, _i32, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "reidmi_rr_csc_workspace_bytes": [_i64, _i64],
+    "reidmi_rr_csc": [_i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i64, _vp],
+    "reidmi_rr_jaccard_rows": [_vp, _i64, _i64, _i64, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp,
+                               _u16, _f32, _vp, _i64, _vp, _i64, _vp],
     "reidmi_attn_lpad": [_i32],
     "reidmi_prof_enable": [_i32],
     "reidmi_gemm_set_variant": [_i32],

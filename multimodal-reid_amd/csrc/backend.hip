@@ -343,6 +343,18 @@ int distmat_launch(const float* q, int64_t Q, int64_t ldq, const float* g, int64
     return distmat_impl(false, q, Q, ldq, g, G, ldg, D, out, ldo, ws, s);
 }
 
+// Euclidean distance with precomputed squared row norms qq[Q], gg[G] (row_sqnorm_kernel).
+int distmat_pre_launch(const float* q, int64_t Q, int64_t ldq, const float* g, int64_t G, int64_t ldg, int64_t D,
+                       const float* qq, const float* gg, float* out, int64_t ldo, hipStream_t s) {
+    RM_REQUIRE(Q >= 0 && G >= 0 && D > 0 && ldq >= D && ldg >= D && ldo >= G && qq && gg, "distmat: bad shape");
+    if (Q == 0 || G == 0) return OK;
+    dim3 grid(ceil_div(G, DM_BN), ceil_div(Q, DM_BM));
+    RM_REQUIRE(grid.y <= 65535, "distmat: too many query rows for one launch");
+    hipLaunchKernelGGL(distmat_f32_kernel<false>, grid, dim3(256), 0, s, q, g, qq, gg, Q, G, D, ldq, ldg, out, ldo);
+    RM_LAUNCHED();
+    return OK;
+}
+
 }  // namespace reidmi
 
 using namespace reidmi;

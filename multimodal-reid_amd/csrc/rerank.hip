@@ -7,6 +7,9 @@
 //   R4 query expansion V_qe = mean of k2 rows    qe_kernel            (ELL, fp16)      reranking.py:73-78
 //   R5 inverted index                            csc_count/scan/fill  (CSC)            reranking.py:80-82
 //   R6+R7 Jaccard with sequential fp16 sums, blend with od, slice [:Q, Q:]  jaccard_kernel  reranking.py:84-100
+// Two drivers: one-call (reidmi_rerank*: N x N distance materialised, capacity-sized ELL
+// rows) and staged (reidmi_rr_*: row ranges over exactly sized CSR buffers, distance rows
+// in chunks or recomputed, shardable over ranks; see multimodal_reid_amd/reranking.py).
 // The reference keeps V, V_qe as dense N x N fp16 (2 x 35 GB at MSMT17) and loops in Python;
 // here V/V_qe are row-sorted ELL (column index + fp16 bits) and the inverted index is CSC,
 // so memory is O(N * nnz) and every stage is a data-parallel kernel.
@@ -14,12 +17,16 @@
 // (pinned against numpy 2.2.6), float32 pairwise sum, fp16 ufuncs = op in fp32 then RNE.
 #include "common.h"
 
+#include <hipcub/hipcub.hpp>
+
 namespace reidmi {
 
 int topk_launch(const float* x, int64_t rows, int64_t cols, int64_t ldx, const float* row_div, int k,
                 int32_t* out_idx, float* out_val, int64_t ldo, hipStream_t s);
 int distmat_launch(const float* q, int64_t Q, int64_t ldq, const float* g, int64_t G, int64_t ldg, int64_t D,
                    float* out, int64_t ldo, float* ws, hipStream_t s);
+int distmat_pre_launch(const float* q, int64_t Q, int64_t ldq, const float* g, int64_t G, int64_t ldg, int64_t D,
+                       const float* qq, const float* gg, float* out, int64_t ldo, hipStream_t s);
 
 constexpr int VCAP = 1408;   // >= (k1+1) + (k1+1)(round(k1/2)+1) unique entries for k1 <= 50
 constexpr int QCAP = 4096;   // V_qe row capacity
@@ -90,13 +97,59 @@ __device__ float pairwise_f32(const float* a, int n) {
     return ret;
 }
 
+// ------------------------------------------------------------------ row views
+// A set of sparse rows: CSR (off != nullptr: row r = [off[r], off[r+1])) or fixed-capacity
+// ELL (off == nullptr: row r = [r*cap, r*cap + nnz[r])).  Columns ascending in every row.
+struct Rows {
+    const int64_t* off;
+    const int32_t* nnz;
+    int64_t cap;
+    const int32_t* col;
+    const uint16_t* val;
+    __device__ __forceinline__ int64_t beg(int64_t r) const { return off ? off[r] : r * cap; }
+    __device__ __forceinline__ int len(int64_t r) const { return (int)(off ? off[r + 1] - off[r] : nnz[r]); }
+};
+
+// Where original_dist entries come from: a materialised matrix (od != nullptr: entry
+// (i, c) = od[(i - row0) * ld + c]) or recomputed from the features with the distance
+// kernel's exact arithmetic — an fmaf chain over k ascending, then fmaf(-2, dot, |i|^2 +
+// |c|^2) (backend.hip distmat_f32_kernel; the fp32 MFMA accumulates in the same order).
+struct DistSrc {
+    const float* od;
+    int64_t ld, row0;
+    const float* feat;
+    int64_t ldf;
+    int D;
+    const float* sqn;
+};
+
+__device__ __forceinline__ float dist_at(const DistSrc& s, int64_t i, int64_t c) {
+    if (s.od) return s.od[(i - s.row0) * s.ld + c];
+    const float* a = s.feat + i * s.ldf;
+    const float* b = s.feat + c * s.ldf;
+    float acc = 0.0f;
+    int k = 0;
+    if ((s.ldf & 3) == 0) {
+        for (; k + 4 <= s.D; k += 4) {
+            const float4 x = *(const float4*)(a + k), y = *(const float4*)(b + k);
+            acc = __builtin_fmaf(x.x, y.x, acc);
+            acc = __builtin_fmaf(x.y, y.y, acc);
+            acc = __builtin_fmaf(x.z, y.z, acc);
+            acc = __builtin_fmaf(x.w, y.w, acc);
+        }
+    }
+    for (; k < s.D; k++) acc = __builtin_fmaf(a[k], b[k], acc);
+    return __builtin_fmaf(-2.0f, acc, s.sqn[i] + s.sqn[c]);
+}
+
 // ------------------------------------------------------------------ R2 helpers
-__global__ void rowmax_kernel(const float* __restrict__ D, int64_t N, int64_t ld, float* __restrict__ out) {
+__global__ void rowmax_kernel(const float* __restrict__ D, int64_t rows, int64_t cols, int64_t ld,
+                              float* __restrict__ out) {
     const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (r >= N) return;
+    if (r >= rows) return;
     const int lane = threadIdx.x & 63;
     float m = -__builtin_inff();
-    for (int64_t j = lane; j < N; j += 64) m = fmaxf(m, D[r * ld + j]);
+    for (int64_t j = lane; j < cols; j += 64) m = fmaxf(m, D[r * ld + j]);
     m = wave_max(m);
     if (lane == 0) out[r] = m;
 }
@@ -148,18 +201,20 @@ __device__ __forceinline__ int pow2_ceil_i(int n) {
     return p;
 }
 
-// One 256-thread workgroup per row i of od.  R: initial_rank [N][ldr] (stable argsort prefix).
-__global__ __launch_bounds__(256) void kreciprocal_kernel(const float* __restrict__ OD, int64_t ld,
-                                                          const float* __restrict__ rowdiv, const int32_t* __restrict__ R,
-                                                          int64_t ldr, int64_t N, int kf, int kh1,
-                                                          int32_t* __restrict__ vcol, uint16_t* __restrict__ vval,
-                                                          int32_t* __restrict__ vnnz, int32_t* __restrict__ flags) {
+// One 256-thread workgroup per row i = row0 + blockIdx.x of od (output row blockIdx.x).
+// R: initial_rank [N][ldr] (stable argsort prefix), rowdiv[N] the od divisors.
+__global__ __launch_bounds__(256) void kreciprocal_kernel(DistSrc ds, const float* __restrict__ rowdiv,
+                                                          const int32_t* __restrict__ R, int64_t ldr, int64_t row0,
+                                                          int kf, int kh1, int32_t* __restrict__ vcol,
+                                                          uint16_t* __restrict__ vval, int32_t* __restrict__ vnnz,
+                                                          int32_t* __restrict__ flags) {
     __shared__ int32_t kr[64];
     __shared__ int32_t lst[2048];
     __shared__ float w[2048];
     __shared__ int s_nk, s_n, s_nu;
     __shared__ float s_sum;
-    const int64_t i = blockIdx.x;
+    const int64_t b = blockIdx.x;
+    const int64_t i = row0 + b;
     const int tid = threadIdx.x;
     // k-reciprocal set of i at depth k1 (reranking.py:53-56), kept in forward order
     if (tid < 64) {
@@ -191,12 +246,12 @@ __global__ __launch_bounds__(256) void kreciprocal_kernel(const float* __restric
             if (row_has(R, ldr, c, kh1, a)) cset[nc++] = c;
         }
         int inter = 0;
-        for (int b = 0; b < nc; b++)
+        for (int q = 0; q < nc; q++)
             for (int c = 0; c < nk; c++)
-                if (cset[b] == kr[c]) { inter++; break; }
+                if (cset[q] == kr[c]) { inter++; break; }
         if ((double)inter > 2.0 / 3.0 * (double)nc) {
             const int base = atomicAdd(&s_n, nc);
-            for (int b = 0; b < nc; b++) lst[base + b] = cset[b];
+            for (int q = 0; q < nc; q++) lst[base + q] = cset[q];
         }
     }
     __syncthreads();
@@ -215,44 +270,44 @@ __global__ __launch_bounds__(256) void kreciprocal_kernel(const float* __restric
     __syncthreads();
     const int nu = s_nu;
     const float dv = rowdiv[i];
-    for (int t = tid; t < nu; t += blockDim.x) w[t] = np_expf(-(OD[i * ld + lst[t]] / dv));
+    for (int t = tid; t < nu; t += blockDim.x) w[t] = np_expf(-(dist_at(ds, i, lst[t]) / dv));
     __syncthreads();
     if (tid == 0) s_sum = pairwise_f32(w, nu);
     __syncthreads();
     if (nu > VCAP) {
-        if (tid == 0) { atomicOr(flags, RR_VCAP); vnnz[i] = 0; }
+        if (tid == 0) { atomicOr(flags, RR_VCAP); vnnz[b] = 0; }
         return;
     }
     const float sum = s_sum;
     for (int t = tid; t < nu; t += blockDim.x) {
-        vcol[i * VCAP + t] = lst[t];
-        vval[i * VCAP + t] = f2h_bits(w[t] / sum);
+        vcol[b * VCAP + t] = lst[t];
+        vval[b * VCAP + t] = f2h_bits(w[t] / sum);
     }
-    if (tid == 0) vnnz[i] = nu;
+    if (tid == 0) vnnz[b] = nu;
 }
 
 // --------------------------------------------------------------------- R4: QE
-// V_qe[i] = fp16( (sum_{j<k2, in order} fp32(V[R[i][j]])) / k2 ) over the union of columns.
-// Entries of the k2 (column-sorted) rows are staged in LDS; the first occurrence of each
-// column owns it and sums that column over all k2 rows in j order (binary search).
-__global__ __launch_bounds__(256) void qe_kernel(const int32_t* __restrict__ R, int64_t ldr, int k2,
-                                                 const int32_t* __restrict__ vcol, const uint16_t* __restrict__ vval,
-                                                 const int32_t* __restrict__ vnnz, int32_t* __restrict__ qcol,
-                                                 uint16_t* __restrict__ qval, int32_t* __restrict__ qnnz,
-                                                 int32_t* __restrict__ flags) {
+// V_qe[i] = fp16( (sum_{j<k2, in order} fp32(V[R[i][j]])) / k2 ) over the union of columns,
+// i = row0 + blockIdx.x (output row blockIdx.x).  Entries of the k2 (column-sorted) rows
+// are staged in LDS; the first occurrence of each column owns it and sums that column over
+// all k2 rows in j order (binary search).
+__global__ __launch_bounds__(256) void qe_kernel(const int32_t* __restrict__ R, int64_t ldr, int k2, int64_t row0,
+                                                 Rows V, int32_t* __restrict__ qcol, uint16_t* __restrict__ qval,
+                                                 int32_t* __restrict__ qnnz, int32_t* __restrict__ flags) {
     __shared__ int32_t scol[LCAP];
     __shared__ uint16_t sval[LCAP];
     __shared__ int soff[33];
     __shared__ int32_t ocol[QCAP];
     __shared__ uint16_t oval[QCAP];
     __shared__ int s_no, s_bad;
-    const int64_t i = blockIdx.x;
+    const int64_t b = blockIdx.x;
+    const int64_t i = row0 + b;
     const int tid = threadIdx.x;
     if (tid == 0) {
         int o = 0;
         for (int j = 0; j < k2; j++) {
             soff[j] = o;
-            o += vnnz[R[i * ldr + j]];
+            o += V.len(R[i * ldr + j]);
         }
         soff[k2] = o;
         s_no = 0;
@@ -260,15 +315,16 @@ __global__ __launch_bounds__(256) void qe_kernel(const int32_t* __restrict__ R, 
     }
     __syncthreads();
     if (s_bad) {
-        if (tid == 0) { atomicOr(flags, RR_LCAP); qnnz[i] = 0; }
+        if (tid == 0) { atomicOr(flags, RR_LCAP); qnnz[b] = 0; }
         return;
     }
     for (int j = 0; j < k2; j++) {
         const int64_t r = R[i * ldr + j];
+        const int64_t rb = V.beg(r);
         const int n = soff[j + 1] - soff[j];
         for (int t = tid; t < n; t += blockDim.x) {
-            scol[soff[j] + t] = vcol[r * VCAP + t];
-            sval[soff[j] + t] = vval[r * VCAP + t];
+            scol[soff[j] + t] = V.col[rb + t];
+            sval[soff[j] + t] = V.val[rb + t];
         }
     }
     __syncthreads();
@@ -300,7 +356,7 @@ __global__ __launch_bounds__(256) void qe_kernel(const int32_t* __restrict__ R, 
     __syncthreads();
     const int no = s_no;
     if (no > QCAP) {
-        if (tid == 0) { atomicOr(flags, RR_QCAP); qnnz[i] = 0; }
+        if (tid == 0) { atomicOr(flags, RR_QCAP); qnnz[b] = 0; }
         return;
     }
     // sort (column, bits) pairs by column: reuse the int sort on packed keys
@@ -326,24 +382,24 @@ __global__ __launch_bounds__(256) void qe_kernel(const int32_t* __restrict__ R, 
         }
     for (int t = tid; t < no; t += blockDim.x) {
         const int32_t k = keys[t];
-        qcol[i * QCAP + t] = ocol[k];
-        qval[i * QCAP + t] = oval[k];
+        qcol[b * QCAP + t] = ocol[k];
+        qval[b * QCAP + t] = oval[k];
     }
-    if (tid == 0) qnnz[i] = no;
+    if (tid == 0) qnnz[b] = no;
 }
 
-// ------------------------------------------------------------------ R5: CSC
-__global__ void csc_count_kernel(const int32_t* __restrict__ qcol, const int32_t* __restrict__ qnnz, int64_t N,
-                                 int32_t* __restrict__ cnt) {
-    const int64_t r = blockIdx.x;
-    for (int t = threadIdx.x; t < qnnz[r]; t += blockDim.x) atomicAdd(&cnt[qcol[r * QCAP + t]], 1);
+// ---------------------------------------------------- ELL -> CSR, row lengths
+__global__ void rows_len_kernel(Rows V, int64_t n, int32_t* __restrict__ out) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < n) out[r] = V.len(r);
 }
 
 // exclusive scan of cnt[0..N) into off[0..N] (single workgroup, 1024 threads)
 __global__ __launch_bounds__(1024) void scan_kernel(const int32_t* __restrict__ cnt, int64_t N, int64_t* __restrict__ off) {
     __shared__ int64_t part[1024];
     const int64_t per = (N + 1023) / 1024;
-    const int64_t lo = threadIdx.x * per, hi = lo + per < N ? lo + per : N;
+    const int64_t lo = threadIdx.x * per < N ? threadIdx.x * per : N;
+    const int64_t hi = lo + per < N ? lo + per : N;
     int64_t s = 0;
     for (int64_t k = lo; k < hi; k++) s += cnt[k];
     part[threadIdx.x] = s;
@@ -358,48 +414,87 @@ __global__ __launch_bounds__(1024) void scan_kernel(const int32_t* __restrict__ 
     for (int64_t k = lo; k < hi; k++) { off[k] = acc; acc += cnt[k]; }
 }
 
-__global__ void csc_fill_kernel(const int32_t* __restrict__ qcol, const uint16_t* __restrict__ qval,
-                                const int32_t* __restrict__ qnnz, int64_t N, const int64_t* __restrict__ off,
-                                int32_t* __restrict__ cur, int32_t* __restrict__ irow, uint16_t* __restrict__ ival) {
+// copy rows of V into CSR storage at off[] (one workgroup per row)
+__global__ void rows_pack_kernel(Rows V, const int64_t* __restrict__ off, int32_t* __restrict__ col,
+                                 uint16_t* __restrict__ val) {
     const int64_t r = blockIdx.x;
-    for (int t = threadIdx.x; t < qnnz[r]; t += blockDim.x) {
-        const int32_t c = qcol[r * QCAP + t];
-        const int64_t p = off[c] + atomicAdd(&cur[c], 1);
-        irow[p] = (int32_t)r;
-        ival[p] = qval[r * QCAP + t];
+    const int64_t s = V.beg(r), d = off[r];
+    const int n = V.len(r);
+    for (int t = threadIdx.x; t < n; t += blockDim.x) {
+        col[d + t] = V.col[s + t];
+        val[d + t] = V.val[s + t];
     }
 }
 
+// ------------------------------------------------------------------ R5: CSC
+// invIndex[c] = rows r with V_qe[r, c] != 0 (reranking.py:80-82), rows ascending: the
+// row-major entry list is stably sorted by column (LSD radix sort is stable).
+__global__ void csc_count_kernel(Rows V, int64_t N, int32_t* __restrict__ cnt) {
+    const int64_t r = blockIdx.x;
+    const int64_t s = V.beg(r);
+    const int n = V.len(r);
+    for (int t = threadIdx.x; t < n; t += blockDim.x) atomicAdd(&cnt[V.col[s + t]], 1);
+}
+
+// keys = column, payload = (row << 16) | fp16 bits, in row-major entry order
+__global__ void csc_keys_kernel(Rows V, int32_t* __restrict__ keys, int64_t* __restrict__ pay, const int64_t* __restrict__ dst) {
+    const int64_t r = blockIdx.x;
+    const int64_t s = V.beg(r), d = dst ? dst[r] : s;
+    const int n = V.len(r);
+    for (int t = threadIdx.x; t < n; t += blockDim.x) {
+        keys[d + t] = V.col[s + t];
+        pay[d + t] = (r << 16) | (int64_t)V.val[s + t];
+    }
+}
+
+__global__ void csc_split_kernel(const int64_t* __restrict__ pay, int64_t n, int32_t* __restrict__ irow,
+                                 uint16_t* __restrict__ ival) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    const int64_t p = pay[e];
+    irow[e] = (int32_t)(p >> 16);
+    ival[e] = (uint16_t)(p & 0xffff);
+}
+
 // ----------------------------------------------------------- R6 + R7: Jaccard
-// One workgroup per (query i, chunk of gallery columns).  temp_min[r] (fp16 bits) lives in
-// LDS; the nonzero columns c of V_qe[i] are visited in ascending order and each column's
-// inverted list updates distinct rows, so one barrier per column keeps every temp_min[r]
-// a sequential fp16 sum in ascending c (reranking.py:90-92).  Epilogue: Jaccard in fp16
-// (reranking.py:93), blend with od in fp32 (reranking.py:95), write final[i][r-Q].
-__global__ __launch_bounds__(256) void jaccard_kernel(const float* __restrict__ OD, int64_t ld,
-                                                      const float* __restrict__ rowdiv, int64_t Q, int64_t N,
-                                                      const int32_t* __restrict__ qcol, const uint16_t* __restrict__ qval,
-                                                      const int32_t* __restrict__ qnnz, const int64_t* __restrict__ off,
+// One workgroup per (query i = q0 + blockIdx.y, chunk of gallery columns).  temp_min[r]
+// (fp16 bits) lives in LDS; the nonzero columns c of V_qe[i] are visited in ascending order
+// and each column's inverted list (rows ascending) updates distinct rows, so one barrier per
+// column keeps every temp_min[r] a sequential fp16 sum in ascending c (reranking.py:90-92);
+// the chunk's sub-range of each list is found by binary search.  Epilogue: Jaccard in fp16
+// (reranking.py:93), blend with od in fp32 (reranking.py:95), write final[blockIdx.y][r-Q].
+// od of (i, r) = OD[blockIdx.y * ld + (r - odc0)] / rowdiv[i].
+__global__ __launch_bounds__(256) void jaccard_kernel(const float* __restrict__ OD, int64_t ld, int64_t odc0,
+                                                      const float* __restrict__ rowdiv, int64_t q0, int64_t Q,
+                                                      int64_t N, Rows Vq, const int64_t* __restrict__ off,
                                                       const int32_t* __restrict__ irow, const uint16_t* __restrict__ ival,
                                                       uint16_t lam16, float lam_f, float* __restrict__ out, int64_t ldo) {
     __shared__ uint16_t tmin[JCH];
-    const int64_t i = blockIdx.y;
+    const int64_t y = blockIdx.y;
+    const int64_t i = q0 + y;
     const int64_t base = Q + (int64_t)blockIdx.x * JCH;
     const int64_t end = base + JCH < N ? base + JCH : N;
     const int span = (int)(end - base);
     for (int t = threadIdx.x; t < span; t += blockDim.x) tmin[t] = 0;
     __syncthreads();
-    const int nz = qnnz[i];
+    const int nz = Vq.len(i);
+    const int64_t qb = Vq.beg(i);
     for (int e = 0; e < nz; e++) {
-        const int32_t c = qcol[i * QCAP + e];
-        const float vi = h2f_bits(qval[i * QCAP + e]);
-        const int64_t p0 = off[c], p1 = off[c + 1];
+        const int32_t c = Vq.col[qb + e];
+        const float vi = h2f_bits(Vq.val[qb + e]);
+        int64_t p0 = off[c], p1 = off[c + 1];
+        {
+            int64_t lo = p0, hi = p1;
+            while (lo < hi) { const int64_t m = (lo + hi) >> 1; if (irow[m] < base) lo = m + 1; else hi = m; }
+            p0 = lo;
+            hi = p1;
+            while (lo < hi) { const int64_t m = (lo + hi) >> 1; if (irow[m] < end) lo = m + 1; else hi = m; }
+            p1 = lo;
+        }
         for (int64_t p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
-            const int64_t r = irow[p];
-            if (r < base || r >= end) continue;
+            const int k = (int)(irow[p] - base);
             const float vr = h2f_bits(ival[p]);
             const float mn = vr < vi ? vr : vi;
-            const int k = (int)(r - base);
             tmin[k] = f2h_bits(h2f_bits(tmin[k]) + mn);
         }
         __syncthreads();
@@ -413,8 +508,8 @@ __global__ __launch_bounds__(256) void jaccard_kernel(const float* __restrict__ 
         const uint16_t qt = f2h_bits(tv / h2f_bits(den));
         const uint16_t jac = f2h_bits(1.0f - h2f_bits(qt));
         const float a = h2f_bits(f2h_bits(h2f_bits(jac) * lam));
-        const float b = (OD[i * ld + r] / dv) * lam_f;
-        out[i * ldo + (r - Q)] = a + b;
+        const float b = (OD[y * ld + (r - odc0)] / dv) * lam_f;
+        out[y * ldo + (r - Q)] = a + b;
     }
 }
 
@@ -451,54 +546,116 @@ static RrPlan rr_plan(int64_t N, int k1, int k2, bool need_dist, bool need_t) {
     return p;
 }
 
+static void kr_depths(int k1, int64_t N, int& kf, int& kh1) {
+    kf = (int)(k1 + 1 < N ? k1 + 1 : N);
+    const int kh = (int)__builtin_nearbyint((double)k1 / 2.0);  // int(np.around(k1/2))
+    kh1 = (int)(kh + 1 < N ? kh + 1 : N);
+}
+
+// Unsorted inverted index by atomic fill (the one-call paths: sizes unknown on the host).
+__global__ void csc_fill_kernel(Rows V, int64_t N, const int64_t* __restrict__ off, int32_t* __restrict__ cur,
+                                int32_t* __restrict__ irow, uint16_t* __restrict__ ival) {
+    const int64_t r = blockIdx.x;
+    const int64_t s = V.beg(r);
+    const int n = V.len(r);
+    for (int t = threadIdx.x; t < n; t += blockDim.x) {
+        const int32_t c = V.col[s + t];
+        const int64_t p = off[c] + atomicAdd(&cur[c], 1);
+        irow[p] = (int32_t)r;
+        ival[p] = V.val[s + t];
+    }
+}
+
+// Jaccard over unsorted inverted lists: every chunk scans whole lists and filters rows.
+__global__ __launch_bounds__(256) void jaccard_scan_kernel(const float* __restrict__ OD, int64_t ld,
+                                                           const float* __restrict__ rowdiv, int64_t Q, int64_t N,
+                                                           Rows Vq, const int64_t* __restrict__ off,
+                                                           const int32_t* __restrict__ irow,
+                                                           const uint16_t* __restrict__ ival, uint16_t lam16,
+                                                           float lam_f, float* __restrict__ out, int64_t ldo) {
+    __shared__ uint16_t tmin[JCH];
+    const int64_t i = blockIdx.y;
+    const int64_t base = Q + (int64_t)blockIdx.x * JCH;
+    const int64_t end = base + JCH < N ? base + JCH : N;
+    const int span = (int)(end - base);
+    for (int t = threadIdx.x; t < span; t += blockDim.x) tmin[t] = 0;
+    __syncthreads();
+    const int nz = Vq.len(i);
+    const int64_t qb = Vq.beg(i);
+    for (int e = 0; e < nz; e++) {
+        const int32_t c = Vq.col[qb + e];
+        const float vi = h2f_bits(Vq.val[qb + e]);
+        const int64_t p0 = off[c], p1 = off[c + 1];
+        for (int64_t p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
+            const int64_t r = irow[p];
+            if (r < base || r >= end) continue;
+            const float vr = h2f_bits(ival[p]);
+            const float mn = vr < vi ? vr : vi;
+            const int k = (int)(r - base);
+            tmin[k] = f2h_bits(h2f_bits(tmin[k]) + mn);
+        }
+        __syncthreads();
+    }
+    const float lam = h2f_bits(lam16);
+    const float dv = rowdiv[i];
+    for (int t = threadIdx.x; t < span; t += blockDim.x) {
+        const int64_t r = base + t;
+        const float tv = h2f_bits(tmin[t]);
+        const uint16_t den = f2h_bits(2.0f - tv);
+        const uint16_t qt = f2h_bits(tv / h2f_bits(den));
+        const uint16_t jac = f2h_bits(1.0f - h2f_bits(qt));
+        const float a = h2f_bits(f2h_bits(h2f_bits(jac) * lam));
+        const float b = (OD[i * ld + r] / dv) * lam_f;
+        out[i * ldo + (r - Q)] = a + b;
+    }
+}
+
 // od rows: OD (N x N, row i = distances from item i, scaled by 1/rowdiv[i] on the fly).
 static int rerank_core(const float* OD, int64_t N, int64_t Q, int k1, int k2, uint16_t lam16, float lam_f,
                        float* out, int64_t ldo, char* ws, const RrPlan& P, int32_t* flags, hipStream_t s) {
     float* rmax = (float*)(ws + P.rowmax);
     int32_t* R = (int32_t*)(ws + P.rank);
-    hipLaunchKernelGGL(rowmax_kernel, dim3(ceil_div(N, 4)), dim3(256), 0, s, OD, N, N, rmax);
+    hipLaunchKernelGGL(rowmax_kernel, dim3(ceil_div(N, 4)), dim3(256), 0, s, OD, N, N, N, rmax);
     RM_LAUNCHED();
     int rc;
     if ((rc = topk_launch(OD, N, N, N, rmax, P.K, R, nullptr, P.K, s))) return rc;
-    const int kf = (int)(k1 + 1 < N ? k1 + 1 : N);
-    const int kh = (int)__builtin_nearbyint((double)k1 / 2.0);
-    const int kh1 = (int)(kh + 1 < N ? kh + 1 : N);
+    int kf, kh1;
+    kr_depths(k1, N, kf, kh1);
     RM_REQUIRE(k1 >= 1 && k1 <= 50, "rerank: 1 <= k1 <= 50 (expansion list capacity)");
     int32_t* vcol = (int32_t*)(ws + P.vcol);
     uint16_t* vval = (uint16_t*)(ws + P.vval);
     int32_t* vnnz = (int32_t*)(ws + P.vnnz);
-    hipLaunchKernelGGL(kreciprocal_kernel, dim3((unsigned)N), dim3(256), 0, s, OD, N, rmax, R, (int64_t)P.K, N, kf,
-                       kh1, vcol, vval, vnnz, flags);
+    const DistSrc ds{OD, N, 0, nullptr, 0, 0, nullptr};
+    hipLaunchKernelGGL(kreciprocal_kernel, dim3((unsigned)N), dim3(256), 0, s, ds, rmax, R, (int64_t)P.K, (int64_t)0,
+                       kf, kh1, vcol, vval, vnnz, flags);
     RM_LAUNCHED();
-    int32_t* qcol = (int32_t*)(ws + P.qcol);
-    uint16_t* qval = (uint16_t*)(ws + P.qval);
-    int32_t* qnnz = (int32_t*)(ws + P.qnnz);
+    Rows Vq{nullptr, vnnz, VCAP, vcol, vval};
     if (k2 != 1) {
         RM_REQUIRE(k2 <= 32 && k2 <= P.K, "rerank: k2 must be <= 32");
-        hipLaunchKernelGGL(qe_kernel, dim3((unsigned)N), dim3(256), 0, s, R, (int64_t)P.K, k2, vcol, vval, vnnz, qcol,
-                           qval, qnnz, flags);
+        int32_t* qcol = (int32_t*)(ws + P.qcol);
+        uint16_t* qval = (uint16_t*)(ws + P.qval);
+        int32_t* qnnz = (int32_t*)(ws + P.qnnz);
+        hipLaunchKernelGGL(qe_kernel, dim3((unsigned)N), dim3(256), 0, s, R, (int64_t)P.K, k2, (int64_t)0,
+                           Rows{nullptr, vnnz, VCAP, vcol, vval}, qcol, qval, qnnz, flags);
         RM_LAUNCHED();
-    } else {
-        RM_CHECK_HIP(hipMemcpy2DAsync(qcol, QCAP * 4, vcol, VCAP * 4, VCAP * 4, N, hipMemcpyDeviceToDevice, s));
-        RM_CHECK_HIP(hipMemcpy2DAsync(qval, QCAP * 2, vval, VCAP * 2, VCAP * 2, N, hipMemcpyDeviceToDevice, s));
-        RM_CHECK_HIP(hipMemcpyAsync(qnnz, vnnz, N * 4, hipMemcpyDeviceToDevice, s));
+        Vq = Rows{nullptr, qnnz, QCAP, qcol, qval};
     }
     int32_t* cnt = (int32_t*)(ws + P.cnt);
     int64_t* off = (int64_t*)(ws + P.off);
     int32_t* cur = (int32_t*)(ws + P.cur);
     RM_CHECK_HIP(hipMemsetAsync(cnt, 0, N * 4, s));
     RM_CHECK_HIP(hipMemsetAsync(cur, 0, N * 4, s));
-    hipLaunchKernelGGL(csc_count_kernel, dim3((unsigned)N), dim3(256), 0, s, qcol, qnnz, N, cnt);
+    hipLaunchKernelGGL(csc_count_kernel, dim3((unsigned)N), dim3(256), 0, s, Vq, N, cnt);
     RM_LAUNCHED();
     hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, s, cnt, N, off);
     RM_LAUNCHED();
-    hipLaunchKernelGGL(csc_fill_kernel, dim3((unsigned)N), dim3(256), 0, s, qcol, qval, qnnz, N, off, cur,
+    hipLaunchKernelGGL(csc_fill_kernel, dim3((unsigned)N), dim3(256), 0, s, Vq, N, off, cur,
                        (int32_t*)(ws + P.irow), (uint16_t*)(ws + P.ival));
     RM_LAUNCHED();
     const int64_t G = N - Q;
     if (Q > 0 && G > 0) {
         dim3 grid(ceil_div(G, JCH), (unsigned)Q);
-        hipLaunchKernelGGL(jaccard_kernel, grid, dim3(256), 0, s, OD, N, rmax, Q, N, qcol, qval, qnnz, off,
+        hipLaunchKernelGGL(jaccard_scan_kernel, grid, dim3(256), 0, s, OD, N, rmax, Q, N, Vq, off,
                            (const int32_t*)(ws + P.irow), (const uint16_t*)(ws + P.ival), lam16, lam_f, out, ldo);
         RM_LAUNCHED();
     }
@@ -552,4 +709,162 @@ REIDMI_API int reidmi_rerank_from_dist(const float* dist, const float* add, int6
         OD = T;
     }
     return rerank_core(OD, N, Q, k1, k2, one_minus_lambda_h, lambda_f, final_dist, ldo, ws, P, flags, s);
+}
+
+// ------------------------------------------------------------ staged re-ranking
+// The same R1-R7 as row-range stages over caller-allocated, exactly sized buffers, so the
+// N x N distance is never materialised (row chunks of it are) and the rows can be sharded
+// over ranks with all-gathers between stages (multimodal_reid_amd/reranking.py).
+REIDMI_API int reidmi_rr_caps(int* vcap, int* qcap) {
+    RM_REQUIRE(vcap && qcap, "rr_caps: null");
+    *vcap = VCAP;
+    *qcap = QCAP;
+    return OK;
+}
+
+REIDMI_API int reidmi_rr_rank_rows(const float* feat, int64_t N, int64_t D, int64_t ldf, const float* sqn, int64_t lo,
+                                   int64_t hi, int K, int32_t* rank_out, float* rowmax_out, float* chunk,
+                                   int64_t chunk_rows, void* stream) {
+    RM_REQUIRE(N > 0 && D > 0 && ldf >= D && 0 <= lo && lo <= hi && hi <= N && chunk_rows > 0 && K >= 1 && K <= N,
+               "rr_rank_rows: bad arguments");
+    RM_REQUIRE(N < 0x7fffffff, "rr_rank_rows: too many items");
+    hipStream_t s = (hipStream_t)stream;
+    int rc;
+    for (int64_t a = lo; a < hi; a += chunk_rows) {
+        const int64_t nb = hi - a < chunk_rows ? hi - a : chunk_rows;
+        if ((rc = distmat_pre_launch(feat + a * ldf, nb, ldf, feat, N, ldf, D, sqn + a, sqn, chunk, N, s))) return rc;
+        hipLaunchKernelGGL(rowmax_kernel, dim3(ceil_div(nb, 4)), dim3(256), 0, s, chunk, nb, N, N, rowmax_out + (a - lo));
+        RM_LAUNCHED();
+        if ((rc = topk_launch(chunk, nb, N, N, rowmax_out + (a - lo), K, rank_out + (a - lo) * K, nullptr, K, s)))
+            return rc;
+    }
+    return OK;
+}
+
+REIDMI_API int reidmi_rr_v_rows(const float* feat, int64_t N, int64_t D, int64_t ldf, const float* sqn,
+                                const float* rowmax, const int32_t* rank, int K, int64_t lo, int64_t hi, int k1,
+                                int32_t* vcol, uint16_t* vval, int32_t* vnnz, int32_t* flags, void* stream) {
+    RM_REQUIRE(N > 0 && D > 0 && ldf >= D && 0 <= lo && lo <= hi && hi <= N && flags, "rr_v_rows: bad arguments");
+    RM_REQUIRE(k1 >= 1 && k1 <= 50 && K >= (k1 + 1 < N ? k1 + 1 : N), "rr_v_rows: 1 <= k1 <= 50, K >= k1+1");
+    if (hi == lo) return OK;
+    int kf, kh1;
+    kr_depths(k1, N, kf, kh1);
+    const DistSrc ds{nullptr, 0, 0, feat, ldf, (int)D, sqn};
+    hipLaunchKernelGGL(kreciprocal_kernel, dim3((unsigned)(hi - lo)), dim3(256), 0, (hipStream_t)stream, ds, rowmax,
+                       rank, (int64_t)K, lo, kf, kh1, vcol, vval, vnnz, flags);
+    RM_LAUNCHED();
+    return OK;
+}
+
+REIDMI_API int reidmi_rr_row_offsets(const int32_t* nnz, int64_t rows, int64_t* off, void* stream) {
+    RM_REQUIRE(rows >= 0 && off, "rr_row_offsets: bad arguments");
+    hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, nnz, rows, off);
+    RM_LAUNCHED();
+    return OK;
+}
+
+REIDMI_API int reidmi_rr_pack(const int32_t* ell_col, const uint16_t* ell_val, const int32_t* nnz, int64_t rows,
+                              int64_t cap, const int64_t* off, int32_t* col, uint16_t* val, void* stream) {
+    RM_REQUIRE(rows >= 0 && cap > 0, "rr_pack: bad arguments");
+    if (rows == 0) return OK;
+    hipLaunchKernelGGL(rows_pack_kernel, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream,
+                       Rows{nullptr, nnz, cap, ell_col, ell_val}, off, col, val);
+    RM_LAUNCHED();
+    return OK;
+}
+
+REIDMI_API int reidmi_rr_qe_rows(const int32_t* rank, int K, int k2, int64_t lo, int64_t hi, const int64_t* voff,
+                                 const int32_t* vcol, const uint16_t* vval, int32_t* qcol, uint16_t* qval,
+                                 int32_t* qnnz, int32_t* flags, void* stream) {
+    RM_REQUIRE(0 <= lo && lo <= hi && flags && voff, "rr_qe_rows: bad arguments");
+    RM_REQUIRE(k2 >= 2 && k2 <= 32 && k2 <= K, "rr_qe_rows: 2 <= k2 <= min(32, K) (k2 = 1 means V_qe = V)");
+    if (hi == lo) return OK;
+    hipLaunchKernelGGL(qe_kernel, dim3((unsigned)(hi - lo)), dim3(256), 0, (hipStream_t)stream, rank, (int64_t)K, k2,
+                       lo, Rows{voff, nullptr, 0, vcol, vval}, qcol, qval, qnnz, flags);
+    RM_LAUNCHED();
+    return OK;
+}
+
+namespace reidmi {
+struct CscPlan {
+    int64_t cnt, k0, k1, p0, p1, tmp, tmp_bytes, total;
+};
+static CscPlan csc_plan(int64_t N, int64_t nnz) {
+    CscPlan p{};
+    int64_t o = 0;
+    p.cnt = o; o = al(o + N * 4);
+    p.k0 = o; o = al(o + nnz * 4);
+    p.k1 = o; o = al(o + nnz * 4);
+    p.p0 = o; o = al(o + nnz * 8);
+    p.p1 = o; o = al(o + nnz * 8);
+    size_t tb = 0;
+    hipcub::DoubleBuffer<int32_t> kb(nullptr, nullptr);
+    hipcub::DoubleBuffer<int64_t> pb(nullptr, nullptr);
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kb, pb, (int)(nnz > 0 ? nnz : 1), 0, 32, (hipStream_t)0);
+    p.tmp = o;
+    p.tmp_bytes = (int64_t)tb;
+    o = al(o + (int64_t)tb);
+    p.total = o;
+    return p;
+}
+}  // namespace reidmi
+
+REIDMI_API int64_t reidmi_rr_csc_workspace_bytes(int64_t N, int64_t nnz) { return csc_plan(N, nnz).total; }
+
+REIDMI_API int reidmi_rr_csc(int64_t N, const int64_t* qoff, const int32_t* qcol, const uint16_t* qval, int64_t nnz,
+                             int64_t* coff, int32_t* irow, uint16_t* ival, void* ws_, int64_t ws_bytes, void* stream) {
+    RM_REQUIRE(N > 0 && nnz >= 0 && nnz < 0x7fffffff && qoff && coff, "rr_csc: bad arguments");
+    const CscPlan P = csc_plan(N, nnz);
+    RM_REQUIRE(ws_bytes >= P.total, "rr_csc: workspace too small");
+    hipStream_t s = (hipStream_t)stream;
+    char* ws = (char*)ws_;
+    const Rows V{qoff, nullptr, 0, qcol, qval};
+    int32_t* cnt = (int32_t*)(ws + P.cnt);
+    RM_CHECK_HIP(hipMemsetAsync(cnt, 0, N * 4, s));
+    hipLaunchKernelGGL(csc_count_kernel, dim3((unsigned)N), dim3(256), 0, s, V, N, cnt);
+    RM_LAUNCHED();
+    hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, s, cnt, N, coff);
+    RM_LAUNCHED();
+    if (nnz == 0) return OK;
+    int32_t* k0 = (int32_t*)(ws + P.k0);
+    int64_t* p0 = (int64_t*)(ws + P.p0);
+    hipLaunchKernelGGL(csc_keys_kernel, dim3((unsigned)N), dim3(256), 0, s, V, k0, p0, (const int64_t*)nullptr);
+    RM_LAUNCHED();
+    int bits = 1;
+    while (bits < 32 && ((int64_t)1 << bits) < N) bits++;
+    hipcub::DoubleBuffer<int32_t> kb(k0, (int32_t*)(ws + P.k1));
+    hipcub::DoubleBuffer<int64_t> pb(p0, (int64_t*)(ws + P.p1));
+    size_t tb = (size_t)P.tmp_bytes;
+    RM_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(ws + P.tmp, tb, kb, pb, (int)nnz, 0, bits, s));
+    hipLaunchKernelGGL(csc_split_kernel, dim3(ceil_div(nnz, 256)), dim3(256), 0, s, (const int64_t*)pb.Current(), nnz,
+                       irow, ival);
+    RM_LAUNCHED();
+    return OK;
+}
+
+REIDMI_API int reidmi_rr_jaccard_rows(const float* feat, int64_t N, int64_t D, int64_t ldf, const float* sqn,
+                                      const float* rowmax, int64_t Q, int64_t qlo, int64_t qhi, const int64_t* qoff,
+                                      const int32_t* qcol, const uint16_t* qval, const int64_t* coff,
+                                      const int32_t* irow, const uint16_t* ival, uint16_t one_minus_lambda_h,
+                                      float lambda_f, float* out, int64_t ldo, float* chunk, int64_t chunk_rows,
+                                      void* stream) {
+    const int64_t G = N - Q;
+    RM_REQUIRE(N > 0 && D > 0 && ldf >= D && 0 <= qlo && qlo <= qhi && qhi <= Q && Q <= N && ldo >= G &&
+                   chunk_rows > 0 && chunk_rows <= 65535,
+               "rr_jaccard_rows: bad arguments");
+    if (qhi == qlo || G == 0) return OK;
+    hipStream_t s = (hipStream_t)stream;
+    const Rows Vq{qoff, nullptr, 0, qcol, qval};
+    int rc;
+    for (int64_t a = qlo; a < qhi; a += chunk_rows) {
+        const int64_t nb = qhi - a < chunk_rows ? qhi - a : chunk_rows;
+        // original_dist[a:a+nb, Q:N] (chunk, ld G)
+        if ((rc = distmat_pre_launch(feat + a * ldf, nb, ldf, feat + Q * ldf, G, ldf, D, sqn + a, sqn + Q, chunk, G, s)))
+            return rc;
+        dim3 grid(ceil_div(G, JCH), (unsigned)nb);
+        hipLaunchKernelGGL(jaccard_kernel, grid, dim3(256), 0, s, (const float*)chunk, G, Q, rowmax, a, Q, N, Vq, coff,
+                           irow, ival, one_minus_lambda_h, lambda_f, out + (a - qlo) * ldo, ldo);
+        RM_LAUNCHED();
+    }
+    return OK;
 }

@@ -10,8 +10,10 @@ step this path needs:
   4. all-gather of the per-query results (valid, first-match rank, AP, n_kept: 32 B/query),
      then every rank reduces them in global query order with numpy's own arithmetic, so the
      CMC/mAP are bit-identical for any world size.
-Re-ranking needs every row of the N x N neighbourhood structure; it runs replicated after
-an all-gather of query and gallery features (the rerank stage itself is not sharded yet).
+Re-ranking (reranking.re_ranking_sharded) shards its rows too: rank r owns rows
+shard(N, r, W) of the N = Q + G items for R1-R4 and queries shard(Q, r, W) for R6-R7, with
+all-gathers of initial_rank[:, :K], the od divisors, and the CSR rows of V and V_qe between
+the stages.
 """
 import numpy as np
 import torch
@@ -37,17 +39,44 @@ def gather_rows(x, n_total):
         return x
     sizes = [shard(n_total, r, W)[1] - shard(n_total, r, W)[0] for r in range(W)]
     mx = max(sizes)
-    pad = torch.zeros((mx,) + tuple(x.shape[1:]), device=x.device, dtype=x.dtype)
-    pad[:x.shape[0]] = x
+    dev = _collective_device(x)
+    pad = torch.zeros((mx,) + tuple(x.shape[1:]), device=dev, dtype=x.dtype)
+    pad[:x.shape[0]] = x.to(dev)
     if dist.get_backend() == "nccl":
-        out = torch.empty((W * mx,) + tuple(x.shape[1:]), device=x.device, dtype=x.dtype)
+        out = torch.empty((W * mx,) + tuple(x.shape[1:]), device=dev, dtype=x.dtype)
         dist.all_gather_into_tensor(out, pad)
         parts = [out[r * mx:r * mx + sizes[r]] for r in range(W)]
     else:
         bufs = [torch.empty_like(pad) for _ in range(W)]
         dist.all_gather(bufs, pad)
         parts = [bufs[r][:sizes[r]] for r in range(W)]
-    return torch.cat(parts)
+    return torch.cat(parts).to(x.device)
+
+
+def _collective_device(x):
+    """gloo moves host tensors: device tensors are staged through the host for it."""
+    return x.device if dist.get_backend() == "nccl" else torch.device("cpu")
+
+
+def gather_var(x):
+    """All-gather 1-D pieces of different lengths; returns their concatenation in rank order
+    (same device as x).  Used for the CSR payloads of the sharded re-ranking."""
+    rank, W = world()
+    if W == 1:
+        return x
+    dev = _collective_device(x)
+    dtype = x.dtype
+    x = x.contiguous().view(torch.uint8)  # moved as bytes (gloo has no int16)
+    n = torch.tensor([x.numel()], dtype=torch.int64, device=dev)
+    ns = [torch.empty_like(n) for _ in range(W)]
+    dist.all_gather(ns, n)
+    ns = [int(v.item()) for v in ns]
+    mx = max(max(ns), 1)
+    pad = torch.zeros(mx, dtype=x.dtype, device=dev)
+    pad[:x.numel()] = x.to(dev)
+    bufs = [torch.empty_like(pad) for _ in range(W)]
+    dist.all_gather(bufs, pad)
+    return torch.cat([bufs[r][:ns[r]] for r in range(W)]).to(x.device).view(dtype)
 
 
 def pack_rows(valid, first, ap, nkept):

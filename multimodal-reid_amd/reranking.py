@@ -9,6 +9,8 @@ numpy arithmetic bit for bit (float32 exp/pairwise sums, float16 V / Jaccard), w
 the initial ranking ordered by index (np.argsort(kind="stable")).  The reference's dense
 N x N float16 V / V_qe become sparse row lists, so MSMT17-size galleries fit.
 """
+import ctypes
+
 import numpy as np
 import torch
 
@@ -63,3 +65,145 @@ def re_ranking_device(probFea, galFea, k1, k2, lambda_value, local_distmat=None,
 def re_ranking(probFea, galFea, k1, k2, lambda_value, local_distmat=None, only_local=False):
     """reranking.py:29-100 — returns the re-ranked (Q, G) distance as np.float32."""
     return re_ranking_device(probFea, galFea, k1, k2, lambda_value, local_distmat, only_local).cpu().numpy()
+
+
+# ------------------------------------------------------------------ staged / sharded
+# R1-R7 as row-range stages (reidmi_rr_*): the N x N distance is never materialised (row
+# chunks of it are), intermediate rows are exactly sized CSR, and every stage takes a row
+# range so the work shards over ranks (SURVEY.md §8e).  Bit-identical to re_ranking_device.
+
+class HipStages:
+    """The product's stage kernels (libreidmi)."""
+
+    def __init__(self, feat, num_query, k1, k2, lambda_value, chunk_bytes=2 << 30):
+        _lib.require_cuda(feat)
+        self.feat = _as_dev_f32(feat).contiguous()
+        self.N, self.D = self.feat.shape
+        self.Q = num_query
+        self.k1, self.k2 = k1, k2
+        self.K = min(max(k1 + 1, k2), self.N)
+        self.lam_h, self.lam_f = _lam(lambda_value)
+        self.dev = self.feat.device
+        self.st = _lib.stream()
+        self.sqn = torch.empty(self.N, device=self.dev, dtype=torch.float32)
+        _lib.call("reidmi_row_sqnorm_f32", _lib.ptr(self.feat), self.N, self.D, self.D, _lib.ptr(self.sqn), self.st)
+        self.chunk_rows = int(max(1, min(65535, chunk_bytes // (4 * self.N))))
+        self._chunk = None
+        self.flags = torch.zeros(1, device=self.dev, dtype=torch.int32)
+        vc, qc = ctypes.c_int(), ctypes.c_int()
+        _lib.call("reidmi_rr_caps", ctypes.byref(vc), ctypes.byref(qc))
+        self.vcap, self.qcap = vc.value, qc.value
+
+    def _chunk_buf(self, rows, cols):
+        n = rows * cols
+        if self._chunk is None or self._chunk.numel() < n:
+            self._chunk = torch.empty(n, device=self.dev, dtype=torch.float32)
+        return self._chunk
+
+    def rank_rows(self, lo, hi):
+        R = torch.empty((hi - lo, self.K), device=self.dev, dtype=torch.int32)
+        rmax = torch.empty(hi - lo, device=self.dev, dtype=torch.float32)
+        if hi > lo:
+            cr = min(self.chunk_rows, hi - lo)
+            _lib.call("reidmi_rr_rank_rows", _lib.ptr(self.feat), self.N, self.D, self.D, _lib.ptr(self.sqn), lo, hi,
+                      self.K, _lib.ptr(R), _lib.ptr(rmax), _lib.ptr(self._chunk_buf(cr, self.N)), cr, self.st)
+        return R, rmax
+
+    def offsets(self, nnz):
+        off = torch.empty(nnz.numel() + 1, device=self.dev, dtype=torch.int64)
+        _lib.call("reidmi_rr_row_offsets", _lib.ptr(nnz), nnz.numel(), _lib.ptr(off), self.st)
+        return off
+
+    def _pack(self, ecol, eval_, nnz, cap):
+        off = self.offsets(nnz)
+        total = int(off[-1].item())
+        col = torch.empty(max(total, 1), device=self.dev, dtype=torch.int32)
+        val = torch.empty(max(total, 1), device=self.dev, dtype=torch.int16)
+        _lib.call("reidmi_rr_pack", _lib.ptr(ecol), _lib.ptr(eval_), _lib.ptr(nnz), nnz.numel(), cap, _lib.ptr(off),
+                  _lib.ptr(col), _lib.ptr(val), self.st)
+        return nnz, col[:total], val[:total]
+
+    def v_rows(self, R, rmax, lo, hi):
+        n = hi - lo
+        ecol = torch.empty((max(n, 1), self.vcap), device=self.dev, dtype=torch.int32)
+        evl = torch.empty((max(n, 1), self.vcap), device=self.dev, dtype=torch.int16)
+        nnz = torch.zeros(n, device=self.dev, dtype=torch.int32)
+        _lib.call("reidmi_rr_v_rows", _lib.ptr(self.feat), self.N, self.D, self.D, _lib.ptr(self.sqn), _lib.ptr(rmax),
+                  _lib.ptr(R), self.K, lo, hi, self.k1, _lib.ptr(ecol), _lib.ptr(evl), _lib.ptr(nnz),
+                  _lib.ptr(self.flags), self.st)
+        return self._pack(ecol, evl, nnz, self.vcap)
+
+    def qe_rows(self, R, V, lo, hi):
+        off, col, val = V
+        n = hi - lo
+        ecol = torch.empty((max(n, 1), self.qcap), device=self.dev, dtype=torch.int32)
+        evl = torch.empty((max(n, 1), self.qcap), device=self.dev, dtype=torch.int16)
+        nnz = torch.zeros(n, device=self.dev, dtype=torch.int32)
+        _lib.call("reidmi_rr_qe_rows", _lib.ptr(R), self.K, self.k2, lo, hi, _lib.ptr(off), _lib.ptr(col),
+                  _lib.ptr(val), _lib.ptr(ecol), _lib.ptr(evl), _lib.ptr(nnz), _lib.ptr(self.flags), self.st)
+        return self._pack(ecol, evl, nnz, self.qcap)
+
+    def jaccard_rows(self, rmax, Vq, qlo, qhi):
+        off, col, val = Vq
+        N, Q = self.N, self.Q
+        G = N - Q
+        nnz = int(off[-1].item())
+        L = _lib.load()
+        wsb = L.reidmi_rr_csc_workspace_bytes(N, nnz)
+        ws = torch.empty(max(wsb, 1), device=self.dev, dtype=torch.uint8)
+        coff = torch.empty(N + 1, device=self.dev, dtype=torch.int64)
+        irow = torch.empty(max(nnz, 1), device=self.dev, dtype=torch.int32)
+        ival = torch.empty(max(nnz, 1), device=self.dev, dtype=torch.int16)
+        _lib.call("reidmi_rr_csc", N, _lib.ptr(off), _lib.ptr(col), _lib.ptr(val), nnz, _lib.ptr(coff), _lib.ptr(irow),
+                  _lib.ptr(ival), _lib.ptr(ws), wsb, self.st)
+        del ws
+        out = torch.empty((qhi - qlo, G), device=self.dev, dtype=torch.float32)
+        if qhi > qlo and G > 0:
+            cr = int(max(1, min(65535, qhi - qlo, self.chunk_rows * N // max(G, 1))))
+            _lib.call("reidmi_rr_jaccard_rows", _lib.ptr(self.feat), N, self.D, self.D, _lib.ptr(self.sqn),
+                      _lib.ptr(rmax), Q, qlo, qhi, _lib.ptr(off), _lib.ptr(col), _lib.ptr(val), _lib.ptr(coff),
+                      _lib.ptr(irow), _lib.ptr(ival), self.lam_h, self.lam_f, _lib.ptr(out), G,
+                      _lib.ptr(self._chunk_buf(cr, G)), cr, self.st)
+        return out
+
+    def check(self):
+        _check(self.flags)
+
+
+def _gather_csr(stages, nnz_loc, col_loc, val_loc, N):
+    from . import distributed as rd
+    nnz = rd.gather_rows(nnz_loc, N)
+    col = rd.gather_var(col_loc)
+    val = rd.gather_var(val_loc)
+    return stages.offsets(nnz), col, val
+
+
+def staged_rerank(stages, N, Q):
+    """R1-R7 over this rank's rows (torch.distributed world; world 1 = the whole job).
+    Returns this rank's rows shard(Q, rank, W) of the final (Q, G) distance."""
+    from . import distributed as rd
+    rank, W = rd.world()
+    lo, hi = rd.shard(N, rank, W)
+    R_loc, rmax_loc = stages.rank_rows(lo, hi)                    # R1 + R2 (reranking.py:36-48)
+    R = rd.gather_rows(R_loc, N)
+    rmax = rd.gather_rows(rmax_loc, N)
+    V = _gather_csr(stages, *stages.v_rows(R, rmax, lo, hi), N)  # R3 (reranking.py:51-71)
+    if stages.k2 != 1:
+        Vq = _gather_csr(stages, *stages.qe_rows(R, V, lo, hi), N)  # R4 (reranking.py:73-78)
+    else:
+        Vq = V
+    qlo, qhi = rd.shard(Q, rank, W)
+    out = stages.jaccard_rows(rmax, Vq, qlo, qhi)                 # R5-R7 (reranking.py:80-100)
+    stages.check()
+    return out
+
+
+def re_ranking_sharded(probFea, galFea, k1, k2, lambda_value, chunk_bytes=2 << 30):
+    """Sharded re_ranking: probFea / galFea are the FULL query and gallery features on this
+    rank's GPU (all-gathered after a sharded embed).  Returns this rank's query rows
+    shard(Q, rank, W) of the re-ranked (Q, G) distance as a device tensor; with one process
+    it equals re_ranking_device bit for bit, without the N x N buffers."""
+    Q = probFea.size(0)
+    feat = torch.cat([_as_dev_f32(probFea), _as_dev_f32(galFea)]).contiguous()
+    stages = HipStages(feat, Q, k1, k2, lambda_value, chunk_bytes)
+    return staged_rerank(stages, feat.shape[0], Q)

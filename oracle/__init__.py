@@ -37,7 +37,8 @@ def lib():
     global _LIB
     if _LIB is None:
         path = os.path.join(HERE, "build", "liboracle.so")
-        if not os.path.exists(path):
+        src = os.path.join(HERE, "reid_oracle.c")
+        if not os.path.exists(path) or os.path.getmtime(path) < os.path.getmtime(src):
             build()
         L = ctypes.CDLL(path)
         L.orc_l2norm.argtypes = [_f32p, _f32p, _i64, _i64]
@@ -47,6 +48,11 @@ def lib():
         L.orc_rerank_from_dist.argtypes = [_f32p, _i64, _i64, ctypes.c_int, ctypes.c_int, ctypes.c_uint16,
                                            ctypes.c_float, _f32p, ctypes.c_void_p, ctypes.c_void_p,
                                            ctypes.c_void_p]
+        L.orc_rr_rank_rows.argtypes = [_f32p, _i64, _i64, _i64, _i32p, _f32p]
+        L.orc_rr_v_rows.argtypes = [_f32p, _f32p, _i32p, _i64, _i64, _i64, _i64, ctypes.c_int, _u16p]
+        L.orc_rr_qe_rows.argtypes = [_i32p, _i64, ctypes.c_int, _i64, _i64, _u16p, _i64, _u16p]
+        L.orc_rr_jaccard_rows.argtypes = [_f32p, _f32p, _i64, _i64, _i64, _u16p, _i64, ctypes.c_uint16,
+                                          ctypes.c_float, _f32p]
         L.orc_np_expf.argtypes = [ctypes.c_float]
         L.orc_np_expf.restype = ctypes.c_float
         L.orc_f2h.argtypes = [ctypes.c_float]
@@ -141,3 +147,72 @@ def re_ranking(probFea, galFea, k1, k2, lambda_value):
     """Full reference path: distance from features (oracle arithmetic) then R2-R7."""
     feat = np.concatenate([np.asarray(probFea, np.float32), np.asarray(galFea, np.float32)])
     return rerank_from_dist(distmat(feat, feat), len(probFea), k1, k2, lambda_value)
+
+
+class RerankStages:
+    """Staged re_ranking (R2-R7 over row ranges, orc_rr_*) with the exchange formats of the
+    product's multimodal_reid_amd.reranking.staged_rerank: torch CPU tensors, V / V_qe rows as
+    CSR (nnz, col int32, fp16 bits as int16).  Rows are kept dense inside (small N only)."""
+
+    def __init__(self, feat, num_query, k1, k2, lambda_value):
+        import torch
+        self.torch = torch
+        self.feat = np.ascontiguousarray(np.asarray(feat, np.float32))
+        self.N = self.feat.shape[0]
+        self.Q = num_query
+        self.k1, self.k2 = k1, k2
+        self.K = min(max(k1 + 1, k2), self.N)
+        self.lam_h = np.float16(1 - lambda_value).view(np.uint16)
+        self.lam_f = np.float32(lambda_value)
+
+    def _rows(self, lo, hi):
+        return distmat(self.feat[lo:hi], self.feat)
+
+    def rank_rows(self, lo, hi):
+        R = np.zeros((hi - lo, self.K), np.int32)
+        rmax = np.zeros(hi - lo, np.float32)
+        if hi > lo:
+            lib().orc_rr_rank_rows(self._rows(lo, hi), hi - lo, self.N, self.K, R, rmax)
+        return self.torch.from_numpy(R), self.torch.from_numpy(rmax)
+
+    def offsets(self, nnz):
+        off = np.zeros(nnz.numel() + 1, np.int64)
+        off[1:] = np.cumsum(nnz.numpy().astype(np.int64))
+        return self.torch.from_numpy(off)
+
+    def _to_csr(self, dense):
+        nz = (dense & 0x7fff) != 0
+        nnz = nz.sum(1).astype(np.int32)
+        r, c = np.nonzero(nz)
+        return (self.torch.from_numpy(nnz), self.torch.from_numpy(c.astype(np.int32)),
+                self.torch.from_numpy(dense[r, c].view(np.int16).copy()))
+
+    def _dense(self, V):
+        off, col, val = (t.numpy() for t in V)
+        d = np.zeros((self.N, self.N), np.uint16)
+        rows = np.repeat(np.arange(self.N), np.diff(off))
+        d[rows, col] = val.view(np.uint16)
+        return d
+
+    def v_rows(self, R, rmax, lo, hi):
+        Vr = np.zeros((hi - lo, self.N), np.uint16)
+        if hi > lo:
+            lib().orc_rr_v_rows(self._rows(lo, hi), _c(rmax.numpy(), np.float32), _c(R.numpy(), np.int32), self.N,
+                                self.K, lo, hi, self.k1, Vr)
+        return self._to_csr(Vr)
+
+    def qe_rows(self, R, V, lo, hi):
+        Vq = np.zeros((hi - lo, self.N), np.uint16)
+        if hi > lo:
+            lib().orc_rr_qe_rows(_c(R.numpy(), np.int32), self.K, self.k2, lo, hi, self._dense(V), self.N, Vq)
+        return self._to_csr(Vq)
+
+    def jaccard_rows(self, rmax, Vq, qlo, qhi):
+        out = np.zeros((qhi - qlo, self.N - self.Q), np.float32)
+        if qhi > qlo:
+            lib().orc_rr_jaccard_rows(self._rows(qlo, qhi), _c(rmax.numpy(), np.float32), self.Q, qlo, qhi,
+                                      self._dense(Vq), self.N, int(self.lam_h), float(self.lam_f), out)
+        return self.torch.from_numpy(out)
+
+    def check(self):
+        pass

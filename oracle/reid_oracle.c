@@ -336,3 +336,117 @@ int orc_rerank_from_dist(const float* D, int64_t N, int64_t Q, int k1, int k2, u
     free(cnt); free(inv); free(pos); free(tmin);
     return 0;
 }
+
+/* ------------------------------------------------- staged re_ranking (rows) */
+/* The same R2-R7 as orc_rerank_from_dist, split into row-range stages over a symmetric
+ * distance given as row blocks (the sharded product path's stage boundaries).
+ * Test infrastructure: tests/test_rerank_sharded_gloo.py drives these under the product's
+ * orchestration (multimodal_reid_amd/reranking.py staged_rerank). */
+
+/* R2 for rows lo..hi: Drows [rows][N]; rowmax = row maxima (= column maxima, D symmetric,
+ * reranking.py:46); R [rows][K] = stable argsort prefix of Drows[r] / rowmax[r]. */
+void orc_rr_rank_rows(const float* Drows, int64_t rows, int64_t N, int64_t K, int32_t* R, float* rowmax) {
+    float* od = (float*)malloc(sizeof(float) * (size_t)N);
+    kv_t* tmp = (kv_t*)malloc(sizeof(kv_t) * (size_t)N);
+    int32_t* idx = (int32_t*)malloc(sizeof(int32_t) * (size_t)N);
+    for (int64_t r = 0; r < rows; r++) {
+        const float* d = Drows + r * N;
+        float m = d[0];
+        for (int64_t j = 1; j < N; j++) if (d[j] > m) m = d[j];
+        rowmax[r] = m;
+        for (int64_t j = 0; j < N; j++) od[j] = d[j] / m;
+        argsort_row(od, N, tmp, idx);
+        memcpy(R + r * K, idx, sizeof(int32_t) * (size_t)K);
+    }
+    free(od); free(tmp); free(idx);
+}
+
+/* R3 for rows lo..hi (reranking.py:51-71): Drows [hi-lo][N] distances of those rows,
+ * rowmax [N], R [N][K] (all rows).  Vrows [hi-lo][N] fp16 bits (dense). */
+void orc_rr_v_rows(const float* Drows, const float* rowmax, const int32_t* R, int64_t N, int64_t K, int64_t lo,
+                   int64_t hi, int k1, uint16_t* Vrows) {
+    int kf = (int)(k1 + 1 < N ? k1 + 1 : N);
+    int kh = (int)nearbyint((double)k1 / 2.0);
+    int kh1 = kh + 1 < N ? kh + 1 : (int)N;
+    int32_t* kr = (int32_t*)malloc(sizeof(int32_t) * (size_t)kf);
+    int32_t* ckr = (int32_t*)malloc(sizeof(int32_t) * (size_t)kh1);
+    int32_t* exp_idx = (int32_t*)malloc(sizeof(int32_t) * (size_t)(kf + (int64_t)kf * kh1));
+    float* w = (float*)malloc(sizeof(float) * (size_t)(kf + (int64_t)kf * kh1));
+    memset(Vrows, 0, sizeof(uint16_t) * (size_t)((hi - lo) * N));
+    for (int64_t i = lo; i < hi; i++) {
+        int nk = kreciprocal(R, K, (int32_t)i, kf, kr);
+        int ne = 0;
+        for (int a = 0; a < nk; a++) exp_idx[ne++] = kr[a];
+        for (int a = 0; a < nk; a++) {
+            int nc = kreciprocal(R, K, kr[a], kh1, ckr);
+            int inter = 0;
+            for (int b = 0; b < nc; b++)
+                for (int c = 0; c < nk; c++) if (ckr[b] == kr[c]) { inter++; break; }
+            if ((double)inter > 2.0 / 3.0 * (double)nc)
+                for (int b = 0; b < nc; b++) exp_idx[ne++] = ckr[b];
+        }
+        qsort(exp_idx, (size_t)ne, sizeof(int32_t), cmp_i32);
+        int nu = 0;
+        for (int a = 0; a < ne; a++) if (nu == 0 || exp_idx[a] != exp_idx[nu - 1]) exp_idx[nu++] = exp_idx[a];
+        for (int a = 0; a < nu; a++) w[a] = orc_np_expf(-(Drows[(i - lo) * N + exp_idx[a]] / rowmax[i]));
+        float s = orc_pairwise_f32(w, nu);
+        for (int a = 0; a < nu; a++) Vrows[(i - lo) * N + exp_idx[a]] = orc_f2h(w[a] / s);
+    }
+    free(kr); free(ckr); free(exp_idx); free(w);
+}
+
+/* R4 for rows lo..hi (reranking.py:73-78): V [N][N] (all rows), Vq_rows [hi-lo][N]. */
+void orc_rr_qe_rows(const int32_t* R, int64_t K, int k2, int64_t lo, int64_t hi, const uint16_t* V, int64_t N,
+                    uint16_t* Vq_rows) {
+    float* acc = (float*)malloc(sizeof(float) * (size_t)N);
+    for (int64_t i = lo; i < hi; i++) {
+        for (int64_t c = 0; c < N; c++) acc[c] = 0.0f;
+        for (int r = 0; r < k2; r++) {
+            const uint16_t* row = V + (int64_t)R[i * K + r] * N;
+            for (int64_t c = 0; c < N; c++) acc[c] += orc_h2f(row[c]);
+        }
+        for (int64_t c = 0; c < N; c++) Vq_rows[(i - lo) * N + c] = orc_f2h(acc[c] / (float)k2);
+    }
+    free(acc);
+}
+
+/* R5-R7 for queries qlo..qhi (reranking.py:80-100): Drows [qhi-qlo][N], rowmax [N],
+ * Vq [N][N] (all rows).  out [qhi-qlo][N-Q] float32. */
+void orc_rr_jaccard_rows(const float* Drows, const float* rowmax, int64_t Q, int64_t qlo, int64_t qhi,
+                         const uint16_t* Vq, int64_t N, uint16_t one_minus_lambda_h, float lambda_f, float* out) {
+    int64_t G = N - Q;
+    int64_t* cnt = (int64_t*)calloc((size_t)N + 1, sizeof(int64_t));
+    for (int64_t r = 0; r < N; r++)
+        for (int64_t c = 0; c < N; c++) if (Vq[r * N + c] & 0x7fffu) cnt[c + 1]++;
+    for (int64_t c = 0; c < N; c++) cnt[c + 1] += cnt[c];
+    int32_t* inv = (int32_t*)malloc(sizeof(int32_t) * (size_t)(cnt[N] > 0 ? cnt[N] : 1));
+    int64_t* pos = (int64_t*)malloc(sizeof(int64_t) * (size_t)N);
+    for (int64_t c = 0; c < N; c++) pos[c] = cnt[c];
+    for (int64_t r = 0; r < N; r++)
+        for (int64_t c = 0; c < N; c++) if (Vq[r * N + c] & 0x7fffu) inv[pos[c]++] = (int32_t)r;
+    uint16_t* tmin = (uint16_t*)malloc(sizeof(uint16_t) * (size_t)N);
+    for (int64_t i = qlo; i < qhi; i++) {
+        for (int64_t r = 0; r < N; r++) tmin[r] = 0;
+        for (int64_t c = 0; c < N; c++) {
+            uint16_t vi = Vq[i * N + c];
+            if (!(vi & 0x7fffu)) continue;
+            float fvi = orc_h2f(vi);
+            for (int64_t p = cnt[c]; p < cnt[c + 1]; p++) {
+                int32_t r = inv[p];
+                float fvr = orc_h2f(Vq[(int64_t)r * N + c]);
+                float mn = fvr < fvi ? fvr : fvi;
+                tmin[r] = orc_f2h(orc_h2f(tmin[r]) + mn);
+            }
+        }
+        for (int64_t r = Q; r < N; r++) {
+            float t = orc_h2f(tmin[r]);
+            uint16_t den = orc_f2h(2.0f - t);
+            uint16_t qt = orc_f2h(t / orc_h2f(den));
+            uint16_t jac = orc_f2h(1.0f - orc_h2f(qt));
+            float a = orc_h2f(orc_f2h(orc_h2f(jac) * orc_h2f(one_minus_lambda_h)));
+            float b = (Drows[(i - qlo) * N + r] / rowmax[i]) * lambda_f;
+            out[(i - qlo) * G + (r - Q)] = a + b;
+        }
+    }
+    free(cnt); free(inv); free(pos); free(tmin);
+}

@@ -1,0 +1,82 @@
+"""GPU parity of the staged / sharded re-ranking (reidmi_rr_*, reranking.staged_rerank):
+bit-identical to the one-call kernels (reidmi_rerank) and to the oracle, with the distance
+rows processed in several chunks, and across 2 ranks sharing cuda:0 (gloo, host-staged)."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import reidmi_boot  # noqa: E402
+
+reidmi_boot.load()
+
+import oracle  # noqa: E402
+from multimodal_reid_amd import synthetic as syn  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _feats(Q, G, seed, dim=256, ids=400, noise=3.0):
+    qp, gp, _, _ = syn.labels(Q, G, num_ids=ids, num_cams=6, seed=seed)
+    qf, gf = syn.features(qp, gp, dim=dim, seed=seed, noise=noise)
+    return oracle.l2norm(np.concatenate([qf, gf]))
+
+
+@pytest.mark.parametrize("Q,G,k1,k2", [(100, 500, 50, 15), (100, 500, 20, 6), (64, 700, 20, 1), (300, 2200, 50, 15)])
+def test_staged_bitexact_vs_one_call_and_oracle(gpu, Q, G, k1, k2):
+    from multimodal_reid_amd import reranking
+    feats = _feats(Q, G, seed=Q + k1)
+    f = torch.from_numpy(feats).to(gpu)
+    N = Q + G
+    staged = reranking.re_ranking_sharded(f[:Q], f[Q:], k1, k2, 0.3, chunk_bytes=4 * N * 97).cpu().numpy()
+    one = reranking.re_ranking_device(f[:Q], f[Q:], k1, k2, 0.3).cpu().numpy()
+    assert np.array_equal(staged.view(np.uint32), one.view(np.uint32))
+    if N <= 800:
+        ref = oracle.re_ranking(feats[:Q], feats[Q:], k1, k2, 0.3)
+        assert np.array_equal(staged.view(np.uint32), ref.view(np.uint32))
+
+
+def test_staged_duke_scale_bitexact_vs_one_call(gpu):
+    from multimodal_reid_amd import evaluate, reranking
+    sp = syn.DATASET_SPLITS["dukemtmc"]
+    Q, G = sp["num_query"], sp["num_gallery"]
+    qp, gp, _, _ = syn.labels(Q, G, sp["num_ids"], sp["num_cams"], seed=0, distractor_frac=0.1, junk_frac=0.02)
+    qf, gf = syn.features(qp, gp)
+    qn = evaluate.l2_normalize_device(torch.from_numpy(qf).to(gpu))
+    gn = evaluate.l2_normalize_device(torch.from_numpy(gf).to(gpu))
+    staged = reranking.re_ranking_sharded(qn, gn, 50, 15, 0.3, chunk_bytes=1 << 30)
+    one = reranking.re_ranking_device(qn, gn, 50, 15, 0.3)
+    assert torch.equal(staged.view(torch.int32), one.view(torch.int32))
+
+
+def _worker(rank, world, port, out):
+    import torch.distributed as dist
+    from multimodal_reid_amd import distributed as rd, reranking
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    feats = _feats(120, 900, seed=5)
+    f = torch.from_numpy(feats).cuda()
+    part = reranking.re_ranking_sharded(f[:120], f[120:], 50, 15, 0.3, chunk_bytes=4 * 1020 * 200)
+    out[rank] = rd.gather_rows(part, 120).cpu().numpy()
+    dist.destroy_process_group()
+
+
+def test_sharded_two_ranks_one_gpu(gpu):
+    import torch.multiprocessing as mp
+    from multimodal_reid_amd import reranking
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(2, port, out), nprocs=2, join=True)
+    f = torch.from_numpy(_feats(120, 900, seed=5)).to(gpu)
+    one = reranking.re_ranking_device(f[:120], f[120:], 50, 15, 0.3).cpu().numpy()
+    for r in range(2):
+        assert np.array_equal(out[r].view(np.uint32), one.view(np.uint32))
