@@ -12,7 +12,13 @@ exchange step); each rank scores its query shard against the full gallery; per-q
 results are all-gathered and rank 0 reduces them in query order (bit-identical to N=1).
 Total work is fixed as N grows ("strong").
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--no-cpu-baseline]
+Extra legs in the same JSON line (not part of `value`): "msmt17" = configs[3] / the north
+star's target, MSMT17 end to end on all ranks (sharded embed, all-gather, distmat + CMC/mAP,
+sharded k-reciprocal re-rank + CMC/mAP, wall seconds max over ranks); "rerank" = configs[2]'s
+Duke-size re-rank on rank 0 with the C port timed on a sample; "cpu_baseline".
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--no-cpu-baseline] [--no-rerank]
+                    [--no-msmt17]
 """
 import argparse
 import json
@@ -63,14 +69,14 @@ def gather_rows(x, n_total, world):
 
 
 class Workload:
-    def __init__(self, dev, rank, world, batch, dataset="market1501"):
+    def __init__(self, dev, rank, world, batch, dataset="market1501", model=None):
         sp = syn.DATASET_SPLITS[dataset]
         self.Q, self.G = sp["num_query"], sp["num_gallery"]
         self.q_pids, self.g_pids, self.q_cams, self.g_cams = syn.labels(
             self.Q, self.G, sp["num_ids"], sp["num_cams"], seed=0, distractor_frac=0.1, junk_frac=0.02)
         self.rank, self.world, self.batch, self.dev = rank, world, batch, dev
-        self.sd = syn.vit_state_dict("ViT-B/16", seed=0)
-        self.model = VisionTransformer(self.sd, device=dev)
+        self.sd = syn.vit_state_dict("ViT-B/16", seed=0) if model is None else None
+        self.model = VisionTransformer(self.sd, device=dev) if model is None else model
         # synthetic crops of this rank's shards, resident in HBM as bf16 (U(-1,1))
         gen = torch.Generator(device=dev)
         self.qlo, self.qhi = shard(self.Q, rank, world)
@@ -109,6 +115,58 @@ class Workload:
                                               rows[:, 3].astype(np.int64), self.G, 50, ovf.cpu().numpy())
         t2 = time.perf_counter()
         return cmc, mAP, t1 - t0, t2 - t1
+
+
+def msmt17_leg(model, dev, rank, world, batch):
+    """configs[3] + the north star's target: MSMT17 (11659q x 82161g) end to end — sharded
+    embed of every image (2 TTA passes), RCCL all-gather of the normalised feature blocks,
+    exact distmat + CMC/mAP, then the sharded k-reciprocal re-rank (k1=50, k2=15, lambda=0.3;
+    row-range stages with all-gathers of initial_rank / V / V_qe) + CMC/mAP.  Timed once,
+    after the Market steps (kernels warm); wall seconds are max over ranks."""
+    from multimodal_reid_amd import reranking
+    wl = Workload(dev, rank, world, batch, dataset="msmt17", model=model)
+    Q, G = wl.Q, wl.G
+
+    def sync():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    def rows_to_map(d):
+        valid, first, ap, nkept, ovf = evaluate.eval_rows_device(
+            d, wl.q_pids[wl.qlo:wl.qhi], wl.g_pids, wl.q_cams[wl.qlo:wl.qhi], wl.g_cams)
+        rows = gather_rows(torch.stack([valid.double(), first.double(), ap, nkept.double()], 1), Q, world)
+        rows = rows.cpu().numpy()
+        return evaluate.aggregate_cmc_map(rows[:, 0] > 0, rows[:, 1].astype(np.int64), rows[:, 2],
+                                          rows[:, 3].astype(np.int64), G, 50, ovf.cpu().numpy())
+
+    sync()
+    t0 = time.perf_counter()
+    wl.embed(wl.q_img, wl.q_tta, wl.q_emb)
+    wl.embed(wl.g_img, wl.g_tta, wl.g_emb)
+    qn = gather_rows(evaluate.l2_normalize_device(wl.q_emb), Q, world)
+    gn = gather_rows(evaluate.l2_normalize_device(wl.g_emb), G, world)
+    sync()
+    t1 = time.perf_counter()
+    evaluate.euclidean_distance_device(qn[wl.qlo:wl.qhi], gn, out=wl.dist)
+    _, mAP = rows_to_map(wl.dist)
+    sync()
+    t2 = time.perf_counter()
+    final = reranking.re_ranking_sharded(qn, gn, 50, 15, 0.3)
+    _, mAP_rr = rows_to_map(final)
+    sync()
+    t3 = time.perf_counter()
+    times = torch.tensor([t1 - t0, t2 - t1, t3 - t2], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(times, op=dist.ReduceOp.MAX)
+    te, tv, tr = (float(v) for v in times.cpu())
+    del wl, final, qn, gn
+    torch.cuda.empty_cache()
+    return {"config": f"MSMT17 {Q}q x {G}g, ViT-B/16 2 passes/img, {world} GPU(s): sharded embed + all-gather, "
+                      "exact distmat + CMC/mAP, sharded k-reciprocal re-rank (k1=50 k2=15 lambda=0.3) + CMC/mAP",
+            "imgs_per_s": round((Q + G) / te, 1), "embed_wall_s": round(te, 4), "eval_wall_s": round(tv, 4),
+            "rerank_eval_wall_s": round(tr, 4), "end_to_end_wall_s": round(te + tv + tr, 4),
+            "mAP": round(float(mAP), 6), "mAP_rerank": round(float(mAP_rr), 6)}
 
 
 def rerank_leg(dev, cpu_n=1000, cpu=True):
@@ -195,6 +253,7 @@ def main():
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-rerank", action="store_true")
+    ap.add_argument("--no-msmt17", action="store_true")
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -229,6 +288,7 @@ def main():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    ms17 = None if a.no_msmt17 else msmt17_leg(wl.model, dev, rank, world, a.batch)
     if rank == 0:
         imgs = (wl.Q + wl.G) * a.steps
         avg_ms = ms.value / max(cnt.value, 1)
@@ -260,6 +320,8 @@ def main():
                          "traffic": C_FC_TRAFFIC_BYTES, "traffic_unit": "bytes/launch (PMC)", "avg_launch_ms": round(avg_ms, 4), "launches": cnt.value,
                          "flops_per_launch": fl.value / max(cnt.value, 1)},
         }
+        if ms17 is not None:
+            line["msmt17"] = ms17
         if not a.no_rerank:
             line["rerank"] = rerank_leg(dev, cpu=not a.no_cpu_baseline)
         if not a.no_cpu_baseline:

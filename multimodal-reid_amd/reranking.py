@@ -17,6 +17,7 @@ import torch
 from . import _lib
 from .evaluate import _as_dev_f32, euclidean_distance_device
 
+STAGED_MIN_N = 32768  # from features, N >= this: staged path (no N x N fp32 buffer)
 _CAP_MSG = {1: "V row capacity", 2: "V_qe row capacity (4096)", 4: "query-expansion staging capacity (6144)"}
 
 
@@ -34,6 +35,12 @@ def re_ranking_device(probFea, galFea, k1, k2, lambda_value, local_distmat=None,
     """Device version: returns the (Q, G) fp32 torch tensor on the GPU."""
     Q = probFea.size(0) if isinstance(probFea, torch.Tensor) else len(probFea)
     G = galFea.size(0) if isinstance(galFea, torch.Tensor) else len(galFea)
+    if not (only_local or local_distmat is not None) and Q + G >= STAGED_MIN_N:
+        # N x N buffers would dominate: row-chunked stages, same bits
+        from . import distributed as rd
+        if rd.world()[1] > 1:
+            raise _lib.ReidmiError("re_ranking_device is single-process; use re_ranking_sharded under torch.distributed")
+        return re_ranking_sharded(probFea, galFea, k1, k2, lambda_value)
     dev = torch.device("cuda", torch.cuda.current_device())
     lam_h, lam_f = _lam(lambda_value)
     out = torch.empty((Q, G), device=dev, dtype=torch.float32)
