@@ -35,8 +35,9 @@ static std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
 static size_t used = 0;
 }  // namespace prof
 
-// Tile selection: 0 = auto (>= 256 tiles of 256x256: v5; else v1), 1..5 force
-// v1 (128x128), v2 (256x256), v3 (persistent), v4 (ping-pong), v5 (persistent ping-pong).  Set by reidmi_gemm_set_variant (tests / A-B timing in one process); the
+// Tile selection: 0 = auto (>= 256 tiles of 256x256: v6; else v1), 1..6 force
+// v1 (128x128), v2 (256x256), v3 (persistent), v4 (ping-pong), v5 (persistent ping-pong),
+// v6 (v5 with deferred epilogue-store waits: +1-2 % on the K = 768 shapes).  Set by reidmi_gemm_set_variant (tests / A-B timing in one process); the
 // REIDMI_GEMM_VARIANT environment variable gives the initial value.
 static int g_variant = -1;
 static int variant() {
@@ -742,7 +743,25 @@ __global__ __launch_bounds__(512, 2) void gemm4_bf16_kernel(const __bf16* __rest
 // while a tile's epilogue runs, the next tile's first two K-steps are already landing.
 // The epilogue needs no barrier: group A runs it in the slot where group B computes the
 // tile's last quadrant.  Same MFMA sequence per output as v1-v4 -> bit-identical.
+//
+// DEFER (variant 6): the epilogue's stores are not waited for by the next tile's first
+// K-step.  vmcnt retires in issue order, so v5's first `vmcnt(6)` after an epilogue waits
+// for every store the epilogue issued (one HBM write round trip per tile, with the MFMAs
+// idle).  Here the next tile's first "+1" DMA (B0 of its K-step 1) is issued BEFORE the
+// epilogue, and that step's wait counts the epilogue's memory instructions as allowed to be
+// outstanding: vmcnt(6 + S (+1 bias DMA)), S = EpiVm<EPI>::count (checked against the ISA:
+// global_load/store_dwordx4 per wave and tile).  Only after a full tile (no masked rows,
+// so exactly S instructions were issued) and not for scattered-v^T QKV tiles; otherwise the
+// plain vmcnt(6).  The bias is read from LDS by inline ds_read (the compiler would insert a
+// vmcnt(0) before a ds_read of an LDS-DMA'd slot, draining the in-flight DMA every tile).
 template <int EPI>
+struct EpiVm {  // vector-memory instructions of one full-tile epilogue_tile<EPI, 8> per wave
+    static constexpr int count = EPI == EPI_BF16 || EPI == EPI_GELU_BF16 || EPI == EPI_QKV ? 16
+                                 : EPI == EPI_RESID_F16 || EPI == EPI_F32                 ? 32
+                                                                                          : -1;
+};
+
+template <int EPI, bool DEFER>
 __global__ __launch_bounds__(512, 2) void gemm5_bf16_kernel(const __bf16* __restrict__ A, int64_t lda,
                                                             const __bf16* __restrict__ W, int64_t ldw, int64_t M,
                                                             int N, int K, EpiArgs ea, int tiles_n, int ntiles) {
@@ -880,6 +899,8 @@ __global__ __launch_bounds__(512, 2) void gemm5_bf16_kernel(const __bf16* __rest
     __syncthreads();
     if (wr == 1) G5_BARRIER();
     int buf = 0;
+    constexpr bool CAN_DEFER = DEFER && EpiVm<EPI>::count > 0;
+    bool deferred = false;  // the previous tile's epilogue stores may still be in flight
     for (int tile = first; tile < hi; tile += gx) {
 #pragma unroll
         for (int i = 0; i < 8; i++)
@@ -887,6 +908,7 @@ __global__ __launch_bounds__(512, 2) void gemm5_bf16_kernel(const __bf16* __rest
             for (int j = 0; j < 4; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
         for (int kt = 0; kt < nk; ++kt) {
             const bool has1 = p1.tile < hi, has2 = p2.tile < hi;
+            const bool b0_early = CAN_DEFER && kt == 0 && tile != first;  // issued before the epilogue
             const __bf16* sA = lds5 + buf * G2_STAGE;
             const __bf16* sW = sA + G2_M * GB_K;
             // LOAD 0 / COMPUTE (0,0)
@@ -895,7 +917,7 @@ __global__ __launch_bounds__(512, 2) void gemm5_bf16_kernel(const __bf16* __rest
             if (kt == 0 && has_bias)
                 __builtin_amdgcn_global_load_lds(ea.bias + (tile % tiles_n) * G2_N + lane * 4, (lds_ptr_t)bias_slot,
                                                  16, 0, 0);
-            if (has1) issue_w(buf ^ 1, 0, p1);
+            if (has1 && !b0_early) issue_w(buf ^ 1, 0, p1);
             G5_LDS_DONE();
             G5_BARRIER();
             compute(0, 0);
@@ -919,7 +941,19 @@ __global__ __launch_bounds__(512, 2) void gemm5_bf16_kernel(const __bf16* __rest
             if (has2) {
                 issue_a(buf, 1, p2);
                 G5_LDS_DONE();
-                asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+                if constexpr (CAN_DEFER) {
+                    constexpr int S = EpiVm<EPI>::count;
+                    if (kt == 0 && deferred) {
+                        if (has_bias)
+                            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(S + 7) : "memory");
+                        else
+                            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(S + 6) : "memory");
+                    } else {
+                        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+                    }
+                } else {
+                    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+                }
             } else {
                 G5_LDS_DONE();
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -933,10 +967,30 @@ __global__ __launch_bounds__(512, 2) void gemm5_bf16_kernel(const __bf16* __rest
         }
         const int64_t m0 = (int64_t)(tile / tiles_n) * G2_M;
         const int n0 = (tile % tiles_n) * G2_N;
+        if constexpr (CAN_DEFER) {
+            deferred = false;
+            if (p1.tile < hi) {  // a next tile exists: issue its K-step 1 B0 (skipped in its LOAD 0)
+                issue_w(buf ^ 1, 0, p1);
+                deferred = m0 + G2_M <= M;
+                if constexpr (EPI == EPI_QKV) deferred = deferred && (n0 + ea.n_off) / (ea.heads * 64) != 2;
+            }
+        }
         if (has_bias) {
             float4 b[4];
+            if constexpr (DEFER) {
+                // inline ds_read: no compiler-inserted vmcnt(0) for the LDS-DMA'd slot (retired
+                // by the tile's first K-step wait)
+                const float* bp = bias_slot + wc * 64 + (lane >> 4) * 4;
+                const uint32_t ba = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)bp;
+                asm volatile("ds_read_b128 %0, %1" : "=v"(b[0]) : "v"(ba) : "memory");
+                asm volatile("ds_read_b128 %0, %1 offset:64" : "=v"(b[1]) : "v"(ba) : "memory");
+                asm volatile("ds_read_b128 %0, %1 offset:128" : "=v"(b[2]) : "v"(ba) : "memory");
+                asm volatile("ds_read_b128 %0, %1 offset:192" : "=v"(b[3]) : "v"(ba) : "memory");
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            } else {
 #pragma unroll
-            for (int j = 0; j < 4; j++) b[j] = *(const float4*)(bias_slot + wc * 64 + j * 16 + (lane >> 4) * 4);
+                for (int j = 0; j < 4; j++) b[j] = *(const float4*)(bias_slot + wc * 64 + j * 16 + (lane >> 4) * 4);
+            }
 #pragma unroll
             for (int i = 0; i < 8; i++)
 #pragma unroll
@@ -960,20 +1014,26 @@ static int launch(const void* A, int64_t lda, const void* W, int64_t ldw, int64_
     const int var = variant();
     const int64_t tiles256 = (int64_t)ceil_div(M, G2_M) * (N / G2_N);
     if (N % G2_N == 0 && K >= 2 * GB_K && lda * G2_M < (1ll << 31) && ldw * G2_N < (1ll << 31) &&
-        (var == 5 || (var == 0 && tiles256 >= 256))) {
+        (var == 5 || var == 6 || (var == 0 && tiles256 >= 256))) {
         const int tiles_m = ceil_div(M, G2_M), tiles_n = (int)(N / G2_N);
         const int64_t ntiles = (int64_t)tiles_m * tiles_n;
         RM_REQUIRE(ntiles < (1ll << 31), "gemm: grid too large");
         const size_t lds = 2 * (size_t)G2_STAGE * 2 + 8 * 256 * sizeof(float);
         static bool attr5 = false;
         if (!attr5) {
-            RM_CHECK_HIP(hipFuncSetAttribute((const void*)gemm5_bf16_kernel<EPI>,
+            RM_CHECK_HIP(hipFuncSetAttribute((const void*)gemm5_bf16_kernel<EPI, false>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            RM_CHECK_HIP(hipFuncSetAttribute((const void*)gemm5_bf16_kernel<EPI, true>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
             attr5 = true;
         }
         const int grid = (int)(ntiles < 256 ? ntiles : 256);
-        hipLaunchKernelGGL(gemm5_bf16_kernel<EPI>, dim3((unsigned)grid), dim3(512), lds, s, (const __bf16*)A, lda,
-                           (const __bf16*)W, ldw, M, (int)N, (int)K, ea, tiles_n, (int)ntiles);
+        if (var == 6 || var == 0)
+            hipLaunchKernelGGL((gemm5_bf16_kernel<EPI, true>), dim3((unsigned)grid), dim3(512), lds, s,
+                               (const __bf16*)A, lda, (const __bf16*)W, ldw, M, (int)N, (int)K, ea, tiles_n, (int)ntiles);
+        else
+            hipLaunchKernelGGL((gemm5_bf16_kernel<EPI, false>), dim3((unsigned)grid), dim3(512), lds, s,
+                               (const __bf16*)A, lda, (const __bf16*)W, ldw, M, (int)N, (int)K, ea, tiles_n, (int)ntiles);
         RM_LAUNCHED();
         return OK;
     }
@@ -1078,7 +1138,8 @@ int gemm_bf16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, i
 using namespace reidmi;
 
 REIDMI_API int reidmi_gemm_set_variant(int v) {
-    RM_REQUIRE(v >= 0 && v <= 5, "gemm variant: 0 auto, 1 128x128, 2 256x256, 3 256x256 persistent, 4 ping-pong, 5 persistent ping-pong");
+    RM_REQUIRE(v >= 0 && v <= 6, "gemm variant: 0 auto, 1 128x128, 2 256x256, 3 256x256 persistent, 4 ping-pong, "
+                                 "5 persistent ping-pong, 6 = 5 with deferred epilogue-store waits");
     g_variant = v;
     return OK;
 }

@@ -61,7 +61,7 @@ def test_gemm_epilogues(gpu, epi, M, N, K):
 @pytest.mark.parametrize("M,N,K", [(54016, 768, 768), (1000, 2304, 768), (700, 512, 3072), (70000, 256, 192)])
 def test_gemm_v2_tile_bitexact_vs_v1(gpu, epi, M, N, K):
     """The 256x256 LDS-DMA tiles (v2 plain, v3 persistent, v4 ping-pong, v5 persistent
-    ping-pong; odd K-step counts cross tiles with the stage parity flipped) and the 128x128
+    ping-pong, v6 = v5 with deferred epilogue-store waits; odd K-step counts cross tiles with the stage parity flipped) and the 128x128
     register-staged tile run the same MFMA
     sequence per output element (k-steps ascending), so they agree bit for bit; rows
     past M (clamped source rows) must not leak into the result."""
@@ -71,7 +71,7 @@ def test_gemm_v2_tile_bitexact_vs_v1(gpu, epi, M, N, K):
     W = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16).cuda()
     bias = torch.randn(N, generator=g).cuda()
     outs = []
-    for v in (1, 2, 3, 4, 5):
+    for v in (1, 2, 3, 4, 5, 6):
         L.call("reidmi_gemm_set_variant", v)
         if epi in (0, 1):
             out = torch.zeros(M, N, dtype=torch.bfloat16, device="cuda")

@@ -12,7 +12,7 @@ reidmi_boot.load()
 from multimodal_reid_amd import _lib as L  # noqa: E402
 
 M = int(sys.argv[1]) if len(sys.argv) > 1 else 512 * 211
-SHAPES = [("qkv", 2304, 768, 3), ("out_proj", 768, 768, 2), ("c_fc", 3072, 768, 1), ("c_proj", 768, 3072, 2)]
+SHAPES = [("qkv", 2304, 768, 3), ("out_proj", 768, 768, 6), ("c_fc", 3072, 768, 1), ("c_proj", 768, 3072, 6)]
 VARIANTS = [int(v) for v in (sys.argv[2].split(",") if len(sys.argv) > 2 else ["2", "3"])]
 ROUNDS = 5
 
@@ -27,6 +27,8 @@ def main():
         b = torch.rand(N, device=dev)
         if epi in (2,):
             out = torch.zeros(M, N, device=dev)
+        elif epi == 6:
+            out = torch.zeros(M, N, device=dev, dtype=torch.float16)
         elif epi == 3:
             out = None
         else:
