@@ -214,6 +214,39 @@ def rerank_leg(dev, cpu_n=1000, cpu=True):
     return out
 
 
+def preprocess_leg(dev, n=19281, reps=5):
+    """the test transform (Resize(256,128) -> ToTensor -> Normalize,
+    data_prepare.py:257-261) on the Market split's worth of decoded 128x64 RGB crops, packed
+    and resident in HBM, -> bf16 [n, 3, 256, 128] (reidmi_preprocess_u8).  HBM-bound:
+    algorithmic bytes = n * (128*64*3 read + 3*256*128*2 written)."""
+    import ctypes
+    r = np.random.default_rng(0)
+    h, w = 128, 64
+    pix = torch.from_numpy(r.integers(0, 256, n * h * w * 3, dtype=np.uint8)).to(dev)
+    meta = torch.from_numpy(np.stack([np.arange(n) * h * w * 3, np.full(n, h), np.full(n, w)], 1).astype(np.int64)).to(dev)
+    out = torch.empty((n, 3, 256, 128), dtype=torch.bfloat16, device=dev)
+    mean = (ctypes.c_float * 3)(0.5, 0.5, 0.5)
+    std = (ctypes.c_float * 3)(0.5, 0.5, 0.5)
+
+    def run():
+        _lib.call("reidmi_preprocess_u8", _lib.ptr(pix), _lib.ptr(meta), n, h, w, 256, 128, mean, std, 1,
+                  _lib.ptr(out), _lib.stream(dev))
+
+    run()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    nbytes = n * (h * w * 3 + 3 * 256 * 128 * 2)
+    del pix, out
+    return {"config": f"{n} decoded {h}x{w} RGB crops -> bf16 [n,3,256,128] (Resize bilinear + ToTensor + Normalize, "
+                      "Pillow-exact)", "imgs_per_s": round(n / (ms * 1e-3), 1), "ms": round(ms, 3),
+            "achieved_GBps": round(nbytes / (ms * 1e-3) / 1e9, 1), "peak_GBps": 8000.0}
+
+
 def cpu_baseline(wl, n_img=12, n_q=48):
     """The oracle ("port") on this host: fp32 torch restatement of the encoder on a
     bounded image sample (both TTA passes) + C restatement of distmat/eval on a query
@@ -322,6 +355,7 @@ def main():
         }
         if ms17 is not None:
             line["msmt17"] = ms17
+        line["preprocess"] = preprocess_leg(dev)
         if not a.no_rerank:
             line["rerank"] = rerank_leg(dev, cpu=not a.no_cpu_baseline)
         if not a.no_cpu_baseline:

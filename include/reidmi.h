@@ -250,6 +250,25 @@ int reidmi_feature_tta_avg(const float* x12a, const float* pa, const float* x12b
 int reidmi_feature_tta_mm(const float* x12a, const float* pa, const float* x12b, const float* pb, const float* zs,
                           int64_t B, int64_t W, int64_t E, int64_t ncls, float* emb, int64_t lde, void* stream);
 
+/* ---------------------------------------------------- test-time transforms (§8f) */
+
+/* transforms.Resize((oh, ow)) -> ToTensor() -> Normalize(mean, std)  — data_prepare.py:257-261
+ * (the reference's test transform, applied per image in reidDataset.__getitem__,
+ * data_prepare.py:87-92) on a packed batch of decoded RGB images; bit-exact with
+ * PIL.Image.resize(BILINEAR) (Pillow 12.2, see oracle/transforms_oracle.c).  JPEG decode
+ * stays on the host.
+ * pix: device, concatenated HWC uint8 images; meta: device int64 [B][3] = (byte offset of
+ * the image in pix, h, w) with 0 < h <= max_h, 0 < w <= max_w (images outside are skipped);
+ * mean, stdv: HOST float[3]; out: device [B][3][oh][ow], out_dtype 0 = fp32, 1 = bf16 (RNE).
+ * The flip / pad / crop of the TTA loader (data_prepare.py:263-270) is applied on these
+ * outputs by the encoder (reidmi_vit_forward's tta offsets). */
+int reidmi_preprocess_u8(const uint8_t* pix, const int64_t* meta, int64_t B, int max_h, int max_w, int oh, int ow,
+                         const float* mean, const float* stdv, int out_dtype, void* out, void* stream);
+
+/* On-chip bytes one workgroup of reidmi_preprocess_u8 needs for sources up to max_h x max_w
+ * (the call fails above 160 KiB: resize such images on the host first). */
+int reidmi_preprocess_lds_size(int oh, int ow, int max_h, int max_w, int64_t* bytes);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,105 @@
+"""Test-time image transforms of the reference's loaders, on the GPU.
+
+data_prepare.py:257-270 builds, per image (reidDataset.__getitem__, data_prepare.py:87-92):
+
+    transform_test           = Resize((h, w)) -> ToTensor() -> Normalize(mean, std)
+    transform_test_augmented = Resize((h, w)) -> RandomHorizontalFlip(1.0) -> Pad((10, 5))
+                               -> RandomCrop((h, w)) -> ToTensor() -> Normalize(mean, std)
+
+with mean = std = 0.5 for the ViT (ImageNet statistics for the ResNet).  Here the decoded
+RGB images of a whole batch go to the device as one packed uint8 buffer and
+`reidmi_preprocess_u8` produces the normalised [B, 3, h, w] tensor, bit-exact with
+PIL.Image.resize(BILINEAR) + ToTensor + Normalize (oracle/transforms_oracle.c pins the
+arithmetic against Pillow).  The augmented view's flip / pad / crop commute with ToTensor
+and Normalize, so they are not materialised: the encoder's im2col applies them from per-image
+crop offsets (`tta_offsets`, `zero_shot_learning.embed_pair(tta=...)`).  JPEG decode stays on
+the host (PIL), as in the reference's DataLoader workers.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+
+VIT_MEAN = (0.5, 0.5, 0.5)
+VIT_STD = (0.5, 0.5, 0.5)
+CNN_MEAN = (0.485, 0.456, 0.406)
+CNN_STD = (0.229, 0.224, 0.225)
+
+
+def norm_stats(model_type):
+    """data_prepare.py:260,268: ViT statistics for model_type == "vit", ImageNet otherwise."""
+    return (VIT_MEAN, VIT_STD) if model_type == "vit" else (CNN_MEAN, CNN_STD)
+
+
+def _as_hwc_u8(img):
+    if isinstance(img, np.ndarray):
+        a = img
+    else:  # PIL image: data_prepare.py:88 converts to RGB
+        a = np.asarray(img.convert("RGB"))
+    if a.dtype != np.uint8 or a.ndim != 3 or a.shape[2] != 3:
+        raise ValueError(f"expected an RGB image (PIL or HxWx3 uint8 array), got {a.dtype} {a.shape}")
+    return np.ascontiguousarray(a)
+
+
+def pack_images(images):
+    """Concatenate HWC uint8 images: (flat uint8 buffer, meta int64 [B][3] = (offset, h, w),
+    max_h, max_w)."""
+    arrs = [_as_hwc_u8(im) for im in images]
+    meta = np.zeros((len(arrs), 3), np.int64)
+    off = 0
+    for i, a in enumerate(arrs):
+        meta[i] = (off, a.shape[0], a.shape[1])
+        off += a.size
+    buf = np.concatenate([a.reshape(-1) for a in arrs]) if arrs else np.zeros(0, np.uint8)
+    max_h = int(meta[:, 1].max()) if arrs else 1
+    max_w = int(meta[:, 2].max()) if arrs else 1
+    return buf, meta, max_h, max_w
+
+
+def preprocess(images, height=256, width=128, model_type="vit", dtype=torch.bfloat16, device=None, out=None):
+    """Resize((height, width)) -> ToTensor -> Normalize of a batch of decoded RGB images
+    (PIL images or HxWx3 uint8 arrays of any sizes) -> device tensor [B, 3, height, width]
+    of `dtype` (torch.float32 = exactly the reference's tensor; torch.bfloat16 = that tensor
+    rounded to nearest-even, the encoder's input)."""
+    if dtype not in (torch.float32, torch.bfloat16):
+        raise ValueError("dtype must be torch.float32 or torch.bfloat16")
+    device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    buf, meta, max_h, max_w = pack_images(images)
+    B = meta.shape[0]
+    if out is None:
+        out = torch.empty((B, 3, height, width), dtype=dtype, device=device)
+    elif tuple(out.shape) != (B, 3, height, width) or out.dtype != dtype or not out.is_contiguous():
+        raise ValueError("out must be a contiguous [B, 3, height, width] tensor of `dtype`")
+    if B == 0:
+        return out
+    _lib.require_cuda(out)
+    pix = torch.from_numpy(buf).pin_memory().to(device, non_blocking=True)
+    dmeta = torch.from_numpy(meta).pin_memory().to(device, non_blocking=True)
+    mean, std = norm_stats(model_type)
+    mean_c = (ctypes.c_float * 3)(*mean)
+    std_c = (ctypes.c_float * 3)(*std)
+    _lib.call("reidmi_preprocess_u8", _lib.ptr(pix), _lib.ptr(dmeta), B, max_h, max_w, height, width, mean_c, std_c,
+              0 if dtype == torch.float32 else 1, _lib.ptr(out), _lib.stream(device))
+    # no sync: the pinned staging buffers are recorded against the copy by torch's host
+    # caching allocator, and pix/dmeta are freed stream-ordered on this stream
+    return out
+
+
+class EvalTransform:
+    """Callable stand-in for data_prepare.get_loader's `transform_test` over a whole batch."""
+
+    def __init__(self, image_height=256, image_width=128, model_type="vit", dtype=torch.bfloat16):
+        self.h, self.w, self.model_type, self.dtype = image_height, image_width, model_type, dtype
+
+    def __call__(self, images, device=None):
+        return preprocess(images, self.h, self.w, self.model_type, self.dtype, device)
+
+
+def tta_offsets(n, generator=None):
+    """RandomCrop((h, w)) offsets after Pad((10, 5)) for the augmented view (data_prepare.py:
+    266-267): int32 [n][2] = (top i in [0, 10], left j in [0, 20]), as the encoder's TTA
+    im2col takes them (the reference draws them unseeded inside DataLoader workers)."""
+    g = generator if isinstance(generator, np.random.Generator) else np.random.default_rng(generator)
+    return np.stack([g.integers(0, 11, n), g.integers(0, 21, n)], 1).astype(np.int32)

@@ -11,6 +11,9 @@ Parity status:
     accumulation order is not reproducible; pinned within 2e-6 abs.
   * encoders (oracle/vit_ref.py): fp32 torch restatement pinned to the reference
     modules' fp32 outputs on synthetic weights.
+  * test-time transforms (transforms_oracle.c): Pillow's bilinear resize + ToTensor +
+    Normalize, pinned bit-exact to fixtures made with Pillow 12.2 itself
+    (tests/golden/make_transform_goldens.py).
 """
 import ctypes
 import os
@@ -61,12 +64,38 @@ def lib():
         L.orc_pairwise_f32.restype = ctypes.c_float
         L.orc_pairwise_f64.argtypes = [_f64p, _i64]
         L.orc_pairwise_f64.restype = ctypes.c_double
+        _u8p = np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS")
+        _i = ctypes.c_int
+        L.orc_pil_resize_rgb.argtypes = [_u8p, _i, _i, _i, _i, _u8p]
+        L.orc_to_tensor_normalize.argtypes = [_u8p, _i, _i, _f32p, _f32p, _f32p]
+        L.orc_resize_vertical_first.argtypes = [_i, _i, _i, _i]
         _LIB = L
     return _LIB
 
 
 def _c(a, dt):
     return np.ascontiguousarray(np.asarray(a), dtype=dt)
+
+
+def pil_resize(img, oh, ow):
+    """PIL.Image.resize((ow, oh), BILINEAR) of an HxWx3 uint8 image (transforms_oracle.c)."""
+    img = _c(img, np.uint8)
+    out = np.empty((oh, ow, 3), np.uint8)
+    lib().orc_pil_resize_rgb(img, img.shape[0], img.shape[1], oh, ow, out)
+    return out
+
+
+def to_tensor_normalize(img, mean=(0.5, 0.5, 0.5), std=(0.5, 0.5, 0.5)):
+    """ToTensor() -> Normalize(mean, std) of an HxWx3 uint8 image -> float32 [3, H, W]."""
+    img = _c(img, np.uint8)
+    out = np.empty((3,) + img.shape[:2], np.float32)
+    lib().orc_to_tensor_normalize(img, img.shape[0], img.shape[1], _c(mean, np.float32), _c(std, np.float32), out)
+    return out
+
+
+def eval_transform(img, oh=256, ow=128, mean=(0.5, 0.5, 0.5), std=(0.5, 0.5, 0.5)):
+    """data_prepare.py:257-261: Resize -> ToTensor -> Normalize."""
+    return to_tensor_normalize(pil_resize(img, oh, ow), mean, std)
 
 
 def l2norm(x):

@@ -1,0 +1,113 @@
+"""Test-time transform (data_prepare.py:257-270): the oracle against fixtures made with
+Pillow itself, and the HIP kernel (reidmi_preprocess_u8) against the oracle, bit for bit."""
+import hashlib
+import io
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from conftest import GOLDEN, golden
+
+sys.path.insert(0, GOLDEN)
+from make_transform_goldens import source_image, to_tensor_normalize  # noqa: E402
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def test_oracle_resize_matches_pillow_fixtures():
+    g = golden("transforms.npz")
+    for k, (h, w, oh, ow, seed) in enumerate(g["cases"]):
+        out = oracle.pil_resize(source_image(h, w, seed), int(oh), int(ow))
+        assert sha(out) == g["resized_sha"][k], (h, w, oh, ow)
+        if k < len(g["resized_first"]):
+            assert np.array_equal(out, g["resized_first"][k])
+
+
+def test_oracle_normalize_matches_torchvision_semantics():
+    g = golden("transforms.npz")
+    for k, (h, w, oh, ow, seed) in enumerate(g["cases"][:20]):
+        t = oracle.eval_transform(source_image(h, w, seed), int(oh), int(ow))
+        assert sha(t) == g["normalized_sha"][k], (h, w, oh, ow)
+
+
+def test_oracle_vs_live_pillow_random_sizes():
+    """Pillow is the third-party dependency the reference's Resize runs on (importable here)."""
+    from PIL import Image
+    r = np.random.default_rng(7)
+    for _ in range(60):
+        h, w = int(r.integers(1, 500)), int(r.integers(1, 300))
+        oh, ow = int(r.integers(1, 300)), int(r.integers(1, 200))
+        img = r.integers(0, 256, (h, w, 3), dtype=np.uint8)
+        ref = np.asarray(Image.fromarray(img, "RGB").resize((ow, oh), Image.BILINEAR))
+        assert np.array_equal(oracle.pil_resize(img, oh, ow), ref), (h, w, oh, ow)
+
+
+def test_pack_images_meta():
+    from PIL import Image
+    from multimodal_reid_amd import data_prepare
+    imgs = [source_image(5, 4, 1), Image.fromarray(source_image(3, 7, 2)).convert("L"), source_image(2, 2, 3)]
+    buf, meta, mh, mw = data_prepare.pack_images(imgs)
+    assert meta.tolist() == [[0, 5, 4], [60, 3, 7], [123, 2, 2]] and (mh, mw) == (5, 7)
+    assert buf.size == 135 and np.array_equal(buf[:60], imgs[0].reshape(-1))
+    with pytest.raises(ValueError):
+        data_prepare.pack_images([np.zeros((4, 4), np.uint8)])
+
+
+def _cases():
+    return [tuple(int(v) for v in c) for c in golden("transforms.npz")["cases"]]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_preprocess_kernel_bitexact(gpu, dtype):
+    """One mixed-size batch per output size (Market crops, up/down/identity per axis, tall
+    narrow sources, 1x1) through reidmi_preprocess_u8 vs the oracle."""
+    from multimodal_reid_amd import data_prepare
+    by_out = {}
+    for (h, w, oh, ow, seed) in _cases():
+        by_out.setdefault((oh, ow), []).append(source_image(h, w, seed))
+    for (oh, ow), imgs in by_out.items():
+        got = data_prepare.preprocess(imgs, oh, ow, dtype=dtype).cpu()
+        for i, img in enumerate(imgs):
+            ref = torch.from_numpy(oracle.eval_transform(img, oh, ow))
+            if dtype == torch.bfloat16:
+                ref = ref.to(torch.bfloat16)
+            assert torch.equal(got[i].view(torch.int16 if dtype == torch.bfloat16 else torch.int32),
+                               ref.view(torch.int16 if dtype == torch.bfloat16 else torch.int32)), (img.shape, oh, ow)
+
+
+@pytest.mark.gpu
+def test_preprocess_cnn_stats_and_jpeg_roundtrip(gpu):
+    """ImageNet statistics (model_type != "vit") and PIL-decoded JPEGs (decode stays on the host)."""
+    from PIL import Image
+    from multimodal_reid_amd import data_prepare
+    imgs = []
+    for k, (h, w) in enumerate([(128, 64), (310, 140), (90, 41)]):
+        b = io.BytesIO()
+        Image.fromarray(source_image(h, w, 50 + k)).save(b, format="JPEG", quality=90)
+        imgs.append(Image.open(io.BytesIO(b.getvalue())))
+    got = data_prepare.preprocess(imgs, 256, 128, model_type="resnet", dtype=torch.float32).cpu().numpy()
+    mean, std = data_prepare.norm_stats("resnet")
+    for i, im in enumerate(imgs):
+        ref = oracle.eval_transform(np.asarray(im.convert("RGB")), 256, 128, mean, std)
+        assert np.array_equal(got[i].view(np.uint32), ref.view(np.uint32))
+        assert np.array_equal(ref, to_tensor_normalize(np.asarray(im.convert("RGB").resize((128, 256), Image.BILINEAR)),
+                                                       mean, std))
+
+
+@pytest.mark.gpu
+def test_preprocess_large_batch_matches_per_image(gpu):
+    """A 300-image batch of ragged sizes equals the images processed one by one."""
+    from multimodal_reid_amd import data_prepare
+    r = np.random.default_rng(3)
+    imgs = [source_image(int(r.integers(60, 500)), int(r.integers(30, 250)), 1000 + i) for i in range(300)]
+    batch = data_prepare.preprocess(imgs, dtype=torch.bfloat16)
+    for i in range(0, 300, 37):
+        one = data_prepare.preprocess([imgs[i]], dtype=torch.bfloat16)
+        assert torch.equal(batch[i], one[0])
