@@ -259,7 +259,7 @@ int reidmi_feature_tta_mm(const float* x12a, const float* pa, const float* x12b,
  * stays on the host.
  * pix: device, concatenated HWC uint8 images; meta: device int64 [B][3] = (byte offset of
  * the image in pix, h, w) with 0 < h <= max_h, 0 < w <= max_w (images outside are skipped);
- * mean, stdv: HOST float[3]; out: device [B][3][oh][ow], out_dtype 0 = fp32, 1 = bf16 (RNE).
+ * mean, stdv: HOST float[3]; out: device [B][3][oh][ow] (ow % 4 == 0), out_dtype 0 = fp32, 1 = bf16 (RNE).
  * The flip / pad / crop of the TTA loader (data_prepare.py:263-270) is applied on these
  * outputs by the encoder (reidmi_vit_forward's tta offsets). */
 int reidmi_preprocess_u8(const uint8_t* pix, const int64_t* meta, int64_t B, int max_h, int max_w, int oh, int ow,

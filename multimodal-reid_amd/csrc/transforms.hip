@@ -10,7 +10,7 @@
 // and Normalize and are applied by the encoder's im2col (encoder.hip) on these outputs.
 //
 // Layout: the batch arrives packed (concatenated HWC uint8 images + per-image (byte offset,
-// h, w)); JPEG decode stays on the host.  One workgroup per (image, band of 16 output rows):
+// h, w)); JPEG decode stays on the host.  One workgroup per (image, band of 32 output rows):
 // the band's coefficient rows and its first-pass intermediate (source rows the band reads
 // x ow x 3 bytes) live in LDS, so every source byte is read from L2 a few times and every
 // output element is written once, coalesced along x.  Integer work, HBM-bound on the
@@ -19,7 +19,7 @@
 
 namespace reidmi {
 
-constexpr int PP_BAND = 16;   // output rows per workgroup
+constexpr int PP_BAND = 32;   // output rows per workgroup
 constexpr int PP_PREC = 22;   // Pillow PRECISION_BITS = 32 - 8 - 2
 
 __device__ __forceinline__ double pp_tri(double x) {
@@ -112,13 +112,15 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PPArgs a) {
     __syncthreads();
 
     const int64_t plane = (int64_t)oh * ow;
-    auto emit = [&](int yi, int x, int c, uint8_t p) {
-        const float v = lut[c * 256 + p];
+    // 4 consecutive outputs x..x+3 of channel c, row yi (ow % 4 == 0: 8- or 16-byte stores)
+    auto emit4 = [&](int yi, int x, int c, const uint8_t (&p)[4][3]) {
         const int64_t e = ((int64_t)b * 3 + c) * plane + (int64_t)(y_lo + yi) * ow + x;
+        const float v0 = lut[c * 256 + p[0][c]], v1 = lut[c * 256 + p[1][c]];
+        const float v2 = lut[c * 256 + p[2][c]], v3 = lut[c * 256 + p[3][c]];
         if (a.out_bf16)
-            ((unsigned short*)a.out)[e] = f2bf_bits(v);
+            *(u16x4*)((unsigned short*)a.out + e) = u16x4{f2bf_bits(v0), f2bf_bits(v1), f2bf_bits(v2), f2bf_bits(v3)};
         else
-            ((float*)a.out)[e] = v;
+            *(float4*)((float*)a.out + e) = make_float4(v0, v1, v2, v3);
     };
 
     if (!vfirst) {
@@ -154,32 +156,36 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PPArgs a) {
             }
         }
         __syncthreads();
-        // second pass: vertical -> output rows of the band
-        for (int it = tid; it < nb * ow; it += 256) {
-            const int yi = it / ow, x = it % ow;
-            uint8_t p0, p1, p2;
-            if (need_v) {
-                const int y0 = vb[2 * yi] - r0, n = vb[2 * yi + 1];
-                const int* k = vk + yi * KV;
-                int s0 = 1 << (PP_PREC - 1), s1 = s0, s2 = s0;
-                for (int j = 0; j < n; j++) {
-                    const uint8_t* q = mid + ((int64_t)(y0 + j) * ow + x) * 3;
-                    s0 += (int)q[0] * k[j];
-                    s1 += (int)q[1] * k[j];
-                    s2 += (int)q[2] * k[j];
+        // second pass: vertical -> output rows of the band, 4 consecutive x per thread
+        const int ow4 = ow >> 2;
+        for (int it = tid; it < nb * ow4; it += 256) {
+            const int yi = it / ow4, x = (it % ow4) * 4;
+            uint8_t p[4][3];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                if (need_v) {
+                    const int y0 = vb[2 * yi] - r0, n = vb[2 * yi + 1];
+                    const int* k = vk + yi * KV;
+                    int s0 = 1 << (PP_PREC - 1), s1 = s0, s2 = s0;
+                    for (int j = 0; j < n; j++) {
+                        const uint8_t* q = mid + ((int64_t)(y0 + j) * ow + x + u) * 3;
+                        s0 += (int)q[0] * k[j];
+                        s1 += (int)q[1] * k[j];
+                        s2 += (int)q[2] * k[j];
+                    }
+                    p[u][0] = pp_clip8(s0);
+                    p[u][1] = pp_clip8(s1);
+                    p[u][2] = pp_clip8(s2);
+                } else {
+                    const uint8_t* q = mid + ((int64_t)yi * ow + x + u) * 3;
+                    p[u][0] = q[0];
+                    p[u][1] = q[1];
+                    p[u][2] = q[2];
                 }
-                p0 = pp_clip8(s0);
-                p1 = pp_clip8(s1);
-                p2 = pp_clip8(s2);
-            } else {
-                const uint8_t* q = mid + ((int64_t)yi * ow + x) * 3;
-                p0 = q[0];
-                p1 = q[1];
-                p2 = q[2];
             }
-            emit(yi, x, 0, p0);
-            emit(yi, x, 1, p1);
-            emit(yi, x, 2, p2);
+            emit4(yi, x, 0, p);
+            emit4(yi, x, 1, p);
+            emit4(yi, x, 2, p);
         }
     } else {
         // tall narrow source (h > 100 w): vertical first over all w columns -> mid[yi][x'][c]
@@ -200,20 +206,28 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PPArgs a) {
             m[2] = pp_clip8(s2);
         }
         __syncthreads();
-        for (int it = tid; it < nb * ow; it += 256) {
-            const int yi = it / ow, x = it % ow;
-            const int x0 = hb[2 * x], n = hb[2 * x + 1];
-            const int* k = hk + x * KH;
-            int s0 = 1 << (PP_PREC - 1), s1 = s0, s2 = s0;
-            for (int i = 0; i < n; i++) {
-                const uint8_t* q = mid + ((int64_t)yi * w + x0 + i) * 3;
-                s0 += (int)q[0] * k[i];
-                s1 += (int)q[1] * k[i];
-                s2 += (int)q[2] * k[i];
+        const int ow4 = ow >> 2;
+        for (int it = tid; it < nb * ow4; it += 256) {
+            const int yi = it / ow4, x = (it % ow4) * 4;
+            uint8_t p[4][3];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int x0 = hb[2 * (x + u)], n = hb[2 * (x + u) + 1];
+                const int* k = hk + (x + u) * KH;
+                int s0 = 1 << (PP_PREC - 1), s1 = s0, s2 = s0;
+                for (int i = 0; i < n; i++) {
+                    const uint8_t* q = mid + ((int64_t)yi * w + x0 + i) * 3;
+                    s0 += (int)q[0] * k[i];
+                    s1 += (int)q[1] * k[i];
+                    s2 += (int)q[2] * k[i];
+                }
+                p[u][0] = pp_clip8(s0);
+                p[u][1] = pp_clip8(s1);
+                p[u][2] = pp_clip8(s2);
             }
-            emit(yi, x, 0, pp_clip8(s0));
-            emit(yi, x, 1, pp_clip8(s1));
-            emit(yi, x, 2, pp_clip8(s2));
+            emit4(yi, x, 0, p);
+            emit4(yi, x, 1, p);
+            emit4(yi, x, 2, p);
         }
     }
 }
@@ -249,6 +263,7 @@ REIDMI_API int reidmi_preprocess_u8(const uint8_t* pix, const int64_t* meta, int
     RM_REQUIRE(B >= 0 && oh > 0 && ow > 0 && max_h > 0 && max_w > 0, "preprocess: bad sizes");
     RM_REQUIRE(oh <= 65535 * PP_BAND && B <= 65535, "preprocess: grid too large (split the batch)");
     RM_REQUIRE(out_dtype == 0 || out_dtype == 1, "preprocess: out_dtype must be 0 (fp32) or 1 (bf16)");
+    RM_REQUIRE(ow % 4 == 0, "preprocess: output width must be a multiple of 4");
     RM_REQUIRE(mean && stdv && out && (B == 0 || (pix && meta)), "preprocess: null pointer");
     if (B == 0) return OK;
     PPArgs a{};
