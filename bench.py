@@ -347,7 +347,7 @@ def main():
             "embed_wall_s": round(embed_s / a.steps, 4),
             "mAP": round(float(mAP), 6),
             "rank1": round(float(cmc[0]), 6),
-            "roofline": {"bound": "mfma", "kernel": "gemm5_bf16_kernel<1> (mlp.c_fc + QuickGELU)",
+            "roofline": {"bound": "mfma", "kernel": "gemm5_bf16_kernel<1, true, true> (ln_2-folded fp16 mlp.c_fc + QuickGELU)",
                          "achieved": round(achieved, 1) if achieved else None, "peak": PEAK_BF16_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4) if achieved else None,
                          "traffic": C_FC_TRAFFIC_BYTES, "traffic_unit": "bytes/launch (PMC)", "avg_launch_ms": round(avg_ms, 4), "launches": cnt.value,

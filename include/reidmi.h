@@ -132,6 +132,15 @@ int reidmi_rr_jaccard_rows(const float* feat, int64_t N, int64_t D, int64_t ldf,
 int reidmi_gemm_bf16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N,
                      int64_t K, const float* bias, void* out, int64_t ldc, void* stream);
 
+/* fp16 GEMM (v_mfma_f32_16x16x32_f16) with an optional folded LayerNorm — the QKV / c_fc
+ * GEMMs of the encoders (ln_1 / ln_2 -> in_proj / c_fc, custom_clip_model.py:27-28):
+ * out = epi(rstd_m * (A W^T)_mn + (-mean_m rstd_m) * colsum_n + bias_n), rowstat float2
+ * (rstd, -mean * rstd) with round_up(M, 256) entries (those past M are read, not used) and
+ * colsum [N] fp32, both NULL for a plain GEMM (bias required with them).  A [M][lda], W [N][ldw]
+ * fp16; epi 0 (bf16 out) or 1 (QuickGELU bf16 out); shape rules as reidmi_gemm_bf16. */
+int reidmi_gemm_f16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N, int64_t K,
+                    const float* bias, const void* rowstat, const float* colsum, void* out, int64_t ldc, void* stream);
+
 /* Live timing of the bf16 GEMM launches (HIP events on the launch stream), used by bench.py
  * for the roofline of the dominant kernel.  collect: epi = GEMM epilogue id (-1 = all);
  * returns summed device ms, launch count, algorithmic FLOPs (2MNK) and clears the record. */
@@ -161,8 +170,14 @@ int reidmi_layernorm(const float* x, int64_t rows, int64_t ldx, const int32_t* r
 
 /* Per-block weights of a CLIP transformer block (ResidualAttentionBlock,
  * custom_clip_model.py:8-29 / ResidualAttentionBlock_IVLP, maple.py:579-644).
- * Matrices bf16 in PyTorch [out][in] layout, vectors fp32.  prompt: IVLP VPT_shallow
- * [n_ctx][W] (fp32) that replaces the prompt rows before this block, or NULL. */
+ * Matrices in PyTorch [out][in] layout, vectors fp32.  ln_1 / ln_2 are folded into the
+ * GEMM they feed:
+ *   qkv_w = fp16(in_proj_weight * ln_1.weight[None, :]), qkv_b = in_proj_bias + in_proj_weight @ ln_1.bias,
+ *   qkv_s[n] = sum_k qkv_w[n][k] (of the fp16 values, summed in double);
+ *   fc1_w / fc1_b / fc1_s likewise from mlp.c_fc and ln_2.
+ * out_w, fc2_w bf16.  ln1_w ... ln2_b are kept for reference (not read by the kernels).
+ * prompt: IVLP VPT_shallow [n_ctx][W] (fp32) that replaces the prompt rows before this
+ * block, or NULL. */
 typedef struct reidmi_block_weights {
     const float* ln1_w;
     const float* ln1_b;
@@ -177,6 +192,8 @@ typedef struct reidmi_block_weights {
     const void* fc2_w;
     const float* fc2_b;
     const float* prompt;
+    const float* qkv_s;
+    const float* fc1_s;
 } reidmi_block_weights;
 
 /* Vision tower: custom_clip_model.VisionTransformer (custom_clip_model.py:57-100) and the

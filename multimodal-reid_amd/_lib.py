@@ -26,6 +26,7 @@ SIGNATURES = {
     "reidmi_topk_rows_f32": [_vp, _i64, _i64, _i64, _vp, _i32, _vp, _vp, _i64, _vp],
     "reidmi_eval_rows": [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "reidmi_gemm_bf16": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _i64, _vp],
+    "reidmi_gemm_f16": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _vp],
     "reidmi_rerank_workspace_bytes": [_i64, _i64, _i32, _i32, _i32, _i32],
     "reidmi_rerank": [_vp, _i64, _i64, _i64, _i64, _i32, _i32, _u16, _f32, _vp, _i64, _vp, _i64, _vp, _vp],
     "reidmi_rerank_from_dist": [_vp, _vp, _i64, _i64, _i32, _i32, _i32, _u16, _f32, _vp, _i64, _vp, _i64, _vp,

@@ -5,11 +5,14 @@
 //   vision: custom_clip_model.VisionTransformer.forward (custom_clip_model.py:77-100),
 //           IVLP maple.VisionTransformer.forward (maple.py:754-785, blocks maple.py:617-644)
 //   text:   CLIP.encode_text (maple.py:971-984) / TextEncoder.forward (text_encoder.py:14-24)
-// Per block: LN1 -> QKV GEMM (head-split epilogue) -> fused MHSA -> out_proj GEMM (+residual)
-//            -> LN2 -> c_fc GEMM (+QuickGELU) -> c_proj GEMM (+residual).
+// Per block: LN1 stats -> QKV GEMM (fp16, LN folded, head-split epilogue) -> fused MHSA ->
+//            out_proj GEMM (+residual) -> LN2 stats -> c_fc GEMM (fp16, LN folded, +QuickGELU)
+//            -> c_proj GEMM (+residual).
 // The residual stream x is fp16 in HBM (the reference's GPU dtype, utils.py:145-166; every
-// residual add is computed in fp32 and rounded once); GEMM operands are bf16; LayerNorm
-// statistics are fp32.
+// residual add is computed in fp32 and rounded once).  ln_1 / ln_2 never materialise: the
+// QKV and c_fc GEMMs read x itself (fp16 operands) against W diag(gamma) and apply
+// rstd * acc - mean * rstd * colsum + (b + W beta) in their epilogues (gemm.h).  The other
+// GEMM operands (attention output, QuickGELU output) are bf16; LayerNorm statistics fp32.
 #include "gemm.h"
 
 namespace reidmi {
@@ -40,7 +43,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const TX* x, int64_t row
                                                         const float* __restrict__ beta, float eps,
                                                         float* __restrict__ y32, int64_t ldy32,
                                                         __bf16* __restrict__ y16, int64_t ldy16,
-                                                        _Float16* yh, int64_t ldyh) {
+                                                        _Float16* yh, int64_t ldyh, float2* __restrict__ st) {
     const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= rows) return;
     const int lane = threadIdx.x & 63;
@@ -62,6 +65,10 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const TX* x, int64_t row
         ss += (a * a + b * b) + (c * c + d * d);
     }
     const float rstd = __builtin_amdgcn_rsqf(wave_sum(ss) * invW + eps);
+    if (st) {  // statistics for a LayerNorm folded into the next GEMM (gemm.h EpiArgs)
+        if (lane == 0) st[r] = make_float2(rstd, -mean * rstd);
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < NV; i++) {
         const int f = lane + 64 * i;
@@ -86,7 +93,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const TX* x, int64_t row
 template <typename TX>
 int layernorm(const TX* x, int64_t rows, int64_t ldx, const int32_t* row_idx, int64_t W, const float* g,
               const float* b, float eps, float* y32, int64_t ldy32, __bf16* y16, int64_t ldy16, hipStream_t s,
-              _Float16* yh = nullptr, int64_t ldyh = 0) {
+              _Float16* yh = nullptr, int64_t ldyh = 0, float2* st = nullptr) {
     if (rows == 0) return OK;
     RM_REQUIRE(ldx % 4 == 0 && (!y32 || ldy32 % 4 == 0) && (!y16 || ldy16 % 4 == 0) && (!yh || ldyh % 4 == 0),
                "layernorm: strides");
@@ -94,21 +101,27 @@ int layernorm(const TX* x, int64_t rows, int64_t ldx, const int32_t* row_idx, in
     switch (W) {
         case 512:
             hipLaunchKernelGGL((layernorm_kernel<2, TX>), grid, dim3(256), 0, s, x, rows, ldx, row_idx, g, b, eps, y32,
-                               ldy32, y16, ldy16, yh, ldyh);
+                               ldy32, y16, ldy16, yh, ldyh, st);
             break;
         case 768:
             hipLaunchKernelGGL((layernorm_kernel<3, TX>), grid, dim3(256), 0, s, x, rows, ldx, row_idx, g, b, eps, y32,
-                               ldy32, y16, ldy16, yh, ldyh);
+                               ldy32, y16, ldy16, yh, ldyh, st);
             break;
         case 1024:
             hipLaunchKernelGGL((layernorm_kernel<4, TX>), grid, dim3(256), 0, s, x, rows, ldx, row_idx, g, b, eps, y32,
-                               ldy32, y16, ldy16, yh, ldyh);
+                               ldy32, y16, ldy16, yh, ldyh, st);
             break;
         default:
             return fail(EINVAL_, "layernorm: width must be 512, 768 or 1024");
     }
     RM_LAUNCHED();
     return OK;
+}
+
+// LayerNorm statistics only: st[r] = (rstd, -mean * rstd) of x row r (row stride ldx), the
+// per-row half of a LayerNorm folded into the following fp16 GEMM.
+static int row_stats(const _Float16* x, int64_t rows, int64_t ldx, int64_t W, float2* st, hipStream_t s) {
+    return layernorm(x, rows, ldx, nullptr, W, nullptr, nullptr, 1e-5f, nullptr, 0, nullptr, 0, s, nullptr, 0, st);
 }
 
 // fp16 residual rows -> fp32 output rows (x11 of encode_image / encode_cls)
@@ -225,7 +238,7 @@ __global__ void eot_rows_kernel(const int64_t* __restrict__ tokens, int64_t N, i
 
 // --------------------------------------------------------------- workspace plan
 struct Plan {
-    int64_t x, h, q, k, vt, o, u, rows, total;
+    int64_t x, h, q, k, vt, o, u, rows, st, st_cls, total;
 };
 
 static int64_t al(int64_t v) { return (v + 255) & ~(int64_t)255; }
@@ -242,41 +255,51 @@ static Plan plan(int64_t nseq, int L, int W, int lp, int64_t extra_rows) {
     p.o = off; off = al(off + M * W * 2);
     p.u = off; off = al(off + M * 4 * W * 2);
     p.rows = off; off = al(off + extra_rows * 4);
+    // LayerNorm statistics of every row / of the CLS rows (run_block_cls), padded to whole
+    // 256-row GEMM tiles (the folded GEMM reads them per tile, gemm.h)
+    p.st = off; off = al(off + (M + 256) * 8);
+    p.st_cls = off; off = al(off + (nseq + 256) * 8);
     p.total = off;
     return p;
 }
 
-// One ResidualAttentionBlock on the fp16 residual stream x [nseq*L][W].
+// One ResidualAttentionBlock on the fp16 residual stream x [nseq*L][W].  ln_1 / ln_2 are
+// folded into the QKV / c_fc GEMMs (fp16 operands: x itself and W diag(gamma)); only the
+// per-row statistics are computed here (row_stats), never the normalised activations.
 static int run_block(const reidmi_block_weights& bw, char* ws, const Plan& P, int64_t nseq, int L, int W, int H,
                      bool causal, hipStream_t s) {
     const int64_t M = nseq * L;
     _Float16* x = (_Float16*)(ws + P.x);
-    __bf16* h = (__bf16*)(ws + P.h);
     __bf16* o = (__bf16*)(ws + P.o);
     __bf16* u = (__bf16*)(ws + P.u);
+    float2* st = (float2*)(ws + P.st);
     int rc;
-    if ((rc = layernorm(x, M, W, nullptr, W, bw.ln1_w, bw.ln1_b, 1e-5f, nullptr, 0, h, W, s))) return rc;
+    if ((rc = row_stats(x, M, W, W, st, s))) return rc;  // ln_1 (custom_clip_model.py:27)
     EpiArgs ea{};
     ea.bias = bw.qkv_b;
+    ea.rowstat = st;
+    ea.colsum = bw.qkv_s;
     ea.q = ws + P.q;
     ea.k = ws + P.k;
     ea.vt = ws + P.vt;
     ea.seq = L;
     ea.heads = H;
     ea.lpad = attn_lpad(L);
-    if ((rc = gemm_bf16(EPI_QKV, h, W, bw.qkv_w, W, M, 3 * W, W, ea, s))) return rc;
+    if ((rc = gemm_f16(EPI_QKV, x, W, bw.qkv_w, W, M, 3 * W, W, ea, s))) return rc;
     if ((rc = mhsa(ws + P.q, ws + P.k, ws + P.vt, o, nseq, L, H, causal, s))) return rc;
     EpiArgs er{};
     er.out = x;
     er.ldc = W;
     er.bias = bw.out_b;
     if ((rc = gemm_bf16(EPI_RESID_F16, o, W, bw.out_w, W, M, W, W, er, s))) return rc;
-    if ((rc = layernorm(x, M, W, nullptr, W, bw.ln2_w, bw.ln2_b, 1e-5f, nullptr, 0, h, W, s))) return rc;
+    if ((rc = row_stats(x, M, W, W, st, s))) return rc;  // ln_2 (custom_clip_model.py:28)
     EpiArgs eg{};
     eg.out = u;
     eg.ldc = 4 * W;
     eg.bias = bw.fc1_b;
-    if ((rc = gemm_bf16(EPI_GELU_BF16, h, W, bw.fc1_w, W, M, 4 * W, W, eg, s))) return rc;
+    eg.rowstat = st;
+    eg.colsum = bw.fc1_s;
+    if ((rc = gemm_f16(EPI_GELU_BF16, x, W, bw.fc1_w, W, M, 4 * W, W, eg, s))) return rc;
     EpiArgs e2{};
     e2.out = x;
     e2.ldc = W;
@@ -288,49 +311,58 @@ static int run_block(const reidmi_block_weights& bw, char* ws, const Plan& P, in
 // The last block when only the CLS row of its output is consumed (inference path,
 // zero_shot_learning.py:85-87 reads x12[:,0] / xproj[:,0]): K and V for every token, then
 // Q, attention, out_proj, LN2 and the MLP for the CLS rows only.  Every CLS-row value is
-// computed by the same kernels in the same order as in run_block, so the result is
-// bit-identical to the full block's row 0 (tests/test_gpu_encoder.py checks equality).
+// computed by the same kernels in the same order as in run_block (row statistics are per
+// row, GEMM outputs per element), so the result is bit-identical to the full block's row 0
+// (tests/test_gpu_encoder.py checks equality).
 static int run_block_cls(const reidmi_block_weights& bw, char* ws, const Plan& P, int64_t nseq, int L, int W, int H,
                          hipStream_t s) {
     const int64_t M = nseq * L;
     _Float16* x = (_Float16*)(ws + P.x);
-    __bf16* h = (__bf16*)(ws + P.h);
     __bf16* o = (__bf16*)(ws + P.o);
     __bf16* u = (__bf16*)(ws + P.u);
+    float2* st = (float2*)(ws + P.st);
+    float2* sc = (float2*)(ws + P.st_cls);
+    const int64_t ldc = (int64_t)L * W;  // CLS row of each sequence
     int rc;
-    if ((rc = layernorm(x, M, W, nullptr, W, bw.ln1_w, bw.ln1_b, 1e-5f, nullptr, 0, h, W, s))) return rc;
+    if ((rc = row_stats(x, M, W, W, st, s))) return rc;
+    if ((rc = row_stats(x, nseq, ldc, W, sc, s))) return rc;
     EpiArgs kv{};
     kv.bias = bw.qkv_b + W;
+    kv.rowstat = st;
+    kv.colsum = bw.qkv_s + W;
     kv.k = ws + P.k;
     kv.vt = ws + P.vt;
     kv.seq = L;
     kv.heads = H;
     kv.lpad = attn_lpad(L);
     kv.n_off = W;
-    if ((rc = gemm_bf16(EPI_QKV, h, W, (const __bf16*)bw.qkv_w + (int64_t)W * W, W, M, 2 * W, W, kv, s))) return rc;
+    if ((rc = gemm_f16(EPI_QKV, x, W, (const _Float16*)bw.qkv_w + (int64_t)W * W, W, M, 2 * W, W, kv, s))) return rc;
     EpiArgs qa{};
     qa.bias = bw.qkv_b;
+    qa.rowstat = sc;
+    qa.colsum = bw.qkv_s;
     qa.q = ws + P.q;
     qa.seq = 1;  // one (CLS) row per sequence: q [nseq*H][1][64]
     qa.heads = H;
     qa.lpad = 1;
-    if ((rc = gemm_bf16(EPI_QKV, h, (int64_t)L * W, bw.qkv_w, W, nseq, W, W, qa, s))) return rc;
+    if ((rc = gemm_f16(EPI_QKV, x, ldc, bw.qkv_w, W, nseq, W, W, qa, s))) return rc;
     if ((rc = mhsa_cls(ws + P.q, ws + P.k, ws + P.vt, o, nseq, L, H, s))) return rc;
     EpiArgs er{};
     er.out = x;
-    er.ldc = (int64_t)L * W;
+    er.ldc = ldc;
     er.bias = bw.out_b;
     if ((rc = gemm_bf16(EPI_RESID_F16, o, W, bw.out_w, W, nseq, W, W, er, s))) return rc;
-    if ((rc = layernorm(x, nseq, (int64_t)L * W, nullptr, W, bw.ln2_w, bw.ln2_b, 1e-5f, nullptr, 0, h, W, s)))
-        return rc;
+    if ((rc = row_stats(x, nseq, ldc, W, sc, s))) return rc;
     EpiArgs eg{};
     eg.out = u;
     eg.ldc = 4 * W;
     eg.bias = bw.fc1_b;
-    if ((rc = gemm_bf16(EPI_GELU_BF16, h, W, bw.fc1_w, W, nseq, 4 * W, W, eg, s))) return rc;
+    eg.rowstat = sc;
+    eg.colsum = bw.fc1_s;
+    if ((rc = gemm_f16(EPI_GELU_BF16, x, ldc, bw.fc1_w, W, nseq, 4 * W, W, eg, s))) return rc;
     EpiArgs e2{};
     e2.out = x;
-    e2.ldc = (int64_t)L * W;
+    e2.ldc = ldc;
     e2.bias = bw.fc2_b;
     return gemm_bf16(EPI_RESID_F16, u, 4 * W, bw.fc2_w, 4 * W, nseq, W, 4 * W, e2, s);
 }

@@ -1,4 +1,4 @@
-// gemm.h — bf16 MFMA GEMM with fused epilogues for the CLIP encoders (gfx950).
+// gemm.h — bf16 / fp16 MFMA GEMM with fused epilogues for the CLIP encoders (gfx950).
 //
 // C[M,N] = A[M,K] . W[N,K]^T (+ bias[N]), A row-major bf16 (activations), W row-major bf16
 // (PyTorch Linear / conv weight layout [out, in]), fp32 accumulation on
@@ -41,11 +41,23 @@ struct EpiArgs {
     // PATCH
     const float* pos;  // [1+NP][N]
     int npatch;        // NP
+    // LayerNorm folded into an fp16 GEMM (gemm_f16): with W' = W diag(gamma) (fp16),
+    // s_n = sum_k W'[n,k], b' = b + W beta (the bias above):
+    //   LN(x) W^T + b = rstd_m * (x W'^T)_mn + (-mean_m rstd_m) * s_n + b'_n
+    const float2* rowstat;  // [round_up(M, 256)] (rstd, -mean*rstd) of the A rows (entries
+                            // past M are read, not used), or null (no fold)
+    const float* colsum;    // [N] s_n
 };
 
 // Launch C = A . W^T with epilogue `epi`.  Requires N % 128 == 0, K % 64 == 0,
 // lda/ldw multiples of 8 (16-byte rows); M arbitrary.
 int gemm_bf16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N, int64_t K,
               const EpiArgs& ea, hipStream_t stream);
+
+// Same with fp16 operands (v_mfma_f32_16x16x32_f16): A = the fp16 residual stream, W = an
+// fp16 LayerNorm-folded weight; epi in {EPI_BF16, EPI_GELU_BF16, EPI_QKV}; ea.rowstat /
+// ea.colsum enable the fold.
+int gemm_f16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N, int64_t K,
+             const EpiArgs& ea, hipStream_t stream);
 
 }  // namespace reidmi

@@ -68,6 +68,45 @@ __device__ __forceinline__ float quick_gelu(float x) {
     return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -2.4554669595930157f));
 }
 
+// One 16x16x32 MFMA on 16-byte fragments holding bf16 or (F16) fp16 values.
+template <bool F16>
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& w, const bf16x8& a, const f32x4& c) {
+    if constexpr (F16)
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, w), __builtin_bit_cast(f16x8, a), c, 0,
+                                                      0, 0);
+    else
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, a, c, 0, 0, 0);
+}
+
+// LayerNorm fold (see gemm.h EpiArgs) with the bias: acc <- rstd_m * acc + (-mean_m rstd_m
+// * s_n + b'_n), two FMAs per element (bias b'_n of the lane's columns passed in bn).  Lane
+// layout as epilogue_tile; rows past M read row M-1.
+template <int NI>
+__device__ __forceinline__ void ln_fold(f32x4 (&acc)[NI][4], const float2* __restrict__ rowstat,
+                                        const float* __restrict__ colsum, const float4 (&bn)[4], int64_t mrow,
+                                        int ncol, int64_t M) {
+    const int lane = threadIdx.x & 63;
+    const int cq = (lane >> 4) * 4;
+    float4 sn[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) sn[j] = *(const float4*)(colsum + ncol + j * 16 + cq);
+    float2 rs[NI];
+#pragma unroll
+    for (int i = 0; i < NI; i++) {
+        int64_t m = mrow + i * 16 + (lane & 15);
+        rs[i] = rowstat[m < M ? m : M - 1];
+    }
+#pragma unroll
+    for (int i = 0; i < NI; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            acc[i][j][0] = __builtin_fmaf(rs[i].x, acc[i][j][0], __builtin_fmaf(rs[i].y, sn[j].x, bn[j].x));
+            acc[i][j][1] = __builtin_fmaf(rs[i].x, acc[i][j][1], __builtin_fmaf(rs[i].y, sn[j].y, bn[j].y));
+            acc[i][j][2] = __builtin_fmaf(rs[i].x, acc[i][j][2], __builtin_fmaf(rs[i].y, sn[j].z, bn[j].z));
+            acc[i][j][3] = __builtin_fmaf(rs[i].x, acc[i][j][3], __builtin_fmaf(rs[i].y, sn[j].w, bn[j].w));
+        }
+}
+
 // Epilogue of one wave's output block: NI row groups x 4 column groups of 16x16, lane
 // holding C[m][nb..nb+3] with m = mrow + i*16 + (lane&15), nb = ncol + j*16 + (lane>>4)*4
 // (see gemm.h for the modes).  All loads are hoisted ahead of the stores they feed: bias
@@ -285,7 +324,7 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
     }
 }
 
-template <int EPI>
+template <int EPI, bool F16>
 __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(const __bf16* __restrict__ A, int64_t lda,
                                                            const __bf16* __restrict__ W, int64_t ldw, int64_t M,
                                                            int N, int K, EpiArgs ea, int tiles_n, int nwg) {
@@ -363,13 +402,25 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(const __bf16* __restr
             for (int i = 0; i < 4; i++)
 #pragma unroll
                 for (int j = 0; j < 4; j++)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af[i], acc[i][j], 0, 0, 0);
+                    acc[i][j] = mfma16<F16>(wf[j], af[i], acc[i][j]);
         }
         if (kt + 1 < nk) LSTORE(cur ^ 1);
         __syncthreads();
     }
 
     // ------------------------------------------------------------------ epilogue
+    if constexpr (F16) {
+        if (ea.rowstat) {
+            float4 bn[4];
+            const int cq = (lane >> 4) * 4;
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                bn[j] = ea.bias ? *(const float4*)(ea.bias + n0 + wn * 64 + j * 16 + cq) : make_float4(0.f, 0.f, 0.f, 0.f);
+            ln_fold<4>(acc, ea.rowstat, ea.colsum, bn, m0 + wm * 64, n0 + wn * 64, M);
+            epilogue_tile<EPI, 4, true>(ea, acc, m0 + wm * 64, n0 + wn * 64, M, N);
+            return;
+        }
+    }
     epilogue_tile<EPI, 4>(ea, acc, m0 + wm * 64, n0 + wn * 64, M, N);
 #undef GLOAD
 #undef LSTORE
@@ -658,8 +709,7 @@ __global__ __launch_bounds__(512, 2) void gemm4_bf16_kernel(const __bf16* __rest
             for (int i = 0; i < 4; i++)
 #pragma unroll
                 for (int j = 0; j < 2; j++)
-                    acc[qm * 4 + i][qn * 2 + j] =
-                        __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][ks], fa[i][ks], acc[qm * 4 + i][qn * 2 + j], 0, 0, 0);
+                    acc[qm * 4 + i][qn * 2 + j] = mfma16<false>(fb[j][ks], fa[i][ks], acc[qm * 4 + i][qn * 2 + j]);
     };
 
     const int nk = K / GB_K;
@@ -761,7 +811,7 @@ struct EpiVm {  // vector-memory instructions of one full-tile epilogue_tile<EPI
                                                                                           : -1;
 };
 
-template <int EPI, bool DEFER>
+template <int EPI, bool DEFER, bool F16>
 __global__ __launch_bounds__(512, 2) void gemm5_bf16_kernel(const __bf16* __restrict__ A, int64_t lda,
                                                             const __bf16* __restrict__ W, int64_t ldw, int64_t M,
                                                             int N, int K, EpiArgs ea, int tiles_n, int ntiles) {
@@ -869,8 +919,7 @@ __global__ __launch_bounds__(512, 2) void gemm5_bf16_kernel(const __bf16* __rest
             for (int i = 0; i < 4; i++)
 #pragma unroll
                 for (int j = 0; j < 2; j++)
-                    acc[qm * 4 + i][qn * 2 + j] =
-                        __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][ks], fa[i][ks], acc[qm * 4 + i][qn * 2 + j], 0, 0, 0);
+                    acc[qm * 4 + i][qn * 2 + j] = mfma16<F16>(fb[j][ks], fa[i][ks], acc[qm * 4 + i][qn * 2 + j]);
     };
 
     // Bias of the current tile: one LDS-DMA per wave at the tile's first K-step into the
@@ -878,6 +927,12 @@ __global__ __launch_bounds__(512, 2) void gemm5_bf16_kernel(const __bf16* __rest
     // B0 DMA, so the step's vmcnt(6) retires it.  The epilogue reads it with ds_read.
     const bool has_bias = EPI != EPI_PATCH && ea.bias != nullptr;
     float* bias_slot = (float*)(lds5 + 2 * G2_STAGE) + wid * 256;
+    // Folded LayerNorm (F16): colsum of the tile's 256 columns and (rstd, -mean rstd) of the
+    // wave's 128 rows go to LDS by the same DMA at the tile's first K-step (the rowstat
+    // buffer is padded to whole 256-row tiles, gemm.h).
+    const bool fold = F16 && ea.rowstat != nullptr;
+    float* cs_slot = bias_slot + 8 * 256;
+    float* rs_slot = bias_slot + 16 * 256;
     // streams: p1 = step s+1 (region B0), p2 = step s+2 (A0, B1, A1); requires nk >= 2
     Pos p1, p2;
     {
@@ -917,6 +972,15 @@ __global__ __launch_bounds__(512, 2) void gemm5_bf16_kernel(const __bf16* __rest
             if (kt == 0 && has_bias)
                 __builtin_amdgcn_global_load_lds(ea.bias + (tile % tiles_n) * G2_N + lane * 4, (lds_ptr_t)bias_slot,
                                                  16, 0, 0);
+            if constexpr (F16) {
+                if (kt == 0 && fold) {
+                    __builtin_amdgcn_global_load_lds(ea.colsum + (tile % tiles_n) * G2_N + lane * 4,
+                                                     (lds_ptr_t)cs_slot, 16, 0, 0);
+                    __builtin_amdgcn_global_load_lds((const float*)(ea.rowstat + (int64_t)(tile / tiles_n) * G2_M +
+                                                                    wr * 128) + lane * 4,
+                                                     (lds_ptr_t)rs_slot, 16, 0, 0);
+                }
+            }
             if (has1 && !b0_early) issue_w(buf ^ 1, 0, p1);
             G5_LDS_DONE();
             G5_BARRIER();
@@ -943,8 +1007,10 @@ __global__ __launch_bounds__(512, 2) void gemm5_bf16_kernel(const __bf16* __rest
                 G5_LDS_DONE();
                 if constexpr (CAN_DEFER) {
                     constexpr int S = EpiVm<EPI>::count;
-                    if (kt == 0 && deferred) {
-                        if (has_bias)
+                    if (kt == 0 && deferred) {  // + the first K-step's bias / colsum / rowstat DMAs
+                        if (fold)
+                            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(S + 9) : "memory");
+                        else if (has_bias)
                             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(S + 7) : "memory");
                         else
                             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(S + 6) : "memory");
@@ -991,15 +1057,63 @@ __global__ __launch_bounds__(512, 2) void gemm5_bf16_kernel(const __bf16* __rest
 #pragma unroll
                 for (int j = 0; j < 4; j++) b[j] = *(const float4*)(bias_slot + wc * 64 + j * 16 + (lane >> 4) * 4);
             }
+            if constexpr (F16) {
+                // acc <- rstd * acc + (-mean rstd * s_n + b'_n); without a fold (rstd, s) = (1, 0):
+                // fma(1, acc, fma(0, 0, b)) == acc + b exactly.  One branch-free update (a
+                // branch on acc would duplicate the 128 accumulators).
+                float4 sn[4];
+                float2 rs[8];
+                if (fold) {
+                    if constexpr (DEFER) {
+                        const uint32_t ca = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)(
+                            cs_slot + wc * 64 + (lane >> 4) * 4);
+                        const uint32_t ra = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)(
+                            rs_slot + (lane & 15) * 2);
+                        asm volatile("ds_read_b128 %0, %1" : "=v"(sn[0]) : "v"(ca) : "memory");
+                        asm volatile("ds_read_b128 %0, %1 offset:64" : "=v"(sn[1]) : "v"(ca) : "memory");
+                        asm volatile("ds_read_b128 %0, %1 offset:128" : "=v"(sn[2]) : "v"(ca) : "memory");
+                        asm volatile("ds_read_b128 %0, %1 offset:192" : "=v"(sn[3]) : "v"(ca) : "memory");
+                        asm volatile("ds_read_b64 %0, %1" : "=v"(rs[0]) : "v"(ra) : "memory");
+                        asm volatile("ds_read_b64 %0, %1 offset:128" : "=v"(rs[1]) : "v"(ra) : "memory");
+                        asm volatile("ds_read_b64 %0, %1 offset:256" : "=v"(rs[2]) : "v"(ra) : "memory");
+                        asm volatile("ds_read_b64 %0, %1 offset:384" : "=v"(rs[3]) : "v"(ra) : "memory");
+                        asm volatile("ds_read_b64 %0, %1 offset:512" : "=v"(rs[4]) : "v"(ra) : "memory");
+                        asm volatile("ds_read_b64 %0, %1 offset:640" : "=v"(rs[5]) : "v"(ra) : "memory");
+                        asm volatile("ds_read_b64 %0, %1 offset:768" : "=v"(rs[6]) : "v"(ra) : "memory");
+                        asm volatile("ds_read_b64 %0, %1 offset:896" : "=v"(rs[7]) : "v"(ra) : "memory");
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    } else {
 #pragma unroll
-            for (int i = 0; i < 8; i++)
+                        for (int j = 0; j < 4; j++) sn[j] = *(const float4*)(cs_slot + wc * 64 + j * 16 + (lane >> 4) * 4);
 #pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    acc[i][j][0] += b[j].x;
-                    acc[i][j][1] += b[j].y;
-                    acc[i][j][2] += b[j].z;
-                    acc[i][j][3] += b[j].w;
+                        for (int i = 0; i < 8; i++) rs[i] = *(const float2*)(rs_slot + (i * 16 + (lane & 15)) * 2);
+                    }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; j++) sn[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                    for (int i = 0; i < 8; i++) rs[i] = make_float2(1.f, 0.f);
                 }
+#pragma unroll
+                for (int i = 0; i < 8; i++)
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        acc[i][j][0] = __builtin_fmaf(rs[i].x, acc[i][j][0], __builtin_fmaf(rs[i].y, sn[j].x, b[j].x));
+                        acc[i][j][1] = __builtin_fmaf(rs[i].x, acc[i][j][1], __builtin_fmaf(rs[i].y, sn[j].y, b[j].y));
+                        acc[i][j][2] = __builtin_fmaf(rs[i].x, acc[i][j][2], __builtin_fmaf(rs[i].y, sn[j].z, b[j].z));
+                        acc[i][j][3] = __builtin_fmaf(rs[i].x, acc[i][j][3], __builtin_fmaf(rs[i].y, sn[j].w, b[j].w));
+                    }
+            } else {
+#pragma unroll
+                for (int i = 0; i < 8; i++)
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        acc[i][j][0] += b[j].x;
+                        acc[i][j][1] += b[j].y;
+                        acc[i][j][2] += b[j].z;
+                        acc[i][j][3] += b[j].w;
+                    }
+            }
         }
         epilogue_tile<EPI, 8, true>(ea, acc, m0 + wr * 128, n0 + wc * 64, M, N);
     }
@@ -1008,36 +1122,37 @@ __global__ __launch_bounds__(512, 2) void gemm5_bf16_kernel(const __bf16* __rest
 #undef G5_LDS_DONE
 }
 
-template <int EPI>
+template <int EPI, bool F16>
 static int launch(const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N, int64_t K,
                   const EpiArgs& ea, hipStream_t s) {
-    const int var = variant();
+    int var = variant();
+    if (F16 && var >= 2 && var <= 4) var = 0;  // fp16 operands: v1 / v5 / v6 only
     const int64_t tiles256 = (int64_t)ceil_div(M, G2_M) * (N / G2_N);
     if (N % G2_N == 0 && K >= 2 * GB_K && lda * G2_M < (1ll << 31) && ldw * G2_N < (1ll << 31) &&
         (var == 5 || var == 6 || (var == 0 && tiles256 >= 256))) {
         const int tiles_m = ceil_div(M, G2_M), tiles_n = (int)(N / G2_N);
         const int64_t ntiles = (int64_t)tiles_m * tiles_n;
         RM_REQUIRE(ntiles < (1ll << 31), "gemm: grid too large");
-        const size_t lds = 2 * (size_t)G2_STAGE * 2 + 8 * 256 * sizeof(float);
+        const size_t lds = 2 * (size_t)G2_STAGE * 2 + (F16 ? 3 : 1) * 8 * 256 * sizeof(float);
         static bool attr5 = false;
         if (!attr5) {
-            RM_CHECK_HIP(hipFuncSetAttribute((const void*)gemm5_bf16_kernel<EPI, false>,
+            RM_CHECK_HIP(hipFuncSetAttribute((const void*)gemm5_bf16_kernel<EPI, false, F16>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            RM_CHECK_HIP(hipFuncSetAttribute((const void*)gemm5_bf16_kernel<EPI, true>,
+            RM_CHECK_HIP(hipFuncSetAttribute((const void*)gemm5_bf16_kernel<EPI, true, F16>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
             attr5 = true;
         }
         const int grid = (int)(ntiles < 256 ? ntiles : 256);
         if (var == 6 || var == 0)
-            hipLaunchKernelGGL((gemm5_bf16_kernel<EPI, true>), dim3((unsigned)grid), dim3(512), lds, s,
+            hipLaunchKernelGGL((gemm5_bf16_kernel<EPI, true, F16>), dim3((unsigned)grid), dim3(512), lds, s,
                                (const __bf16*)A, lda, (const __bf16*)W, ldw, M, (int)N, (int)K, ea, tiles_n, (int)ntiles);
         else
-            hipLaunchKernelGGL((gemm5_bf16_kernel<EPI, false>), dim3((unsigned)grid), dim3(512), lds, s,
+            hipLaunchKernelGGL((gemm5_bf16_kernel<EPI, false, F16>), dim3((unsigned)grid), dim3(512), lds, s,
                                (const __bf16*)A, lda, (const __bf16*)W, ldw, M, (int)N, (int)K, ea, tiles_n, (int)ntiles);
         RM_LAUNCHED();
         return OK;
     }
-    if (N % G2_N == 0 && var == 4) {
+    if (!F16 && N % G2_N == 0 && var == 4) {
         const int tiles_m = ceil_div(M, G2_M), tiles_n = (int)(N / G2_N);
         const int64_t nwg = (int64_t)tiles_m * tiles_n;
         RM_REQUIRE(nwg < (1ll << 31), "gemm: grid too large");
@@ -1053,7 +1168,7 @@ static int launch(const void* A, int64_t lda, const void* W, int64_t ldw, int64_
         RM_LAUNCHED();
         return OK;
     }
-    if (N % G2_N == 0 && var == 3) {
+    if (!F16 && N % G2_N == 0 && var == 3) {
         const int tiles_m = ceil_div(M, G2_M), tiles_n = (int)(N / G2_N);
         const int64_t ntiles = (int64_t)tiles_m * tiles_n;
         RM_REQUIRE(ntiles < (1ll << 31), "gemm: grid too large");
@@ -1070,7 +1185,7 @@ static int launch(const void* A, int64_t lda, const void* W, int64_t ldw, int64_
         RM_LAUNCHED();
         return OK;
     }
-    if (N % G2_N == 0 && var != 1 && (var == 2 || (int64_t)ceil_div(M, G2_M) * (N / G2_N) >= 512)) {
+    if (!F16 && N % G2_N == 0 && var != 1 && (var == 2 || (int64_t)ceil_div(M, G2_M) * (N / G2_N) >= 512)) {
         const int tiles_m = ceil_div(M, G2_M), tiles_n = (int)(N / G2_N);
         const int64_t nwg = (int64_t)tiles_m * tiles_n;
         RM_REQUIRE(nwg < (1ll << 31), "gemm: grid too large");
@@ -1089,14 +1204,15 @@ static int launch(const void* A, int64_t lda, const void* W, int64_t ldw, int64_
     const int tiles_m = ceil_div(M, GB_M), tiles_n = (int)(N / GB_N);
     const int64_t nwg = (int64_t)tiles_m * tiles_n;
     RM_REQUIRE(nwg < (1ll << 31), "gemm: grid too large");
-    hipLaunchKernelGGL(gemm_bf16_kernel<EPI>, dim3((unsigned)nwg), dim3(256), 0, s, (const __bf16*)A, lda,
+    hipLaunchKernelGGL((gemm_bf16_kernel<EPI, F16>), dim3((unsigned)nwg), dim3(256), 0, s, (const __bf16*)A, lda,
                        (const __bf16*)W, ldw, M, (int)N, (int)K, ea, tiles_n, (int)nwg);
     RM_LAUNCHED();
     return OK;
 }
 
-int gemm_bf16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N, int64_t K,
-              const EpiArgs& ea, hipStream_t s) {
+template <bool F16>
+static int gemm_any(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N, int64_t K,
+                    const EpiArgs& ea, hipStream_t s) {
     RM_REQUIRE(M >= 0 && N > 0 && K > 0, "gemm: bad shape");
     RM_REQUIRE(N % GB_N == 0 && K % GB_K == 0, "gemm: needs N % 128 == 0 and K % 64 == 0");
     RM_REQUIRE(lda % 8 == 0 && ldw % 8 == 0 && lda >= K && ldw >= K, "gemm: lda/ldw must be >= K and 16-byte rows");
@@ -1119,18 +1235,39 @@ int gemm_bf16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, i
         ev_b = pr.second;
     }
     int rc;
-    switch (epi) {
-        case EPI_BF16: rc = launch<EPI_BF16>(A, lda, W, ldw, M, N, K, ea, s); break;
-        case EPI_GELU_BF16: rc = launch<EPI_GELU_BF16>(A, lda, W, ldw, M, N, K, ea, s); break;
-        case EPI_RESID_F32: rc = launch<EPI_RESID_F32>(A, lda, W, ldw, M, N, K, ea, s); break;
-        case EPI_QKV: rc = launch<EPI_QKV>(A, lda, W, ldw, M, N, K, ea, s); break;
-        case EPI_PATCH: rc = launch<EPI_PATCH>(A, lda, W, ldw, M, N, K, ea, s); break;
-        case EPI_F32: rc = launch<EPI_F32>(A, lda, W, ldw, M, N, K, ea, s); break;
-        case EPI_RESID_F16: rc = launch<EPI_RESID_F16>(A, lda, W, ldw, M, N, K, ea, s); break;
-        default: return fail(EINVAL_, "gemm: unknown epilogue");
+    if constexpr (F16) {
+        switch (epi) {
+            case EPI_BF16: rc = launch<EPI_BF16, true>(A, lda, W, ldw, M, N, K, ea, s); break;
+            case EPI_GELU_BF16: rc = launch<EPI_GELU_BF16, true>(A, lda, W, ldw, M, N, K, ea, s); break;
+            case EPI_QKV: rc = launch<EPI_QKV, true>(A, lda, W, ldw, M, N, K, ea, s); break;
+            default: return fail(EINVAL_, "gemm_f16: epilogue must be EPI_BF16, EPI_GELU_BF16 or EPI_QKV");
+        }
+    } else {
+        switch (epi) {
+            case EPI_BF16: rc = launch<EPI_BF16, false>(A, lda, W, ldw, M, N, K, ea, s); break;
+            case EPI_GELU_BF16: rc = launch<EPI_GELU_BF16, false>(A, lda, W, ldw, M, N, K, ea, s); break;
+            case EPI_RESID_F32: rc = launch<EPI_RESID_F32, false>(A, lda, W, ldw, M, N, K, ea, s); break;
+            case EPI_QKV: rc = launch<EPI_QKV, false>(A, lda, W, ldw, M, N, K, ea, s); break;
+            case EPI_PATCH: rc = launch<EPI_PATCH, false>(A, lda, W, ldw, M, N, K, ea, s); break;
+            case EPI_F32: rc = launch<EPI_F32, false>(A, lda, W, ldw, M, N, K, ea, s); break;
+            case EPI_RESID_F16: rc = launch<EPI_RESID_F16, false>(A, lda, W, ldw, M, N, K, ea, s); break;
+            default: return fail(EINVAL_, "gemm: unknown epilogue");
+        }
     }
     if (ev_b) RM_CHECK_HIP(hipEventRecord(ev_b, s));
     return rc;
+}
+
+int gemm_bf16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N, int64_t K,
+              const EpiArgs& ea, hipStream_t s) {
+    return gemm_any<false>(epi, A, lda, W, ldw, M, N, K, ea, s);
+}
+
+int gemm_f16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N, int64_t K,
+             const EpiArgs& ea, hipStream_t s) {
+    RM_REQUIRE((ea.rowstat == nullptr) == (ea.colsum == nullptr), "gemm_f16: rowstat and colsum go together");
+    RM_REQUIRE(ea.rowstat == nullptr || ea.bias != nullptr, "gemm_f16: a folded LayerNorm needs the folded bias");
+    return gemm_any<true>(epi, A, lda, W, ldw, M, N, K, ea, s);
 }
 
 }  // namespace reidmi
@@ -1173,6 +1310,19 @@ REIDMI_API int reidmi_prof_collect(int epi, double* total_ms, int64_t* count, do
     prof::recs.clear();
     prof::used = 0;
     return OK;
+}
+
+REIDMI_API int reidmi_gemm_f16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N,
+                               int64_t K, const float* bias, const void* rowstat, const float* colsum, void* out,
+                               int64_t ldc, void* stream) {
+    RM_REQUIRE(epi == EPI_BF16 || epi == EPI_GELU_BF16, "reidmi_gemm_f16: epi must be 0 (bf16) or 1 (gelu bf16)");
+    EpiArgs ea{};
+    ea.out = out;
+    ea.ldc = ldc;
+    ea.bias = bias;
+    ea.rowstat = (const float2*)rowstat;
+    ea.colsum = colsum;
+    return gemm_f16(epi, A, lda, W, ldw, M, N, K, ea, (hipStream_t)stream);
 }
 
 REIDMI_API int reidmi_gemm_bf16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N,

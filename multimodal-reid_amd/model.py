@@ -28,7 +28,7 @@ _i32 = ctypes.c_int32
 
 class BlockWeights(ctypes.Structure):
     _fields_ = [(n, _vp) for n in ("ln1_w", "ln1_b", "qkv_w", "qkv_b", "out_w", "out_b", "ln2_w", "ln2_b",
-                                   "fc1_w", "fc1_b", "fc2_w", "fc2_b", "prompt")]
+                                   "fc1_w", "fc1_b", "fc2_w", "fc2_b", "prompt", "qkv_s", "fc1_s")]
 
 
 class VitWeights(ctypes.Structure):
@@ -86,6 +86,22 @@ class _Packer:
         self.keep.append(t)
         return t
 
+    def keep_dev(self, t):
+        t = t.contiguous().to(self.device)
+        self.keep.append(t)
+        return t
+
+
+def fold_layernorm(w, b, gamma, beta):
+    """LayerNorm(gamma, beta) folded into the Linear (w, b) it feeds (load time, fp64):
+    LN(x) w^T + b = rstd (x w'^T - mean s) + b' with w' = fp16(w diag(gamma)),
+    s_n = sum_k w'[n, k] (of the fp16 values) and b' = b + w beta.  Returns (w' fp16, s, b')."""
+    w64, g64 = _t(w).double(), _t(gamma).double()
+    wf = (w64 * g64[None, :]).to(torch.float16)
+    s = wf.double().sum(1).float()
+    bf = (_t(b).double() + w64 @ _t(beta).double()).float()
+    return wf, s, bf
+
 
 def _pack_blocks(sd, prefix, layers, pk):
     arr = (BlockWeights * layers)()
@@ -94,14 +110,20 @@ def _pack_blocks(sd, prefix, layers, pk):
         b = arr[i]
         b.ln1_w = pk.f32(sd[p + "ln_1.weight"]).data_ptr()
         b.ln1_b = pk.f32(sd[p + "ln_1.bias"]).data_ptr()
-        b.qkv_w = pk.bf16(sd[p + "attn.in_proj_weight"]).data_ptr()
-        b.qkv_b = pk.f32(sd[p + "attn.in_proj_bias"]).data_ptr()
+        wf, cs, bf = fold_layernorm(sd[p + "attn.in_proj_weight"], sd[p + "attn.in_proj_bias"],
+                                    sd[p + "ln_1.weight"], sd[p + "ln_1.bias"])
+        b.qkv_w = pk.keep_dev(wf).data_ptr()
+        b.qkv_b = pk.keep_dev(bf).data_ptr()
+        b.qkv_s = pk.keep_dev(cs).data_ptr()
         b.out_w = pk.bf16(sd[p + "attn.out_proj.weight"]).data_ptr()
         b.out_b = pk.f32(sd[p + "attn.out_proj.bias"]).data_ptr()
         b.ln2_w = pk.f32(sd[p + "ln_2.weight"]).data_ptr()
         b.ln2_b = pk.f32(sd[p + "ln_2.bias"]).data_ptr()
-        b.fc1_w = pk.bf16(sd[p + "mlp.c_fc.weight"]).data_ptr()
-        b.fc1_b = pk.f32(sd[p + "mlp.c_fc.bias"]).data_ptr()
+        wf, cs, bf = fold_layernorm(sd[p + "mlp.c_fc.weight"], sd[p + "mlp.c_fc.bias"],
+                                    sd[p + "ln_2.weight"], sd[p + "ln_2.bias"])
+        b.fc1_w = pk.keep_dev(wf).data_ptr()
+        b.fc1_b = pk.keep_dev(bf).data_ptr()
+        b.fc1_s = pk.keep_dev(cs).data_ptr()
         b.fc2_w = pk.bf16(sd[p + "mlp.c_proj.weight"]).data_ptr()
         b.fc2_b = pk.f32(sd[p + "mlp.c_proj.bias"]).data_ptr()
         b.prompt = pk.f32(sd[p + "VPT_shallow"]).data_ptr() if (p + "VPT_shallow") in sd else None

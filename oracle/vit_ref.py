@@ -6,10 +6,12 @@ over the same state-dict layout libreidmi packs.
 
 TEST INFRASTRUCTURE ONLY (tests/, smoke(), bench.py cpu_baseline leg).
 
-``bf16=True`` rounds exactly where the HIP kernels do — to bfloat16 for GEMM operands,
-q/k/v, softmax probabilities before P.V and the attention output, and to float16 for the
-residual stream x (patch/CLS rows, ln_pre output, every residual add: the reference's own
-GPU dtype) — so tests can separate kernel bugs from the precision the MI355X path runs at.  With bf16=False it is the reference's fp32
+``bf16=True`` rounds exactly where the HIP kernels do — to bfloat16 for the out_proj /
+c_proj / patch / proj GEMM operands, q/k/v, softmax probabilities before P.V and the
+attention output, to float16 for the residual stream x (patch/CLS rows, ln_pre output,
+every residual add: the reference's own GPU dtype), and ln_1 / ln_2 folded into fp16 QKV /
+c_fc GEMMs on x (`_ln_linear`) — so tests can separate kernel bugs from the precision the
+MI355X path runs at.  With bf16=False it is the reference's fp32
 math, pinned to tests/golden/vit_b16.npz and text.npz (made by the reference modules).
 """
 import numpy as np
@@ -33,11 +35,28 @@ def _ln(x, w, b):
     return F.layer_norm(x, (x.shape[-1],), _t(w), _t(b), 1e-5)
 
 
+def _ln_linear(x, g, beta, w, b, emulate):
+    """LayerNorm(g, beta) then Linear(w, b).  emulate: as the kernels compute it — LN folded
+    into an fp16 GEMM on the fp16 residual x: rstd * (x @ w'^T) - mean * rstd * s + b' with
+    w' = fp16(w * g), s = row sums of w', b' = b + w @ beta (model.fold_layernorm)."""
+    if not emulate:
+        return _ln(x, g, beta) @ _t(w).t() + _t(b)
+    W = x.shape[-1]
+    mean = x.sum(-1, keepdim=True) / W
+    var = ((x - mean) ** 2).sum(-1, keepdim=True) / W
+    rstd = 1.0 / torch.sqrt(var + 1e-5)
+    w64 = _t(w).double()
+    wf = (w64 * _t(g).double()[None, :]).half()
+    s = wf.double().sum(1).float()
+    bf = (_t(b).double() + w64 @ _t(beta).double()).float()
+    return rstd * (x @ wf.float().t()) + (-mean * rstd) * s + bf
+
+
 def block(x, sd, p, heads, causal=False, bf16=False):
     """ResidualAttentionBlock.forward (custom_clip_model.py:26-29) on x [B, L, W]."""
     B, L, W = x.shape
-    h = _r(_ln(x, sd[p + "ln_1.weight"], sd[p + "ln_1.bias"]), bf16)
-    qkv = h @ _r(_t(sd[p + "attn.in_proj_weight"]), bf16).t() + _t(sd[p + "attn.in_proj_bias"])
+    qkv = _ln_linear(x, sd[p + "ln_1.weight"], sd[p + "ln_1.bias"], sd[p + "attn.in_proj_weight"],
+                     sd[p + "attn.in_proj_bias"], bf16)
     qkv = _r(qkv, bf16).reshape(B, L, 3, heads, 64).permute(2, 0, 3, 1, 4)
     q, k, v = qkv[0], qkv[1], qkv[2]
     s = (q @ k.transpose(-1, -2)) * 0.125
@@ -49,8 +68,8 @@ def block(x, sd, p, heads, causal=False, bf16=False):
     o = (_r(e, bf16) @ v) / den
     o = _r(o.permute(0, 2, 1, 3).reshape(B, L, W), bf16)
     x = _h(x + (o @ _r(_t(sd[p + "attn.out_proj.weight"]), bf16).t() + _t(sd[p + "attn.out_proj.bias"])), bf16)
-    h = _r(_ln(x, sd[p + "ln_2.weight"], sd[p + "ln_2.bias"]), bf16)
-    u = h @ _r(_t(sd[p + "mlp.c_fc.weight"]), bf16).t() + _t(sd[p + "mlp.c_fc.bias"])
+    u = _ln_linear(x, sd[p + "ln_2.weight"], sd[p + "ln_2.bias"], sd[p + "mlp.c_fc.weight"],
+                   sd[p + "mlp.c_fc.bias"], bf16)
     u = _r(u * torch.sigmoid(1.702 * u), bf16)
     return _h(x + (u @ _r(_t(sd[p + "mlp.c_proj.weight"]), bf16).t() + _t(sd[p + "mlp.c_proj.bias"])), bf16)
 

@@ -93,6 +93,43 @@ def test_gemm_v2_tile_bitexact_vs_v1(gpu, epi, M, N, K):
     assert (outs[1][rows].float() - ref).abs().max() <= 1e-2 * (ref.abs().max() + 1)
 
 
+@pytest.mark.parametrize("epi", [0, 1])
+@pytest.mark.parametrize("M,N,K", [(300, 256, 768), (70000, 768, 768), (5000, 3072, 1024)])
+def test_gemm_f16_layernorm_fold(gpu, epi, M, N, K):
+    """ln_1 / ln_2 folded into the fp16 QKV / c_fc GEMM (model.fold_layernorm + row statistics):
+    epi(LN(x) W^T + b) against fp64 torch on the same fp16 x, rows with large means (the
+    cancellation the fold must survive); v1 and v6 tiles bit-identical."""
+    from multimodal_reid_amd.model import fold_layernorm
+    L = _lib()
+    g = torch.Generator().manual_seed(M + N + K)
+    x = (torch.randn(M, K, generator=g) * (0.5 + torch.rand(M, 1, generator=g) * 3)
+         + torch.randn(M, 1, generator=g) * 8).half()
+    gam, bet = 1 + 0.3 * torch.randn(K, generator=g), 0.2 * torch.randn(K, generator=g)
+    W, b = torch.randn(N, K, generator=g) / K ** 0.5, 0.1 * torch.randn(N, generator=g)
+    wf, cs, bf = fold_layernorm(W, b, gam, bet)
+    xd = x.double()
+    mean = xd.mean(1, keepdim=True)
+    rstd = 1 / torch.sqrt(((xd - mean) ** 2).mean(1, keepdim=True) + 1e-5)
+    rs = torch.cat([rstd, -mean * rstd], 1).float()
+    rs = torch.cat([rs, torch.full((256, 2), float("nan"))]).contiguous()  # padded to whole tiles
+    ref = ((xd - mean) * rstd * gam.double() + bet.double()) @ W.double().t() + b.double()
+    if epi == 1:
+        ref = ref * torch.sigmoid(1.702 * ref)
+    dx, dw, dcs, dbf, drs = (t.cuda() for t in (x, wf, cs, bf, rs))
+    outs = []
+    for v in (1, 6):
+        L.call("reidmi_gemm_set_variant", v)
+        out = torch.zeros(M, N, dtype=torch.bfloat16, device="cuda")
+        L.call("reidmi_gemm_f16", epi, L.ptr(dx), K, L.ptr(dw), K, M, N, K, L.ptr(dbf), L.ptr(drs), L.ptr(dcs),
+               L.ptr(out), N, L.stream())
+        outs.append(out)
+    L.call("reidmi_gemm_set_variant", 0)
+    assert torch.equal(outs[0], outs[1])
+    got = outs[0].double().cpu()
+    assert (got - ref).abs().max() <= 1e-2 * (ref.abs().max() + 1)
+    assert _cos(got.numpy(), ref.numpy()).min() >= 0.9999
+
+
 @pytest.mark.parametrize("W", [512, 768, 1024])
 def test_layernorm(gpu, W):
     L = _lib()
