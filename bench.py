@@ -41,13 +41,13 @@ from multimodal_reid_amd.model import VisionTransformer  # noqa: E402
 
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 EPI_GELU = 1  # the c_fc GEMM (+QuickGELU epilogue): the largest single kernel per block
-# HBM-side bytes per c_fc launch (M = 512*211, N = 3072, K = 768) from rocprofv3 PMC passes
-# (tools/prof_round.sh -> profiles/r01/pmc_c_fc_gemm.csv, mean of the 5 timed launches):
-# FETCH_SIZE 525 459 KiB doubled (gfx950 reports half of 16-B/lane streaming reads,
-# MI355X_MICROARCH.md "HBM") + WRITE_SIZE 648 192 KiB.  FETCH_SIZE also counts
-# Infinity-Cache hits (the 4.7 MB weight panel re-read by every tile).  Algorithmic: A
-# 166 MB + W 4.7 MB + out 664 MB = 835 MB.
-C_FC_TRAFFIC_BYTES = (2 * 525459 + 648192) * 1024
+# HBM-side bytes per c_fc launch (ln_2-folded fp16 GEMM, M = 512*211, N = 3072, K = 768) from
+# rocprofv3 PMC passes (tools/prof_round.sh -> profiles/r01/pmc_c_fc_fold_{FETCH,WRITE}_SIZE.csv,
+# mean of the 5 timed launches): FETCH_SIZE 511 608 KiB doubled (gfx950 reports half of
+# 16-B/lane streaming reads, MI355X_MICROARCH.md "HBM") + WRITE_SIZE 648 192 KiB.  FETCH_SIZE
+# also counts Infinity-Cache hits (the 4.7 MB weight panel re-read by every tile).
+# Algorithmic: A 166 MB + W 4.7 MB + out 664 MB = 835 MB.
+C_FC_TRAFFIC_BYTES = (2 * 511608 + 648192) * 1024
 
 
 def shard(n, rank, world):
