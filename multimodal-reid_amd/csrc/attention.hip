@@ -62,11 +62,19 @@ __global__ __launch_bounds__(512) void mhsa_kernel(const __bf16* __restrict__ q,
             if (pc + 1 < vpieces || lane < vlast_lanes)  // never read or write past the blob
                 __builtin_amdgcn_global_load_lds(vh + pc * 512 + lane * 8, (lds_ptr_t)(sV + pc * 512), 16, 0, 0);
     };
+    // Q rows of this wave's queries; queries >= L load row L-1 (finite; never stored).
+    // Inline-asm loads: hipcc does not track them, so it inserts no vmcnt(0) of its own
+    // before the prefetched registers are used (which would also drain the O stores); the
+    // kernel's counted waits retire them, and `pin` orders every use after that wait.
     auto load_q = [&](int64_t bh, bf16x8* qf) {
-        const __bf16* qh = q + bh * L * 64;
-#pragma unroll
-        for (int ks = 0; ks < 4; ks++)
-            qf[ks] = qi < L ? *(const bf16x8*)(qh + (int64_t)qi * 64 + ks * 16 + hh * 8) : bf16x8{};
+        const __bf16* qh = q + (bh * L + (qi < L ? qi : L - 1)) * 64 + hh * 8;
+        asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(qf[0]) : "v"(qh) : "memory");
+        asm volatile("global_load_dwordx4 %0, %1, off offset:32" : "=v"(qf[1]) : "v"(qh) : "memory");
+        asm volatile("global_load_dwordx4 %0, %1, off offset:64" : "=v"(qf[2]) : "v"(qh) : "memory");
+        asm volatile("global_load_dwordx4 %0, %1, off offset:96" : "=v"(qf[3]) : "v"(qh) : "memory");
+    };
+    auto pin = [&](bf16x8* qf) {
+        asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]));
     };
     auto zero_pad = [&](int stage) {  // V^T key columns [L, LP) were DMA'd from padding
         __bf16* sV = lds + stage * stage_elems + LP * 64;
@@ -83,15 +91,16 @@ __global__ __launch_bounds__(512) void mhsa_kernel(const __bf16* __restrict__ q,
     bf16x8 qf[4];
     load_q(bh, qf);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    pin(qf);
     __syncthreads();
     zero_pad(0);
     __syncthreads();
     for (; bh < nbh; bh += gridDim.x) {
         const int64_t nxt = bh + gridDim.x;
         bf16x8 qn[4];
-        if (nxt < nbh) {
-            issue(nxt, stage ^ 1);
+        if (nxt < nbh) {  // Q first: the compiler's wait for qn then never covers the DMA
             load_q(nxt, qn);
+            issue(nxt, stage ^ 1);
         }
         const __bf16* sK = lds + stage * stage_elems;
         const __bf16* sV = sK + LP * 64;
@@ -162,14 +171,25 @@ __global__ __launch_bounds__(512) void mhsa_kernel(const __bf16* __restrict__ q,
                     }
             }
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+        // Wait for the next head's K/V DMA and Q loads only: the 8 O stores this wave just
+        // issued (when it owns queries) are the youngest vector-memory ops and stay in flight
+        // (vmcnt retires in issue order).
+        // Raw barriers: __syncthreads() would add a vmcnt(0) (a workgroup release covers the
+        // stores) and drain them anyway.  LDS-DMA data is ordered for other waves' ds_reads
+        // by each issuing wave's vmcnt + this barrier; zero_pad's ds_writes by lgkmcnt(0).
+        if (wid * 32 < L)
+            asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
         if (nxt < nbh) {
             zero_pad(stage ^ 1);
+            pin(qn);
 #pragma unroll
             for (int ks = 0; ks < 4; ks++) qf[ks] = qn[ks];
         }
-        __syncthreads();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
         stage ^= 1;
     }
 }
@@ -266,14 +286,20 @@ __global__ __launch_bounds__(256) void mhsa_cls_kernel(const __bf16* __restrict_
     }
     sum = wave_sum(sum);
     __builtin_amdgcn_wave_barrier();
+    // lane d: p . V^T[d][:].  All row loads are issued before the first use (a rolled loop
+    // waited one HBM round trip per 8 keys); same summation order as before.
     const __bf16* vr = vt + (bh * 64 + lane) * (int64_t)lpad;
-    float acc = 0.f;
-    for (int t0 = 0; t0 < L; t0 += 8) {
-        const bf16x8 v = *(const bf16x8*)(vr + t0);
+    bf16x8 vv[32];
 #pragma unroll
-        for (int e = 0; e < 8; e++)
-            if (t0 + e < L) acc += sp[wid][t0 + e] * (float)v[e];
-    }
+    for (int i = 0; i < 32; i++)
+        if (i * 8 < L) vv[i] = *(const bf16x8*)(vr + i * 8);
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 32; i++)
+        if (i * 8 < L)
+#pragma unroll
+            for (int e = 0; e < 8; e++)
+                if (i * 8 + e < L) acc += sp[wid][i * 8 + e] * (float)vv[i][e];
     const int64_t b = bh / H, h = bh % H;
     o[b * (int64_t)H * 64 + h * 64 + lane] = (__bf16)(acc / sum);
 }
