@@ -49,6 +49,11 @@ int reidmi_distmat_f32(const float* q, int64_t Q, int64_t ldq, const float* g, i
 int reidmi_cosine_f32(const float* q, int64_t Q, int64_t ldq, const float* g, int64_t G, int64_t ldg, int64_t D,
                       float* out, int64_t ldo, float* ws, void* stream);
 
+/* Distance kernel selection for tests / A-B timing: 0 = auto (K-step-32 pipelined kernel when
+ * D, ldq, ldg are multiples of 4 and the operands 16-byte aligned), 1 = single-stage kernel.
+ * Both run the same MFMA sequence per output: bit-identical. */
+int reidmi_distmat_set_variant(int v);
+
 /* np.argsort(x, axis=1)[:, :k] with ties in index order (kind="stable") — evaluate.py:40,
  * reranking.py:48.  row_div (nullable): rows are divided by row_div[row] first
  * (reranking.py:46 column-max normalisation of a symmetric distance).  k <= 64.

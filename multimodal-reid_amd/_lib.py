@@ -23,6 +23,7 @@ SIGNATURES = {
     "reidmi_l2norm_f32": [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp],
     "reidmi_distmat_f32": [_vp, _i64, _i64, _vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp],
     "reidmi_cosine_f32": [_vp, _i64, _i64, _vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp],
+    "reidmi_distmat_set_variant": [_i32],
     "reidmi_topk_rows_f32": [_vp, _i64, _i64, _i64, _vp, _i32, _vp, _vp, _i64, _vp],
     "reidmi_eval_rows": [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "reidmi_gemm_bf16": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _i64, _vp],

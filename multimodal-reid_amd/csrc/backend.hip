@@ -99,6 +99,114 @@ __global__ __launch_bounds__(256) void distmat_f32_kernel(
             }
 }
 
+// Pipelined variant (D, ldq, ldg multiples of 4, 16-byte aligned rows): K-step 32, two LDS
+// stages, the next K-step's operands loaded as coalesced float4 (8 lanes per 128-byte row
+// segment) into registers while the current one is multiplied, one barrier per K-step.
+// LDS rows padded by 1 dword so the transposed scalar stores are conflict-free.  The MFMA
+// sequence per output (k pairs ascending on v_mfma_f32_32x32x2_f32) is the one above, so the
+// result is bit-identical to distmat_f32_kernel (and to the oracle's fmaf chain).
+constexpr int DM2_BK = 32, DM2_LD = DM_BM + 1;
+
+template <bool COSINE>
+__global__ __launch_bounds__(256, 2) void distmat2_f32_kernel(
+    const float* __restrict__ q, const float* __restrict__ g, const float* __restrict__ qq,
+    const float* __restrict__ gg, int64_t Q, int64_t G, int64_t D, int64_t ldq, int64_t ldg,
+    float* __restrict__ out, int64_t ldo) {
+    __shared__ float sA[2][DM2_BK][DM2_LD];
+    __shared__ float sB[2][DM2_BK][DM2_LD];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid >> 1, wn = wid & 1;
+    const int64_t bm = (int64_t)blockIdx.y * DM_BM, bn = (int64_t)blockIdx.x * DM_BN;
+    // staging slots: float4 f = tid + 256u -> row f >> 3, k group (f & 7) * 4
+    const float* pa[4];
+    const float* pb[4];
+    bool va[4], vb[4];
+    int srow[4], sk[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const int f = tid + 256 * u;
+        srow[u] = f >> 3;
+        sk[u] = (f & 7) * 4;
+        va[u] = bm + srow[u] < Q;
+        vb[u] = bn + srow[u] < G;
+        pa[u] = q + (va[u] ? bm + srow[u] : 0) * ldq + sk[u];
+        pb[u] = g + (vb[u] ? bn + srow[u] : 0) * ldg + sk[u];
+    }
+    float4 ra[4], rb[4];
+    auto gload = [&](int64_t k0) {
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const bool kin = k0 + sk[u] < D;  // D % 4 == 0: a float4 is wholly in or out
+            ra[u] = va[u] && kin ? *(const float4*)(pa[u] + k0) : make_float4(0.f, 0.f, 0.f, 0.f);
+            rb[u] = vb[u] && kin ? *(const float4*)(pb[u] + k0) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto lstore = [&](int st) {
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            sA[st][sk[u] + 0][srow[u]] = ra[u].x;
+            sA[st][sk[u] + 1][srow[u]] = ra[u].y;
+            sA[st][sk[u] + 2][srow[u]] = ra[u].z;
+            sA[st][sk[u] + 3][srow[u]] = ra[u].w;
+            sB[st][sk[u] + 0][srow[u]] = rb[u].x;
+            sB[st][sk[u] + 1][srow[u]] = rb[u].y;
+            sB[st][sk[u] + 2][srow[u]] = rb[u].z;
+            sB[st][sk[u] + 3][srow[u]] = rb[u].w;
+        }
+    };
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++) acc[a][b] = f32x16{};
+    gload(0);
+    lstore(0);
+    __syncthreads();
+    const int64_t nk = (D + DM2_BK - 1) / DM2_BK;
+    for (int64_t kt = 0; kt < nk; kt++) {
+        const int cur = (int)(kt & 1);
+        if (kt + 1 < nk) gload((kt + 1) * DM2_BK);
+#pragma unroll
+        for (int s = 0; s < DM2_BK / 2; s++) {
+            const int kr = 2 * s + (lane >> 5);
+            const float a0 = sA[cur][kr][wm * 64 + (lane & 31)];
+            const float a1 = sA[cur][kr][wm * 64 + 32 + (lane & 31)];
+            const float b0 = sB[cur][kr][wn * 64 + (lane & 31)];
+            const float b1 = sB[cur][kr][wn * 64 + 32 + (lane & 31)];
+            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+        }
+        if (kt + 1 < nk) lstore(cur ^ 1);
+        __syncthreads();
+    }
+#pragma unroll
+    for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+        for (int nt = 0; nt < 2; nt++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                int64_t i = bm + wm * 64 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                int64_t j = bn + wn * 64 + nt * 32 + (lane & 31);
+                if (i < Q && j < G) {
+                    if constexpr (COSINE) {
+                        const float c = acc[mt][nt][r] * (1.0f / (__builtin_sqrtf(qq[i]) * __builtin_sqrtf(gg[j])));
+                        out[i * ldo + j] = acosf(fminf(fmaxf(c, -1.0f + 1e-5f), 1.0f - 1e-5f));
+                    } else {
+                        out[i * ldo + j] = __builtin_fmaf(-2.0f, acc[mt][nt][r], qq[i] + gg[j]);
+                    }
+                }
+            }
+}
+
+int g_dm_variant = 0;
+static int distmat_variant() { return g_dm_variant; }
+
+static bool dm2_ok(const float* q, int64_t ldq, const float* g, int64_t ldg, int64_t D) {
+    return D % 4 == 0 && ldq % 4 == 0 && ldg % 4 == 0 && ((uintptr_t)q & 15) == 0 && ((uintptr_t)g & 15) == 0;
+}
+
 // ---------------------------------------------------------------- key helpers
 __device__ __forceinline__ bool key_less(float av, int ai, float bv, int bi) {
     return av < bv || (av == bv && ai < bi);
@@ -350,12 +458,23 @@ int distmat_pre_launch(const float* q, int64_t Q, int64_t ldq, const float* g, i
     if (Q == 0 || G == 0) return OK;
     dim3 grid(ceil_div(G, DM_BN), ceil_div(Q, DM_BM));
     RM_REQUIRE(grid.y <= 65535, "distmat: too many query rows for one launch");
-    hipLaunchKernelGGL(distmat_f32_kernel<false>, grid, dim3(256), 0, s, q, g, qq, gg, Q, G, D, ldq, ldg, out, ldo);
+    if (dm2_ok(q, ldq, g, ldg, D) && distmat_variant() != 1)
+        hipLaunchKernelGGL(distmat2_f32_kernel<false>, grid, dim3(256), 0, s, q, g, qq, gg, Q, G, D, ldq, ldg, out, ldo);
+    else
+        hipLaunchKernelGGL(distmat_f32_kernel<false>, grid, dim3(256), 0, s, q, g, qq, gg, Q, G, D, ldq, ldg, out, ldo);
     RM_LAUNCHED();
     return OK;
 }
 
 }  // namespace reidmi
+
+// Distance-kernel selection (tests / A-B timing): 0 = auto (pipelined when the operands allow),
+// 1 = the single-stage kernel.
+REIDMI_API int reidmi_distmat_set_variant(int v) {
+    RM_REQUIRE(v == 0 || v == 1, "distmat variant: 0 auto, 1 single-stage");
+    reidmi::g_dm_variant = v;
+    return reidmi::OK;
+}
 
 using namespace reidmi;
 
@@ -393,10 +512,19 @@ int reidmi::distmat_impl(bool cosine, const float* q, int64_t Q, int64_t ldq, co
     RM_LAUNCHED();
     dim3 grid(ceil_div(G, DM_BN), ceil_div(Q, DM_BM));
     RM_REQUIRE(grid.y <= 65535, "distmat: too many query rows for one launch");
-    if (cosine)
-        hipLaunchKernelGGL(distmat_f32_kernel<true>, grid, dim3(256), 0, s, q, g, qq, gg, Q, G, D, ldq, ldg, out, ldo);
-    else
-        hipLaunchKernelGGL(distmat_f32_kernel<false>, grid, dim3(256), 0, s, q, g, qq, gg, Q, G, D, ldq, ldg, out, ldo);
+    const bool v2 = dm2_ok(q, ldq, g, ldg, D) && distmat_variant() != 1;
+    if (cosine) {
+        if (v2)
+            hipLaunchKernelGGL(distmat2_f32_kernel<true>, grid, dim3(256), 0, s, q, g, qq, gg, Q, G, D, ldq, ldg, out, ldo);
+        else
+            hipLaunchKernelGGL(distmat_f32_kernel<true>, grid, dim3(256), 0, s, q, g, qq, gg, Q, G, D, ldq, ldg, out, ldo);
+    } else {
+        if (v2)
+            hipLaunchKernelGGL(distmat2_f32_kernel<false>, grid, dim3(256), 0, s, q, g, qq, gg, Q, G, D, ldq, ldg, out,
+                               ldo);
+        else
+            hipLaunchKernelGGL(distmat_f32_kernel<false>, grid, dim3(256), 0, s, q, g, qq, gg, Q, G, D, ldq, ldg, out, ldo);
+    }
     RM_LAUNCHED();
     return OK;
 }

@@ -35,9 +35,14 @@ def test_distmat_bitexact(gpu, Q, G, D):
     r = np.random.default_rng(Q * 7 + G)
     q = r.standard_normal((Q, D)).astype(np.float32)
     g = r.standard_normal((G, D)).astype(np.float32)
-    d = _ev().euclidean_distance(torch.from_numpy(q), torch.from_numpy(g))
-    assert isinstance(d, np.ndarray) and d.dtype == np.float32
-    assert np.array_equal(d.view(np.uint32), oracle.distmat(q, g).view(np.uint32))
+    ref = oracle.distmat(q, g).view(np.uint32)
+    from multimodal_reid_amd import _lib
+    for v in (0, 1):  # pipelined K-step-32 kernel (D % 4 == 0) and the single-stage one
+        _lib.call("reidmi_distmat_set_variant", v)
+        d = _ev().euclidean_distance(torch.from_numpy(q), torch.from_numpy(g))
+        assert isinstance(d, np.ndarray) and d.dtype == np.float32
+        assert np.array_equal(d.view(np.uint32), ref), v
+    _lib.call("reidmi_distmat_set_variant", 0)
 
 
 def test_distmat_matches_reference_fixture(gpu):
