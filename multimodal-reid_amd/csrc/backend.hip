@@ -116,7 +116,14 @@ __global__ __launch_bounds__(256, 2) void distmat2_f32_kernel(
     __shared__ float sB[2][DM2_BK][DM2_LD];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid >> 1, wn = wid & 1;
-    const int64_t bm = (int64_t)blockIdx.y * DM_BM, bn = (int64_t)blockIdx.x * DM_BN;
+    // 1-D grid, XCD-contiguous: workgroups bid, bid+8, ... share an XCD (round-robin
+    // dispatch) and get consecutive tiles, row tile fastest, so the row tiles of one gallery
+    // panel run back to back on one XCD and its panel is fetched into that L2 once.
+    const int64_t tiles_m = (Q + DM_BM - 1) / DM_BM;
+    const int64_t nwg = (int64_t)gridDim.x;
+    const int64_t bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int64_t wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    const int64_t bm = (wg % tiles_m) * DM_BM, bn = (wg / tiles_m) * DM_BN;
     // staging slots: float4 f = tid + 256u -> row f >> 3, k group (f & 7) * 4
     const float* pa[4];
     const float* pb[4];
@@ -459,7 +466,8 @@ int distmat_pre_launch(const float* q, int64_t Q, int64_t ldq, const float* g, i
     dim3 grid(ceil_div(G, DM_BN), ceil_div(Q, DM_BM));
     RM_REQUIRE(grid.y <= 65535, "distmat: too many query rows for one launch");
     if (dm2_ok(q, ldq, g, ldg, D) && distmat_variant() != 1)
-        hipLaunchKernelGGL(distmat2_f32_kernel<false>, grid, dim3(256), 0, s, q, g, qq, gg, Q, G, D, ldq, ldg, out, ldo);
+        hipLaunchKernelGGL(distmat2_f32_kernel<false>, dim3((unsigned)((int64_t)grid.x * grid.y)), dim3(256), 0, s, q, g,
+                           qq, gg, Q, G, D, ldq, ldg, out, ldo);
     else
         hipLaunchKernelGGL(distmat_f32_kernel<false>, grid, dim3(256), 0, s, q, g, qq, gg, Q, G, D, ldq, ldg, out, ldo);
     RM_LAUNCHED();
@@ -513,14 +521,15 @@ int reidmi::distmat_impl(bool cosine, const float* q, int64_t Q, int64_t ldq, co
     dim3 grid(ceil_div(G, DM_BN), ceil_div(Q, DM_BM));
     RM_REQUIRE(grid.y <= 65535, "distmat: too many query rows for one launch");
     const bool v2 = dm2_ok(q, ldq, g, ldg, D) && distmat_variant() != 1;
+    const dim3 grid1((unsigned)((int64_t)grid.x * grid.y));
     if (cosine) {
         if (v2)
-            hipLaunchKernelGGL(distmat2_f32_kernel<true>, grid, dim3(256), 0, s, q, g, qq, gg, Q, G, D, ldq, ldg, out, ldo);
+            hipLaunchKernelGGL(distmat2_f32_kernel<true>, grid1, dim3(256), 0, s, q, g, qq, gg, Q, G, D, ldq, ldg, out, ldo);
         else
             hipLaunchKernelGGL(distmat_f32_kernel<true>, grid, dim3(256), 0, s, q, g, qq, gg, Q, G, D, ldq, ldg, out, ldo);
     } else {
         if (v2)
-            hipLaunchKernelGGL(distmat2_f32_kernel<false>, grid, dim3(256), 0, s, q, g, qq, gg, Q, G, D, ldq, ldg, out,
+            hipLaunchKernelGGL(distmat2_f32_kernel<false>, grid1, dim3(256), 0, s, q, g, qq, gg, Q, G, D, ldq, ldg, out,
                                ldo);
         else
             hipLaunchKernelGGL(distmat_f32_kernel<false>, grid, dim3(256), 0, s, q, g, qq, gg, Q, G, D, ldq, ldg, out, ldo);
