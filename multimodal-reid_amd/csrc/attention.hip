@@ -29,6 +29,7 @@ __device__ __forceinline__ int kswz(int r, int kc) { return r * 64 + ((kc ^ ((r 
 //     of O^T = V^T P^T (accumulator-as-operand), V^T read with the same key permutation;
 //   O^T[d][q] comes out as 4 runs of 4 consecutive d per lane -> 8-byte stores.
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef float f32x2v __attribute__((ext_vector_type(2)));
 
 template <int NKB, bool CAUSAL>
 __global__ __launch_bounds__(512) void mhsa_kernel(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
@@ -129,16 +130,22 @@ __global__ __launch_bounds__(512) void mhsa_kernel(const __bf16* __restrict__ q,
                     mx = fmaxf(mx, s[kb][r]);
                 }
             mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+            // exponent argument and running sums on packed-fp32 VALU (v_pk_fma_f32 /
+            // v_pk_add_f32: two elements per instruction); two partial sums (even / odd r).
             const float mb = -mx * scale_log2;
-            float sum = 0.f;
+            const f32x2v sc2 = {scale_log2, scale_log2}, mb2 = {mb, mb};
+            f32x2v sum2 = {0.f, 0.f};
 #pragma unroll
             for (int kb = 0; kb < NKB; kb++)
 #pragma unroll
-                for (int r = 0; r < 16; r++) {
-                    const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kb][r], scale_log2, mb));
-                    s[kb][r] = p;
-                    sum += p;
+                for (int r = 0; r < 16; r += 2) {
+                    const f32x2v t = __builtin_elementwise_fma(f32x2v{s[kb][r], s[kb][r + 1]}, sc2, mb2);
+                    const f32x2v p = {__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
+                    s[kb][r] = p.x;
+                    s[kb][r + 1] = p.y;
+                    sum2 += p;
                 }
+            float sum = sum2.x + sum2.y;
             sum += __shfl_xor(sum, 32, 64);
             const float inv = 1.0f / sum;
             f32x16 oacc[2] = {f32x16{}, f32x16{}};

@@ -138,42 +138,68 @@ __global__ void rows_f16_to_f32_kernel(const _Float16* __restrict__ x, int64_t r
 // col[b*NP + p][k], k = c*P*P + ky*P + kx (conv1.weight flattening), zero for k >= 3P^2.
 // Optional TTA (data_prepare.py:263-270 on a normalised crop): flip, Pad((10,5)) with
 // value -1 (= 0 before Normalize(0.5,0.5)), crop at (top i, left j).
-template <typename TI>
-__global__ void im2col_kernel(const TI* __restrict__ img, int64_t B, int H, int Wd, int P, int S, int gw, int NP,
-                              int kpad, const int32_t* __restrict__ tta, __bf16* __restrict__ col) {
-    const int64_t chunks = B * NP * (kpad / 8);
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= chunks) return;
-    const int kc = (int)(e % (kpad / 8));
-    const int64_t bp = e / (kpad / 8);
-    const int64_t b = bp / NP;
-    const int p = (int)(bp % NP);
-    const int py = p / gw, px = p % gw;
-    int ti = 0, tj = 0;
+// One workgroup per (image, patch row py): the P source rows of all 3 channels that the
+// row's gw patches read (shifted by the TTA offset; rows outside the image = -1) are staged
+// in LDS as fp32 by coalesced 16-byte loads, then the gw * kpad outputs are written as
+// 16-byte chunks (consecutive threads -> consecutive chunks).  The stride-S overlap (each
+// pixel in up to 2x2 patches) is served from LDS, so HBM sees each image once.
+// PT: the patch size as a compile-time constant (16: ViT-B/16, 14: ViT-L/14; 0 = runtime).
+template <typename TI, int PT>
+__global__ __launch_bounds__(256) void im2col_kernel(const TI* __restrict__ img, int H, int Wd, int P_, int S,
+                                                     int gh, int gw, int kpad, const int32_t* __restrict__ tta,
+                                                     __bf16* __restrict__ col) {
+    extern __shared__ float srow[];  // [3][P][Wd]
+    const int P = PT > 0 ? PT : P_;
+    const int b = blockIdx.x / gh, py = blockIdx.x - (blockIdx.x / gh) * gh;
     const bool aug = tta != nullptr;
-    if (aug) { ti = tta[2 * b]; tj = tta[2 * b + 1]; }
-    const TI* im = img + b * 3 * (int64_t)H * Wd;
-    bf16x8 out;
-    const int PP = P * P;
+    const int ti = aug ? tta[2 * b] : 0, tj = aug ? tta[2 * b + 1] : 0;
+    const int y0 = py * S + (aug ? ti - 5 : 0);
+    const TI* im = img + (int64_t)b * 3 * H * Wd;
+    constexpr int V = 16 / sizeof(TI);  // elements per 16-byte load (Wd % V == 0, checked at launch)
+    const int vpr = Wd / V;             // loads per source row
+    for (int e = threadIdx.x; e < 3 * P * vpr; e += blockDim.x) {
+        const int cr = e / vpr, xv = e - cr * vpr;  // cr = c * P + ky
+        const int c = cr / P, y = y0 + (cr - c * P);
+        float* d = srow + cr * Wd + xv * V;
+        if (y >= 0 && y < H) {
+            const uint4 raw = *(const uint4*)(im + ((int64_t)c * H + y) * Wd + xv * V);
+            if constexpr (sizeof(TI) == 2) {
+                const bf16x8 v = __builtin_bit_cast(bf16x8, raw);
 #pragma unroll
-    for (int u = 0; u < 8; u++) {
-        const int k = kc * 8 + u;
-        float v = 0.f;
-        if (k < 3 * PP) {
-            const int c = k / PP, rem = k % PP, ky = rem / P, kx = rem % P;
-            int y = py * S + ky, x = px * S + kx;
-            bool inb = true;
-            if (aug) {
-                y = y + ti - 5;
-                x = x + tj - 10;
-                inb = y >= 0 && y < H && x >= 0 && x < Wd;
-                x = Wd - 1 - x;
+                for (int u = 0; u < 8; u++) d[u] = (float)v[u];
+            } else {
+                *(uint4*)d = raw;
             }
-            v = inb ? (float)im[((int64_t)c * H + y) * Wd + x] : -1.0f;
+        } else {
+#pragma unroll
+            for (int u = 0; u < V; u++) d[u] = -1.0f;
         }
-        out[u] = (__bf16)v;
     }
-    *(bf16x8*)(col + bp * kpad + kc * 8) = out;
+    __syncthreads();
+    const int kch = kpad / 8, PP = P * P;
+    __bf16* out = col + ((int64_t)b * gh * gw + (int64_t)py * gw) * kpad;
+    for (int e = threadIdx.x; e < gw * kch; e += blockDim.x) {
+        const int px = e / kch, kc = e - px * kch;
+        bf16x8 o;
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int k = kc * 8 + u;
+            float v = 0.f;
+            if (k < 3 * PP) {
+                const int c = k / PP, rem = k - c * PP, ky = rem / P, kx = rem - ky * P;
+                int x = px * S + kx;
+                bool inb = true;
+                if (aug) {
+                    x = x + tj - 10;
+                    inb = x >= 0 && x < Wd;
+                    x = Wd - 1 - x;
+                }
+                v = inb ? srow[(c * P + ky) * Wd + x] : -1.0f;
+            }
+            o[u] = (__bf16)v;
+        }
+        *(bf16x8*)(out + (int64_t)px * kpad + kc * 8) = o;
+    }
 }
 
 // x[b*L+0] = class_emb + pos[0]; IVLP: x[b*L+1+NP+i] = half(vpt[i]) (maple.py:765-767).
@@ -413,13 +439,25 @@ REIDMI_API int reidmi_vit_forward(const reidmi_vit_weights* w, const void* image
     __bf16* col = (__bf16*)(ws + P.u);
     const int64_t M = B * L;
     // patch embed (+pos), CLS/VPT rows, ln_pre
-    const int64_t chunks = B * NP * (w->kpad / 8);
-    if (images_bf16)
-        hipLaunchKernelGGL(im2col_kernel<__bf16>, dim3(ceil_div(chunks, 256)), dim3(256), 0, s,
-                           (const __bf16*)images, B, H, Wimg, w->patch, w->stride, w->grid_w, NP, w->kpad, tta, col);
-    else
-        hipLaunchKernelGGL(im2col_kernel<float>, dim3(ceil_div(chunks, 256)), dim3(256), 0, s,
-                           (const float*)images, B, H, Wimg, w->patch, w->stride, w->grid_w, NP, w->kpad, tta, col);
+    RM_REQUIRE(B * w->grid_h < (1ll << 31) && Wimg % 8 == 0, "vit: im2col needs B * grid_h < 2^31 and width % 8 == 0");
+    {
+        const dim3 g((unsigned)(B * w->grid_h)), t(256);
+        const size_t lds = (size_t)3 * w->patch * Wimg * sizeof(float);
+        RM_REQUIRE(lds <= 64 * 1024, "vit: image too wide for the im2col row stage");
+#define RM_IM2COL(TI, PT)                                                                                      \
+    hipLaunchKernelGGL((im2col_kernel<TI, PT>), g, t, lds, s, (const TI*)images, H, Wimg, w->patch, w->stride, \
+                       w->grid_h, w->grid_w, w->kpad, tta, col)
+        if (images_bf16) {
+            if (w->patch == 16) RM_IM2COL(__bf16, 16);
+            else if (w->patch == 14) RM_IM2COL(__bf16, 14);
+            else RM_IM2COL(__bf16, 0);
+        } else {
+            if (w->patch == 16) RM_IM2COL(float, 16);
+            else if (w->patch == 14) RM_IM2COL(float, 14);
+            else RM_IM2COL(float, 0);
+        }
+#undef RM_IM2COL
+    }
     RM_LAUNCHED();
     EpiArgs ep{};
     ep.out = x;

@@ -68,6 +68,15 @@ __device__ __forceinline__ float quick_gelu(float x) {
     return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -2.4554669595930157f));
 }
 
+// Two QuickGELUs with the multiplies and the add on packed-fp32 VALU (v_pk_mul_f32 /
+// v_pk_add_f32); the same operations in the same order as quick_gelu, so bit-identical.
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2v quick_gelu2(f32x2v x) {
+    const f32x2v y = x * -2.4554669595930157f;
+    const f32x2v d = f32x2v{__builtin_amdgcn_exp2f(y.x), __builtin_amdgcn_exp2f(y.y)} + 1.0f;
+    return x * f32x2v{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+}
+
 // One 16x16x32 MFMA on 16-byte fragments holding bf16 or (F16) fp16 values.
 template <bool F16>
 __device__ __forceinline__ f32x4 mfma16(const bf16x8& w, const bf16x8& a, const f32x4& c) {
@@ -203,7 +212,7 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
         };
         auto src_row = [&](int64_t m) -> const float* {
             if constexpr (EPI == EPI_RESID_F32) return (const float*)ea.out + m * ea.ldc + ncol + cq;
-            else return ea.pos + (1 + m % ea.npatch) * (int64_t)N + ncol + cq;
+            else return ea.pos + (1 + (uint32_t)m % (uint32_t)ea.npatch) * (int64_t)N + ncol + cq;
         };
         auto store_batch = [&](int i0) {
 #pragma unroll
@@ -218,7 +227,8 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
                         *(float4*)(d + j * 16) = make_float4(v[0], v[1], v[2], v[3]);
                     }
                 } else {  // patch rows of the fp16 residual stream
-                    _Float16* d = (_Float16*)ea.out + ((m / ea.npatch) * ea.seq + 1 + m % ea.npatch) * ea.ldc + ncol + cq;
+                    const uint32_t img = (uint32_t)m / (uint32_t)ea.npatch, p = (uint32_t)m - img * (uint32_t)ea.npatch;
+                    _Float16* d = (_Float16*)ea.out + ((int64_t)img * ea.seq + 1 + p) * ea.ldc + ncol + cq;
 #pragma unroll
                     for (int j = 0; j < 4; j++) {
                         const f32x4 v = acc[i0 + ii][j];
@@ -264,24 +274,34 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
         return;
     }
     // bf16 outputs.  v^T tiles of the head split keep the scattered 2-byte stores.
+    // Head split: the wave's 64 columns lie inside one of q / k / v (wd is a multiple of 64),
+    // so the q/k/v selector and the column's offset inside it are wave-uniform; the token
+    // index (b, t) of a row comes from one 32-bit division per row group (M < 2^31, checked
+    // at launch) instead of 64-bit divisions per fragment.
+    [[maybe_unused]] int qkv_sel = 0, qkv_c0 = 0;
     if constexpr (EPI == EPI_QKV) {
         const int wd = ea.heads * 64;
-        if ((ncol + ea.n_off) / wd == 2) {  // uniform per tile (wd % tile width == 0)
+        const int nb = __builtin_amdgcn_readfirstlane(ncol + ea.n_off);
+        qkv_sel = nb / wd;
+        qkv_c0 = nb - qkv_sel * wd;
+        if (qkv_sel == 2) {
+            const uint32_t seq = (uint32_t)ea.seq;
+            const int64_t lp = ea.lpad;
 #pragma unroll
             for (int i = 0; i < NI; i++) {
                 const int64_t m = mrow + i * 16 + (lane & 15);
                 if (m >= M) continue;
-                const int64_t b = m / ea.seq, t = m % ea.seq;
+                const uint32_t b = (uint32_t)m / seq, t = (uint32_t)m - b * seq;
+                __bf16* vb = (__bf16*)ea.vt + (int64_t)b * ea.heads * 64 * lp + t;
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     const f32x4 v = acc[i][j];
-                    const int nq = ncol + j * 16 + cq + ea.n_off;
-                    const int h = (nq % wd) >> 6, d = nq & 63;
-                    __bf16* dst = (__bf16*)ea.vt + ((b * ea.heads + h) * 64 + d) * (int64_t)ea.lpad + t;
+                    const int hd = qkv_c0 + j * 16 + cq;  // h * 64 + d
+                    __bf16* dst = vb + (int64_t)hd * lp;
                     dst[0] = (__bf16)v[0];
-                    dst[ea.lpad] = (__bf16)v[1];
-                    dst[2 * (int64_t)ea.lpad] = (__bf16)v[2];
-                    dst[3 * (int64_t)ea.lpad] = (__bf16)v[3];
+                    dst[lp] = (__bf16)v[1];
+                    dst[2 * lp] = (__bf16)v[2];
+                    dst[3 * lp] = (__bf16)v[3];
                 }
             }
             return;
@@ -295,14 +315,24 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
 #pragma unroll
     for (int i = 0; i < NI; i++) {
         const int64_t m = mrow + i * 16 + (lane & 15);
+        [[maybe_unused]] __bf16* qkrow = nullptr;  // QKV: q / k row (b, h = 0, t)
+        if constexpr (EPI == EPI_QKV) {
+            const uint32_t seq = (uint32_t)ea.seq;
+            const uint32_t b = (uint32_t)m / seq, t = (uint32_t)m - b * seq;
+            qkrow = (__bf16*)(qkv_sel == 0 ? ea.q : ea.k) + ((int64_t)b * ea.heads * ea.seq + t) * 64;
+        }
 #pragma unroll
         for (int jp = 0; jp < 2; jp++) {
             f32x4 a = acc[i][2 * jp], c = acc[i][2 * jp + 1];
             if constexpr (EPI == EPI_GELU_BF16) {
 #pragma unroll
-                for (int e = 0; e < 4; e++) {
-                    a[e] = quick_gelu(a[e]);
-                    c[e] = quick_gelu(c[e]);
+                for (int e = 0; e < 4; e += 2) {
+                    const f32x2v ga = quick_gelu2(f32x2v{a[e], a[e + 1]});
+                    const f32x2v gc = quick_gelu2(f32x2v{c[e], c[e + 1]});
+                    a[e] = ga.x;
+                    a[e + 1] = ga.y;
+                    c[e] = gc.x;
+                    c[e + 1] = gc.y;
                 }
             }
             const auto lo = __builtin_amdgcn_permlane16_swap(cvt_pk_bf16(a[0], a[1]), cvt_pk_bf16(c[0], c[1]), false, false);
@@ -311,12 +341,8 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
             const int col = ncol + (2 * jp + (q & 1)) * 16 + (q >> 1) * 8;
             if (m >= M) continue;
             if constexpr (EPI == EPI_QKV) {
-                const int wd = ea.heads * 64;
-                const int nq = col + ea.n_off;
-                const int h = (nq % wd) >> 6, d = nq & 63;
-                const int64_t b = m / ea.seq, t = m % ea.seq;
-                __bf16* dst = (__bf16*)(nq < wd ? ea.q : ea.k) + ((b * ea.heads + h) * ea.seq + t) * 64 + d;
-                *(uint4*)dst = v;
+                const int hd = qkv_c0 + (col - ncol);  // h * 64 + d
+                *(uint4*)(qkrow + (int64_t)(hd >> 6) * ea.seq * 64 + (hd & 63)) = v;
             } else {
                 *(uint4*)((__bf16*)ea.out + m * ea.ldc + col) = v;
             }
@@ -1122,14 +1148,294 @@ __global__ __launch_bounds__(512, 2) void gemm5_bf16_kernel(const __bf16* __rest
 #undef G5_LDS_DONE
 }
 
+// v7: v5's persistent 256x256x64 tile and LDS-DMA streams with TWO sections per K-step
+// instead of four: LOAD X reads A quadrant 0 and both W quadrants (16 ds_read_b128), COMPUTE X
+// runs the 32 MFMAs of output quadrants (0,0),(0,1); LOAD Y reads A quadrant 1, COMPUTE Y
+// runs (1,0),(1,1).  Each compute section is 512 MFMA cycles (v5: 256), so the loading
+// partner's LDS latency, DMA issue and lgkmcnt drain fit inside it, at half the barriers.
+// Region refill: A0/W0/W1 of a stage are last read in LOAD X of step s (both halves, one
+// barrier apart) -> refilled for step s+2 in LOAD Y of step s; A1 last read in LOAD Y of
+// step s -> refilled for step s+2 in LOAD X of step s+1.  Every wait is vmcnt(8) (plus the
+// tile's bias/colsum/rowstat pieces at its first K-step).  Per accumulator the MFMA chain
+// (K ascending) is v5's, so results are bit-identical.
+template <int EPI, bool F16>
+__global__ __launch_bounds__(512, 2) void gemm7_bf16_kernel(const __bf16* __restrict__ A, int64_t lda,
+                                                            const __bf16* __restrict__ W, int64_t ldw, int64_t M,
+                                                            int N, int K, EpiArgs ea, int tiles_n, int ntiles) {
+    extern __shared__ __attribute__((aligned(16))) __bf16 lds5[];
+    const int G = gridDim.x;
+    const int bid = blockIdx.x;
+    const int ng = G < 8 ? G : 8;
+    const int xg = bid % ng, gx = G / ng + ((G % ng) > xg ? 1 : 0);
+    const int lo = (int)((int64_t)ntiles * xg / ng), hi = (int)((int64_t)ntiles * (xg + 1) / ng);
+    const int first = lo + bid / ng;
+    if (first >= hi) return;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = wid >> 2, wc = wid & 3;
+    const int nk = K / GB_K;
+
+    int rowA[2][2], kcA[2][2], offA[2][2], offW[2][2];
+    uint32_t offAb[2][2], offWb[2][2];
+#pragma unroll
+    for (int h = 0; h < 2; h++)
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const int pc = 2 * wid + u;
+            const int ra = 128 * (pc >> 3) + 64 * h + 8 * (pc & 7);
+            const int rb = 64 * (pc >> 2) + 32 * h + 8 * (pc & 3);
+            const int r1 = ra + (lane >> 3), r2 = rb + (lane >> 3);
+            rowA[h][u] = r1;
+            kcA[h][u] = ((lane & 7) ^ ((r1 >> 1) & 7)) * 8;
+            offAb[h][u] = (uint32_t)(r1 * (int)lda + kcA[h][u]) * 2u;
+            offWb[h][u] = (uint32_t)(r2 * (int)ldw + ((lane & 7) ^ ((r2 >> 1) & 7)) * 8) * 2u;
+            offA[h][u] = ra * GB_K;
+            offW[h][u] = G2_M * GB_K + rb * GB_K;
+        }
+    struct Pos {
+        int tile, kt;
+        int64_t m0;
+        int n0;
+        bool full;
+    };
+    auto set_tile = [&](Pos& p, int tile) {
+        p.tile = tile;
+        p.kt = 0;
+        p.m0 = (int64_t)(tile / tiles_n) * G2_M;
+        p.n0 = (tile % tiles_n) * G2_N;
+        p.full = p.m0 + G2_M <= M;
+    };
+    auto advance = [&](Pos& p) {
+        if (++p.kt == nk) set_tile(p, p.tile + gx);
+    };
+    auto issue_a = [&](int stage, int h, const Pos& p) {
+        const __bf16* base = A + p.m0 * lda + p.kt * GB_K;
+        if (p.full) {
+#pragma unroll
+            for (int u = 0; u < 2; u++)
+                __builtin_amdgcn_global_load_lds((const char*)base + offAb[h][u],
+                                                 (lds_ptr_t)(lds5 + stage * G2_STAGE + offA[h][u]), 16, 0, 0);
+        } else {
+            const int lim = (int)(M - p.m0);
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const int r = rowA[h][u] < lim ? rowA[h][u] : lim - 1;
+                __builtin_amdgcn_global_load_lds((const char*)base + (uint32_t)(r * (int)lda + kcA[h][u]) * 2u,
+                                                 (lds_ptr_t)(lds5 + stage * G2_STAGE + offA[h][u]), 16, 0, 0);
+            }
+        }
+    };
+    auto issue_w = [&](int stage, int h, const Pos& p) {
+        const __bf16* base = W + (int64_t)p.n0 * ldw + p.kt * GB_K;
+#pragma unroll
+        for (int u = 0; u < 2; u++)
+            __builtin_amdgcn_global_load_lds((const char*)base + offWb[h][u],
+                                             (lds_ptr_t)(lds5 + stage * G2_STAGE + offW[h][u]), 16, 0, 0);
+    };
+#define G7_BARRIER()                              \
+    do {                                          \
+        __builtin_amdgcn_sched_barrier(0);        \
+        __builtin_amdgcn_s_barrier();             \
+        __builtin_amdgcn_sched_barrier(0);        \
+    } while (0)
+#define G7_LDS_DONE() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+#define G7_VM(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
+
+    bf16x8 fa[4][2], fb[4][2];
+    f32x4 acc[8][4];
+    auto load_a = [&](const __bf16* sA, int qm) {
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int ks = 0; ks < 2; ks++)
+                fa[i][ks] = *(const bf16x8*)(sA + swz(wr * 128 + qm * 64 + i * 16 + (lane & 15), ks * 4 + (lane >> 4)));
+    };
+    auto load_b = [&](const __bf16* sW) {
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+#pragma unroll
+            for (int ks = 0; ks < 2; ks++)
+                fb[j][ks] = *(const bf16x8*)(sW + swz(wc * 64 + (j >> 1) * 32 + (j & 1) * 16 + (lane & 15),
+                                                      ks * 4 + (lane >> 4)));
+    };
+    auto compute = [&](int qm) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ks++)
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    acc[qm * 4 + i][j] = mfma16<F16>(fb[j][ks], fa[i][ks], acc[qm * 4 + i][j]);
+    };
+
+    const bool has_bias = EPI != EPI_PATCH && ea.bias != nullptr;
+    float* bias_slot = (float*)(lds5 + 2 * G2_STAGE) + wid * 256;
+    const bool fold = F16 && ea.rowstat != nullptr;
+    float* cs_slot = bias_slot + 8 * 256;
+    float* rs_slot = bias_slot + 16 * 256;
+    // streams: pX = step s+1 (A1, issued in LOAD X), pY = step s+2 (A0, W0, W1, LOAD Y)
+    Pos pX, pY;
+    {
+        Pos p0;
+        set_tile(p0, first);
+        issue_a(0, 0, p0);
+        issue_w(0, 0, p0);
+        issue_w(0, 1, p0);
+        issue_a(0, 1, p0);
+        pX = p0;
+        advance(pX);  // step 1: inside the first tile (nk >= 2)
+        issue_a(1, 0, pX);
+        issue_w(1, 0, pX);
+        issue_w(1, 1, pX);
+        pY = pX;
+        advance(pY);
+        G7_VM(8);  // step 0's A0/W0/W1 landed
+    }
+    __syncthreads();
+    if (wr == 1) G7_BARRIER();
+    int buf = 0;
+    for (int tile = first; tile < hi; tile += gx) {
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int kt = 0; kt < nk; ++kt) {
+            const bool hasX = pX.tile < hi, hasY = pY.tile < hi;
+            const __bf16* sA = lds5 + buf * G2_STAGE;
+            const __bf16* sW = sA + G2_M * GB_K;
+            // LOAD X / COMPUTE X
+            load_a(sA, 0);
+            load_b(sW);
+            int nb = 0;  // tile-start pieces (bias, colsum, rowstat), issued before pX's
+            if (kt == 0 && has_bias) {
+                __builtin_amdgcn_global_load_lds(ea.bias + (tile % tiles_n) * G2_N + lane * 4, (lds_ptr_t)bias_slot,
+                                                 16, 0, 0);
+                nb = 1;
+            }
+            if constexpr (F16) {
+                if (kt == 0 && fold) {
+                    __builtin_amdgcn_global_load_lds(ea.colsum + (tile % tiles_n) * G2_N + lane * 4,
+                                                     (lds_ptr_t)cs_slot, 16, 0, 0);
+                    __builtin_amdgcn_global_load_lds((const float*)(ea.rowstat + (int64_t)(tile / tiles_n) * G2_M +
+                                                                    wr * 128) + lane * 4,
+                                                     (lds_ptr_t)rs_slot, 16, 0, 0);
+                    nb += 2;
+                }
+            }
+            nb = __builtin_amdgcn_readfirstlane(nb);
+            if (hasX) issue_a(buf ^ 1, 1, pX);
+            G7_LDS_DONE();
+            // A1 of this step (issued one LOAD X ago) landed
+            if (!hasX) G7_VM(0);
+            else if (nb == 0) G7_VM(8);
+            else if (nb == 1) G7_VM(9);
+            else G7_VM(11);
+            G7_BARRIER();
+            compute(0);
+            G7_BARRIER();
+            // LOAD Y / COMPUTE Y
+            load_a(sA, 1);
+            if (hasY) {
+                issue_a(buf, 0, pY);
+                issue_w(buf, 0, pY);
+                issue_w(buf, 1, pY);
+            }
+            G7_LDS_DONE();
+            // A0/W0/W1 of step s+1 (issued one LOAD Y ago) landed
+            if (hasY) {
+                if (nb == 0) G7_VM(8);
+                else if (nb == 1) G7_VM(9);
+                else G7_VM(11);
+            } else if (hasX) {
+                if (nb == 0) G7_VM(2);
+                else if (nb == 1) G7_VM(3);
+                else G7_VM(5);
+            } else {
+                G7_VM(0);
+            }
+            G7_BARRIER();
+            compute(1);
+            G7_BARRIER();
+            advance(pX);
+            advance(pY);
+            buf ^= 1;
+        }
+        const int64_t m0 = (int64_t)(tile / tiles_n) * G2_M;
+        const int n0 = (tile % tiles_n) * G2_N;
+        if (has_bias) {
+            // the tile-start pieces were retired by K-step 1's LOAD X wait (nk >= 2)
+            float4 b[4];
+            const float* bp = bias_slot + wc * 64 + (lane >> 4) * 4;
+            const uint32_t ba = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)bp;
+            asm volatile("ds_read_b128 %0, %1" : "=v"(b[0]) : "v"(ba) : "memory");
+            asm volatile("ds_read_b128 %0, %1 offset:64" : "=v"(b[1]) : "v"(ba) : "memory");
+            asm volatile("ds_read_b128 %0, %1 offset:128" : "=v"(b[2]) : "v"(ba) : "memory");
+            asm volatile("ds_read_b128 %0, %1 offset:192" : "=v"(b[3]) : "v"(ba) : "memory");
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if constexpr (F16) {
+                float4 sn[4];
+                float2 rs[8];
+                if (fold) {
+                    const uint32_t ca = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)(
+                        cs_slot + wc * 64 + (lane >> 4) * 4);
+                    const uint32_t ra = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)(
+                        rs_slot + (lane & 15) * 2);
+                    asm volatile("ds_read_b128 %0, %1" : "=v"(sn[0]) : "v"(ca) : "memory");
+                    asm volatile("ds_read_b128 %0, %1 offset:64" : "=v"(sn[1]) : "v"(ca) : "memory");
+                    asm volatile("ds_read_b128 %0, %1 offset:128" : "=v"(sn[2]) : "v"(ca) : "memory");
+                    asm volatile("ds_read_b128 %0, %1 offset:192" : "=v"(sn[3]) : "v"(ca) : "memory");
+                    asm volatile("ds_read_b64 %0, %1" : "=v"(rs[0]) : "v"(ra) : "memory");
+                    asm volatile("ds_read_b64 %0, %1 offset:128" : "=v"(rs[1]) : "v"(ra) : "memory");
+                    asm volatile("ds_read_b64 %0, %1 offset:256" : "=v"(rs[2]) : "v"(ra) : "memory");
+                    asm volatile("ds_read_b64 %0, %1 offset:384" : "=v"(rs[3]) : "v"(ra) : "memory");
+                    asm volatile("ds_read_b64 %0, %1 offset:512" : "=v"(rs[4]) : "v"(ra) : "memory");
+                    asm volatile("ds_read_b64 %0, %1 offset:640" : "=v"(rs[5]) : "v"(ra) : "memory");
+                    asm volatile("ds_read_b64 %0, %1 offset:768" : "=v"(rs[6]) : "v"(ra) : "memory");
+                    asm volatile("ds_read_b64 %0, %1 offset:896" : "=v"(rs[7]) : "v"(ra) : "memory");
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; j++) sn[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                    for (int i = 0; i < 8; i++) rs[i] = make_float2(1.f, 0.f);
+                }
+#pragma unroll
+                for (int i = 0; i < 8; i++)
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        acc[i][j][0] = __builtin_fmaf(rs[i].x, acc[i][j][0], __builtin_fmaf(rs[i].y, sn[j].x, b[j].x));
+                        acc[i][j][1] = __builtin_fmaf(rs[i].x, acc[i][j][1], __builtin_fmaf(rs[i].y, sn[j].y, b[j].y));
+                        acc[i][j][2] = __builtin_fmaf(rs[i].x, acc[i][j][2], __builtin_fmaf(rs[i].y, sn[j].z, b[j].z));
+                        acc[i][j][3] = __builtin_fmaf(rs[i].x, acc[i][j][3], __builtin_fmaf(rs[i].y, sn[j].w, b[j].w));
+                    }
+            } else {
+#pragma unroll
+                for (int i = 0; i < 8; i++)
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        acc[i][j][0] += b[j].x;
+                        acc[i][j][1] += b[j].y;
+                        acc[i][j][2] += b[j].z;
+                        acc[i][j][3] += b[j].w;
+                    }
+            }
+        }
+        epilogue_tile<EPI, 8, true>(ea, acc, m0 + wr * 128, n0 + wc * 64, M, N);
+    }
+    if (wr == 0) G7_BARRIER();
+#undef G7_BARRIER
+#undef G7_LDS_DONE
+#undef G7_VM
+}
+
 template <int EPI, bool F16>
 static int launch(const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N, int64_t K,
                   const EpiArgs& ea, hipStream_t s) {
     int var = variant();
-    if (F16 && var >= 2 && var <= 4) var = 0;  // fp16 operands: v1 / v5 / v6 only
+    if (F16 && var >= 2 && var <= 4) var = 0;  // fp16 operands: v1 / v5 / v6 / v7 only
     const int64_t tiles256 = (int64_t)ceil_div(M, G2_M) * (N / G2_N);
     if (N % G2_N == 0 && K >= 2 * GB_K && lda * G2_M < (1ll << 31) && ldw * G2_N < (1ll << 31) &&
-        (var == 5 || var == 6 || (var == 0 && tiles256 >= 256))) {
+        (var == 5 || var == 6 || var == 7 || (var == 0 && tiles256 >= 256))) {
         const int tiles_m = ceil_div(M, G2_M), tiles_n = (int)(N / G2_N);
         const int64_t ntiles = (int64_t)tiles_m * tiles_n;
         RM_REQUIRE(ntiles < (1ll << 31), "gemm: grid too large");
@@ -1143,7 +1449,16 @@ static int launch(const void* A, int64_t lda, const void* W, int64_t ldw, int64_
             attr5 = true;
         }
         const int grid = (int)(ntiles < 256 ? ntiles : 256);
-        if (var == 6 || var == 0)
+        if (var == 7) {
+            static bool attr7 = false;
+            if (!attr7) {
+                RM_CHECK_HIP(hipFuncSetAttribute((const void*)gemm7_bf16_kernel<EPI, F16>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+                attr7 = true;
+            }
+            hipLaunchKernelGGL((gemm7_bf16_kernel<EPI, F16>), dim3((unsigned)grid), dim3(512), lds, s,
+                               (const __bf16*)A, lda, (const __bf16*)W, ldw, M, (int)N, (int)K, ea, tiles_n, (int)ntiles);
+        } else if (var == 6 || var == 0)
             hipLaunchKernelGGL((gemm5_bf16_kernel<EPI, true, F16>), dim3((unsigned)grid), dim3(512), lds, s,
                                (const __bf16*)A, lda, (const __bf16*)W, ldw, M, (int)N, (int)K, ea, tiles_n, (int)ntiles);
         else
@@ -1214,6 +1529,7 @@ template <bool F16>
 static int gemm_any(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N, int64_t K,
                     const EpiArgs& ea, hipStream_t s) {
     RM_REQUIRE(M >= 0 && N > 0 && K > 0, "gemm: bad shape");
+    RM_REQUIRE((epi != EPI_QKV && epi != EPI_PATCH) || M < (1ll << 31), "gemm: head split / patch rows need M < 2^31");
     RM_REQUIRE(N % GB_N == 0 && K % GB_K == 0, "gemm: needs N % 128 == 0 and K % 64 == 0");
     RM_REQUIRE(lda % 8 == 0 && ldw % 8 == 0 && lda >= K && ldw >= K, "gemm: lda/ldw must be >= K and 16-byte rows");
     RM_REQUIRE((epi != EPI_BF16 && epi != EPI_GELU_BF16 && epi != EPI_RESID_F16) ||
@@ -1275,8 +1591,8 @@ int gemm_f16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, in
 using namespace reidmi;
 
 REIDMI_API int reidmi_gemm_set_variant(int v) {
-    RM_REQUIRE(v >= 0 && v <= 6, "gemm variant: 0 auto, 1 128x128, 2 256x256, 3 256x256 persistent, 4 ping-pong, "
-                                 "5 persistent ping-pong, 6 = 5 with deferred epilogue-store waits");
+    RM_REQUIRE(v >= 0 && v <= 7, "gemm variant: 0 auto, 1 128x128, 2 256x256, 3 256x256 persistent, 4 ping-pong, "
+                                 "5 persistent ping-pong, 6 = 5 with deferred epilogue-store waits, 7 = 5 with two sections per K-step");
     g_variant = v;
     return OK;
 }

@@ -61,7 +61,7 @@ def test_gemm_epilogues(gpu, epi, M, N, K):
 @pytest.mark.parametrize("M,N,K", [(54016, 768, 768), (1000, 2304, 768), (700, 512, 3072), (70000, 256, 192)])
 def test_gemm_v2_tile_bitexact_vs_v1(gpu, epi, M, N, K):
     """The 256x256 LDS-DMA tiles (v2 plain, v3 persistent, v4 ping-pong, v5 persistent
-    ping-pong, v6 = v5 with deferred epilogue-store waits; odd K-step counts cross tiles with the stage parity flipped) and the 128x128
+    ping-pong, v6 = v5 with deferred epilogue-store waits, v7 = v5 with two sections per K-step; odd K-step counts cross tiles with the stage parity flipped) and the 128x128
     register-staged tile run the same MFMA
     sequence per output element (k-steps ascending), so they agree bit for bit; rows
     past M (clamped source rows) must not leak into the result."""
@@ -71,7 +71,7 @@ def test_gemm_v2_tile_bitexact_vs_v1(gpu, epi, M, N, K):
     W = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16).cuda()
     bias = torch.randn(N, generator=g).cuda()
     outs = []
-    for v in (1, 2, 3, 4, 5, 6):
+    for v in (1, 2, 3, 4, 5, 6, 7):
         L.call("reidmi_gemm_set_variant", v)
         if epi in (0, 1):
             out = torch.zeros(M, N, dtype=torch.bfloat16, device="cuda")
@@ -98,7 +98,7 @@ def test_gemm_v2_tile_bitexact_vs_v1(gpu, epi, M, N, K):
 def test_gemm_f16_layernorm_fold(gpu, epi, M, N, K):
     """ln_1 / ln_2 folded into the fp16 QKV / c_fc GEMM (model.fold_layernorm + row statistics):
     epi(LN(x) W^T + b) against fp64 torch on the same fp16 x, rows with large means (the
-    cancellation the fold must survive); v1 and v6 tiles bit-identical."""
+    cancellation the fold must survive); v1, v6 and v7 tiles bit-identical."""
     from multimodal_reid_amd.model import fold_layernorm
     L = _lib()
     g = torch.Generator().manual_seed(M + N + K)
@@ -117,14 +117,15 @@ def test_gemm_f16_layernorm_fold(gpu, epi, M, N, K):
         ref = ref * torch.sigmoid(1.702 * ref)
     dx, dw, dcs, dbf, drs = (t.cuda() for t in (x, wf, cs, bf, rs))
     outs = []
-    for v in (1, 6):
+    for v in (1, 6, 7):
         L.call("reidmi_gemm_set_variant", v)
         out = torch.zeros(M, N, dtype=torch.bfloat16, device="cuda")
         L.call("reidmi_gemm_f16", epi, L.ptr(dx), K, L.ptr(dw), K, M, N, K, L.ptr(dbf), L.ptr(drs), L.ptr(dcs),
                L.ptr(out), N, L.stream())
         outs.append(out)
     L.call("reidmi_gemm_set_variant", 0)
-    assert torch.equal(outs[0], outs[1])
+    for o in outs[1:]:
+        assert torch.equal(outs[0], o)
     got = outs[0].double().cpu()
     assert (got - ref).abs().max() <= 1e-2 * (ref.abs().max() + 1)
     assert _cos(got.numpy(), ref.numpy()).min() >= 0.9999
