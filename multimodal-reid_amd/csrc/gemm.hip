@@ -37,8 +37,11 @@ static size_t used = 0;
 
 // Tile selection: 0 = auto (>= 256 tiles of 256x256: v6; else v1), 1..6 force
 // v1 (128x128), v2 (256x256), v3 (persistent), v4 (ping-pong), v5 (persistent ping-pong),
-// v6 (v5 with deferred epilogue-store waits: +1-2 % on the K = 768 shapes).  Set by reidmi_gemm_set_variant (tests / A-B timing in one process); the
-// REIDMI_GEMM_VARIANT environment variable gives the initial value.
+// v6 (v5 with deferred epilogue-store waits: +1-2 % on the K = 768 shapes); A/B-only:
+// v7 (two 32-MFMA sections per K-step: 1-3 % SLOWER than v5/v6, kept as the measured
+// negative), v8 / v9 (v6 with the residual epilogue loading 2 / 4 row groups per batch
+// instead of all 8).  Set by reidmi_gemm_set_variant (tests / A-B timing in one process);
+// the REIDMI_GEMM_VARIANT environment variable gives the initial value.
 static int g_variant = -1;
 static int variant() {
     if (g_variant < 0) {
@@ -122,7 +125,7 @@ __device__ __forceinline__ void ln_fold(f32x4 (&acc)[NI][4], const float2* __res
 // once per tile, residual / pos-embed rows in batches of NB row groups — otherwise the
 // compiler (which cannot prove `out` does not alias `bias`/`pos`) serialises one memory
 // round trip per fragment.
-template <int EPI, int NI, bool BIAS_DONE = false>
+template <int EPI, int NI, bool BIAS_DONE = false, int RNB = 2>
 __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI][4], int64_t mrow, int ncol,
                                               int64_t M, int N) {
     const int lane = threadIdx.x & 63;
@@ -163,7 +166,10 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
             }
         _Float16* xo = (_Float16*)ea.out;
         auto colp = [&](int jp) { return ncol + (2 * jp + (q & 1)) * 16 + (q >> 1) * 8; };
-        constexpr int NB = 2;  // row groups per batch: 4 x 16-byte loads in flight per lane
+        // row groups per batch (2*NB 16-byte loads in flight per lane).  The persistent tiles
+        // load the whole residual block at once (RNB = 8: +6 % on out_proj at K = 768, where
+        // the epilogue's HBM round trips are not amortised; v8 / v9 keep 2 / 4 for A/B).
+        constexpr int NB = RNB < NI ? RNB : NI;
         auto store_batch = [&](int i0) {
 #pragma unroll
             for (int ii = 0; ii < NB; ii++) {
@@ -837,7 +843,7 @@ struct EpiVm {  // vector-memory instructions of one full-tile epilogue_tile<EPI
                                                                                           : -1;
 };
 
-template <int EPI, bool DEFER, bool F16>
+template <int EPI, bool DEFER, bool F16, int RNB = 8>
 __global__ __launch_bounds__(512, 2) void gemm5_bf16_kernel(const __bf16* __restrict__ A, int64_t lda,
                                                             const __bf16* __restrict__ W, int64_t ldw, int64_t M,
                                                             int N, int K, EpiArgs ea, int tiles_n, int ntiles) {
@@ -1141,7 +1147,7 @@ __global__ __launch_bounds__(512, 2) void gemm5_bf16_kernel(const __bf16* __rest
                     }
             }
         }
-        epilogue_tile<EPI, 8, true>(ea, acc, m0 + wr * 128, n0 + wc * 64, M, N);
+        epilogue_tile<EPI, 8, true, RNB>(ea, acc, m0 + wr * 128, n0 + wc * 64, M, N);
     }
     if (wr == 0) G5_BARRIER();
 #undef G5_BARRIER
@@ -1435,7 +1441,7 @@ static int launch(const void* A, int64_t lda, const void* W, int64_t ldw, int64_
     if (F16 && var >= 2 && var <= 4) var = 0;  // fp16 operands: v1 / v5 / v6 / v7 only
     const int64_t tiles256 = (int64_t)ceil_div(M, G2_M) * (N / G2_N);
     if (N % G2_N == 0 && K >= 2 * GB_K && lda * G2_M < (1ll << 31) && ldw * G2_N < (1ll << 31) &&
-        (var == 5 || var == 6 || var == 7 || (var == 0 && tiles256 >= 256))) {
+        (var >= 5 || (var == 0 && tiles256 >= 256))) {
         const int tiles_m = ceil_div(M, G2_M), tiles_n = (int)(N / G2_N);
         const int64_t ntiles = (int64_t)tiles_m * tiles_n;
         RM_REQUIRE(ntiles < (1ll << 31), "gemm: grid too large");
@@ -1458,6 +1464,23 @@ static int launch(const void* A, int64_t lda, const void* W, int64_t ldw, int64_
             }
             hipLaunchKernelGGL((gemm7_bf16_kernel<EPI, F16>), dim3((unsigned)grid), dim3(512), lds, s,
                                (const __bf16*)A, lda, (const __bf16*)W, ldw, M, (int)N, (int)K, ea, tiles_n, (int)ntiles);
+        } else if (var == 8 || var == 9) {  // A/B: the residual epilogue's old load batches
+            static bool attr89 = false;
+            if (!attr89) {
+                RM_CHECK_HIP(hipFuncSetAttribute((const void*)gemm5_bf16_kernel<EPI, true, F16, 2>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+                RM_CHECK_HIP(hipFuncSetAttribute((const void*)gemm5_bf16_kernel<EPI, true, F16, 4>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+                attr89 = true;
+            }
+            if (var == 8)
+                hipLaunchKernelGGL((gemm5_bf16_kernel<EPI, true, F16, 2>), dim3((unsigned)grid), dim3(512), lds, s,
+                                   (const __bf16*)A, lda, (const __bf16*)W, ldw, M, (int)N, (int)K, ea, tiles_n,
+                                   (int)ntiles);
+            else
+                hipLaunchKernelGGL((gemm5_bf16_kernel<EPI, true, F16, 4>), dim3((unsigned)grid), dim3(512), lds, s,
+                                   (const __bf16*)A, lda, (const __bf16*)W, ldw, M, (int)N, (int)K, ea, tiles_n,
+                                   (int)ntiles);
         } else if (var == 6 || var == 0)
             hipLaunchKernelGGL((gemm5_bf16_kernel<EPI, true, F16>), dim3((unsigned)grid), dim3(512), lds, s,
                                (const __bf16*)A, lda, (const __bf16*)W, ldw, M, (int)N, (int)K, ea, tiles_n, (int)ntiles);
@@ -1591,8 +1614,8 @@ int gemm_f16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, in
 using namespace reidmi;
 
 REIDMI_API int reidmi_gemm_set_variant(int v) {
-    RM_REQUIRE(v >= 0 && v <= 7, "gemm variant: 0 auto, 1 128x128, 2 256x256, 3 256x256 persistent, 4 ping-pong, "
-                                 "5 persistent ping-pong, 6 = 5 with deferred epilogue-store waits, 7 = 5 with two sections per K-step");
+    RM_REQUIRE(v >= 0 && v <= 9, "gemm variant: 0 auto, 1 128x128, 2 256x256, 3 256x256 persistent, 4 ping-pong, "
+                                 "5 persistent ping-pong, 6 = 5 with deferred epilogue-store waits, 7 = 5 with two sections per K-step, 8 / 9 = 6 with 2 / 4 (default 8) residual row groups per load batch");
     g_variant = v;
     return OK;
 }

@@ -71,7 +71,7 @@ def test_gemm_v2_tile_bitexact_vs_v1(gpu, epi, M, N, K):
     W = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16).cuda()
     bias = torch.randn(N, generator=g).cuda()
     outs = []
-    for v in (1, 2, 3, 4, 5, 6, 7):
+    for v in (1, 2, 3, 4, 5, 6, 7, 8, 9):
         L.call("reidmi_gemm_set_variant", v)
         if epi in (0, 1):
             out = torch.zeros(M, N, dtype=torch.bfloat16, device="cuda")
