@@ -17,7 +17,7 @@ star's target, MSMT17 end to end on all ranks (sharded embed, all-gather, distma
 sharded k-reciprocal re-rank + CMC/mAP, wall seconds max over ranks); "rerank" = configs[2]'s
 Duke-size re-rank on rank 0 with the C port timed on a sample; "cpu_baseline".
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--no-cpu-baseline] [--no-rerank]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B (default 1024)] [--no-cpu-baseline] [--no-rerank]
                     [--no-msmt17]
 """
 import argparse
@@ -41,13 +41,15 @@ from multimodal_reid_amd.model import VisionTransformer  # noqa: E402
 
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 EPI_GELU = 1  # the c_fc GEMM (+QuickGELU epilogue): the largest single kernel per block
-# HBM-side bytes per c_fc launch (ln_2-folded fp16 GEMM, M = 512*211, N = 3072, K = 768) from
-# rocprofv3 PMC passes (tools/prof_round.sh -> profiles/r01/pmc_c_fc_fold_{FETCH,WRITE}_SIZE.csv,
-# mean of the 5 timed launches): FETCH_SIZE 511 608 KiB doubled (gfx950 reports half of
-# 16-B/lane streaming reads, MI355X_MICROARCH.md "HBM") + WRITE_SIZE 648 192 KiB.  FETCH_SIZE
-# also counts Infinity-Cache hits (the 4.7 MB weight panel re-read by every tile).
-# Algorithmic: A 166 MB + W 4.7 MB + out 664 MB = 835 MB.
-C_FC_TRAFFIC_BYTES = (2 * 511608 + 648192) * 1024
+# HBM-side bytes per c_fc launch (ln_2-folded fp16 GEMM, M = 1024*211 (the default batch),
+# N = 3072, K = 768) from rocprofv3 PMC passes (tools/prof_round.sh ->
+# profiles/r01/pmc_c_fc_fold_b1024_{FETCH,WRITE}_SIZE.csv, mean of the 5 timed launches):
+# FETCH_SIZE 1 103 090 KiB doubled (gfx950 reports half of 16-B/lane streaming reads,
+# MI355X_MICROARCH.md "HBM") + WRITE_SIZE 1 296 384 KiB.  FETCH_SIZE also counts
+# Infinity-Cache hits: the 4.7 MB weight (393 KB per 256-column panel) is re-read by every
+# one of the 10 128 tiles and does not stay in a 4 MB XCD L2.
+# Algorithmic: A 332 MB + W 4.7 MB + out 1 327 MB = 1.66 GB.
+C_FC_TRAFFIC_BYTES = (2 * 1103090 + 1296384) * 1024
 
 
 def shard(n, rank, world):
@@ -283,7 +285,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=512)
+    ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-rerank", action="store_true")
     ap.add_argument("--no-msmt17", action="store_true")
@@ -315,7 +317,12 @@ def main():
     elapsed = time.perf_counter() - t0
     import ctypes
     ms, cnt, fl = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
-    L.reidmi_prof_collect(EPI_GELU, ctypes.byref(ms), ctypes.byref(cnt), ctypes.byref(fl))
+    # persistent-tile c_fc launches only (>= half a full batch; the CLS-only last block's small
+    # c_fc runs a different kernel), so avg_launch_ms is comparable with that kernel's row
+    # in the rocprofv3 --stats summary
+    full = 2.0 * a.batch * 211 * 3072 * 768
+    L.reidmi_prof_collect_min(EPI_GELU, ctypes.c_double(0.5 * full), ctypes.byref(ms), ctypes.byref(cnt),
+                              ctypes.byref(fl))
     L.reidmi_prof_enable(0)
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)

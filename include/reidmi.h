@@ -151,6 +151,9 @@ int reidmi_gemm_f16(int epi, const void* A, int64_t lda, const void* W, int64_t 
  * returns summed device ms, launch count, algorithmic FLOPs (2MNK) and clears the record. */
 int reidmi_prof_enable(int on);
 int reidmi_prof_collect(int epi, double* total_ms, int64_t* count, double* flops);
+/* Same, counting only launches of >= min_flops (e.g. the full-batch launches of a kernel,
+ * so that the average matches that kernel's row in a rocprofv3 --stats summary). */
+int reidmi_prof_collect_min(int epi, double min_flops, double* total_ms, int64_t* count, double* flops);
 
 /* GEMM tile selection: 0 = auto, 1 = 128x128x64 (4 waves), 2 = 256x256x64 (8 waves, LDS-DMA),
  * 3 = variant 2 persistent (one workgroup per CU, cross-tile prefetch), 4 = 256x256 ping-pong

@@ -46,6 +46,7 @@ SIGNATURES = {
     "reidmi_prof_enable": [_i32],
     "reidmi_gemm_set_variant": [_i32],
     "reidmi_prof_collect": [_i32, _vp, _vp, _vp],
+    "reidmi_prof_collect_min": [_i32, ctypes.c_double, _vp, _vp, _vp],
     "reidmi_mhsa_bf16": [_vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp],
     "reidmi_layernorm": [_vp, _i64, _i64, _vp, _i64, _vp, _vp, _f32, _vp, _i64, _vp, _i64, _vp],
     "reidmi_feature_tta_avg": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _i64, _vp],

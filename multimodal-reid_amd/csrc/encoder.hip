@@ -124,6 +124,42 @@ static int row_stats(const _Float16* x, int64_t rows, int64_t ldx, int64_t W, fl
     return layernorm(x, rows, ldx, nullptr, W, nullptr, nullptr, 1e-5f, nullptr, 0, nullptr, 0, s, nullptr, 0, st);
 }
 
+// Row statistics from the residual epilogue's 64-column partials pst[b * rows + r]
+// (Chan et al.'s pairwise combination): mean = sum / W, M2 = sum_b M2_b + 64 (mean_b - mean)^2, rstd = rsq(M2 / W +
+// eps) -> st[r] = (rstd, -mean * rstd), replacing a statistics pass over x.
+__global__ void rowstat_combine_kernel(const float2* __restrict__ pst, int nb, int64_t rows, float invw, float eps,
+                                       float2* __restrict__ st) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= rows) return;
+    float2 v[16];  // nb <= 16 (W <= 1024)
+#pragma unroll
+    for (int b = 0; b < 16; b++)
+        if (b < nb) v[b] = pst[b * rows + r];
+    float sum = 0.f;
+#pragma unroll
+    for (int b = 0; b < 16; b++)
+        if (b < nb) sum += v[b].x;
+    const float mean = sum * invw;
+    float m2 = 0.f;
+#pragma unroll
+    for (int b = 0; b < 16; b++) {
+        if (b >= nb) break;
+        const float d = v[b].x * (1.0f / 64) - mean;
+        m2 += __builtin_fmaf(64.0f * d, d, v[b].y);
+    }
+    const float rstd = __builtin_amdgcn_rsqf(m2 * invw + eps);
+    st[r] = make_float2(rstd, -mean * rstd);
+}
+
+static int row_stats_from_partials(const float2* pst, int64_t rows, int W, float2* st, hipStream_t s) {
+    if (rows == 0) return OK;
+    RM_REQUIRE(W % 64 == 0 && W <= 1024, "row statistics: width must be a multiple of 64, <= 1024");
+    hipLaunchKernelGGL(rowstat_combine_kernel, dim3(ceil_div(rows, 256)), dim3(256), 0, s, pst, W / 64, rows,
+                       1.0f / W, 1e-5f, st);
+    RM_LAUNCHED();
+    return OK;
+}
+
 // fp16 residual rows -> fp32 output rows (x11 of encode_image / encode_cls)
 __global__ void rows_f16_to_f32_kernel(const _Float16* __restrict__ x, int64_t rows, int64_t ldx, int W,
                                        float* __restrict__ y) {
@@ -264,7 +300,7 @@ __global__ void eot_rows_kernel(const int64_t* __restrict__ tokens, int64_t N, i
 
 // --------------------------------------------------------------- workspace plan
 struct Plan {
-    int64_t x, h, q, k, vt, o, u, rows, st, st_cls, total;
+    int64_t x, h, q, k, vt, o, u, rows, st, st_cls, pst, total;
 };
 
 static int64_t al(int64_t v) { return (v + 255) & ~(int64_t)255; }
@@ -285,6 +321,9 @@ static Plan plan(int64_t nseq, int L, int W, int lp, int64_t extra_rows) {
     // 256-row GEMM tiles (the folded GEMM reads them per tile, gemm.h)
     p.st = off; off = al(off + (M + 256) * 8);
     p.st_cls = off; off = al(off + (nseq + 256) * 8);
+    // LayerNorm partials [W/64][M] (sum, centred sum of squares) written by the residual
+    // GEMM epilogues (gemm.h EpiArgs::pstat)
+    p.pst = off; off = al(off + M * (W / 64) * 8);
     p.total = off;
     return p;
 }
@@ -292,15 +331,19 @@ static Plan plan(int64_t nseq, int L, int W, int lp, int64_t extra_rows) {
 // One ResidualAttentionBlock on the fp16 residual stream x [nseq*L][W].  ln_1 / ln_2 are
 // folded into the QKV / c_fc GEMMs (fp16 operands: x itself and W diag(gamma)); only the
 // per-row statistics are computed here (row_stats), never the normalised activations.
+// x_pst: the partials at P.pst describe x as it is now (written by the previous block's
+// c_proj epilogue and not overwritten since), so ln_1's statistics are combined from them.
 static int run_block(const reidmi_block_weights& bw, char* ws, const Plan& P, int64_t nseq, int L, int W, int H,
-                     bool causal, hipStream_t s) {
+                     bool causal, bool x_pst, hipStream_t s) {
     const int64_t M = nseq * L;
+    float2* pst = (float2*)(ws + P.pst);
     _Float16* x = (_Float16*)(ws + P.x);
     __bf16* o = (__bf16*)(ws + P.o);
     __bf16* u = (__bf16*)(ws + P.u);
     float2* st = (float2*)(ws + P.st);
     int rc;
-    if ((rc = row_stats(x, M, W, W, st, s))) return rc;  // ln_1 (custom_clip_model.py:27)
+    // ln_1 (custom_clip_model.py:27)
+    if ((rc = x_pst ? row_stats_from_partials(pst, M, W, st, s) : row_stats(x, M, W, W, st, s))) return rc;
     EpiArgs ea{};
     ea.bias = bw.qkv_b;
     ea.rowstat = st;
@@ -317,8 +360,10 @@ static int run_block(const reidmi_block_weights& bw, char* ws, const Plan& P, in
     er.out = x;
     er.ldc = W;
     er.bias = bw.out_b;
+    er.pstat = pst;
+    er.ldp = M;
     if ((rc = gemm_bf16(EPI_RESID_F16, o, W, bw.out_w, W, M, W, W, er, s))) return rc;
-    if ((rc = row_stats(x, M, W, W, st, s))) return rc;  // ln_2 (custom_clip_model.py:28)
+    if ((rc = row_stats_from_partials(pst, M, W, st, s))) return rc;  // ln_2 (custom_clip_model.py:28)
     EpiArgs eg{};
     eg.out = u;
     eg.ldc = 4 * W;
@@ -330,6 +375,8 @@ static int run_block(const reidmi_block_weights& bw, char* ws, const Plan& P, in
     e2.out = x;
     e2.ldc = W;
     e2.bias = bw.fc2_b;
+    e2.pstat = pst;  // for the next block's ln_1
+    e2.ldp = M;
     if ((rc = gemm_bf16(EPI_RESID_F16, u, 4 * W, bw.fc2_w, 4 * W, M, W, 4 * W, e2, s))) return rc;
     return OK;
 }
@@ -341,7 +388,7 @@ static int run_block(const reidmi_block_weights& bw, char* ws, const Plan& P, in
 // row, GEMM outputs per element), so the result is bit-identical to the full block's row 0
 // (tests/test_gpu_encoder.py checks equality).
 static int run_block_cls(const reidmi_block_weights& bw, char* ws, const Plan& P, int64_t nseq, int L, int W, int H,
-                         hipStream_t s) {
+                         bool x_pst, hipStream_t s) {
     const int64_t M = nseq * L;
     _Float16* x = (_Float16*)(ws + P.x);
     __bf16* o = (__bf16*)(ws + P.o);
@@ -350,7 +397,8 @@ static int run_block_cls(const reidmi_block_weights& bw, char* ws, const Plan& P
     float2* sc = (float2*)(ws + P.st_cls);
     const int64_t ldc = (int64_t)L * W;  // CLS row of each sequence
     int rc;
-    if ((rc = row_stats(x, M, W, W, st, s))) return rc;
+    if ((rc = x_pst ? row_stats_from_partials((const float2*)(ws + P.pst), M, W, st, s) : row_stats(x, M, W, W, st, s)))
+        return rc;
     if ((rc = row_stats(x, nseq, ldc, W, sc, s))) return rc;
     EpiArgs kv{};
     kv.bias = bw.qkv_b + W;
@@ -482,8 +530,11 @@ REIDMI_API int reidmi_vit_forward(const reidmi_vit_weights* w, const void* image
                                L - w->n_ctx, w->n_ctx, bw.prompt);
             RM_LAUNCHED();
         }
-        if (i == 11 && !full) rc = run_block_cls(bw, ws, P, B, L, W, w->heads, s);
-        else rc = run_block(bw, ws, P, B, L, W, w->heads, false, s);
+        // x's partials are current unless this is block 0 (x from ln_pre) or prompt rows
+        // were just overwritten (IVLP)
+        const bool x_pst = i > 0 && !(bw.prompt && w->n_ctx > 0);
+        if (i == 11 && !full) rc = run_block_cls(bw, ws, P, B, L, W, w->heads, x_pst, s);
+        else rc = run_block(bw, ws, P, B, L, W, w->heads, false, x_pst, s);
         if (rc) return rc;
         if (i == 10 && out_x11) {  // resblocks[:11] output (fp16 stream -> fp32)
             const int64_t r11 = full ? M : B;
@@ -535,7 +586,8 @@ REIDMI_API int reidmi_text_forward(const reidmi_text_weights* w, const int64_t* 
                                w->n_ctx, bw.prompt);
             RM_LAUNCHED();
         }
-        if ((rc = run_block(bw, ws, P, N, L, W, w->heads, true, s))) return rc;
+        const bool x_pst = i > 0 && !(bw.prompt && w->n_ctx > 0);
+        if ((rc = run_block(bw, ws, P, N, L, W, w->heads, true, x_pst, s))) return rc;
     }
     hipLaunchKernelGGL(eot_rows_kernel, dim3(ceil_div(N, 256)), dim3(256), 0, s, tokens, N, L, rows);
     RM_LAUNCHED();

@@ -47,6 +47,12 @@ struct EpiArgs {
     const float2* rowstat;  // [round_up(M, 256)] (rstd, -mean*rstd) of the A rows (entries
                             // past M are read, not used), or null (no fold)
     const float* colsum;    // [N] s_n
+    // EPI_RESID_F16: LayerNorm partials of the updated rows, or null.  pstat[c * ldp + m]
+    // = (sum, sum of (v - sum/64)^2) of row m over columns [64c, 64c + 64) of the fp16
+    // values written (column-block-major, ldp >= M: 16 consecutive rows per store and
+    // coalesced reads in the encoder's rowstat_combine_kernel)
+    float2* pstat;
+    int64_t ldp;
 };
 
 // Launch C = A . W^T with epilogue `epi`.  Requires N % 128 == 0, K % 64 == 0,

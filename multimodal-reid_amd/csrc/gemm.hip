@@ -174,13 +174,39 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
 #pragma unroll
             for (int ii = 0; ii < NB; ii++) {
                 const int64_t m = mrow + (i0 + ii) * 16 + (lane & 15);
-                if (m >= M) continue;
+                const bool live = m < M;
+                f16x8 h[2];
 #pragma unroll
                 for (int jp = 0; jp < 2; jp++) {
                     const f32x4 a = acc[i0 + ii][2 * jp], b = acc[i0 + ii][2 * jp + 1];
-                    const f16x8 h = {(_Float16)a[0], (_Float16)a[1], (_Float16)a[2], (_Float16)a[3],
-                                     (_Float16)b[0], (_Float16)b[1], (_Float16)b[2], (_Float16)b[3]};
-                    *(f16x8*)(xo + m * ea.ldc + colp(jp)) = h;
+                    h[jp] = f16x8{(_Float16)a[0], (_Float16)a[1], (_Float16)a[2], (_Float16)a[3],
+                                  (_Float16)b[0], (_Float16)b[1], (_Float16)b[2], (_Float16)b[3]};
+                    if (live) *(f16x8*)(xo + m * ea.ldc + colp(jp)) = h[jp];
+                }
+                if (ea.pstat) {
+                    // LayerNorm partials of the new fp16 row values over this wave's 64 columns
+                    // (the 4 lane groups hold 16 each): sum, then the centred sum of squares
+                    f32x2v sp = {0.f, 0.f};
+#pragma unroll
+                    for (int jp = 0; jp < 2; jp++)
+#pragma unroll
+                        for (int e = 0; e < 8; e += 2) sp += f32x2v{(float)h[jp][e], (float)h[jp][e + 1]};
+                    float sum = sp.x + sp.y;
+                    sum += __shfl_xor(sum, 16, 64);
+                    sum += __shfl_xor(sum, 32, 64);
+                    const f32x2v mu = {sum * (1.0f / 64), sum * (1.0f / 64)};
+                    f32x2v dp = {0.f, 0.f};
+#pragma unroll
+                    for (int jp = 0; jp < 2; jp++)
+#pragma unroll
+                        for (int e = 0; e < 8; e += 2) {
+                            const f32x2v d = f32x2v{(float)h[jp][e], (float)h[jp][e + 1]} - mu;
+                            dp = __builtin_elementwise_fma(d, d, dp);
+                        }
+                    float m2 = dp.x + dp.y;
+                    m2 += __shfl_xor(m2, 16, 64);
+                    m2 += __shfl_xor(m2, 32, 64);
+                    if (live && (lane >> 4) == 0) ea.pstat[(ncol >> 6) * ea.ldp + m] = make_float2(sum, m2);
                 }
             }
         };
@@ -1630,12 +1656,13 @@ REIDMI_API int reidmi_prof_enable(int on) {
 
 // Sum of device time (ms), launch count and algorithmic FLOPs of the recorded GEMM launches
 // with epilogue `epi` (-1: all).  Waits for the recorded events; then clears the record.
-REIDMI_API int reidmi_prof_collect(int epi, double* total_ms, int64_t* count, double* flops) {
+REIDMI_API int reidmi_prof_collect_min(int epi, double min_flops, double* total_ms, int64_t* count, double* flops) {
     std::lock_guard<std::mutex> g(prof::mu);
     double t = 0, f = 0;
     int64_t n = 0;
     for (auto& r : prof::recs) {
         if (epi >= 0 && r.epi != epi) continue;
+        if (r.flops < min_flops) continue;
         RM_CHECK_HIP(hipEventSynchronize(r.b));
         float ms = 0;
         RM_CHECK_HIP(hipEventElapsedTime(&ms, r.a, r.b));
@@ -1649,6 +1676,10 @@ REIDMI_API int reidmi_prof_collect(int epi, double* total_ms, int64_t* count, do
     prof::recs.clear();
     prof::used = 0;
     return OK;
+}
+
+REIDMI_API int reidmi_prof_collect(int epi, double* total_ms, int64_t* count, double* flops) {
+    return reidmi_prof_collect_min(epi, 0.0, total_ms, count, flops);
 }
 
 REIDMI_API int reidmi_gemm_f16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N,
