@@ -127,23 +127,21 @@ static int row_stats(const _Float16* x, int64_t rows, int64_t ldx, int64_t W, fl
 // Row statistics from the residual epilogue's 64-column partials pst[b * rows + r]
 // (Chan et al.'s pairwise combination): mean = sum / W, M2 = sum_b M2_b + 64 (mean_b - mean)^2, rstd = rsq(M2 / W +
 // eps) -> st[r] = (rstd, -mean * rstd), replacing a statistics pass over x.
-__global__ void rowstat_combine_kernel(const float2* __restrict__ pst, int nb, int64_t rows, float invw, float eps,
-                                       float2* __restrict__ st) {
+template <int NB>
+__global__ __launch_bounds__(256) void rowstat_combine_kernel(const float2* __restrict__ pst, int64_t rows, float invw,
+                                                              float eps, float2* __restrict__ st) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= rows) return;
-    float2 v[16];  // nb <= 16 (W <= 1024)
+    float2 v[NB];
 #pragma unroll
-    for (int b = 0; b < 16; b++)
-        if (b < nb) v[b] = pst[b * rows + r];
+    for (int b = 0; b < NB; b++) v[b] = pst[b * rows + r];
     float sum = 0.f;
 #pragma unroll
-    for (int b = 0; b < 16; b++)
-        if (b < nb) sum += v[b].x;
+    for (int b = 0; b < NB; b++) sum += v[b].x;
     const float mean = sum * invw;
     float m2 = 0.f;
 #pragma unroll
-    for (int b = 0; b < 16; b++) {
-        if (b >= nb) break;
+    for (int b = 0; b < NB; b++) {
         const float d = v[b].x * (1.0f / 64) - mean;
         m2 += __builtin_fmaf(64.0f * d, d, v[b].y);
     }
@@ -153,9 +151,13 @@ __global__ void rowstat_combine_kernel(const float2* __restrict__ pst, int nb, i
 
 static int row_stats_from_partials(const float2* pst, int64_t rows, int W, float2* st, hipStream_t s) {
     if (rows == 0) return OK;
-    RM_REQUIRE(W % 64 == 0 && W <= 1024, "row statistics: width must be a multiple of 64, <= 1024");
-    hipLaunchKernelGGL(rowstat_combine_kernel, dim3(ceil_div(rows, 256)), dim3(256), 0, s, pst, W / 64, rows,
-                       1.0f / W, 1e-5f, st);
+    const dim3 g((unsigned)ceil_div(rows, 256)), t(256);
+    switch (W) {
+        case 512: hipLaunchKernelGGL(rowstat_combine_kernel<8>, g, t, 0, s, pst, rows, 1.0f / W, 1e-5f, st); break;
+        case 768: hipLaunchKernelGGL(rowstat_combine_kernel<12>, g, t, 0, s, pst, rows, 1.0f / W, 1e-5f, st); break;
+        case 1024: hipLaunchKernelGGL(rowstat_combine_kernel<16>, g, t, 0, s, pst, rows, 1.0f / W, 1e-5f, st); break;
+        default: return fail(EINVAL_, "row statistics: width must be 512, 768 or 1024");
+    }
     RM_LAUNCHED();
     return OK;
 }
