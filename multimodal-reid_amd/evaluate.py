@@ -140,7 +140,9 @@ def eval_func(distmat, q_pids, g_pids, q_camids, g_camids, max_rank=50):
 
 
 class R1_mAP_eval():
-    """evaluate.py:91-135.  Features stay on the GPU (the reference copies them to the CPU)."""
+    """evaluate.py:91-135.  Features stay on the GPU (the reference copies them to the CPU).
+    As in the reference, ``max_rank`` is stored but compute() scores with eval_func's
+    default 50 (evaluate.py:132): the CMC is 50 long whatever max_rank was given."""
 
     def __init__(self, num_query, max_rank=50, feat_norm=True, reranking=False):
         super(R1_mAP_eval, self).__init__()
@@ -178,7 +180,7 @@ class R1_mAP_eval():
         else:
             print('=> Computing DistMat with euclidean_distance')
             distmat = euclidean_distance_device(qf, gf)
-        cmc, mAP = eval_func_device(distmat, q_pids, g_pids, q_camids, g_camids, self.max_rank)
+        cmc, mAP = eval_func_device(distmat, q_pids, g_pids, q_camids, g_camids)
         print("Rank@{:d}:{:.1%}, Rank@{:d}:{:.1%}, Rank@{:d}:{:.1%}, mAP:{:.1%}".format(
             1, cmc[0], 5, cmc[4], 10, cmc[9], mAP))
         return cmc, mAP

@@ -194,6 +194,47 @@ def features(q_pids, g_pids, dim=1280, seed=0, noise=4.0):
     return out[:len(q_pids)], out[len(q_pids):]
 
 
+def _upsample_rows_cols(a, H, W):
+    """Separable linear interpolation (align_corners=True) of [..., h, w] to [..., H, W]."""
+    h, w = a.shape[-2:]
+    ys, xs = np.linspace(0, h - 1, H), np.linspace(0, w - 1, W)
+    y0 = np.minimum(ys.astype(np.int64), h - 2)
+    x0 = np.minimum(xs.astype(np.int64), w - 2)
+    fy, fx = (ys - y0)[:, None], (xs - x0)[None, :]
+    a = a.astype(np.float64)
+    r = a[..., y0, :] * (1 - fy) + a[..., y0 + 1, :] * fy
+    return r[..., x0] * (1 - fx) + r[..., x0 + 1] * fx
+
+
+def identity_crops(pids, cams, seed=0, noise=0.6, detail=0.3, cast=0.02, shift=1, height=256, width=128,
+                   offset=0):
+    """Identity-structured synthetic crops for end-to-end accuracy parity: each pid > 0 has
+    a smooth base image (a 16x8 U(-1,1) grid, linearly upsampled) plus a fixed high-frequency
+    texture; each camera adds a colour cast and a horizontal shift; each image adds its own
+    Gaussian noise.  pid <= 0 images (distractors / junk) get their own base.  Values are
+    clipped to [-1, 1] (the post-Normalize range).  Image k depends only on
+    (seed, pids[k], cams[k], offset + k)."""
+    out = np.empty((len(pids), 3, height, width), np.float32)
+    cache = {}
+
+    def base(key):
+        if key not in cache:
+            r = _rng(f"idbase{key}", seed)
+            b = _upsample_rows_cols(r.uniform(-1, 1, (3, 16, 8)), height, width)
+            cache[key] = b + detail * r.uniform(-1, 1, (3, height, width))
+        return cache[key]
+
+    for k, (p, c) in enumerate(zip(pids, cams)):
+        rk = _rng(f"idimg{offset + k}", seed)
+        b = base(int(p)) if p > 0 else base(f"x{offset + k}")
+        rc = _rng(f"idcam{int(c)}", seed)
+        cc = cast * rc.standard_normal(3)[:, None, None]
+        sh = int(rc.integers(-shift, shift + 1))
+        img = np.roll(b, sh, axis=2) + cc + noise * rk.standard_normal((3, height, width))
+        out[k] = np.clip(img, -1.0, 1.0).astype(np.float32)
+    return out
+
+
 def token_ids(n, ctx=77, vocab=49408, seed=0, min_len=4, max_len=20):
     """Synthetic CLIP token rows: SOT 49406, random body, EOT 49407 (the max id, so
     ``argmax`` finds it, text_encoder.py:23), zero padding."""
@@ -205,3 +246,58 @@ def token_ids(n, ctx=77, vocab=49408, seed=0, min_len=4, max_len=20):
         out[k, 1:ln - 1] = r.integers(1, vocab - 2, ln - 2)
         out[k, ln - 1] = vocab - 1
     return out
+
+
+def openai_state_dict(model="ViT-B/16", seed=0, vpt_ctx=0, text_ctx=0, input_res=224):
+    """OpenAI-CLIP key layout (``visual.*`` + top-level text keys + ``logit_scale``) as
+    maple.build_model (maple.py:1044-1098) consumes it: the vision tower at its
+    pretraining resolution (square grid, e.g. 14x14 + 1 positional rows for ViT-B/16 at
+    224), so build_model's bicubic resize to the stride-12 grid is exercised.  IVLP
+    extras with ``vpt_ctx`` / ``text_ctx`` > 0 (``visual.VPT``,
+    ``visual.transformer.resblocks.{i}.VPT_shallow``, ``transformer.resblocks.{i}.VPT_shallow``)."""
+    P = VIT_SPECS[model]["patch"]
+    vis = vit_state_dict(model, height=input_res, width=input_res, stride=P, seed=seed, vpt_ctx=vpt_ctx)
+    sd = {"visual." + k: v for k, v in vis.items()}
+    sd.update(text_state_dict(seed=seed, text_ctx=text_ctx))
+    sd["logit_scale"] = np.array(np.log(1 / 0.07), np.float32)
+    return sd
+
+
+def clipreid_checkpoint(model="ViT-B/16", seed=0, height=256, width=128, stride=12):
+    """CLIP-ReID checkpoint key layout that utils.model_adaptor reads (utils.py:184-221):
+    ``image_encoder.*`` (the stride-12 vision tower), ``text_encoder.*`` (the text tower,
+    zero_shot_learning.py:31-34) and the BNNeck ``bottleneck.*`` / ``bottleneck_proj.*``
+    BatchNorm1d buffers (utils.py:128-142)."""
+    vis = vit_state_dict(model, height=height, width=width, stride=stride, seed=seed)
+    sd = {"image_encoder." + k: v for k, v in vis.items()}
+    sd.update({"text_encoder." + k: v for k, v in text_state_dict(seed=seed).items()})
+    W, E = VIT_SPECS[model]["width"], VIT_SPECS[model]["out_dim"]
+    for name, n in (("bottleneck", W), ("bottleneck_proj", E)):
+        sd[name + ".weight"] = _normal(name + ".weight", (n,), 0.05, seed, mean=1.0)
+        sd[name + ".bias"] = np.zeros(n, np.float32)
+        sd[name + ".running_mean"] = _normal(name + ".running_mean", (n,), 0.1, seed)
+        sd[name + ".running_var"] = np.abs(_normal(name + ".running_var", (n,), 0.1, seed, mean=1.0))
+        sd[name + ".num_batches_tracked"] = np.array(100, np.int64)
+    return sd
+
+
+_FP16_SUFFIXES = ("conv1.weight", "attn.in_proj_weight", "attn.in_proj_bias", "attn.out_proj.weight",
+                  "attn.out_proj.bias", "mlp.c_fc.weight", "mlp.c_fc.bias", "mlp.c_proj.weight",
+                  "mlp.c_proj.bias", "proj", "text_projection")
+
+
+def round_like_convert_weights(sd):
+    """The values convert_weights (utils.py:145-166, maple.py:992-1013) leaves in a model:
+    Conv/Linear weights and biases, the MHA in_proj, ``proj`` and ``text_projection``
+    rounded to fp16 (and back to fp32); LayerNorm, embeddings and prompts untouched."""
+    out = {}
+    for k, v in sd.items():
+        if k.split(".")[-1] in ("proj", "text_projection") or k.endswith(_FP16_SUFFIXES[:-2]):
+            v = np.asarray(v, np.float32).astype(np.float16).astype(np.float32)
+        out[k] = v
+    return out
+
+
+def glue_cls_features(n, dim, seed=0):
+    """[n, dim] fp32 stand-in CLS features for the inference() glue fixtures."""
+    return _normal(f"glue{dim}", (n, dim), 1.0, seed)

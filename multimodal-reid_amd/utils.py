@@ -8,8 +8,9 @@
 CLIP-ReID checkpoints store the towers under ``image_encoder.*`` / ``text_encoder.*``
 (utils.py:211-214, zero_shot_learning.py:31-34); OpenAI CLIP state dicts under
 ``visual.*`` and top-level text keys.  Checkpoints are read with
-``torch.load(weights_only=True)`` (no pickle code execution); the reference's
-``torch.jit.load`` archives are tried first, as utils.py:171-175 does.
+``torch.load(weights_only=True)`` only (no pickle or TorchScript code is executed; the
+reference tries ``torch.jit.load`` first, utils.py:171-175 — a TorchScript archive is
+refused here: re-save its ``state_dict()`` with ``torch.save``).
 BNNeck (utils.py:128-142) is constructed and loaded but, as in the reference's eval
 (zero_shot_learning.py:91-92), never applied.
 """
@@ -19,14 +20,14 @@ from .model import CLIP, TextTransformer, VisionTransformer, resize_pos_embed  #
 
 
 def load_checkpoint(path):
-    try:
-        m = torch.jit.load(path, map_location="cpu")
-        return {k: v for k, v in m.state_dict().items()}
-    except Exception:
-        sd = torch.load(path, map_location="cpu", weights_only=True)
-        if isinstance(sd, dict) and "state_dict" in sd:
-            sd = sd["state_dict"]
-        return {k[7:] if k.startswith("module.") else k: v for k, v in sd.items()}
+    """State dict of a checkpoint file, weights-only (utils.py:17-55,171-175 semantics:
+    a ``state_dict`` entry is unwrapped, a DataParallel ``module.`` prefix stripped)."""
+    sd = torch.load(path, map_location="cpu", weights_only=True)
+    if isinstance(sd, dict) and "state_dict" in sd:
+        sd = sd["state_dict"]
+    if not isinstance(sd, dict):
+        raise ValueError(f"{path}: not a state dict")
+    return {k[7:] if k.startswith("module.") else k: v for k, v in sd.items()}
 
 
 class BNNeck:

@@ -69,9 +69,10 @@ def inference(model, bottleneck, bottleneck_proj, zeroshot_weights, loader, load
 
 
 def get_cmc_map(gallery_embeddings, query_embeddings, gallery_labels, query_labels, gallery_cams, query_cams,
-                max_rank=50, reranking=False):
-    """zero_shot_learning.py:137-153 (R1_mAP_eval with max_rank=50, feat_norm=True)."""
-    evaluator = R1_mAP_eval(len(query_labels), max_rank=max_rank, feat_norm=True, reranking=reranking)
+                reranking=False):
+    """zero_shot_learning.py:137-153 (R1_mAP_eval with max_rank=50, feat_norm=True);
+    ``reranking=True`` selects R1_mAP_eval's k-reciprocal branch (evaluate.py:124-127)."""
+    evaluator = R1_mAP_eval(len(query_labels), max_rank=50, feat_norm=True, reranking=reranking)
     evaluator.reset()
     evaluator.update((torch.cat((query_embeddings.float(), gallery_embeddings.float()), dim=0),
                       torch.cat((torch.as_tensor(query_labels), torch.as_tensor(gallery_labels)), dim=0),
@@ -79,13 +80,19 @@ def get_cmc_map(gallery_embeddings, query_embeddings, gallery_labels, query_labe
     return evaluator.compute()
 
 
-def zeroshot_classifier(text_model, class_tokens):
-    """zero_shot_learning.py:37-55 (augmented templates): per class, encode its template
-    token rows, L2-normalise, mean over templates, L2-normalise.  ``class_tokens`` is a list
-    of int64 [n_templates, 77] arrays (the CLIP BPE tokenizer is not available here, so
-    callers pass token ids)."""
+def zeroshot_classifier(text_model, class_tokens, augmented_template=True):
+    """zero_shot_learning.py:37-55.  Augmented templates (:39-49): per class, encode its
+    template token rows, L2-normalise, mean over templates, L2-normalise; ``class_tokens``
+    is a list of int64 [n_templates, 77] arrays.  Plain (:50-54): one token row per class
+    ([n_cls, 77]), encoded and L2-normalised.  (The CLIP BPE vocabulary is not available
+    offline, so callers pass token ids.)"""
     from .ops import class_mean_normalize_device
-    rows = [torch.as_tensor(np.asarray(t)) for t in class_tokens]
-    counts = [r.shape[0] for r in rows]
-    feats = text_model.encode_text(torch.cat(rows, 0))
+    if augmented_template:
+        rows = [torch.as_tensor(np.asarray(t)).reshape(-1, np.asarray(t).shape[-1]) for t in class_tokens]
+        counts = [r.shape[0] for r in rows]
+        tokens = torch.cat(rows, 0)
+    else:
+        tokens = torch.as_tensor(np.asarray(class_tokens))
+        counts = [1] * tokens.shape[0]
+    feats = text_model.encode_text(tokens)
     return class_mean_normalize_device(feats, counts)

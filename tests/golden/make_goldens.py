@@ -3,6 +3,12 @@
 Runs only in the build container (it imports /root/reference read-only; the
 reference never travels to the GPU box).  Modules imported as-is, no stubs:
 evaluate.py, reranking.py, custom_clip_model.py, text_encoder.py.
+maple.py, utils.py and zero_shot_learning.py import the absent third-party packages
+(OpenAI ``clip``, ``torchvision``, ``timm``, ``bs4``); they are imported with the
+import-only stand-ins under tests/golden/refstubs/ (see its README) and their eval-path
+functions (maple.build_model + IVLP towers, utils.model_adaptor / resize_pos_embed,
+zero_shot_learning.load_model's zeroshot_classifier, inference, get_cmc_map) run
+verbatim, with ``.cuda()`` made the identity on CPU.
 Inputs come from multimodal_reid_amd.synthetic, so the GPU box regenerates the
 exact same inputs/weights from seeds and only the outputs are stored here.
 
@@ -14,6 +20,7 @@ is ``kind="stable"`` — the reference code path is otherwise untouched.
     python tests/golden/make_goldens.py [--out tests/golden]
 """
 import argparse
+import contextlib
 import os
 import sys
 import types
@@ -60,13 +67,65 @@ class _StableNp(types.ModuleType):
 
 
 def _with_stable(mod, fn, *args, **kw):
+    """Run fn with ``np`` of module(s) ``mod`` swapped for the stable-argsort proxy."""
+    mods = mod if isinstance(mod, (list, tuple)) else [mod]
     proxy = _StableNp()
-    saved = mod.np
-    mod.np = proxy
+    saved = [m.np for m in mods]
+    for m in mods:
+        m.np = proxy
     try:
         return fn(*args, **kw), proxy
     finally:
-        mod.np = saved
+        for m, v in zip(mods, saved):
+            m.np = v
+
+
+REFSTUBS = os.path.join(HERE, "refstubs")
+
+
+def _stubbed():
+    """maple / utils / zero_shot_learning from /root/reference, with the refstubs/
+    stand-ins for the absent third-party packages."""
+    if REFSTUBS not in sys.path:
+        sys.path.insert(0, REFSTUBS)
+    import clip  # noqa: F401  (stub)
+    import maple
+    import utils as ref_utils
+    import zero_shot_learning as ref_zsl
+    return clip, maple, ref_utils, ref_zsl
+
+
+@contextlib.contextmanager
+def _cpu_cuda():
+    """``.cuda()`` as the identity: the reference's eval functions move tensors and
+    modules to the GPU (zero_shot_learning.py:81,104, utils.py:262); here they stay on CPU."""
+    saved = (torch.Tensor.cuda, torch.nn.Module.cuda)
+    torch.Tensor.cuda = lambda self, *a, **k: self
+    torch.nn.Module.cuda = lambda self, *a, **k: self
+    try:
+        yield
+    finally:
+        torch.Tensor.cuda, torch.nn.Module.cuda = saved
+
+
+def _torch_sd(sd):
+    return {k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()}
+
+
+IVLP_DESIGN = {"trainer": "IVLP", "vision_depth": 12, "language_depth": 12, "vision_ctx": 2,
+               "language_ctx": 2}  # zero_shot_learning.py:19-23
+
+
+def _small_clip(maple, text_sd=None):
+    """maple.CLIP with the CoOp trainer, a 1-layer width-768 stand-in vision tower (replaced
+    by model_adaptor or unused) and the 12-layer CLIP text tower (maple.py:846-935)."""
+    m = maple.CLIP(512, 21, 10, 1, 768, 16, 77, 49408, 512, 8, 12,
+                   {"trainer": "CoOp", "vision_depth": 0, "language_depth": 0, "vision_ctx": 0,
+                    "language_ctx": 0}, 12)
+    if text_sd is not None:
+        missing, unexpected = m.load_state_dict(_torch_sd(text_sd), strict=False)
+        assert not unexpected and all(k.startswith("visual.") or k == "logit_scale" for k in missing), unexpected
+    return m.eval()
 
 
 def backend_fixtures(out):
@@ -230,11 +289,191 @@ def text_fixtures(out):
     print("text fixtures ok")
 
 
+def ivlp_fixtures(out):
+    """IVLP CLIP built by the reference's maple.build_model (maple.py:1044-1098) from an
+    OpenAI-layout state dict (14x14 grid -> bicubic to 21x10, fp16 convert_weights), then
+    run in fp32 (``model.float()``: weights keep their fp16-rounded values): vision tower
+    with 2 VPT tokens + per-block VPT_shallow (maple.py:617-644,754-785) and
+    encode_text with per-block text prompts (maple.py:630-640,971-984)."""
+    _, maple, _, _ = _stubbed()
+    torch.manual_seed(0)
+    sd = syn.openai_state_dict("ViT-B/16", seed=6, vpt_ctx=2, text_ctx=2)
+    model = maple.build_model(_torch_sd(sd), 256, 128, IVLP_DESIGN).float().eval()
+    imgs = syn.images(2, seed=6)
+    tokens = syn.token_ids(5, seed=6)
+    with torch.no_grad():
+        x11, x12, xp = model.encode_image(torch.from_numpy(imgs))
+        txt = model.encode_text(torch.from_numpy(tokens))
+    assert x12.shape == (2, 213, 768)
+    pos = model.visual.positional_embedding.detach()
+    np.savez_compressed(os.path.join(out, "ivlp.npz"), tokens=tokens, x12cls=x12[:, 0].numpy(),
+                        x11cls=x11[:, 0].numpy(), projcls=xp[:, 0].numpy(), x12_prompt=x12[1, -2:].numpy(),
+                        proj_tok=xp[0, 100:103].numpy(), text_feat=txt.numpy(), pos_resized=pos.numpy())
+    print("ivlp fixtures ok")
+
+
+def glue_fixtures(out):
+    """zero_shot_learning.inference (:61-134), non-mm and --mm, on fake encoder outputs,
+    and load_model's zeroshot_classifier (:37-55) on the reference maple.CLIP.encode_text."""
+    _, maple, _, ref_zsl = _stubbed()
+    nb, B = 3, 4
+    # per-(batch, view) CLS features: view v of batch b is row 2b+v (regenerated from seeds on the GPU box)
+    cls12 = syn.glue_cls_features(2 * nb * B, 768, seed=12).reshape(2 * nb, B, 768)
+    clsp = syn.glue_cls_features(2 * nb * B, 512, seed=13).reshape(2 * nb, B, 512)
+    zs = syn.glue_cls_features(37, 512, seed=14)
+    zs = zs / np.linalg.norm(zs, axis=1, keepdims=True)
+
+    class Enc:
+        """model.encode_image with known outputs: batch b's plain view is row 2b, its
+        augmented view row 2b+1 (images[0, 0, 0, 0] = b + 0.5 * aug tags the batch)."""
+
+        def eval(self):
+            return self
+
+        def encode_image(self, images):
+            r = int(round(2 * float(images[0, 0, 0, 0])))
+            x12 = torch.from_numpy(np.repeat(cls12[r][:, None], 3, 1))
+            xp = torch.from_numpy(np.repeat(clsp[r][:, None], 3, 1))
+            return x12 + 1, x12, xp
+
+    def loader(aug):
+        for b in range(nb):
+            img = torch.zeros(B, 3, 4, 4)
+            img[:, 0, 0, 0] = b + 0.5 * aug
+            yield img, torch.arange(B) + 10 * b, torch.full((B,), b), torch.zeros(B), torch.arange(B)
+
+    class _B:
+        def eval(self):
+            return self
+
+    res = {}
+    with _cpu_cuda(), torch.no_grad():
+        for mm in (False, True):
+            emb, tg, cm, sq = ref_zsl.inference(Enc(), _B(), _B(), torch.from_numpy(zs), loader(0), loader(1),
+                                                mm, "vit")
+            res["emb_mm" if mm else "emb"] = emb.numpy()
+        res["targets"], res["cams"] = tg.numpy(), cm.numpy()
+    # zeroshot_classifier inside load_model, augmented templates (list per class) and plain (one string)
+    import argparse as _ap
+    import clip
+    text_sd = syn.text_state_dict(seed=8)
+    model = _small_clip(maple, text_sd)
+    clip.LOAD_HOOK = lambda name: model
+    classnames = [f"{1 + c:04d}" for c in range(6)]
+    templates = {}
+    tok_all = syn.token_ids(6 * 5 + 6, seed=15)
+    for c, name in enumerate(classnames):
+        texts = [f"class {name} template {t}" for t in range(5)]
+        templates[name] = texts
+        for t, text in enumerate(texts):
+            clip.TOKENS[text] = tok_all[c * 5 + t]
+    plain = {name: f"a photo of person {name}" for name in classnames}
+    for c, name in enumerate(classnames):
+        clip.TOKENS[plain[name]] = tok_all[30 + c]
+    with _cpu_cuda():
+        ref_zsl.params = _ap.Namespace(training_mode="coop", augmented_template=True)
+        zw_aug, _ = ref_zsl.load_model("ViT-B/16", classnames, templates, None)
+        ref_zsl.params = _ap.Namespace(training_mode="coop", augmented_template=False)
+        zw_plain, _ = ref_zsl.load_model("ViT-B/16", classnames, plain, None)
+    res.update(zeroshot_aug=zw_aug.numpy(), zeroshot_plain=zw_plain.numpy(), zeroshot_tokens=tok_all)
+    np.savez_compressed(os.path.join(out, "glue.npz"), **res)
+    print("glue fixtures ok", zw_aug.shape, zw_plain.shape)
+
+
+def adaptor_fixtures(out):
+    """utils.model_adaptor (utils.py:169-262) on a CLIP-ReID-layout checkpoint file
+    (torch.jit.load fails -> torch.load, image_encoder.* -> custom VisionTransformer,
+    strict load, fp16 convert_weights), then encode_image in the reference's GPU dtype
+    (fp16 weights and activations, fp32 LayerNorm) and in fp32; utils.resize_pos_embed
+    (utils.py:111-125) of square pretrained grids to the stride-12 grid."""
+    import tempfile
+    _, maple, ref_utils, _ = _stubbed()
+    ck = syn.clipreid_checkpoint("ViT-B/16", seed=10)
+    base = _small_clip(maple)
+    imgs = torch.from_numpy(syn.images(3, seed=10))
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "ckpt.pth")
+        torch.save(_torch_sd(ck), path)
+        with _cpu_cuda():
+            model, bn, bnp = ref_utils.model_adaptor(base, 256, 128, path, "vit", "coop")
+    with torch.no_grad():
+        _, h12, hp = model.encode_image(imgs)  # fp16 (CLIP.encode_image casts to conv1's dtype)
+        assert h12.dtype == torch.float16
+        model.visual.float()
+        _, x12, xp = model.encode_image(imgs)
+    res = dict(x12cls=x12[:, 0].numpy(), projcls=xp[:, 0].numpy(), x12cls_fp16=h12[:, 0].float().numpy(),
+               projcls_fp16=hp[:, 0].float().numpy(),
+               bn_running_mean=bn.bottleneck.running_mean.numpy(), bnp_weight=bnp.bottleneck_proj.weight.detach().numpy())
+    for model_name, grid in (("ViT-B/16", 14), ("ViT-L/14", 16)):
+        W = syn.VIT_SPECS[model_name]["width"]
+        pe = syn._normal(f"pe{grid}", (grid * grid + 1, W), W ** -0.5, 16)
+        new = torch.zeros(211, W)
+        r = ref_utils.resize_pos_embed(torch.from_numpy(pe), new, 21, 10)
+        res[f"resized_{grid}"] = r.numpy()
+    np.savez_compressed(os.path.join(out, "adaptor.npz"), **res)
+    print("adaptor fixtures ok")
+
+
+def e2e_fixtures(out):
+    """End-to-end accuracy parity (BASELINE north star: mAP within 1e-3, rank lists):
+    the reference's own eval pipeline on identity-structured synthetic crops —
+    utils.model_adaptor (CLIP-ReID checkpoint) -> zero_shot_learning.inference (plain +
+    flip/pad/crop TTA loader, bs 32) -> get_cmc_map (R1_mAP_eval, max_rank 50) and
+    R1_mAP_eval(reranking=True) (k1=50, k2=15, lambda 0.3) — run twice: in the
+    reference's GPU dtype (fp16 weights/activations) and in fp32.  Stable-argsort proxy
+    for the rank lists."""
+    import tempfile
+    _, maple, ref_utils, ref_zsl = _stubbed()
+    Q, G, bs = 128, 512, 64
+    qp, gp, qc, gc = syn.labels(Q, G, num_ids=100, num_cams=6, seed=21, distractor_frac=0.1)
+    pids, cams = np.concatenate([qp, gp]), np.concatenate([qc, gc])
+    imgs = syn.identity_crops(pids, cams, seed=21)
+    offs = syn.tta_offsets(Q + G, seed=21)
+    aug = syn.tta_images_np(imgs, offs)
+    ck = syn.clipreid_checkpoint("ViT-B/16", seed=20)
+    base = _small_clip(maple)
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "ckpt.pth")
+        torch.save(_torch_sd(ck), path)
+        with _cpu_cuda():
+            model, bn, bnp = ref_utils.model_adaptor(base, 256, 128, path, "vit", "coop")
+
+    def loader(lo, hi, x):
+        for s in range(lo, hi, bs):
+            e = min(s + bs, hi)
+            yield (torch.from_numpy(x[s:e]), torch.from_numpy(pids[s:e]), torch.from_numpy(cams[s:e]),
+                   torch.zeros(e - s, dtype=torch.int64), torch.arange(s, e))
+
+    res = dict(q_pids=qp, g_pids=gp, q_cams=qc, g_cams=gc, tta_offsets=offs)
+    for tag in ("fp16", "fp32"):
+        if tag == "fp32":
+            model.visual.float()
+        with _cpu_cuda(), torch.no_grad():
+            eg, tg, cg, _ = ref_zsl.inference(model, bn, bnp, None, loader(Q, Q + G, imgs), loader(Q, Q + G, aug),
+                                              False, "vit")
+            eq, tq, cq, _ = ref_zsl.inference(model, bn, bnp, None, loader(0, Q, imgs), loader(0, Q, aug),
+                                              False, "vit")
+        assert eg.dtype == (torch.float16 if tag == "fp16" else torch.float32)
+        (cmc, mAP), px = _with_stable(ref_eval, ref_zsl.get_cmc_map, eg, eq, tg, tq, cg, cq)
+        res[f"feat32_{tag}"] = torch.cat([eq[:16], eg[:16]]).float().numpy()  # first 16 q + 16 g rows
+        res[f"cmc_{tag}"], res[f"map_{tag}"] = cmc, np.float64(mAP)
+        res[f"rank50_{tag}"] = px.calls[0][:, :50].astype(np.int32)
+        ev = ref_eval.R1_mAP_eval(Q, max_rank=50, feat_norm=True, reranking=True)
+        ev.reset()
+        ev.update((torch.cat([eq, eg]).float(), torch.cat([tq, tg]), torch.cat([cq, cg])))
+        (rcmc, rmap), px = _with_stable([ref_eval, ref_rr], ev.compute)
+        res[f"cmc_rr_{tag}"], res[f"map_rr_{tag}"] = rcmc, np.float64(rmap)
+        res[f"rank50_rr_{tag}"] = px.calls[-1][:, :50].astype(np.int32)
+        print("e2e", tag, "mAP", mAP, "rank1", cmc[0], "rerank mAP", rmap)
+    np.savez_compressed(os.path.join(out, "e2e.npz"), **res)
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=HERE)
     ap.add_argument("--only", default="")
     a = ap.parse_args()
-    todo = a.only.split(",") if a.only else ["backend", "rerank", "vit", "vitl", "text"]
+    todo = a.only.split(",") if a.only else ["backend", "rerank", "vit", "vitl", "text", "ivlp", "glue",
+                                              "adaptor", "e2e"]
     for t in todo:
         globals()[f"{t}_fixtures"](a.out)

@@ -99,6 +99,22 @@ def test_r1_map_eval_end_to_end(gpu):
     assert np.abs(cmc - g["cmc_r1map"]).max() <= 1.0 / 100 + 1e-7  # at most one query flips on a near-tie
 
 
+@pytest.mark.parametrize("max_rank", [10, 20, 50])
+def test_r1_map_eval_max_rank_is_not_forwarded(gpu, max_rank):
+    """The reference's compute() calls eval_func with its default max_rank=50
+    (evaluate.py:132) whatever R1_mAP_eval was constructed with (prompt_learning.py:636
+    passes 10): the CMC is 50 long and equal to the max_rank=50 result."""
+    g = golden("backend_small.npz")
+    qf, gf, qp, gp, qc, gc = _inputs()
+    ev = _ev().R1_mAP_eval(100, max_rank=max_rank, feat_norm=True)
+    ev.reset()
+    ev.update((torch.from_numpy(np.concatenate([qf, gf])), np.concatenate([qp, gp]), np.concatenate([qc, gc])))
+    cmc, mAP = ev.compute()
+    assert cmc.shape == (50,)
+    assert abs(mAP - g["map_r1map"]) < 1e-6
+    assert np.abs(cmc - g["cmc_r1map"]).max() <= 1.0 / 100 + 1e-7
+
+
 def test_eval_market_scale_rows_vs_oracle(gpu):
     sp = syn.DATASET_SPLITS["market1501"]
     qp, gp, qc, gc = syn.labels(sp["num_query"], sp["num_gallery"], sp["num_ids"], sp["num_cams"], seed=7,

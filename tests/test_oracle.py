@@ -158,3 +158,23 @@ def test_text_oracle_vs_reference():
     with torch.no_grad():
         f = vit_ref.text_forward(sd, g["tokens"])
     assert np.abs(f.numpy() - g["text_feat"]).max() < 2e-5
+
+
+def test_ivlp_oracle_vs_reference_build_model():
+    """oracle IVLP towers (vision VPT + per-block VPT_shallow, text prompts) vs the
+    reference's maple.build_model CLIP (maple.py:617-644,754-785,971-984) run in fp32 on
+    convert_weights-rounded weights: pins the IVLP restatement to the reference."""
+    from oracle import vit_ref
+    from multimodal_reid_amd.model import resize_pos_embed
+    g = golden("ivlp.npz")
+    sd = syn.round_like_convert_weights(syn.openai_state_dict("ViT-B/16", seed=6, vpt_ctx=2, text_ctx=2))
+    vis = {k[len("visual."):]: v for k, v in sd.items() if k.startswith("visual.")}
+    vis["positional_embedding"] = resize_pos_embed(vis["positional_embedding"], 21, 10).numpy()
+    txt = {k: v for k, v in sd.items() if not k.startswith("visual.")}
+    imgs = syn.images(2, seed=6)
+    with torch.no_grad():
+        x11, x12, xp = vit_ref.vit_forward(vis, imgs)
+        t = vit_ref.text_forward(txt, g["tokens"])
+    for got, ref in ((x12[:, 0], g["x12cls"]), (x11[:, 0], g["x11cls"]), (xp[:, 0], g["projcls"]),
+                     (x12[1, -2:], g["x12_prompt"]), (xp[0, 100:103], g["proj_tok"]), (t, g["text_feat"])):
+        assert np.abs(got.numpy() - ref).max() < 2e-5
