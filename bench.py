@@ -39,7 +39,7 @@ from multimodal_reid_amd import _lib, evaluate, synthetic as syn  # noqa: E402
 from multimodal_reid_amd import zero_shot_learning as zsl  # noqa: E402
 from multimodal_reid_amd.model import VisionTransformer  # noqa: E402
 
-PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_F16_TFLOPS = 2500.0  # MI355X dense fp16/bf16 MFMA (MI355X_MICROARCH.md)
 EPI_GELU = 1  # the c_fc GEMM (+QuickGELU epilogue): the largest single kernel per block
 # HBM-side bytes per c_fc launch (ln_2-folded fp16 GEMM, M = 1024*211 (the default batch),
 # N = 3072, K = 768) from rocprofv3 PMC passes (tools/prof_round.sh ->
@@ -79,13 +79,13 @@ class Workload:
         self.rank, self.world, self.batch, self.dev = rank, world, batch, dev
         self.sd = syn.vit_state_dict("ViT-B/16", seed=0) if model is None else None
         self.model = VisionTransformer(self.sd, device=dev) if model is None else model
-        # synthetic crops of this rank's shards, resident in HBM as bf16 (U(-1,1))
+        # synthetic crops of this rank's shards, resident in HBM as fp16 (U(-1,1))
         gen = torch.Generator(device=dev)
         self.qlo, self.qhi = shard(self.Q, rank, world)
         self.glo, self.ghi = shard(self.G, rank, world)
         gen.manual_seed(1000 + rank)
-        self.q_img = (torch.rand((self.qhi - self.qlo, 3, 256, 128), generator=gen, device=dev) * 2 - 1).bfloat16()
-        self.g_img = (torch.rand((self.ghi - self.glo, 3, 256, 128), generator=gen, device=dev) * 2 - 1).bfloat16()
+        self.q_img = (torch.rand((self.qhi - self.qlo, 3, 256, 128), generator=gen, device=dev) * 2 - 1).half()
+        self.g_img = (torch.rand((self.ghi - self.glo, 3, 256, 128), generator=gen, device=dev) * 2 - 1).half()
         self.q_tta = torch.from_numpy(syn.tta_offsets(self.qhi - self.qlo, seed=1, offset=self.qlo)).to(dev)
         self.g_tta = torch.from_numpy(syn.tta_offsets(self.ghi - self.glo, seed=2, offset=self.glo)).to(dev)
         D = self.model.width + self.model.out_dim
@@ -219,14 +219,14 @@ def rerank_leg(dev, cpu_n=1000, cpu=True):
 def preprocess_leg(dev, n=19281, reps=5):
     """the test transform (Resize(256,128) -> ToTensor -> Normalize,
     data_prepare.py:257-261) on the Market split's worth of decoded 128x64 RGB crops, packed
-    and resident in HBM, -> bf16 [n, 3, 256, 128] (reidmi_preprocess_u8).  HBM-bound:
+    and resident in HBM, -> fp16 [n, 3, 256, 128] (reidmi_preprocess_u8).  HBM-bound:
     algorithmic bytes = n * (128*64*3 read + 3*256*128*2 written)."""
     import ctypes
     r = np.random.default_rng(0)
     h, w = 128, 64
     pix = torch.from_numpy(r.integers(0, 256, n * h * w * 3, dtype=np.uint8)).to(dev)
     meta = torch.from_numpy(np.stack([np.arange(n) * h * w * 3, np.full(n, h), np.full(n, w)], 1).astype(np.int64)).to(dev)
-    out = torch.empty((n, 3, 256, 128), dtype=torch.bfloat16, device=dev)
+    out = torch.empty((n, 3, 256, 128), dtype=torch.float16, device=dev)
     mean = (ctypes.c_float * 3)(0.5, 0.5, 0.5)
     std = (ctypes.c_float * 3)(0.5, 0.5, 0.5)
 
@@ -244,7 +244,7 @@ def preprocess_leg(dev, n=19281, reps=5):
     ms = e0.elapsed_time(e1) / reps
     nbytes = n * (h * w * 3 + 3 * 256 * 128 * 2)
     del pix, out
-    return {"config": f"{n} decoded {h}x{w} RGB crops -> bf16 [n,3,256,128] (Resize bilinear + ToTensor + Normalize, "
+    return {"config": f"{n} decoded {h}x{w} RGB crops -> fp16 [n,3,256,128] (Resize bilinear + ToTensor + Normalize, "
                       "Pillow-exact)", "imgs_per_s": round(n / (ms * 1e-3), 1), "ms": round(ms, 3),
             "achieved_GBps": round(nbytes / (ms * 1e-3) / 1e9, 1), "peak_GBps": 8000.0}
 
@@ -344,7 +344,7 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "fp16",
             "data": "synthetic U(-1,1) 256x128 crops in HBM, random-init ViT-B/16 (CLIP init scales)",
             "config": {"workload": "Market-1501 full eval: 3368q x 15913g, ViT-B/16 stride-12 (211 tokens), "
                                    "2 passes/img (plain + flip/pad/crop TTA), exact-fp32 distmat, CMC/mAP",
@@ -354,9 +354,9 @@ def main():
             "embed_wall_s": round(embed_s / a.steps, 4),
             "mAP": round(float(mAP), 6),
             "rank1": round(float(cmc[0]), 6),
-            "roofline": {"bound": "mfma", "kernel": "gemm5_bf16_kernel<1, true, true> (ln_2-folded fp16 mlp.c_fc + QuickGELU)",
-                         "achieved": round(achieved, 1) if achieved else None, "peak": PEAK_BF16_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4) if achieved else None,
+            "roofline": {"bound": "mfma", "kernel": "gemm_persistent_kernel<1> (ln_2-folded fp16 mlp.c_fc + QuickGELU)",
+                         "achieved": round(achieved, 1) if achieved else None, "peak": PEAK_F16_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_F16_TFLOPS, 4) if achieved else None,
                          "traffic": C_FC_TRAFFIC_BYTES, "traffic_unit": "bytes/launch (PMC)", "avg_launch_ms": round(avg_ms, 4), "launches": cnt.value,
                          "flops_per_launch": fl.value / max(cnt.value, 1)},
         }

@@ -127,26 +127,21 @@ int reidmi_rr_jaccard_rows(const float* feat, int64_t N, int64_t D, int64_t ldf,
 
 /* ------------------------------------------------------------------ encoders */
 
-/* bf16 GEMM C = A . W^T (+bias) on v_mfma_f32_16x16x32_bf16, fp32 accumulation.
- * A [M][lda] bf16, W [N][ldw] bf16 (Linear weight layout), N % 128 == 0, K % 64 == 0.
- * epi: 0 -> out bf16 = acc+bias; 1 -> out bf16 = QuickGELU(acc+bias); 2 -> out fp32 += acc+bias;
- *      5 -> out fp32 = acc+bias; 6 -> out fp16 += acc+bias (sum in fp32, one rounding: the
- *      encoders' fp16 residual stream).  (nn.Linear / mlp.c_fc+QuickGELU / residual adds of
- *      custom_clip_model.py:8-29.)  bias nullable (fp32).  bf16/fp16 outputs: ldc % 8 == 0,
- *      16-byte aligned out. */
-int reidmi_gemm_bf16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N,
-                     int64_t K, const float* bias, void* out, int64_t ldc, void* stream);
-
-/* fp16 GEMM (v_mfma_f32_16x16x32_f16) with an optional folded LayerNorm — the QKV / c_fc
- * GEMMs of the encoders (ln_1 / ln_2 -> in_proj / c_fc, custom_clip_model.py:27-28):
+/* fp16 GEMM C = A . W^T (+bias) on v_mfma_f32_16x16x32_f16, fp32 accumulation (the
+ * reference's GPU dtype: utils.py:145-166 converts Linear/conv/MHA weights to fp16), with an
+ * optional folded LayerNorm — the QKV / c_fc GEMMs of the encoders (ln_1 / ln_2 -> in_proj /
+ * c_fc, custom_clip_model.py:27-28):
  * out = epi(rstd_m * (A W^T)_mn + (-mean_m rstd_m) * colsum_n + bias_n), rowstat float2
  * (rstd, -mean * rstd) with round_up(M, 256) entries (those past M are read, not used) and
- * colsum [N] fp32, both NULL for a plain GEMM (bias required with them).  A [M][lda], W [N][ldw]
- * fp16; epi 0 (bf16 out) or 1 (QuickGELU bf16 out); shape rules as reidmi_gemm_bf16. */
+ * colsum [N] fp32, both NULL for a plain GEMM (bias required with them).
+ * A [M][lda], W [N][ldw] fp16 (Linear weight layout), N % 128 == 0, K % 64 == 0.
+ * epi: 0 -> out fp16 = acc+bias; 1 -> out fp16 = QuickGELU(acc+bias); 5 -> out fp32 = acc+bias;
+ *      6 -> out fp16 += acc+bias (sum in fp32, one rounding: the encoders' fp16 residual
+ *      stream).  bias nullable (fp32).  fp16 outputs: ldc % 8 == 0, 16-byte aligned out. */
 int reidmi_gemm_f16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N, int64_t K,
                     const float* bias, const void* rowstat, const float* colsum, void* out, int64_t ldc, void* stream);
 
-/* Live timing of the bf16 GEMM launches (HIP events on the launch stream), used by bench.py
+/* Live timing of the GEMM launches (HIP events on the launch stream), used by bench.py
  * for the roofline of the dominant kernel.  collect: epi = GEMM epilogue id (-1 = all);
  * returns summed device ms, launch count, algorithmic FLOPs (2MNK) and clears the record. */
 int reidmi_prof_enable(int on);
@@ -155,23 +150,25 @@ int reidmi_prof_collect(int epi, double* total_ms, int64_t* count, double* flops
  * so that the average matches that kernel's row in a rocprofv3 --stats summary). */
 int reidmi_prof_collect_min(int epi, double min_flops, double* total_ms, int64_t* count, double* flops);
 
-/* GEMM tile selection: 0 = auto, 1 = 128x128x64 (4 waves), 2 = 256x256x64 (8 waves, LDS-DMA),
- * 3 = variant 2 persistent (one workgroup per CU, cross-tile prefetch), 4 = 256x256 ping-pong
- * section schedule with region-level DMA, 5 = variant 4 persistent (the auto choice for
- * >= 256 tiles).  All variants are bit-identical. */
-int reidmi_gemm_set_variant(int v);
+/* GEMM tile selection (tests): 0 = auto (the persistent 256x256x64 LDS-DMA tile for >= 256
+ * tiles, else 128x128x64), 1 = force 128x128, 2 = force persistent.  Bit-identical results. */
+int reidmi_gemm_set_tile(int t);
+
+/* Persistent tile walk: the XCDs are split into ngroups (1, 2, 4, 8) groups, each owning
+ * 1/ngroups of the N-tiles (smaller weight share per XCD L2).  Bit-identical results. */
+int reidmi_gemm_set_walk(int ngroups);
 
 /* Key padding used for an L-token sequence by the attention kernel (rows of v^T). */
 int reidmi_attn_lpad(int L);
 
 /* softmax(Q K^T / 8 [+causal]) V per (sequence, head): the SDPA of nn.MultiheadAttention
  * (custom_clip_model.py:22-24; causal text mask maple.py:956-962).  q,k [nseq*H][L][64],
- * vt [nseq*H][64][reidmi_attn_lpad(L)], o [nseq*L][H*64]; all bf16.  L <= 256. */
-int reidmi_mhsa_bf16(const void* q, const void* k, const void* vt, void* o, int64_t nseq, int L, int H, int causal,
+ * vt [nseq*H][64][reidmi_attn_lpad(L)], o [nseq*L][H*64]; all fp16.  L <= 256. */
+int reidmi_mhsa_f16(const void* q, const void* k, const void* vt, void* o, int64_t nseq, int L, int H, int causal,
                      void* stream);
 
 /* LayerNorm over rows of width W in {512,768,1024} (fp32 math, eps) — custom_clip_model.py:43-49.
- * Row r of the output reads input row row_idx ? row_idx[r] : r.  y32 / y16 (bf16) nullable. */
+ * Row r of the output reads input row row_idx ? row_idx[r] : r.  y32 / y16 (fp16) nullable. */
 int reidmi_layernorm(const float* x, int64_t rows, int64_t ldx, const int32_t* row_idx, int64_t W,
                      const float* gamma, const float* beta, float eps, float* y32, int64_t ldy32, void* y16,
                      int64_t ldy16, void* stream);
@@ -183,7 +180,7 @@ int reidmi_layernorm(const float* x, int64_t rows, int64_t ldx, const int32_t* r
  *   qkv_w = fp16(in_proj_weight * ln_1.weight[None, :]), qkv_b = in_proj_bias + in_proj_weight @ ln_1.bias,
  *   qkv_s[n] = sum_k qkv_w[n][k] (of the fp16 values, summed in double);
  *   fc1_w / fc1_b / fc1_s likewise from mlp.c_fc and ln_2.
- * out_w, fc2_w bf16.  ln1_w ... ln2_b are kept for reference (not read by the kernels).
+ * out_w, fc2_w fp16.  ln1_w ... ln2_b are kept for reference (not read by the kernels).
  * prompt: IVLP VPT_shallow [n_ctx][W] (fp32) that replaces the prompt rows before this
  * block, or NULL. */
 typedef struct reidmi_block_weights {
@@ -207,7 +204,7 @@ typedef struct reidmi_block_weights {
 /* Vision tower: custom_clip_model.VisionTransformer (custom_clip_model.py:57-100) and the
  * IVLP variant maple.VisionTransformer (maple.py:722-785) when n_ctx > 0.
  * conv_w: conv1.weight [W][3*P*P] flattened (c,ky,kx) and zero-padded to kpad (multiple of
- * 64), bf16.  proj_t: proj^T [out_dim][W] bf16.  blocks: HOST array of `layers` entries. */
+ * 64), fp16.  proj_t: proj^T [out_dim][W] fp16.  blocks: HOST array of `layers` entries. */
 typedef struct reidmi_vit_weights {
     int32_t width, layers, heads, patch, stride, out_dim, grid_h, grid_w, n_ctx, kpad;
     const void* conv_w;
@@ -226,20 +223,20 @@ typedef struct reidmi_vit_weights {
 int64_t reidmi_vit_workspace_bytes(const reidmi_vit_weights* w, int64_t B, int full);
 
 /* encode_image: runs resblocks[:11] then resblocks[11] (custom_clip_model.py:91-92, also for
- * deeper towers), ln_post and proj.  images [B][3][H][Wimg] fp32 (images_bf16 = 0) or bf16,
+ * deeper towers), ln_post and proj.  images [B][3][H][Wimg] fp32 (images_f16 = 0) or fp16,
  * already normalised.  tta (nullable, device int32 [B][2]): apply the augmented loader's
  * flip + Pad((10,5)) + crop at (top, left) on the fly (data_prepare.py:263-270).
  * full = 0: out_x12 [B][W] = ln_post(x12)[:,0], out_proj [B][E] = (x12 @ proj)[:,0],
  *           out_x11 [B][W] = x11[:,0] (nullable)          (zero_shot_learning.py:84-87)
  * full = 1: out_x12 [B][L][W], out_proj [B][L][E], out_x11 [B][L][W] (nullable)
  *           — the (x11, x12, xproj) triple of encode_image. */
-int reidmi_vit_forward(const reidmi_vit_weights* w, const void* images, int images_bf16, int64_t B, int H,
+int reidmi_vit_forward(const reidmi_vit_weights* w, const void* images, int images_f16, int64_t B, int H,
                        int Wimg, const int32_t* tta, int full, float* out_x12, float* out_proj, float* out_x11,
                        void* ws, int64_t ws_bytes, void* stream);
 
 /* Text tower: CLIP.encode_text (maple.py:971-984) from token ids, or
  * text_encoder.TextEncoder.forward (text_encoder.py:14-24) from pre-embedded prompts.
- * tok_emb [vocab][W] fp32, pos_emb [ctx][W] fp32, proj_t = text_projection^T [E][W] bf16. */
+ * tok_emb [vocab][W] fp32, pos_emb [ctx][W] fp32, proj_t = text_projection^T [E][W] fp16. */
 typedef struct reidmi_text_weights {
     int32_t width, layers, heads, ctx, vocab, out_dim, n_ctx;
     const float* tok_emb;
@@ -284,7 +281,7 @@ int reidmi_feature_tta_mm(const float* x12a, const float* pa, const float* x12b,
  * stays on the host.
  * pix: device, concatenated HWC uint8 images; meta: device int64 [B][3] = (byte offset of
  * the image in pix, h, w) with 0 < h <= max_h, 0 < w <= max_w (images outside are skipped);
- * mean, stdv: HOST float[3]; out: device [B][3][oh][ow] (ow % 4 == 0), out_dtype 0 = fp32, 1 = bf16 (RNE).
+ * mean, stdv: HOST float[3]; out: device [B][3][oh][ow] (ow % 4 == 0), out_dtype 0 = fp32, 1 = fp16 (RNE).
  * The flip / pad / crop of the TTA loader (data_prepare.py:263-270) is applied on these
  * outputs by the encoder (reidmi_vit_forward's tta offsets). */
 int reidmi_preprocess_u8(const uint8_t* pix, const int64_t* meta, int64_t B, int max_h, int max_w, int oh, int ow,

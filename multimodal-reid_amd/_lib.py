@@ -26,7 +26,6 @@ SIGNATURES = {
     "reidmi_distmat_set_variant": [_i32],
     "reidmi_topk_rows_f32": [_vp, _i64, _i64, _i64, _vp, _i32, _vp, _vp, _i64, _vp],
     "reidmi_eval_rows": [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
-    "reidmi_gemm_bf16": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _i64, _vp],
     "reidmi_gemm_f16": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _vp],
     "reidmi_rerank_workspace_bytes": [_i64, _i64, _i32, _i32, _i32, _i32],
     "reidmi_rerank": [_vp, _i64, _i64, _i64, _i64, _i32, _i32, _u16, _f32, _vp, _i64, _vp, _i64, _vp, _vp],
@@ -44,10 +43,11 @@ SIGNATURES = {
                                _u16, _f32, _vp, _i64, _vp, _i64, _vp],
     "reidmi_attn_lpad": [_i32],
     "reidmi_prof_enable": [_i32],
-    "reidmi_gemm_set_variant": [_i32],
+    "reidmi_gemm_set_tile": [_i32],
+    "reidmi_gemm_set_walk": [_i32],
     "reidmi_prof_collect": [_i32, _vp, _vp, _vp],
     "reidmi_prof_collect_min": [_i32, ctypes.c_double, _vp, _vp, _vp],
-    "reidmi_mhsa_bf16": [_vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp],
+    "reidmi_mhsa_f16": [_vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp],
     "reidmi_layernorm": [_vp, _i64, _i64, _vp, _i64, _vp, _vp, _f32, _vp, _i64, _vp, _i64, _vp],
     "reidmi_feature_tta_avg": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _i64, _vp],
     "reidmi_feature_tta_mm": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _vp, _i64, _vp],

@@ -7,8 +7,9 @@
 // One workgroup per (sequence, head), one wave per 32-query block.  K [Lp][64] and V^T
 // [64][Lp] of the head live in LDS for the whole sweep (L <= 256 fits: one key sweep, no
 // online rescaling).  Row max / row sum are in-lane plus one xor-shuffle (lane ^ 32).
-// Inputs from the QKV GEMM epilogue: q,k [B*H][L][64] bf16, vt [B*H][64][Lp] bf16.
-// Output o [B*L][H*64] bf16 (token-major: the A operand of out_proj).
+// Inputs from the QKV GEMM epilogue: q,k [B*H][L][64] fp16, vt [B*H][64][Lp] fp16 (the
+// reference's GPU dtype); P is rounded to fp16 for the P.V MFMAs.
+// Output o [B*L][H*64] fp16 (token-major: the A operand of out_proj).
 #include "common.h"
 
 namespace reidmi {
@@ -23,7 +24,7 @@ __device__ __forceinline__ int kswz(int r, int kc) { return r * 64 + ((kc ^ ((r 
 // piece, XOR swizzle applied on the source address) and V^T of the next head as one
 // contiguous blob (its HBM row stride == its LDS row stride, see attn_lpad), both while
 // the current head is being computed; Q of the next head is prefetched into registers.
-//   S^T[key][q] = K Q^T on v_mfma_f32_32x32x16_bf16; lane (q = lane&31, h = lane>>5) holds
+//   S^T[key][q] = K Q^T on v_mfma_f32_32x32x16_f16; lane (q = lane&31, h = lane>>5) holds
 //     keys kb*32 + (r&3) + 8(r>>2) + 4h in s[kb][r];
 //   P stays in registers: registers 8s'..8s'+7 of block kb are the B fragment of key-step s'
 //     of O^T = V^T P^T (accumulator-as-operand), V^T read with the same key permutation;
@@ -32,11 +33,11 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef float f32x2v __attribute__((ext_vector_type(2)));
 
 template <int NKB, bool CAUSAL>
-__global__ __launch_bounds__(512) void mhsa_kernel(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
-                                                   const __bf16* __restrict__ vt, __bf16* __restrict__ o, int L,
+__global__ __launch_bounds__(512) void mhsa_kernel(const _Float16* __restrict__ q, const _Float16* __restrict__ k,
+                                                   const _Float16* __restrict__ vt, _Float16* __restrict__ o, int L,
                                                    int H, int vstride, int64_t nbh, float scale_log2) {
     constexpr int LP = NKB * 32;
-    extern __shared__ __attribute__((aligned(16))) __bf16 lds[];
+    extern __shared__ __attribute__((aligned(16))) _Float16 lds[];
     const int stage_elems = LP * 64 + 64 * vstride;  // K [LP][64] then V^T [64][vstride]
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -49,10 +50,10 @@ __global__ __launch_bounds__(512) void mhsa_kernel(const __bf16* __restrict__ q,
     const int vlast_lanes = (vbytes - (vpieces - 1) * 1024) / 16;
 
     auto issue = [&](int64_t bh, int stage) {
-        __bf16* sK = lds + stage * stage_elems;
-        __bf16* sV = sK + LP * 64;
-        const __bf16* kh = k + bh * L * 64;
-        const __bf16* vh = vt + bh * 64 * (int64_t)vstride;
+        _Float16* sK = lds + stage * stage_elems;
+        _Float16* sV = sK + LP * 64;
+        const _Float16* kh = k + bh * L * 64;
+        const _Float16* vh = vt + bh * 64 * (int64_t)vstride;
         for (int pc = wid; pc < kpieces; pc += nw) {
             int r = 8 * pc + (lane >> 3);
             const int kc = (lane & 7) ^ ((r >> 1) & 7);
@@ -67,21 +68,21 @@ __global__ __launch_bounds__(512) void mhsa_kernel(const __bf16* __restrict__ q,
     // Inline-asm loads: hipcc does not track them, so it inserts no vmcnt(0) of its own
     // before the prefetched registers are used (which would also drain the O stores); the
     // kernel's counted waits retire them, and `pin` orders every use after that wait.
-    auto load_q = [&](int64_t bh, bf16x8* qf) {
-        const __bf16* qh = q + (bh * L + (qi < L ? qi : L - 1)) * 64 + hh * 8;
+    auto load_q = [&](int64_t bh, f16x8* qf) {
+        const _Float16* qh = q + (bh * L + (qi < L ? qi : L - 1)) * 64 + hh * 8;
         asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(qf[0]) : "v"(qh) : "memory");
         asm volatile("global_load_dwordx4 %0, %1, off offset:32" : "=v"(qf[1]) : "v"(qh) : "memory");
         asm volatile("global_load_dwordx4 %0, %1, off offset:64" : "=v"(qf[2]) : "v"(qh) : "memory");
         asm volatile("global_load_dwordx4 %0, %1, off offset:96" : "=v"(qf[3]) : "v"(qh) : "memory");
     };
-    auto pin = [&](bf16x8* qf) {
+    auto pin = [&](f16x8* qf) {
         asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]));
     };
     auto zero_pad = [&](int stage) {  // V^T key columns [L, LP) were DMA'd from padding
-        __bf16* sV = lds + stage * stage_elems + LP * 64;
+        _Float16* sV = lds + stage * stage_elems + LP * 64;
         for (int c = tid; c < 64 * (LP - L); c += blockDim.x) {
             const int d = c / (LP - L), t = L + c % (LP - L);
-            sV[d * vstride + t] = (__bf16)0.0f;
+            sV[d * vstride + t] = (_Float16)0.0f;
         }
     };
 
@@ -89,7 +90,7 @@ __global__ __launch_bounds__(512) void mhsa_kernel(const __bf16* __restrict__ q,
     if (bh >= nbh) return;
     int stage = 0;
     issue(bh, 0);
-    bf16x8 qf[4];
+    f16x8 qf[4];
     load_q(bh, qf);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     pin(qf);
@@ -98,13 +99,13 @@ __global__ __launch_bounds__(512) void mhsa_kernel(const __bf16* __restrict__ q,
     __syncthreads();
     for (; bh < nbh; bh += gridDim.x) {
         const int64_t nxt = bh + gridDim.x;
-        bf16x8 qn[4];
+        f16x8 qn[4];
         if (nxt < nbh) {  // Q first: the compiler's wait for qn then never covers the DMA
             load_q(nxt, qn);
             issue(nxt, stage ^ 1);
         }
-        const __bf16* sK = lds + stage * stage_elems;
-        const __bf16* sV = sK + LP * 64;
+        const _Float16* sK = lds + stage * stage_elems;
+        const _Float16* sV = sK + LP * 64;
         if (wid * 32 < L) {
             f32x16 s[NKB];
 #pragma unroll
@@ -112,8 +113,8 @@ __global__ __launch_bounds__(512) void mhsa_kernel(const __bf16* __restrict__ q,
                 f32x16 a = f32x16{};
 #pragma unroll
                 for (int ks = 0; ks < 4; ks++) {
-                    const bf16x8 kf = *(const bf16x8*)(sK + kswz(kb * 32 + ql, 2 * ks + hh));
-                    a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], a, 0, 0, 0);
+                    const f16x8 kf = *(const f16x8*)(sK + kswz(kb * 32 + ql, 2 * ks + hh));
+                    a = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[ks], a, 0, 0, 0);
                 }
                 s[kb] = a;
             }
@@ -153,28 +154,28 @@ __global__ __launch_bounds__(512) void mhsa_kernel(const __bf16* __restrict__ q,
             for (int kb = 0; kb < NKB; kb++)
 #pragma unroll
                 for (int sp = 0; sp < 2; sp++) {
-                    bf16x8 pf;
+                    f16x8 pf;
 #pragma unroll
-                    for (int j = 0; j < 8; j++) pf[j] = (__bf16)s[kb][8 * sp + j];
+                    for (int j = 0; j < 8; j++) pf[j] = (_Float16)s[kb][8 * sp + j];
 #pragma unroll
                     for (int db = 0; db < 2; db++) {
-                        const __bf16* vr = sV + (db * 32 + ql) * vstride + kb * 32 + 16 * sp + 4 * hh;
-                        const bf16x4 v0 = *(const bf16x4*)(vr);
-                        const bf16x4 v1 = *(const bf16x4*)(vr + 8);
-                        const bf16x8 vf = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-                        oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, oacc[db], 0, 0, 0);
+                        const _Float16* vr = sV + (db * 32 + ql) * vstride + kb * 32 + 16 * sp + 4 * hh;
+                        const f16x4 v0 = *(const f16x4*)(vr);
+                        const f16x4 v1 = *(const f16x4*)(vr + 8);
+                        const f16x8 vf = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+                        oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, pf, oacc[db], 0, 0, 0);
                     }
                 }
             if (qi < L) {
                 const int64_t b = bh / H, hd = bh % H;
-                __bf16* orow = o + (b * L + qi) * (int64_t)(H * 64) + hd * 64;
+                _Float16* orow = o + (b * L + qi) * (int64_t)(H * 64) + hd * 64;
 #pragma unroll
                 for (int db = 0; db < 2; db++)
 #pragma unroll
                     for (int g = 0; g < 4; g++) {
-                        bf16x4 w = {(__bf16)(oacc[db][4 * g] * inv), (__bf16)(oacc[db][4 * g + 1] * inv),
-                                    (__bf16)(oacc[db][4 * g + 2] * inv), (__bf16)(oacc[db][4 * g + 3] * inv)};
-                        *(bf16x4*)(orow + db * 32 + 8 * g + 4 * hh) = w;
+                        f16x4 w = {(_Float16)(oacc[db][4 * g] * inv), (_Float16)(oacc[db][4 * g + 1] * inv),
+                                    (_Float16)(oacc[db][4 * g + 2] * inv), (_Float16)(oacc[db][4 * g + 3] * inv)};
+                        *(f16x4*)(orow + db * 32 + 8 * g + 4 * hh) = w;
                     }
             }
         }
@@ -240,7 +241,7 @@ static int launch_mhsa(const void* q, const void* k, const void* vt, void* o, in
     const int waves = (L + 31) / 32;
     const int64_t grid = nbh < num_cu() ? nbh : num_cu();
     hipLaunchKernelGGL((mhsa_kernel<NKB, CAUSAL>), dim3((unsigned)grid), dim3(64 * waves), lds, s,
-                       (const __bf16*)q, (const __bf16*)k, (const __bf16*)vt, (__bf16*)o, L, H, vs, nbh,
+                       (const _Float16*)q, (const _Float16*)k, (const _Float16*)vt, (_Float16*)o, L, H, vs, nbh,
                        scale_log2);
     RM_LAUNCHED();
     return OK;
@@ -250,8 +251,8 @@ static int launch_mhsa(const void* q, const void* k, const void* vt, void* o, in
 // q [nseq*H][64] (the CLS rows), k [nseq*H][L][64], vt [nseq*H][64][lpad] -> o [nseq][H*64].
 // Lane t-strided scores, wave-reduced softmax, probabilities through LDS, lane d sums
 // p_t * V^T[d][t] over its contiguous row.
-__global__ __launch_bounds__(256) void mhsa_cls_kernel(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
-                                                       const __bf16* __restrict__ vt, __bf16* __restrict__ o,
+__global__ __launch_bounds__(256) void mhsa_cls_kernel(const _Float16* __restrict__ q, const _Float16* __restrict__ k,
+                                                       const _Float16* __restrict__ vt, _Float16* __restrict__ o,
                                                        int64_t nbh, int L, int H, int lpad, float scale_log2) {
     __shared__ float sp[4][256];
     __shared__ float sq[4][64];
@@ -260,7 +261,7 @@ __global__ __launch_bounds__(256) void mhsa_cls_kernel(const __bf16* __restrict_
     if (bh >= nbh) return;
     sq[wid][lane] = (float)q[bh * 64 + lane];
     __builtin_amdgcn_wave_barrier();
-    const __bf16* kh = k + bh * (int64_t)L * 64;
+    const _Float16* kh = k + bh * (int64_t)L * 64;
     float sv[4];
     float mx = -__builtin_inff();
 #pragma unroll
@@ -269,10 +270,10 @@ __global__ __launch_bounds__(256) void mhsa_cls_kernel(const __bf16* __restrict_
         float a = -__builtin_inff();
         if (t < L) {
             a = 0.f;
-            const bf16x8* kr = (const bf16x8*)(kh + (int64_t)t * 64);
+            const f16x8* kr = (const f16x8*)(kh + (int64_t)t * 64);
 #pragma unroll
             for (int c = 0; c < 8; c++) {
-                const bf16x8 kv = kr[c];
+                const f16x8 kv = kr[c];
 #pragma unroll
                 for (int e = 0; e < 8; e++) a += sq[wid][c * 8 + e] * (float)kv[e];
             }
@@ -287,19 +288,19 @@ __global__ __launch_bounds__(256) void mhsa_cls_kernel(const __bf16* __restrict_
     for (int j = 0; j < 4; j++) {
         const int t = lane + 64 * j;
         const float p = t < L ? __builtin_amdgcn_exp2f(sv[j] - mx) : 0.f;
-        // bf16-rounded probabilities, as the blocked kernel feeds its P.V MFMAs
-        sp[wid][t] = (float)(__bf16)p;
+        // fp16-rounded probabilities, as the blocked kernel feeds its P.V MFMAs
+        sp[wid][t] = (float)(_Float16)p;
         sum += p;
     }
     sum = wave_sum(sum);
     __builtin_amdgcn_wave_barrier();
     // lane d: p . V^T[d][:].  All row loads are issued before the first use (a rolled loop
     // waited one HBM round trip per 8 keys); same summation order as before.
-    const __bf16* vr = vt + (bh * 64 + lane) * (int64_t)lpad;
-    bf16x8 vv[32];
+    const _Float16* vr = vt + (bh * 64 + lane) * (int64_t)lpad;
+    f16x8 vv[32];
 #pragma unroll
     for (int i = 0; i < 32; i++)
-        if (i * 8 < L) vv[i] = *(const bf16x8*)(vr + i * 8);
+        if (i * 8 < L) vv[i] = *(const f16x8*)(vr + i * 8);
     float acc = 0.f;
 #pragma unroll
     for (int i = 0; i < 32; i++)
@@ -308,15 +309,15 @@ __global__ __launch_bounds__(256) void mhsa_cls_kernel(const __bf16* __restrict_
             for (int e = 0; e < 8; e++)
                 if (i * 8 + e < L) acc += sp[wid][i * 8 + e] * (float)vv[i][e];
     const int64_t b = bh / H, h = bh % H;
-    o[b * (int64_t)H * 64 + h * 64 + lane] = (__bf16)(acc / sum);
+    o[b * (int64_t)H * 64 + h * 64 + lane] = (_Float16)(acc / sum);
 }
 
 int mhsa_cls(const void* q, const void* k, const void* vt, void* o, int64_t nseq, int L, int H, hipStream_t s) {
     const int lp = attn_lpad(L);
     RM_REQUIRE(lp > 0, "mhsa_cls: sequence length must be <= 256");
     const int64_t nbh = nseq * H;
-    hipLaunchKernelGGL(mhsa_cls_kernel, dim3(ceil_div(nbh, 4)), dim3(256), 0, s, (const __bf16*)q, (const __bf16*)k,
-                       (const __bf16*)vt, (__bf16*)o, nbh, L, H, lp, 0.125f * 1.4426950408889634f);
+    hipLaunchKernelGGL(mhsa_cls_kernel, dim3(ceil_div(nbh, 4)), dim3(256), 0, s, (const _Float16*)q, (const _Float16*)k,
+                       (const _Float16*)vt, (_Float16*)o, nbh, L, H, lp, 0.125f * 1.4426950408889634f);
     RM_LAUNCHED();
     return OK;
 }
@@ -357,7 +358,7 @@ using namespace reidmi;
 
 REIDMI_API int reidmi_attn_lpad(int L) { return attn_lpad(L); }
 
-REIDMI_API int reidmi_mhsa_bf16(const void* q, const void* k, const void* vt, void* o, int64_t nseq, int L, int H,
+REIDMI_API int reidmi_mhsa_f16(const void* q, const void* k, const void* vt, void* o, int64_t nseq, int L, int H,
                                 int causal, void* stream) {
     return mhsa(q, k, vt, o, nseq, L, H, causal != 0, (hipStream_t)stream);
 }

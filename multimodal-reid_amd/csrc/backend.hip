@@ -308,35 +308,39 @@ __global__ __launch_bounds__(256) void topk_rows_kernel(const float* __restrict_
 
 // ------------------------------------------------------------------- eval rows
 // numpy pairwise sum (PW_BLOCKSIZE 128, 8 accumulators) of an n-long float64 vector that
-// is zero except at sorted positions pos[0..m) with values val[]: adding +0.0 is exact,
+// is zero except at sorted positions pos(0..m) with values val(t): adding +0.0 is exact,
 // so only the tree structure over the nonzeros matters.  Iterative post-order walk.
-__device__ double leaf_sum(const int64_t* pos, const double* val, int lo, int hi, int64_t off, int64_t n) {
+// POS / VAL: callables t -> int64 position / double value.
+template <typename POS, typename VAL>
+__device__ double leaf_sum(POS pos, VAL val, int lo, int hi, int64_t off, int64_t n) {
     if (n < 8) {
         double res = 0.0;
-        for (int t = lo; t < hi; t++) res += val[t];
+        for (int t = lo; t < hi; t++) res += val(t);
         return res;
     }
     double r[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const int64_t main_end = n - (n % 8);
     int t = lo;
-    for (; t < hi && pos[t] - off < main_end; t++) {
-        int64_t p = pos[t] - off;
-        r[p & 7] += val[t];
+    for (; t < hi && pos(t) - off < main_end; t++) {
+        int64_t p = pos(t) - off;
+        r[p & 7] += val(t);
     }
     double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-    for (; t < hi; t++) res += val[t];
+    for (; t < hi; t++) res += val(t);
     return res;
 }
 
-__device__ int lower_pos(const int64_t* pos, int lo, int hi, int64_t x) {
+template <typename POS>
+__device__ int lower_pos(POS pos, int lo, int hi, int64_t x) {
     while (lo < hi) {
         int mid = (lo + hi) >> 1;
-        if (pos[mid] < x) lo = mid + 1; else hi = mid;
+        if (pos(mid) < x) lo = mid + 1; else hi = mid;
     }
     return lo;
 }
 
-__device__ double pairwise_sparse(const int64_t* pos, const double* val, int m, int64_t n) {
+template <typename POS, typename VAL>
+__device__ double pairwise_sparse(POS pos, VAL val, int m, int64_t n) {
     struct Frame { int64_t off, n, n2; int lo, hi, mid, stage; double left; };
     Frame st[48];
     int sp = 0;
@@ -367,12 +371,194 @@ __device__ double pairwise_sparse(const int64_t* pos, const double* val, int m, 
     return ret;
 }
 
+// Per query (evaluate.py:40-80): positives = gallery items with the query's pid and another
+// camera, junk = same pid and same camera (removed, :55-56), everything else a kept
+// negative.  With the positives sorted by (distance, index) — np.argsort(kind="stable") —
+// the rank of positive k among the kept items is
+//     rank_k = #{all j : key_j < key_pk} - #{junk i : key_i < key_pk},
+// so one pass over the distance row that bins EVERY item by how many positives precede it
+// (b(j) = #{p : key_p < key_j}; rank_k + 1 + junk_before(k) = sum_{t <= k} hist[t]) gives all
+// ranks; AP = numpy's pairwise sum of (k+1)/(rank_k+1) at positions rank_k over the kept
+// length, / m (:73-79); first = rank_0 (the CMC step, :65-68).
+//
+// eval_rows_wave_kernel: one wave per query, 4 queries per 256-thread workgroup, ~8 KiB of
+// LDS per wave (so ~16 waves per CU keep loads in flight).  Pass 1 streams the gallery
+// labels (int64 pid / camera, L2-resident: every query reads the same 2 x 8 B per item) and
+// compacts the positives' and junk items' indices with ballots; their distances are then
+// gathered and the positives bitonic-sorted in LDS.  Pass 2 reads the distance row once
+// (16-byte loads after a scalar head to 16-byte alignment), skipping items beyond the last
+// positive, and bins the rest by binary search into an LDS histogram.  A wave-wide scan
+// turns the histogram into ranks; lane 0 does the AP sum.  Queries with more than
+// EVW_MAXP positives or EVW_MAXJ junk items are left to eval_rows_kernel (valid = 2).
+constexpr int EVW_MAXP = 512, EVW_MAXJ = 256, EVW_WAVES = 4;
+
+struct EvWaveLds {
+    float pv[EVW_MAXP];
+    int pi[EVW_MAXP];
+    int hist[EVW_MAXP + 1];
+    float jv[EVW_MAXJ];
+    int ji[EVW_MAXJ];
+};
+
+#define EVW_SYNC()                                          \
+    do {                                                    \
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
+        __builtin_amdgcn_wave_barrier();                    \
+    } while (0)
+
+__global__ __launch_bounds__(256) void eval_rows_wave_kernel(
+    const float* __restrict__ dist, int64_t Q, int64_t G, int64_t ld, const int64_t* __restrict__ qp,
+    const int64_t* __restrict__ gp, const int64_t* __restrict__ qc, const int64_t* __restrict__ gc,
+    int32_t* __restrict__ valid, int64_t* __restrict__ first, double* __restrict__ ap,
+    int64_t* __restrict__ nkept) {
+    __shared__ EvWaveLds sm[EVW_WAVES];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t q = (int64_t)blockIdx.x * EVW_WAVES + w;
+    if (q >= Q) return;  // whole waves only: no workgroup barrier below
+    EvWaveLds& L = sm[w];
+    const float* row = dist + q * ld;
+    const int64_t qpid = qp[q], qcam = qc[q];
+    const uint64_t below = (1ull << lane) - 1;
+    // ---- pass 1: labels -> positive / junk index lists
+    int m = 0, nj = 0;
+    constexpr int U1 = 4;
+    for (int64_t j0 = 0; j0 < G; j0 += 64 * U1) {
+        int64_t pid[U1], cam[U1];
+#pragma unroll
+        for (int u = 0; u < U1; u++) {
+            const int64_t j = j0 + u * 64 + lane;
+            pid[u] = j < G ? gp[j] : qpid + 1;
+            cam[u] = j < G ? gc[j] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < U1; u++) {
+            const int64_t j = j0 + u * 64 + lane;
+            const bool same = pid[u] == qpid;
+            const bool pos = same && cam[u] != qcam, junk = same && cam[u] == qcam;
+            const uint64_t mp = __ballot(pos), mj = __ballot(junk);
+            if (pos) {
+                const int s = m + __popcll(mp & below);
+                if (s < EVW_MAXP) L.pi[s] = (int)j;
+            }
+            if (junk) {
+                const int s = nj + __popcll(mj & below);
+                if (s < EVW_MAXJ) L.ji[s] = (int)j;
+            }
+            m += __popcll(mp);
+            nj += __popcll(mj);
+        }
+    }
+    if (lane == 0) nkept[q] = G - nj;
+    if (m == 0) {
+        if (lane == 0) { valid[q] = 0; first[q] = -1; ap[q] = 0.0; }
+        return;
+    }
+    if (m > EVW_MAXP || nj > EVW_MAXJ) {  // eval_rows_kernel (one workgroup per query) takes it
+        if (lane == 0) valid[q] = 2;
+        return;
+    }
+    EVW_SYNC();
+    // ---- gather the positives' / junk distances, sort the positives by (value, index)
+    int P = 1;
+    while (P < m) P <<= 1;
+    for (int t = lane; t < P; t += 64) {
+        if (t < m) L.pv[t] = row[L.pi[t]];
+        else { L.pv[t] = __builtin_inff(); L.pi[t] = 0x7fffffff; }
+    }
+    for (int t = lane; t < nj; t += 64) L.jv[t] = row[L.ji[t]];
+    for (int t = lane; t <= m; t += 64) L.hist[t] = 0;
+    EVW_SYNC();
+    for (int k = 2; k <= P; k <<= 1)
+        for (int jj = k >> 1; jj > 0; jj >>= 1) {
+            for (int t = lane; t < P; t += 64) {
+                const int o = t ^ jj;
+                if (o > t) {
+                    const bool up = (t & k) == 0;
+                    const float av = L.pv[t], bv = L.pv[o];
+                    const int ai = L.pi[t], bi = L.pi[o];
+                    if (key_less(bv, bi, av, ai) == up) { L.pv[t] = bv; L.pv[o] = av; L.pi[t] = bi; L.pi[o] = ai; }
+                }
+            }
+            EVW_SYNC();
+        }
+    // ---- pass 2: bin every item of the row by the number of positives before it
+    const float lv = L.pv[m - 1];
+    const int li = L.pi[m - 1];
+    auto bin = [&](float v, int j) {
+        if (key_less(lv, li, v, j)) return;  // after the last positive: b = m, not needed
+        int lo = 0, hi = m;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (key_less(L.pv[mid], L.pi[mid], v, j)) lo = mid + 1; else hi = mid;
+        }
+        __hip_atomic_fetch_add(&L.hist[lo], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    };
+    const int head = (int)(((16 - ((uintptr_t)row & 15)) & 15) >> 2);  // scalar items before 16-B alignment
+    const int h = head < G ? head : (int)G;
+    if (lane < h) bin(row[lane], lane);
+    const int64_t nv = (G - h) >> 2;  // float4 groups
+    const float4* r4 = (const float4*)(row + h);
+    constexpr int U2 = 4;
+    for (int64_t g0 = 0; g0 < nv; g0 += 64 * U2) {
+        float4 v[U2];
+#pragma unroll
+        for (int u = 0; u < U2; u++) {
+            const int64_t g = g0 + u * 64 + lane;
+            v[u] = g < nv ? r4[g] : make_float4(__builtin_inff(), 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < U2; u++) {
+            const int64_t g = g0 + u * 64 + lane;
+            if (g < nv) {
+                const int j = h + (int)g * 4;
+                bin(v[u].x, j);
+                bin(v[u].y, j + 1);
+                bin(v[u].z, j + 2);
+                bin(v[u].w, j + 3);
+            }
+        }
+    }
+    for (int64_t j = h + nv * 4 + lane; j < G; j += 64) bin(row[j], (int)j);
+    EVW_SYNC();
+    // ---- ranks: inclusive scan of hist, minus the item itself and the junk before it
+    int carry = 0;
+    for (int c0 = 0; c0 < m; c0 += 64) {
+        const int k = c0 + lane;
+        int v = k < m ? L.hist[k] : 0;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(v, o, 64);
+            if (lane >= o) v += t;
+        }
+        const int incl = v + carry;
+        carry = __shfl(incl, 63, 64);
+        if (k < m) {
+            const float pvk = L.pv[k];
+            const int pik = L.pi[k];
+            int jb = 0;
+            for (int t = 0; t < nj; t++) jb += key_less(L.jv[t], L.ji[t], pvk, pik);
+            L.hist[k] = incl - 1 - jb;  // rank_k (0-based position among the kept items)
+        }
+    }
+    EVW_SYNC();
+    if (lane == 0) {
+        const int* rk = L.hist;
+        const int64_t n = G - nj;
+        valid[q] = 1;
+        first[q] = rk[0];
+        ap[q] = pairwise_sparse([&](int t) { return (int64_t)rk[t]; },
+                                [&](int t) { return (double)(t + 1) / (double)(rk[t] + 1); }, m, n) /
+                (double)m;
+    }
+}
+#undef EVW_SYNC
+
 constexpr int EV_MAXP = 2048;
 
-// One workgroup per query row.  Positives (same pid, other camera) are collected and
-// sorted; every other kept gallery item is binned by how many positives precede it
-// (binary search), so rank(positive k) = k + #kept negatives before it.  Junk (same pid
-// and camera) is removed exactly as evaluate.py:55-56.
+// Fallback for the queries eval_rows_wave_kernel left (valid == 2: more than EVW_MAXP
+// positives or EVW_MAXJ junk items): one workgroup per query, up to EV_MAXP positives.
+// Positives are collected and sorted; every other kept gallery item is binned by how many
+// positives precede it (binary search).  Queries beyond EV_MAXP set *overflow.
 __global__ __launch_bounds__(256) void eval_rows_kernel(
     const float* __restrict__ dist, int64_t G, int64_t ld, const int64_t* __restrict__ qp,
     const int64_t* __restrict__ gp, const int64_t* __restrict__ qc, const int64_t* __restrict__ gc,
@@ -385,6 +571,7 @@ __global__ __launch_bounds__(256) void eval_rows_kernel(
     __shared__ double rv[EV_MAXP];
     __shared__ int s_m, s_junk;
     const int64_t q = blockIdx.x;
+    if (valid[q] != 2) return;
     const float* row = dist + q * ld;
     const int64_t qpid = qp[q], qcam = qc[q];
     if (threadIdx.x == 0) { s_m = 0; s_junk = 0; }
@@ -409,24 +596,21 @@ __global__ __launch_bounds__(256) void eval_rows_kernel(
     for (int t = threadIdx.x; t <= m; t += blockDim.x) hist[t] = 0;
     __syncthreads();
     bitonic_sort_kv(pv, pi, P);
-    if (m > 0) {
-        for (int64_t j = threadIdx.x; j < G; j += blockDim.x) {
-            if (gp[j] == qpid) continue;  // positives counted separately, junk removed
-            const float v = row[j];
-            int lo = 0, hi = m;
-            while (lo < hi) {
-                int mid = (lo + hi) >> 1;
-                if (key_less(pv[mid], pi[mid], v, (int)j)) lo = mid + 1; else hi = mid;
-            }
-            if (lo < m) atomicAdd(&hist[lo], 1);
+    for (int64_t j = threadIdx.x; j < G; j += blockDim.x) {
+        if (gp[j] == qpid) continue;  // positives counted separately, junk removed
+        const float v = row[j];
+        int lo = 0, hi = m;
+        while (lo < hi) {
+            int mid = (lo + hi) >> 1;
+            if (key_less(pv[mid], pi[mid], v, (int)j)) lo = mid + 1; else hi = mid;
         }
+        if (lo < m) atomicAdd(&hist[lo], 1);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         const int64_t n = G - s_junk;
         nkept[q] = n;
-        valid[q] = m > 0;
-        if (m == 0) { first[q] = -1; ap[q] = 0.0; return; }
+        valid[q] = 1;
         int64_t cum = 0;
         for (int k = 0; k < m; k++) {
             cum += hist[k];
@@ -434,7 +618,7 @@ __global__ __launch_bounds__(256) void eval_rows_kernel(
             rv[k] = (double)(k + 1) / (double)(rk[k] + 1);
         }
         first[q] = rk[0];
-        ap[q] = pairwise_sparse(rk, rv, m, n) / (double)m;
+        ap[q] = pairwise_sparse([&](int t) { return rk[t]; }, [&](int t) { return rv[t]; }, m, n) / (double)m;
     }
 }
 
@@ -558,9 +742,15 @@ REIDMI_API int reidmi_eval_rows(const float* dist, int64_t Q, int64_t G, int64_t
                                 int64_t* first, double* ap, int64_t* nkept, int32_t* overflow, void* stream) {
     RM_REQUIRE(Q >= 0 && G > 0 && ldd >= G && G < 0x7fffffff, "eval_rows: bad shape");
     RM_REQUIRE(overflow != nullptr, "eval_rows: overflow flag pointer required");
+    RM_REQUIRE(((uintptr_t)dist & 3) == 0, "eval_rows: dist must be 4-byte aligned");
     if (Q == 0) return OK;
-    hipLaunchKernelGGL(eval_rows_kernel, dim3((unsigned)Q), dim3(256), 0, (hipStream_t)stream, dist, G, ldd, q_pids,
-                       g_pids, q_cams, g_cams, valid, first, ap, nkept, overflow);
+    hipStream_t s = (hipStream_t)stream;
+    RM_REQUIRE(ceil_div(Q, EVW_WAVES) < (1ll << 31), "eval_rows: too many queries");
+    hipLaunchKernelGGL(eval_rows_wave_kernel, dim3((unsigned)ceil_div(Q, EVW_WAVES)), dim3(64 * EVW_WAVES), 0, s,
+                       dist, Q, G, ldd, q_pids, g_pids, q_cams, g_cams, valid, first, ap, nkept);
+    RM_LAUNCHED();
+    hipLaunchKernelGGL(eval_rows_kernel, dim3((unsigned)Q), dim3(256), 0, s, dist, G, ldd, q_pids, g_pids, q_cams,
+                       g_cams, valid, first, ap, nkept, overflow);
     RM_LAUNCHED();
     return OK;
 }

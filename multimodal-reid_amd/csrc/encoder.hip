@@ -11,8 +11,9 @@
 // The residual stream x is fp16 in HBM (the reference's GPU dtype, utils.py:145-166; every
 // residual add is computed in fp32 and rounded once).  ln_1 / ln_2 never materialise: the
 // QKV and c_fc GEMMs read x itself (fp16 operands) against W diag(gamma) and apply
-// rstd * acc - mean * rstd * colsum + (b + W beta) in their epilogues (gemm.h).  The other
-// GEMM operands (attention output, QuickGELU output) are bf16; LayerNorm statistics fp32.
+// rstd * acc - mean * rstd * colsum + (b + W beta) in their epilogues (gemm.h).  Every other
+// GEMM / attention operand (patch columns, q / k / v, softmax probabilities, attention and
+// QuickGELU outputs, ln_post / ln_final rows) is fp16 too; LayerNorm statistics fp32.
 #include "gemm.h"
 
 namespace reidmi {
@@ -42,7 +43,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const TX* x, int64_t row
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, float eps,
                                                         float* __restrict__ y32, int64_t ldy32,
-                                                        __bf16* __restrict__ y16, int64_t ldy16,
+                                                        _Float16* __restrict__ y16, int64_t ldy16,
                                                         _Float16* yh, int64_t ldyh, float2* __restrict__ st) {
     const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= rows) return;
@@ -80,8 +81,8 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const TX* x, int64_t row
         o.w = (v[i].w - mean) * rstd * g.w + b.w;
         if (y32) ((float4*)(y32 + r * ldy32))[f] = o;
         if (y16) {
-            bf16x4 h = {(__bf16)o.x, (__bf16)o.y, (__bf16)o.z, (__bf16)o.w};
-            ((bf16x4*)(y16 + r * ldy16))[f] = h;
+            f16x4 h = {(_Float16)o.x, (_Float16)o.y, (_Float16)o.z, (_Float16)o.w};
+            ((f16x4*)(y16 + r * ldy16))[f] = h;
         }
         if (yh) {  // may alias x (in-place ln_pre): the whole row is in registers already
             f16x4 h = {(_Float16)o.x, (_Float16)o.y, (_Float16)o.z, (_Float16)o.w};
@@ -92,7 +93,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const TX* x, int64_t row
 
 template <typename TX>
 int layernorm(const TX* x, int64_t rows, int64_t ldx, const int32_t* row_idx, int64_t W, const float* g,
-              const float* b, float eps, float* y32, int64_t ldy32, __bf16* y16, int64_t ldy16, hipStream_t s,
+              const float* b, float eps, float* y32, int64_t ldy32, _Float16* y16, int64_t ldy16, hipStream_t s,
               _Float16* yh = nullptr, int64_t ldyh = 0, float2* st = nullptr) {
     if (rows == 0) return OK;
     RM_REQUIRE(ldx % 4 == 0 && (!y32 || ldy32 % 4 == 0) && (!y16 || ldy16 % 4 == 0) && (!yh || ldyh % 4 == 0),
@@ -185,7 +186,7 @@ __global__ void rows_f16_to_f32_kernel(const _Float16* __restrict__ x, int64_t r
 template <typename TI, int PT>
 __global__ __launch_bounds__(256) void im2col_kernel(const TI* __restrict__ img, int H, int Wd, int P_, int S,
                                                      int gh, int gw, int kpad, const int32_t* __restrict__ tta,
-                                                     __bf16* __restrict__ col) {
+                                                     _Float16* __restrict__ col) {
     extern __shared__ float srow[];  // [3][P][Wd]
     const int P = PT > 0 ? PT : P_;
     const int b = blockIdx.x / gh, py = blockIdx.x - (blockIdx.x / gh) * gh;
@@ -202,7 +203,7 @@ __global__ __launch_bounds__(256) void im2col_kernel(const TI* __restrict__ img,
         if (y >= 0 && y < H) {
             const uint4 raw = *(const uint4*)(im + ((int64_t)c * H + y) * Wd + xv * V);
             if constexpr (sizeof(TI) == 2) {
-                const bf16x8 v = __builtin_bit_cast(bf16x8, raw);
+                const f16x8 v = __builtin_bit_cast(f16x8, raw);
 #pragma unroll
                 for (int u = 0; u < 8; u++) d[u] = (float)v[u];
             } else {
@@ -215,10 +216,10 @@ __global__ __launch_bounds__(256) void im2col_kernel(const TI* __restrict__ img,
     }
     __syncthreads();
     const int kch = kpad / 8, PP = P * P;
-    __bf16* out = col + ((int64_t)b * gh * gw + (int64_t)py * gw) * kpad;
+    _Float16* out = col + ((int64_t)b * gh * gw + (int64_t)py * gw) * kpad;
     for (int e = threadIdx.x; e < gw * kch; e += blockDim.x) {
         const int px = e / kch, kc = e - px * kch;
-        bf16x8 o;
+        f16x8 o;
 #pragma unroll
         for (int u = 0; u < 8; u++) {
             const int k = kc * 8 + u;
@@ -234,9 +235,9 @@ __global__ __launch_bounds__(256) void im2col_kernel(const TI* __restrict__ img,
                 }
                 v = inb ? srow[(c * P + ky) * Wd + x] : -1.0f;
             }
-            o[u] = (__bf16)v;
+            o[u] = (_Float16)v;
         }
-        *(bf16x8*)(out + (int64_t)px * kpad + kc * 8) = o;
+        *(f16x8*)(out + (int64_t)px * kpad + kc * 8) = o;
     }
 }
 
@@ -340,8 +341,8 @@ static int run_block(const reidmi_block_weights& bw, char* ws, const Plan& P, in
     const int64_t M = nseq * L;
     float2* pst = (float2*)(ws + P.pst);
     _Float16* x = (_Float16*)(ws + P.x);
-    __bf16* o = (__bf16*)(ws + P.o);
-    __bf16* u = (__bf16*)(ws + P.u);
+    _Float16* o = (_Float16*)(ws + P.o);
+    _Float16* u = (_Float16*)(ws + P.u);
     float2* st = (float2*)(ws + P.st);
     int rc;
     // ln_1 (custom_clip_model.py:27)
@@ -364,7 +365,7 @@ static int run_block(const reidmi_block_weights& bw, char* ws, const Plan& P, in
     er.bias = bw.out_b;
     er.pstat = pst;
     er.ldp = M;
-    if ((rc = gemm_bf16(EPI_RESID_F16, o, W, bw.out_w, W, M, W, W, er, s))) return rc;
+    if ((rc = gemm_f16(EPI_RESID_F16, o, W, bw.out_w, W, M, W, W, er, s))) return rc;
     if ((rc = row_stats_from_partials(pst, M, W, st, s))) return rc;  // ln_2 (custom_clip_model.py:28)
     EpiArgs eg{};
     eg.out = u;
@@ -372,36 +373,46 @@ static int run_block(const reidmi_block_weights& bw, char* ws, const Plan& P, in
     eg.bias = bw.fc1_b;
     eg.rowstat = st;
     eg.colsum = bw.fc1_s;
-    if ((rc = gemm_f16(EPI_GELU_BF16, x, W, bw.fc1_w, W, M, 4 * W, W, eg, s))) return rc;
+    if ((rc = gemm_f16(EPI_GELU_H16, x, W, bw.fc1_w, W, M, 4 * W, W, eg, s))) return rc;
     EpiArgs e2{};
     e2.out = x;
     e2.ldc = W;
     e2.bias = bw.fc2_b;
     e2.pstat = pst;  // for the next block's ln_1
     e2.ldp = M;
-    if ((rc = gemm_bf16(EPI_RESID_F16, u, 4 * W, bw.fc2_w, 4 * W, M, W, 4 * W, e2, s))) return rc;
+    if ((rc = gemm_f16(EPI_RESID_F16, u, 4 * W, bw.fc2_w, 4 * W, M, W, 4 * W, e2, s))) return rc;
     return OK;
+}
+
+__global__ void gather_rowstat_kernel(const float2* __restrict__ st, int64_t nseq, int L, float2* __restrict__ sc) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < nseq) sc[b] = st[b * L];
 }
 
 // The last block when only the CLS row of its output is consumed (inference path,
 // zero_shot_learning.py:85-87 reads x12[:,0] / xproj[:,0]): K and V for every token, then
 // Q, attention, out_proj, LN2 and the MLP for the CLS rows only.  Every CLS-row value is
-// computed by the same kernels in the same order as in run_block (row statistics are per
-// row, GEMM outputs per element), so the result is bit-identical to the full block's row 0
-// (tests/test_gpu_encoder.py checks equality).
+// computed by the same kernels as in run_block (GEMM outputs per element), but its
+// statistics come from a pass over the CLS rows, where run_block combines the residual
+// epilogues' partials (a different fp32 summation order), and its attention is the
+// single-query kernel: equal to the full block's row 0 up to fp32 rounding
+// (tests/test_gpu_encoder.py bounds the difference).
 static int run_block_cls(const reidmi_block_weights& bw, char* ws, const Plan& P, int64_t nseq, int L, int W, int H,
                          bool x_pst, hipStream_t s) {
     const int64_t M = nseq * L;
     _Float16* x = (_Float16*)(ws + P.x);
-    __bf16* o = (__bf16*)(ws + P.o);
-    __bf16* u = (__bf16*)(ws + P.u);
+    _Float16* o = (_Float16*)(ws + P.o);
+    _Float16* u = (_Float16*)(ws + P.u);
     float2* st = (float2*)(ws + P.st);
     float2* sc = (float2*)(ws + P.st_cls);
     const int64_t ldc = (int64_t)L * W;  // CLS row of each sequence
     int rc;
     if ((rc = x_pst ? row_stats_from_partials((const float2*)(ws + P.pst), M, W, st, s) : row_stats(x, M, W, W, st, s)))
         return rc;
-    if ((rc = row_stats(x, nseq, ldc, W, sc, s))) return rc;
+    // the CLS rows' ln_1 statistics are rows b*L of st (so Q, K and V of a CLS row use the
+    // same statistics); gathered into the padded per-sequence buffer the Q GEMM reads
+    hipLaunchKernelGGL(gather_rowstat_kernel, dim3(ceil_div(nseq, 256)), dim3(256), 0, s, st, nseq, L, sc);
+    RM_LAUNCHED();
     EpiArgs kv{};
     kv.bias = bw.qkv_b + W;
     kv.rowstat = st;
@@ -427,7 +438,7 @@ static int run_block_cls(const reidmi_block_weights& bw, char* ws, const Plan& P
     er.out = x;
     er.ldc = ldc;
     er.bias = bw.out_b;
-    if ((rc = gemm_bf16(EPI_RESID_F16, o, W, bw.out_w, W, nseq, W, W, er, s))) return rc;
+    if ((rc = gemm_f16(EPI_RESID_F16, o, W, bw.out_w, W, nseq, W, W, er, s))) return rc;
     if ((rc = row_stats(x, nseq, ldc, W, sc, s))) return rc;
     EpiArgs eg{};
     eg.out = u;
@@ -435,12 +446,12 @@ static int run_block_cls(const reidmi_block_weights& bw, char* ws, const Plan& P
     eg.bias = bw.fc1_b;
     eg.rowstat = sc;
     eg.colsum = bw.fc1_s;
-    if ((rc = gemm_f16(EPI_GELU_BF16, x, ldc, bw.fc1_w, W, nseq, 4 * W, W, eg, s))) return rc;
+    if ((rc = gemm_f16(EPI_GELU_H16, x, ldc, bw.fc1_w, W, nseq, 4 * W, W, eg, s))) return rc;
     EpiArgs e2{};
     e2.out = x;
     e2.ldc = ldc;
     e2.bias = bw.fc2_b;
-    return gemm_bf16(EPI_RESID_F16, u, 4 * W, bw.fc2_w, 4 * W, nseq, W, 4 * W, e2, s);
+    return gemm_f16(EPI_RESID_F16, u, 4 * W, bw.fc2_w, 4 * W, nseq, W, 4 * W, e2, s);
 }
 
 static int vit_check(const reidmi_vit_weights* w) {
@@ -459,7 +470,7 @@ using namespace reidmi;
 REIDMI_API int reidmi_layernorm(const float* x, int64_t rows, int64_t ldx, const int32_t* row_idx, int64_t W,
                                 const float* gamma, const float* beta, float eps, float* y32, int64_t ldy32, void* y16,
                                 int64_t ldy16, void* stream) {
-    return layernorm(x, rows, ldx, row_idx, W, gamma, beta, eps, y32, ldy32, (__bf16*)y16, ldy16,
+    return layernorm(x, rows, ldx, row_idx, W, gamma, beta, eps, y32, ldy32, (_Float16*)y16, ldy16,
                      (hipStream_t)stream);
 }
 
@@ -469,7 +480,7 @@ REIDMI_API int64_t reidmi_vit_workspace_bytes(const reidmi_vit_weights* w, int64
     return plan(B, L, w->width, attn_lpad(L), 0).total;
 }
 
-REIDMI_API int reidmi_vit_forward(const reidmi_vit_weights* w, const void* images, int images_bf16, int64_t B, int H,
+REIDMI_API int reidmi_vit_forward(const reidmi_vit_weights* w, const void* images, int images_f16, int64_t B, int H,
                                   int Wimg, const int32_t* tta, int full, float* out_x12, float* out_proj,
                                   float* out_x11, void* ws_, int64_t ws_bytes, void* stream) {
     int rc;
@@ -485,8 +496,8 @@ REIDMI_API int reidmi_vit_forward(const reidmi_vit_weights* w, const void* image
     if (B == 0) return OK;
     char* ws = (char*)ws_;
     _Float16* x = (_Float16*)(ws + P.x);
-    __bf16* h = (__bf16*)(ws + P.h);
-    __bf16* col = (__bf16*)(ws + P.u);
+    _Float16* h = (_Float16*)(ws + P.h);
+    _Float16* col = (_Float16*)(ws + P.u);
     const int64_t M = B * L;
     // patch embed (+pos), CLS/VPT rows, ln_pre
     RM_REQUIRE(B * w->grid_h < (1ll << 31) && Wimg % 8 == 0, "vit: im2col needs B * grid_h < 2^31 and width % 8 == 0");
@@ -497,10 +508,10 @@ REIDMI_API int reidmi_vit_forward(const reidmi_vit_weights* w, const void* image
 #define RM_IM2COL(TI, PT)                                                                                      \
     hipLaunchKernelGGL((im2col_kernel<TI, PT>), g, t, lds, s, (const TI*)images, H, Wimg, w->patch, w->stride, \
                        w->grid_h, w->grid_w, w->kpad, tta, col)
-        if (images_bf16) {
-            if (w->patch == 16) RM_IM2COL(__bf16, 16);
-            else if (w->patch == 14) RM_IM2COL(__bf16, 14);
-            else RM_IM2COL(__bf16, 0);
+        if (images_f16) {
+            if (w->patch == 16) RM_IM2COL(_Float16, 16);
+            else if (w->patch == 14) RM_IM2COL(_Float16, 14);
+            else RM_IM2COL(_Float16, 0);
         } else {
             if (w->patch == 16) RM_IM2COL(float, 16);
             else if (w->patch == 14) RM_IM2COL(float, 14);
@@ -515,7 +526,7 @@ REIDMI_API int reidmi_vit_forward(const reidmi_vit_weights* w, const void* image
     ep.pos = w->pos_emb;
     ep.npatch = NP;
     ep.seq = L;
-    if ((rc = gemm_bf16(EPI_PATCH, col, w->kpad, w->conv_w, w->kpad, B * NP, W, w->kpad, ep, s))) return rc;
+    if ((rc = gemm_f16(EPI_PATCH, col, w->kpad, w->conv_w, w->kpad, B * NP, W, w->kpad, ep, s))) return rc;
     RM_REQUIRE(w->n_ctx == 0 || w->vpt != nullptr, "vit: n_ctx > 0 needs vpt");
     const int64_t ce = B * (1 + w->n_ctx) * W;
     hipLaunchKernelGGL(cls_rows_kernel, dim3(ceil_div(ce, 256)), dim3(256), 0, s, x, B, L, W, w->class_emb,
@@ -552,7 +563,7 @@ REIDMI_API int reidmi_vit_forward(const reidmi_vit_weights* w, const void* image
     EpiArgs eo{};
     eo.out = out_proj;
     eo.ldc = E;
-    if ((rc = gemm_bf16(EPI_F32, h, W, w->proj_t, W, rows, E, W, eo, s))) return rc;
+    if ((rc = gemm_f16(EPI_F32, h, W, w->proj_t, W, rows, E, W, eo, s))) return rc;
     return OK;
 }
 
@@ -573,7 +584,7 @@ REIDMI_API int reidmi_text_forward(const reidmi_text_weights* w, const int64_t* 
     if (N == 0) return OK;
     char* ws = (char*)ws_;
     _Float16* x = (_Float16*)(ws + P.x);
-    __bf16* h = (__bf16*)(ws + P.h);
+    _Float16* h = (_Float16*)(ws + P.h);
     int32_t* rows = (int32_t*)(ws + P.rows);
     const int64_t te = N * L * (W / 4);
     hipLaunchKernelGGL(text_embed_kernel, dim3(ceil_div(te, 256)), dim3(256), 0, s, x, tokens, prompts, w->tok_emb,
@@ -597,5 +608,5 @@ REIDMI_API int reidmi_text_forward(const reidmi_text_weights* w, const int64_t* 
     EpiArgs eo{};
     eo.out = out;
     eo.ldc = E;
-    return gemm_bf16(EPI_F32, h, W, w->proj_t, W, N, E, W, eo, s);
+    return gemm_f16(EPI_F32, h, W, w->proj_t, W, N, E, W, eo, s);
 }

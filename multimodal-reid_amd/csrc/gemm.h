@@ -1,25 +1,24 @@
-// gemm.h — bf16 / fp16 MFMA GEMM with fused epilogues for the CLIP encoders (gfx950).
+// gemm.h — fp16 MFMA GEMM with fused epilogues for the CLIP encoders (gfx950).
 //
-// C[M,N] = A[M,K] . W[N,K]^T (+ bias[N]), A row-major bf16 (activations), W row-major bf16
+// C[M,N] = A[M,K] . W[N,K]^T (+ bias[N]), A row-major fp16 (activations), W row-major fp16
 // (PyTorch Linear / conv weight layout [out, in]), fp32 accumulation on
-// v_mfma_f32_16x16x32_bf16.  Epilogues implement the ops that follow each GEMM in
-// custom_clip_model.py:8-29 / maple.py:617-644 so no elementwise pass touches HBM:
-//   EPI_BF16      out bf16 = acc + bias                       (generic)
-//   EPI_GELU_BF16 out bf16 = QuickGELU(acc + bias)            (mlp.c_fc + gelu, :14-16,52-54)
-//   EPI_RESID_F32 x fp32 += acc + bias                        (out_proj / c_proj + residual, :27-28)
-//   EPI_QKV       q,k -> [B,H,L,64] bf16, v -> [B,H,64,Lp]    (attn.in_proj + head split)
+// v_mfma_f32_16x16x32_f16 (the reference's own GPU dtype, utils.py:145-166).  Epilogues
+// implement the ops that follow each GEMM in custom_clip_model.py:8-29 / maple.py:617-644
+// so no elementwise pass touches HBM:
+//   EPI_H16       out fp16 = acc + bias                       (generic)
+//   EPI_GELU_H16  out fp16 = QuickGELU(acc + bias)            (mlp.c_fc + gelu, :14-16,52-54)
+//   EPI_QKV       q,k -> [B,H,L,64] fp16, v -> [B,H,64,Lp]    (attn.in_proj + head split)
 //   EPI_PATCH     x[b*L+1+p] = acc + pos[1+p]  fp16           (conv1 + pos-embed, :78-86)
 //   EPI_F32       out fp32 = acc + bias                       (proj / text_projection)
-//   EPI_RESID_F16 x fp16 += acc + bias (fp32 sum, one rounding) (the encoders' residual stream)
+//   EPI_RESID_F16 x fp16 += acc + bias (fp32 sum, one rounding) (out_proj / c_proj + residual, :27-28)
 #pragma once
 #include "common.h"
 
 namespace reidmi {
 
 enum Epi : int {
-    EPI_BF16 = 0,
-    EPI_GELU_BF16 = 1,
-    EPI_RESID_F32 = 2,
+    EPI_H16 = 0,
+    EPI_GELU_H16 = 1,
     EPI_QKV = 3,
     EPI_PATCH = 4,
     EPI_F32 = 5,
@@ -27,7 +26,7 @@ enum Epi : int {
 };
 
 struct EpiArgs {
-    void* out;          // bf16 / fp32 output (or residual x for RESID, x for PATCH)
+    void* out;          // fp16 / fp32 output (or residual x for RESID, x for PATCH)
     int64_t ldc;        // row stride of out (elements)
     const float* bias;  // [N] or null
     // QKV head split
@@ -41,7 +40,7 @@ struct EpiArgs {
     // PATCH
     const float* pos;  // [1+NP][N]
     int npatch;        // NP
-    // LayerNorm folded into an fp16 GEMM (gemm_f16): with W' = W diag(gamma) (fp16),
+    // LayerNorm folded into the GEMM: with W' = W diag(gamma) (fp16),
     // s_n = sum_k W'[n,k], b' = b + W beta (the bias above):
     //   LN(x) W^T + b = rstd_m * (x W'^T)_mn + (-mean_m rstd_m) * s_n + b'_n
     const float2* rowstat;  // [round_up(M, 256)] (rstd, -mean*rstd) of the A rows (entries
@@ -55,14 +54,8 @@ struct EpiArgs {
     int64_t ldp;
 };
 
-// Launch C = A . W^T with epilogue `epi`.  Requires N % 128 == 0, K % 64 == 0,
-// lda/ldw multiples of 8 (16-byte rows); M arbitrary.
-int gemm_bf16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N, int64_t K,
-              const EpiArgs& ea, hipStream_t stream);
-
-// Same with fp16 operands (v_mfma_f32_16x16x32_f16): A = the fp16 residual stream, W = an
-// fp16 LayerNorm-folded weight; epi in {EPI_BF16, EPI_GELU_BF16, EPI_QKV}; ea.rowstat /
-// ea.colsum enable the fold.
+// Launch C = A . W^T with epilogue `epi`.  Requires N % 128 == 0, K % 64 == 0, lda/ldw
+// multiples of 8 (16-byte rows); M arbitrary.  ea.rowstat / ea.colsum enable the fold.
 int gemm_f16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N, int64_t K,
              const EpiArgs& ea, hipStream_t stream);
 

@@ -1,19 +1,19 @@
-// gemm.hip — bf16 MFMA GEMM (C = A . W^T) with fused epilogues; see gemm.h.
+// gemm.hip — fp16 MFMA GEMM (C = A . W^T) with fused epilogues; see gemm.h.
 //
-// Tiling (MI355X / gfx950): 128x128x64 block tile, 256 threads = 4 waves as 2x2, each
-// wave owns 64x64 = 4x4 tiles of v_mfma_f32_16x16x32_bf16.  Operand tiles are staged
-// global -> registers -> LDS (double-buffered, one barrier per K-step: the loads for
-// tile k+1 are in flight while tile k is multiplied).  LDS rows are 128 B; 16-byte
-// chunks are XOR-swizzled with (row>>1)&7 so the fragment reads (16 rows x 4 chunks per
-// ds_read_b128 lane group) are bank-conflict free.  Operands are swapped in the MFMA
-// (W fragment as A, activation fragment as B) so each lane ends up holding one output
-// row and 4 consecutive output columns: epilogue loads/stores are 8-16 B per lane.
-// Block ids are remapped XCD-contiguously (consecutive tiles of one A row panel share
-// an XCD's L2).
+// Every operand is fp16 (the reference's GPU dtype, utils.py:145-166), fp32 accumulation on
+// v_mfma_f32_16x16x32_f16.  Two tilings, bit-identical per output element (same MFMA chain,
+// K ascending):
+//  * gemm_tile_kernel (small M: the CLS-only last block, proj, the text tower's heads):
+//    128x128x64 block tile, 256 threads = 4 waves as 2x2, each wave 64x64 = 4x4 MFMA tiles;
+//    operands staged global -> registers -> LDS (double-buffered, one barrier per K-step).
+//  * gemm_persistent_kernel (>= 256 tiles of 256x256): see its header below.
+// LDS rows are 128 B; 16-byte chunks are XOR-swizzled with (row>>1)&7 so the fragment
+// reads (16 rows x 4 chunks per ds_read_b128 lane group) are bank-conflict free.  Operands
+// are swapped in the MFMA (W fragment as A, activation fragment as B) so each lane ends up
+// holding one output row and 4 consecutive output columns: epilogue loads/stores are 8-16 B
+// per lane.
 #include "gemm.h"
 
-#include <cstdlib>
-#include <type_traits>
 #include <mutex>
 #include <vector>
 
@@ -35,59 +35,35 @@ static std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
 static size_t used = 0;
 }  // namespace prof
 
-// Tile selection: 0 = auto (>= 256 tiles of 256x256: v6; else v1), 1..6 force
-// v1 (128x128), v2 (256x256), v3 (persistent), v4 (ping-pong), v5 (persistent ping-pong),
-// v6 (v5 with deferred epilogue-store waits: +1-2 % on the K = 768 shapes); A/B-only:
-// v7 (two 32-MFMA sections per K-step: 1-3 % SLOWER than v5/v6, kept as the measured
-// negative), v8 / v9 (v6 with the residual epilogue loading 2 / 4 row groups per batch
-// instead of all 8).  Set by reidmi_gemm_set_variant (tests / A-B timing in one process);
-// the REIDMI_GEMM_VARIANT environment variable gives the initial value.
-static int g_variant = -1;
-static int variant() {
-    if (g_variant < 0) {
-        const char* e = getenv("REIDMI_GEMM_VARIANT");
-        g_variant = e ? atoi(e) : 0;
-    }
-    return g_variant;
-}
+// Tile selection for tests (reidmi_gemm_set_tile): 0 = auto (persistent 256x256 tile when
+// the GEMM has >= 256 of them, else 128x128), 1 = force 128x128, 2 = force persistent.
+static int g_tile = 0;
+// Persistent tile walk (reidmi_gemm_set_walk; see gemm_persistent_kernel): N-groups the
+// XCDs are split into (1 = every XCD walks all N-tiles of its M range).
+static int g_ngroups = 1;
 
 constexpr int GB_M = 128, GB_N = 128, GB_K = 64;
 
 __device__ __forceinline__ int swz(int r, int kc) { return r * GB_K + ((kc ^ ((r >> 1) & 7)) << 3); }
 
-// one v_cvt_pk_bf16_f32 (RNE, NaN-preserving) per pair
-__device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
-    uint32_t r;
-    asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-
-__device__ __forceinline__ uint2 pack_bf16x4(float a, float b, float c, float d) {
-    return make_uint2(cvt_pk_bf16(a, b), cvt_pk_bf16(c, d));
-}
-
-__device__ __forceinline__ float quick_gelu(float x) {
-    // x * sigmoid(1.702 x) = x / (1 + 2^(-1.702 log2(e) x))   (custom_clip_model.py:52-54)
-    return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -2.4554669595930157f));
-}
-
-// Two QuickGELUs with the multiplies and the add on packed-fp32 VALU (v_pk_mul_f32 /
-// v_pk_add_f32); the same operations in the same order as quick_gelu, so bit-identical.
+typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
 typedef float f32x2v __attribute__((ext_vector_type(2)));
+
+// one v_cvt_pk_f16_f32 (RNE) per pair
+__device__ __forceinline__ uint32_t cvt_pk_f16(float a, float b) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2v{a, b}, f16x2v));
+}
+
+// Two QuickGELUs, x * sigmoid(1.702 x) = x / (1 + 2^(-1.702 log2(e) x))
+// (custom_clip_model.py:52-54), with the multiplies and the add on packed-fp32 VALU.
 __device__ __forceinline__ f32x2v quick_gelu2(f32x2v x) {
     const f32x2v y = x * -2.4554669595930157f;
     const f32x2v d = f32x2v{__builtin_amdgcn_exp2f(y.x), __builtin_amdgcn_exp2f(y.y)} + 1.0f;
     return x * f32x2v{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
 }
 
-// One 16x16x32 MFMA on 16-byte fragments holding bf16 or (F16) fp16 values.
-template <bool F16>
-__device__ __forceinline__ f32x4 mfma16(const bf16x8& w, const bf16x8& a, const f32x4& c) {
-    if constexpr (F16)
-        return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, w), __builtin_bit_cast(f16x8, a), c, 0,
-                                                      0, 0);
-    else
-        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, a, c, 0, 0, 0);
+__device__ __forceinline__ f32x4 mfma16(const f16x8& w, const f16x8& a, const f32x4& c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(w, a, c, 0, 0, 0);
 }
 
 // LayerNorm fold (see gemm.h EpiArgs) with the bias: acc <- rstd_m * acc + (-mean_m rstd_m
@@ -122,10 +98,10 @@ __device__ __forceinline__ void ln_fold(f32x4 (&acc)[NI][4], const float2* __res
 // Epilogue of one wave's output block: NI row groups x 4 column groups of 16x16, lane
 // holding C[m][nb..nb+3] with m = mrow + i*16 + (lane&15), nb = ncol + j*16 + (lane>>4)*4
 // (see gemm.h for the modes).  All loads are hoisted ahead of the stores they feed: bias
-// once per tile, residual / pos-embed rows in batches of NB row groups — otherwise the
+// once per tile, residual rows all at once, pos-embed rows in batches — otherwise the
 // compiler (which cannot prove `out` does not alias `bias`/`pos`) serialises one memory
 // round trip per fragment.
-template <int EPI, int NI, bool BIAS_DONE = false, int RNB = 2>
+template <int EPI, int NI, bool BIAS_DONE = false>
 __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI][4], int64_t mrow, int ncol,
                                               int64_t M, int N) {
     const int lane = threadIdx.x & 63;
@@ -145,7 +121,7 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
             }
     }
     if constexpr (EPI == EPI_RESID_F16) {
-        // Pair the fp32 accumulators first (v_permlane16_swap, see the bf16 path below; swap
+        // Pair the fp32 accumulators first (v_permlane16_swap, see the fp16 path below; swap
         // whole uint4 images — per-element f32x4 read-modify-write around the builtin was
         // mis-lowered by hipcc 7.2, duplicating element 0 into elements 1..3):
         // afterwards lane group q holds columns colp(jp) .. +7 of its row in acc[i][2jp]
@@ -166,10 +142,9 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
             }
         _Float16* xo = (_Float16*)ea.out;
         auto colp = [&](int jp) { return ncol + (2 * jp + (q & 1)) * 16 + (q >> 1) * 8; };
-        // row groups per batch (2*NB 16-byte loads in flight per lane).  The persistent tiles
-        // load the whole residual block at once (RNB = 8: +6 % on out_proj at K = 768, where
-        // the epilogue's HBM round trips are not amortised; v8 / v9 keep 2 / 4 for A/B).
-        constexpr int NB = RNB < NI ? RNB : NI;
+        // the whole residual block is loaded before the first store (NI row groups, 2*NI
+        // 16-byte loads in flight per lane: +6 % on out_proj at K = 768 over batches of 2)
+        constexpr int NB = NI;
         auto store_batch = [&](int i0) {
 #pragma unroll
             for (int ii = 0; ii < NB; ii++) {
@@ -234,7 +209,7 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
         store_batch(NI - NB);
         return;
     }
-    if constexpr (EPI == EPI_RESID_F32 || EPI == EPI_PATCH) {
+    if constexpr (EPI == EPI_PATCH) {
         // software-pipelined: the loads of batch n+1 are issued before the stores of batch n,
         // so no wait ever covers a store (vmcnt retires in issue order).
         constexpr int NB = 2;  // row groups per batch: 8 float4 loads in flight per lane
@@ -243,29 +218,20 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
             return m < M ? m : M - 1;  // clamped rows are loaded but not stored
         };
         auto src_row = [&](int64_t m) -> const float* {
-            if constexpr (EPI == EPI_RESID_F32) return (const float*)ea.out + m * ea.ldc + ncol + cq;
-            else return ea.pos + (1 + (uint32_t)m % (uint32_t)ea.npatch) * (int64_t)N + ncol + cq;
+            return ea.pos + (1 + (uint32_t)m % (uint32_t)ea.npatch) * (int64_t)N + ncol + cq;
         };
         auto store_batch = [&](int i0) {
 #pragma unroll
             for (int ii = 0; ii < NB; ii++) {
                 const int64_t m = mrow + (i0 + ii) * 16 + (lane & 15);
                 if (m >= M) continue;
-                if constexpr (EPI == EPI_RESID_F32) {
-                    float* d = (float*)ea.out + m * ea.ldc + ncol + cq;
+                // patch rows of the fp16 residual stream
+                const uint32_t img = (uint32_t)m / (uint32_t)ea.npatch, p = (uint32_t)m - img * (uint32_t)ea.npatch;
+                _Float16* d = (_Float16*)ea.out + ((int64_t)img * ea.seq + 1 + p) * ea.ldc + ncol + cq;
 #pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        const f32x4 v = acc[i0 + ii][j];
-                        *(float4*)(d + j * 16) = make_float4(v[0], v[1], v[2], v[3]);
-                    }
-                } else {  // patch rows of the fp16 residual stream
-                    const uint32_t img = (uint32_t)m / (uint32_t)ea.npatch, p = (uint32_t)m - img * (uint32_t)ea.npatch;
-                    _Float16* d = (_Float16*)ea.out + ((int64_t)img * ea.seq + 1 + p) * ea.ldc + ncol + cq;
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        const f32x4 v = acc[i0 + ii][j];
-                        *(f16x4*)(d + j * 16) = f16x4{(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
-                    }
+                for (int j = 0; j < 4; j++) {
+                    const f32x4 v = acc[i0 + ii][j];
+                    *(f16x4*)(d + j * 16) = f16x4{(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
                 }
             }
         };
@@ -305,7 +271,7 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
         }
         return;
     }
-    // bf16 outputs.  v^T tiles of the head split keep the scattered 2-byte stores.
+    // fp16 outputs.  v^T tiles of the head split keep the scattered 2-byte stores.
     // Head split: the wave's 64 columns lie inside one of q / k / v (wd is a multiple of 64),
     // so the q/k/v selector and the column's offset inside it are wave-uniform; the token
     // index (b, t) of a row comes from one 32-bit division per row group (M < 2^31, checked
@@ -324,16 +290,16 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
                 const int64_t m = mrow + i * 16 + (lane & 15);
                 if (m >= M) continue;
                 const uint32_t b = (uint32_t)m / seq, t = (uint32_t)m - b * seq;
-                __bf16* vb = (__bf16*)ea.vt + (int64_t)b * ea.heads * 64 * lp + t;
+                _Float16* vb = (_Float16*)ea.vt + (int64_t)b * ea.heads * 64 * lp + t;
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     const f32x4 v = acc[i][j];
                     const int hd = qkv_c0 + j * 16 + cq;  // h * 64 + d
-                    __bf16* dst = vb + (int64_t)hd * lp;
-                    dst[0] = (__bf16)v[0];
-                    dst[lp] = (__bf16)v[1];
-                    dst[2 * lp] = (__bf16)v[2];
-                    dst[3 * lp] = (__bf16)v[3];
+                    _Float16* dst = vb + (int64_t)hd * lp;
+                    dst[0] = (_Float16)v[0];
+                    dst[lp] = (_Float16)v[1];
+                    dst[2 * lp] = (_Float16)v[2];
+                    dst[3 * lp] = (_Float16)v[3];
                 }
             }
             return;
@@ -347,16 +313,16 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
 #pragma unroll
     for (int i = 0; i < NI; i++) {
         const int64_t m = mrow + i * 16 + (lane & 15);
-        [[maybe_unused]] __bf16* qkrow = nullptr;  // QKV: q / k row (b, h = 0, t)
+        [[maybe_unused]] _Float16* qkrow = nullptr;  // QKV: q / k row (b, h = 0, t)
         if constexpr (EPI == EPI_QKV) {
             const uint32_t seq = (uint32_t)ea.seq;
             const uint32_t b = (uint32_t)m / seq, t = (uint32_t)m - b * seq;
-            qkrow = (__bf16*)(qkv_sel == 0 ? ea.q : ea.k) + ((int64_t)b * ea.heads * ea.seq + t) * 64;
+            qkrow = (_Float16*)(qkv_sel == 0 ? ea.q : ea.k) + ((int64_t)b * ea.heads * ea.seq + t) * 64;
         }
 #pragma unroll
         for (int jp = 0; jp < 2; jp++) {
             f32x4 a = acc[i][2 * jp], c = acc[i][2 * jp + 1];
-            if constexpr (EPI == EPI_GELU_BF16) {
+            if constexpr (EPI == EPI_GELU_H16) {
 #pragma unroll
                 for (int e = 0; e < 4; e += 2) {
                     const f32x2v ga = quick_gelu2(f32x2v{a[e], a[e + 1]});
@@ -367,8 +333,8 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
                     c[e + 1] = gc.y;
                 }
             }
-            const auto lo = __builtin_amdgcn_permlane16_swap(cvt_pk_bf16(a[0], a[1]), cvt_pk_bf16(c[0], c[1]), false, false);
-            const auto hi = __builtin_amdgcn_permlane16_swap(cvt_pk_bf16(a[2], a[3]), cvt_pk_bf16(c[2], c[3]), false, false);
+            const auto lo = __builtin_amdgcn_permlane16_swap(cvt_pk_f16(a[0], a[1]), cvt_pk_f16(c[0], c[1]), false, false);
+            const auto hi = __builtin_amdgcn_permlane16_swap(cvt_pk_f16(a[2], a[3]), cvt_pk_f16(c[2], c[3]), false, false);
             const uint4 v = make_uint4(lo[0], hi[0], lo[1], hi[1]);
             const int col = ncol + (2 * jp + (q & 1)) * 16 + (q >> 1) * 8;
             if (m >= M) continue;
@@ -376,17 +342,17 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
                 const int hd = qkv_c0 + (col - ncol);  // h * 64 + d
                 *(uint4*)(qkrow + (int64_t)(hd >> 6) * ea.seq * 64 + (hd & 63)) = v;
             } else {
-                *(uint4*)((__bf16*)ea.out + m * ea.ldc + col) = v;
+                *(uint4*)((_Float16*)ea.out + m * ea.ldc + col) = v;
             }
         }
     }
 }
 
-template <int EPI, bool F16>
-__global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(const __bf16* __restrict__ A, int64_t lda,
-                                                           const __bf16* __restrict__ W, int64_t ldw, int64_t M,
+template <int EPI>
+__global__ __launch_bounds__(256, 2) void gemm_tile_kernel(const _Float16* __restrict__ A, int64_t lda,
+                                                           const _Float16* __restrict__ W, int64_t ldw, int64_t M,
                                                            int N, int K, EpiArgs ea, int tiles_n, int nwg) {
-    __shared__ __attribute__((aligned(16))) __bf16 smem[2][2][GB_M * GB_K];
+    __shared__ __attribute__((aligned(16))) _Float16 smem[2][2][GB_M * GB_K];
     const int bid = blockIdx.x;
     const int xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
     const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
@@ -397,8 +363,8 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(const __bf16* __restr
     const int wm = wid >> 1, wn = wid & 1;
 
     // per-thread staging slots: 4 x 16 B of A and of W per K-step
-    const __bf16* gA[4];
-    const __bf16* gW[4];
+    const _Float16* gA[4];
+    const _Float16* gW[4];
     int soff[4];
     bool aval[4];
 #pragma unroll
@@ -446,439 +412,114 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(const __bf16* __restr
     for (int kt = 0; kt < nk; ++kt) {
         const int cur = kt & 1;
         if (kt + 1 < nk) GLOAD((kt + 1) * GB_K);
-        const __bf16* sA = smem[cur][0];
-        const __bf16* sW = smem[cur][1];
+        const _Float16* sA = smem[cur][0];
+        const _Float16* sW = smem[cur][1];
 #pragma unroll
         for (int ks = 0; ks < 2; ks++) {
-            bf16x8 af[4], wf[4];
+            f16x8 af[4], wf[4];
             const int kc = ks * 4 + (lane >> 4);
 #pragma unroll
-            for (int i = 0; i < 4; i++) af[i] = *(const bf16x8*)(sA + swz(wm * 64 + i * 16 + (lane & 15), kc));
+            for (int i = 0; i < 4; i++) af[i] = *(const f16x8*)(sA + swz(wm * 64 + i * 16 + (lane & 15), kc));
 #pragma unroll
-            for (int j = 0; j < 4; j++) wf[j] = *(const bf16x8*)(sW + swz(wn * 64 + j * 16 + (lane & 15), kc));
+            for (int j = 0; j < 4; j++) wf[j] = *(const f16x8*)(sW + swz(wn * 64 + j * 16 + (lane & 15), kc));
 #pragma unroll
             for (int i = 0; i < 4; i++)
 #pragma unroll
                 for (int j = 0; j < 4; j++)
-                    acc[i][j] = mfma16<F16>(wf[j], af[i], acc[i][j]);
+                    acc[i][j] = mfma16(wf[j], af[i], acc[i][j]);
         }
         if (kt + 1 < nk) LSTORE(cur ^ 1);
         __syncthreads();
     }
 
     // ------------------------------------------------------------------ epilogue
-    if constexpr (F16) {
-        if (ea.rowstat) {
-            float4 bn[4];
-            const int cq = (lane >> 4) * 4;
+    if (ea.rowstat) {
+        float4 bn[4];
+        const int cq = (lane >> 4) * 4;
 #pragma unroll
-            for (int j = 0; j < 4; j++)
-                bn[j] = ea.bias ? *(const float4*)(ea.bias + n0 + wn * 64 + j * 16 + cq) : make_float4(0.f, 0.f, 0.f, 0.f);
-            ln_fold<4>(acc, ea.rowstat, ea.colsum, bn, m0 + wm * 64, n0 + wn * 64, M);
-            epilogue_tile<EPI, 4, true>(ea, acc, m0 + wm * 64, n0 + wn * 64, M, N);
-            return;
-        }
+        for (int j = 0; j < 4; j++)
+            bn[j] = ea.bias ? *(const float4*)(ea.bias + n0 + wn * 64 + j * 16 + cq) : make_float4(0.f, 0.f, 0.f, 0.f);
+        ln_fold<4>(acc, ea.rowstat, ea.colsum, bn, m0 + wm * 64, n0 + wn * 64, M);
+        epilogue_tile<EPI, 4, true>(ea, acc, m0 + wm * 64, n0 + wn * 64, M, N);
+        return;
     }
     epilogue_tile<EPI, 4>(ea, acc, m0 + wm * 64, n0 + wn * 64, M, N);
 #undef GLOAD
 #undef LSTORE
 }
 
-
-// ===================================================================== v2 tile
-// 256x256x64 block tile, 512 threads = 8 waves as 2 (M) x 4 (N), 128x64 per wave
-// (8x4 tiles of 16x16x32): half the LDS bytes per FLOP of the 64x64-per-wave v1 tile.
-// Operands go HBM -> LDS by global_load_lds_dwordx4 (no VGPR staging): one wave-instruction
-// fills 1 KiB = 8 LDS rows of 128 B, lane l -> row 8j + l/8, physical 16-B chunk l%8.  The
-// (row>>1)&7 XOR swizzle is applied on the per-lane SOURCE address (logical chunk
-// kc = physical ^ swz(row)), and the same XOR on the ds_read side, so LDS stays lane-linear
-// and fragment reads stay conflict-free.  Two LDS stages (2 x 64 KiB): tile t+1 streams in
-// while tile t is multiplied; one vmcnt(0) + barrier per K-step.  All LDS is one dynamic
-// array (a second __shared__ object makes hipcc drain vmcnt before every ds_read).
+// ================================================================ persistent tile
+// 256x256x64 block tile, 512 threads = 8 waves as 2 (M) x 4 (N), 128x64 per wave (8x4 tiles
+// of 16x16x32): half the LDS bytes per FLOP of the 64x64-per-wave 128x128 tile.  Operands go
+// HBM -> LDS by global_load_lds_dwordx4 (no VGPR staging): one wave-instruction fills 1 KiB =
+// 8 LDS rows of 128 B, lane l -> row 8j + l/8, physical 16-B chunk l%8.  The (row>>1)&7 XOR
+// swizzle is applied on the per-lane SOURCE address (logical chunk kc = physical ^ swz(row)),
+// and the same XOR on the ds_read side, so LDS stays lane-linear and fragment reads stay
+// conflict-free.  All LDS is one dynamic array (a second __shared__ object makes hipcc drain
+// vmcnt before every ds_read).
 constexpr int G2_M = 256, G2_N = 256;
-constexpr int G2_STAGE = (G2_M + G2_N) * GB_K;  // bf16 elements per stage
+constexpr int G2_STAGE = (G2_M + G2_N) * GB_K;  // fp16 elements per stage
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-template <int EPI>
-__global__ __launch_bounds__(512, 2) void gemm2_bf16_kernel(const __bf16* __restrict__ A, int64_t lda,
-                                                            const __bf16* __restrict__ W, int64_t ldw, int64_t M,
-                                                            int N, int K, EpiArgs ea, int tiles_n, int nwg) {
-    extern __shared__ __attribute__((aligned(16))) __bf16 lds2[];
-    const int bid = blockIdx.x;
-    const int xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
-    const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
-    const int tm = wg / tiles_n, tn = wg % tiles_n;
-    const int64_t m0 = (int64_t)tm * G2_M;
-    const int n0 = tn * G2_N;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wid >> 2, wn = wid & 3;
-
-    // glds sources: wave wid fills 1-KiB pieces j = 4*wid + u (u < 4) of A and of W
-    const __bf16* srcA[4];
-    const __bf16* srcW[4];
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-        const int j = wid * 4 + u;
-        const int r = 8 * j + (lane >> 3);
-        const int kc = (lane & 7) ^ ((r >> 1) & 7);
-        int64_t gm = m0 + r;
-        gm = gm < M ? gm : M - 1;  // rows past M read a valid row; their outputs are dropped
-        srcA[u] = A + gm * lda + kc * 8;
-        srcW[u] = W + (int64_t)(n0 + r) * ldw + kc * 8;
-    }
-#define G2_ISSUE(stage, k0)                                                                              \
-    do {                                                                                                 \
-        __bf16* base_ = lds2 + (stage) * G2_STAGE;                                                       \
-        _Pragma("unroll") for (int u = 0; u < 4; u++) {                                                  \
-            const int j = wid * 4 + u;                                                                   \
-            __builtin_amdgcn_global_load_lds(srcA[u] + (k0), (lds_ptr_t)(base_ + j * 512), 16, 0, 0);    \
-            __builtin_amdgcn_global_load_lds(srcW[u] + (k0), (lds_ptr_t)(base_ + G2_M * GB_K + j * 512), \
-                                             16, 0, 0);                                                  \
-        }                                                                                                \
-    } while (0)
-
-    f32x4 acc[8][4];
-#pragma unroll
-    for (int i = 0; i < 8; i++)
-#pragma unroll
-        for (int j = 0; j < 4; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    G2_ISSUE(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    const int nk = K / GB_K;
-    for (int kt = 0; kt < nk; ++kt) {
-        const int cur = kt & 1;
-        if (kt + 1 < nk) G2_ISSUE(cur ^ 1, (kt + 1) * GB_K);
-        const __bf16* sA = lds2 + cur * G2_STAGE;
-        const __bf16* sW = sA + G2_M * GB_K;
-#pragma unroll
-        for (int ks = 0; ks < 2; ks++) {
-            const int kc = ks * 4 + (lane >> 4);
-            bf16x8 wf[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++) wf[j] = *(const bf16x8*)(sW + swz(wn * 64 + j * 16 + (lane & 15), kc));
-            bf16x8 af[8];
-#pragma unroll
-            for (int i = 0; i < 8; i++) af[i] = *(const bf16x8*)(sA + swz(wm * 128 + i * 16 + (lane & 15), kc));
-            __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-            for (int i = 0; i < 8; i++)
-#pragma unroll
-                for (int j = 0; j < 4; j++)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af[i], acc[i][j], 0, 0, 0);
-            __builtin_amdgcn_s_setprio(0);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-    }
-#undef G2_ISSUE
-    epilogue_tile<EPI, 8>(ea, acc, m0 + wm * 128, n0 + wn * 64, M, N);
-}
-
-
-// ===================================================================== v3 tile
-// v2's 256x256x64 tile and LDS-DMA staging, made persistent and software-pipelined:
-//  * grid = min(#tiles, 256) workgroups (one per CU); each XCD group (bid % 8) walks a
-//    contiguous range of tiles (consecutive tiles share the A row panel in that XCD's L2);
-//  * during the last K-step of a tile the first K-step of the workgroup's next tile is
-//    already streaming into the free LDS stage, so a tile's prologue latency is hidden;
-//  * inside a K-step the fragments of k-step 1 are read while the MFMAs of k-step 0 run.
-// Same MFMA sequence per output element as v1/v2 -> bit-identical results.
-template <int EPI>
-__global__ __launch_bounds__(512, 2) void gemm3_bf16_kernel(const __bf16* __restrict__ A, int64_t lda,
-                                                            const __bf16* __restrict__ W, int64_t ldw, int64_t M,
-                                                            int N, int K, EpiArgs ea, int tiles_n, int ntiles) {
-    extern __shared__ __attribute__((aligned(16))) __bf16 lds3[];
-    const int G = gridDim.x;
-    const int bid = blockIdx.x;
-    // XCD group x = bid % ng owns tiles [lo_x, hi_x); its members j = bid / ng stride by its size
-    const int ng = G < 8 ? G : 8;
-    const int x = bid % ng, gx = G / ng + ((G % ng) > x ? 1 : 0);
-    const int j = bid / ng;
-    const int lo = (int)((int64_t)ntiles * x / ng), hi = (int)((int64_t)ntiles * (x + 1) / ng);
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wid >> 2, wn = wid & 3;
-    const int nk = K / GB_K;
-
-    // glds piece jj = 4*wid + u covers LDS rows 8jj..8jj+7; lane -> row 8jj + lane/8
-    const int lrow = lane >> 3, lchunk = lane & 7;
-    auto issue = [&](int tile, int k0, int stage) {
-        const int64_t m0 = (int64_t)(tile / tiles_n) * G2_M;
-        const int n0 = (tile % tiles_n) * G2_N;
-        __bf16* base = lds3 + stage * G2_STAGE;
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int jj = wid * 4 + u;
-            const int r = 8 * jj + lrow;
-            const int kc = (lchunk ^ ((r >> 1) & 7)) * 8;
-            int64_t gm = m0 + r;
-            gm = gm < M ? gm : M - 1;
-            __builtin_amdgcn_global_load_lds(A + gm * lda + k0 + kc, (lds_ptr_t)(base + jj * 512), 16, 0, 0);
-            __builtin_amdgcn_global_load_lds(W + (int64_t)(n0 + r) * ldw + k0 + kc,
-                                             (lds_ptr_t)(base + G2_M * GB_K + jj * 512), 16, 0, 0);
-        }
-    };
-
-    int tile = lo + j;
-    if (tile >= hi) return;
-    int stage = 0;
-    issue(tile, 0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (; tile < hi; tile += gx) {
-        const int next = tile + gx;
-        f32x4 acc[8][4];
-#pragma unroll
-        for (int i = 0; i < 8; i++)
-#pragma unroll
-            for (int jn = 0; jn < 4; jn++) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
-        for (int kt = 0; kt < nk; ++kt) {
-            if (kt + 1 < nk) issue(tile, (kt + 1) * GB_K, stage ^ 1);
-            else if (next < hi) issue(next, 0, stage ^ 1);
-            const __bf16* sA = lds3 + stage * G2_STAGE;
-            const __bf16* sW = sA + G2_M * GB_K;
-            const int kc0 = lane >> 4, kc1 = 4 + (lane >> 4);
-            bf16x8 wf0[4], wf1[4], a0[8], a1[8];
-#pragma unroll
-            for (int jn = 0; jn < 4; jn++) wf0[jn] = *(const bf16x8*)(sW + swz(wn * 64 + jn * 16 + (lane & 15), kc0));
-#pragma unroll
-            for (int i = 0; i < 8; i++) a0[i] = *(const bf16x8*)(sA + swz(wm * 128 + i * 16 + (lane & 15), kc0));
-#pragma unroll
-            for (int jn = 0; jn < 4; jn++) wf1[jn] = *(const bf16x8*)(sW + swz(wn * 64 + jn * 16 + (lane & 15), kc1));
-            __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-            for (int i = 0; i < 8; i++) {
-                // k-step 1 fragment of row block i streams in behind k-step 0's MFMAs
-                a1[i] = *(const bf16x8*)(sA + swz(wm * 128 + i * 16 + (lane & 15), kc1));
-#pragma unroll
-                for (int jn = 0; jn < 4; jn++)
-                    acc[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf0[jn], a0[i], acc[i][jn], 0, 0, 0);
-            }
-#pragma unroll
-            for (int i = 0; i < 8; i++)
-#pragma unroll
-                for (int jn = 0; jn < 4; jn++)
-                    acc[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf1[jn], a1[i], acc[i][jn], 0, 0, 0);
-            __builtin_amdgcn_s_setprio(0);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            stage ^= 1;
-        }
-        const int64_t m0 = (int64_t)(tile / tiles_n) * G2_M;
-        const int n0 = (tile % tiles_n) * G2_N;
-        epilogue_tile<EPI, 8>(ea, acc, m0 + wm * 128, n0 + wn * 64, M, N);
-    }
-}
-
-
-// ===================================================================== v4 tile
-// 256x256x64, 8 waves, LDS-DMA staging as v2, with a ping-pong section schedule: every
-// K-tile is 4 LOAD sections (ds_read fragments of one 64x32 output quadrant, issue a share
-// of the next K-tile's LDS-DMA, lgkmcnt(0)) interleaved with 4 COMPUTE sections (16
-// register-only MFMAs), one workgroup barrier after each section.  Waves 4-7 start one
-// barrier late, so on each SIMD (waves w and w+4) one wave's LOAD runs beside the other's
-// COMPUTE.  Quadrant order (0,0),(0,1),(1,1),(1,0) reuses A or B fragments between
-// sections (12+4+8+4 reads per K-tile).  Hazards (slot = barrier interval, group B = one
-// slot behind): next-tile DMA is issued in LOAD 0/1 of tile t into the buffer last read in
-// LOAD 3 of tile t-1 (retired by lgkmcnt(0) before its barrier); every wave drains its DMA
-// with vmcnt(0) at the end of LOAD 3, a barrier before any wave's LOAD 0 of tile t+1.
-// Same MFMA sequence per output element as v1-v3 -> bit-identical results.
-template <int EPI>
-__global__ __launch_bounds__(512, 2) void gemm4_bf16_kernel(const __bf16* __restrict__ A, int64_t lda,
-                                                            const __bf16* __restrict__ W, int64_t ldw, int64_t M,
-                                                            int N, int K, EpiArgs ea, int tiles_n, int nwg) {
-    extern __shared__ __attribute__((aligned(16))) __bf16 lds4[];
-    const int bid = blockIdx.x;
-    const int xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
-    const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
-    const int tm = wg / tiles_n, tn = wg % tiles_n;
-    const int64_t m0 = (int64_t)tm * G2_M;
-    const int n0 = tn * G2_N;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wr = wid >> 2, wc = wid & 3;
-
-    // Region DMA: each operand stage is 4 regions of 128 LDS rows (16 pieces of 8 rows):
-    //   A0 = rows {0..63, 128..191} (quadrant qm=0 of both wave rows), A1 = the other 128;
-    //   B0 = W rows {wc*64 + 0..31}, B1 = W rows {wc*64 + 32..63}.
-    // Wave w moves pieces 2w, 2w+1 of a region.  Piece p of region (half h) covers rows
-    // A: 128*(p>>3) + 64*h + 8*(p&7) + lane/8;  B: 64*(p>>2) + 32*h + 8*(p&3) + lane/8.
-    const __bf16* srcA[2][2];
-    const __bf16* srcW[2][2];
-    int offA[2][2], offW[2][2];
-#pragma unroll
-    for (int h = 0; h < 2; h++)
-#pragma unroll
-        for (int u = 0; u < 2; u++) {
-            const int pc = 2 * wid + u;
-            const int ra = 128 * (pc >> 3) + 64 * h + 8 * (pc & 7);
-            const int rb = 64 * (pc >> 2) + 32 * h + 8 * (pc & 3);
-            const int r1 = ra + (lane >> 3), r2 = rb + (lane >> 3);
-            int64_t gm = m0 + r1;
-            gm = gm < M ? gm : M - 1;
-            srcA[h][u] = A + gm * lda + ((lane & 7) ^ ((r1 >> 1) & 7)) * 8;
-            srcW[h][u] = W + (int64_t)(n0 + r2) * ldw + ((lane & 7) ^ ((r2 >> 1) & 7)) * 8;
-            offA[h][u] = ra * GB_K;
-            offW[h][u] = G2_M * GB_K + rb * GB_K;
-        }
-#define G4_ISSUE_A(stage, h, k0)                                                                             \
-    _Pragma("unroll") for (int u = 0; u < 2; u++) __builtin_amdgcn_global_load_lds(                          \
-        srcA[h][u] + (k0), (lds_ptr_t)(lds4 + (stage) * G2_STAGE + offA[h][u]), 16, 0, 0)
-#define G4_ISSUE_W(stage, h, k0)                                                                             \
-    _Pragma("unroll") for (int u = 0; u < 2; u++) __builtin_amdgcn_global_load_lds(                          \
-        srcW[h][u] + (k0), (lds_ptr_t)(lds4 + (stage) * G2_STAGE + offW[h][u]), 16, 0, 0)
-#define G4_BARRIER()                              \
-    do {                                          \
-        __builtin_amdgcn_sched_barrier(0);        \
-        __builtin_amdgcn_s_barrier();             \
-        __builtin_amdgcn_sched_barrier(0);        \
-    } while (0)
-#define G4_LDS_DONE() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
-
-    bf16x8 fa[4][2], fb[2][2];
-    f32x4 acc[8][4];
-#pragma unroll
-    for (int i = 0; i < 8; i++)
-#pragma unroll
-        for (int j = 0; j < 4; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    auto load_a = [&](const __bf16* sA, int qm) {
-#pragma unroll
-        for (int i = 0; i < 4; i++)
-#pragma unroll
-            for (int ks = 0; ks < 2; ks++)
-                fa[i][ks] = *(const bf16x8*)(sA + swz(wr * 128 + qm * 64 + i * 16 + (lane & 15), ks * 4 + (lane >> 4)));
-    };
-    auto load_b = [&](const __bf16* sW, int qn) {
-#pragma unroll
-        for (int j = 0; j < 2; j++)
-#pragma unroll
-            for (int ks = 0; ks < 2; ks++)
-                fb[j][ks] = *(const bf16x8*)(sW + swz(wc * 64 + qn * 32 + j * 16 + (lane & 15), ks * 4 + (lane >> 4)));
-    };
-    auto compute = [&](int qm, int qn) {
-#pragma unroll
-        for (int ks = 0; ks < 2; ks++)
-#pragma unroll
-            for (int i = 0; i < 4; i++)
-#pragma unroll
-                for (int j = 0; j < 2; j++)
-                    acc[qm * 4 + i][qn * 2 + j] = mfma16<false>(fb[j][ks], fa[i][ks], acc[qm * 4 + i][qn * 2 + j]);
-    };
-
-    const int nk = K / GB_K;
-    // prologue: tile 0 whole, tile 1 without B0 (B0 of tile t+1 goes out in LOAD 0 of tile t)
-    G4_ISSUE_A(0, 0, 0);
-    G4_ISSUE_A(0, 1, 0);
-    G4_ISSUE_W(0, 0, 0);
-    G4_ISSUE_W(0, 1, 0);
-    if (nk > 1) {
-        G4_ISSUE_A(1, 0, GB_K);
-        G4_ISSUE_W(1, 1, GB_K);
-        G4_ISSUE_A(1, 1, GB_K);
-        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    if (wr == 1) G4_BARRIER();
-    // K-tile t reads stage t&1; region R of stage t&1 is refilled with tile t+2 right after
-    // its last read (LOAD 0: A0, B0; LOAD 1: B1; LOAD 2: A1; LOAD 3: B0 again):
-    //   LOAD 0 issues B0(t+1)  [stage t+1's B0 last read in LOAD 3 of tile t-1]
-    //   LOAD 1 issues A0(t+2), LOAD 2 issues B1(t+2), LOAD 3 issues A1(t+2)
-    // At the end of LOAD 3 everything of tile t+1 must have landed: only the 3 regions of
-    // tile t+2 (6 pieces per wave) may still be in flight -> vmcnt(6).
-    auto kstep = [&](int kt, auto n1_tag, auto n2_tag) {
-        constexpr bool N1 = decltype(n1_tag)::value;  // tile kt+1 exists
-        constexpr bool N2 = decltype(n2_tag)::value;  // tile kt+2 exists
-        const int buf = kt & 1;
-        const __bf16* sA = lds4 + buf * G2_STAGE;
-        const __bf16* sW = sA + G2_M * GB_K;
-        // LOAD 0 / COMPUTE (0,0)
-        load_a(sA, 0);
-        load_b(sW, 0);
-        if constexpr (N1) { G4_ISSUE_W(buf ^ 1, 0, (kt + 1) * GB_K); }
-        G4_LDS_DONE();
-        G4_BARRIER();
-        compute(0, 0);
-        G4_BARRIER();
-        // LOAD 1 / COMPUTE (0,1)
-        load_b(sW, 1);
-        if constexpr (N2) { G4_ISSUE_A(buf, 0, (kt + 2) * GB_K); }
-        G4_LDS_DONE();
-        G4_BARRIER();
-        compute(0, 1);
-        G4_BARRIER();
-        // LOAD 2 / COMPUTE (1,1)
-        load_a(sA, 1);
-        if constexpr (N2) { G4_ISSUE_W(buf, 1, (kt + 2) * GB_K); }
-        G4_LDS_DONE();
-        G4_BARRIER();
-        compute(1, 1);
-        G4_BARRIER();
-        // LOAD 3 / COMPUTE (1,0)
-        load_b(sW, 0);
-        if constexpr (N2) { G4_ISSUE_A(buf, 1, (kt + 2) * GB_K); }
-        G4_LDS_DONE();
-        if constexpr (N2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-        else if constexpr (N1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        G4_BARRIER();
-        compute(1, 0);
-        G4_BARRIER();
-    };
-    using T_ = std::integral_constant<bool, true>;
-    using F_ = std::integral_constant<bool, false>;
-    int kt = 0;
-    for (; kt + 2 < nk; ++kt) kstep(kt, T_{}, T_{});
-    if (kt + 1 < nk) { kstep(kt, T_{}, F_{}); ++kt; }
-    kstep(kt, F_{}, F_{});
-    if (wr == 0) G4_BARRIER();
-#undef G4_ISSUE_A
-#undef G4_ISSUE_W
-#undef G4_BARRIER
-#undef G4_LDS_DONE
-    epilogue_tile<EPI, 8>(ea, acc, m0 + wr * 128, n0 + wc * 64, M, N);
-}
-
-// ===================================================================== v5 tile
-// v4's region-DMA ping-pong schedule made persistent (grid = min(#tiles, 256), tile walk
-// as v3).  The two DMA streams — "+1" (region B0 of the next K-step) and "+2" (A0, B1, A1
-// of the K-step after) — run over the workgroup's concatenated (tile, K-step) sequence, so
-// while a tile's epilogue runs, the next tile's first two K-steps are already landing.
-// The epilogue needs no barrier: group A runs it in the slot where group B computes the
-// tile's last quadrant.  Same MFMA sequence per output as v1-v4 -> bit-identical.
+// Schedule (per K-step of 64): 4 LOAD sections (ds_read of the fragments of one 64x32
+// output quadrant, issue a share of the DMA for a later K-step, lgkmcnt(0)) interleaved with
+// 4 COMPUTE sections (16 register-only MFMAs), one raw s_barrier after each section.  Waves
+// 4-7 run one barrier behind waves 0-3, so on every SIMD (waves w and w+4) one wave reads LDS
+// while the other multiplies.  Quadrant order (0,0),(0,1),(1,1),(1,0) reuses A or W
+// fragments between sections.  Region DMA: each operand stage is 4 regions of 128 LDS rows
+// (16 pieces of 8 rows): A0 = rows {0..63, 128..191} (quadrant 0 of both wave rows), A1 =
+// the other 128; B0 = W rows {wc*64 + 0..31}, B1 = W rows {wc*64 + 32..63}; wave w moves
+// pieces 2w, 2w+1 of a region.  A region is refilled for K-step s+2 right after its last read
+// in K-step s, so the only wait is one counted vmcnt(6) per K-step.
 //
-// DEFER (variant 6): the epilogue's stores are not waited for by the next tile's first
-// K-step.  vmcnt retires in issue order, so v5's first `vmcnt(6)` after an epilogue waits
-// for every store the epilogue issued (one HBM write round trip per tile, with the MFMAs
-// idle).  Here the next tile's first "+1" DMA (B0 of its K-step 1) is issued BEFORE the
-// epilogue, and that step's wait counts the epilogue's memory instructions as allowed to be
-// outstanding: vmcnt(6 + S (+1 bias DMA)), S = EpiVm<EPI>::count (checked against the ISA:
-// global_load/store_dwordx4 per wave and tile).  Only after a full tile (no masked rows,
-// so exactly S instructions were issued) and not for scattered-v^T QKV tiles; otherwise the
-// plain vmcnt(6).  The bias is read from LDS by inline ds_read (the compiler would insert a
-// vmcnt(0) before a ds_read of an LDS-DMA'd slot, draining the in-flight DMA every tile).
+// Persistent: grid = min(#tiles, 256) (one workgroup per CU).  The two DMA streams — "+1"
+// (region B0 of the next K-step) and "+2" (A0, B1, A1 of the K-step after) — run over the
+// workgroup's concatenated (tile, K-step) sequence, so while a tile's epilogue runs, the next
+// tile's first two K-steps are already landing.  The epilogue needs no barrier: group A runs
+// it in the slot where group B computes the tile's last quadrant.
+//
+// Tile walk (XCD-aware): workgroup b runs on XCD b % 8.  The XCDs are split into `ngroups`
+// groups; group k owns the N-tiles [k T_n / ngroups, (k+1) T_n / ngroups), and each XCD of
+// the group owns a contiguous range of that group's (M-tile, N-tile) sequence (M-major), its
+// 32 workgroups striding through it — so the tiles an XCD runs at once share A row panels in
+// its L2, and with ngroups > 1 the W panels an XCD re-reads shrink to its N share.
+//
+// Deferred epilogue stores: the epilogue's stores are not waited for by the next tile's first
+// K-step.  vmcnt retires in issue order, so a plain `vmcnt(6)` after an epilogue would wait
+// for every store the epilogue issued (one HBM write round trip per tile, MFMAs idle).  The
+// next tile's first "+1" DMA (B0 of its K-step 1) is issued BEFORE the epilogue, and that
+// step's wait counts the epilogue's memory instructions as allowed to be outstanding:
+// vmcnt(6 + S (+ the tile's bias / colsum / rowstat DMAs)), S = EpiVm<EPI>::count (global
+// load/store instructions per wave and full tile, counted from the ISA; with LayerNorm
+// partials the residual epilogue issues 8 more stores, so S is then a lower bound — safe,
+// as vmcnt retires in order).  Only after a full tile (no masked rows) and not for
+// scattered-v^T QKV tiles; otherwise the plain vmcnt(6).  The bias is read from LDS by
+// inline ds_read (the compiler would insert a vmcnt(0) before a ds_read of an LDS-DMA'd
+// slot, draining the in-flight DMA every tile).  All tilings run the same MFMA chain per
+// output element -> bit-identical results.
 template <int EPI>
 struct EpiVm {  // vector-memory instructions of one full-tile epilogue_tile<EPI, 8> per wave
-    static constexpr int count = EPI == EPI_BF16 || EPI == EPI_GELU_BF16 || EPI == EPI_QKV ? 16
+    static constexpr int count = EPI == EPI_H16 || EPI == EPI_GELU_H16 || EPI == EPI_QKV ? 16
                                  : EPI == EPI_RESID_F16 || EPI == EPI_F32                 ? 32
                                                                                           : -1;
 };
 
-template <int EPI, bool DEFER, bool F16, int RNB = 8>
-__global__ __launch_bounds__(512, 2) void gemm5_bf16_kernel(const __bf16* __restrict__ A, int64_t lda,
-                                                            const __bf16* __restrict__ W, int64_t ldw, int64_t M,
-                                                            int N, int K, EpiArgs ea, int tiles_n, int ntiles) {
-    extern __shared__ __attribute__((aligned(16))) __bf16 lds5[];
+template <int EPI>
+__global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16* __restrict__ A, int64_t lda,
+                                                                 const _Float16* __restrict__ W, int64_t ldw,
+                                                                 int64_t M, int N, int K, EpiArgs ea, int tiles_m,
+                                                                 int tiles_n, int ngroups) {
+    extern __shared__ __attribute__((aligned(16))) _Float16 lds[];
     const int G = gridDim.x;
     const int bid = blockIdx.x;
     const int ng = G < 8 ? G : 8;
     const int xg = bid % ng, gx = G / ng + ((G % ng) > xg ? 1 : 0);
-    const int lo = (int)((int64_t)ntiles * xg / ng), hi = (int)((int64_t)ntiles * (xg + 1) / ng);
+    const int ngr = (ng == 8 && 8 % ngroups == 0 && ngroups <= tiles_n) ? ngroups : 1;
+    const int xper = ng / ngr, grp = xg / xper, xs = xg - grp * xper;
+    const int nb0 = tiles_n * grp / ngr, tnk = tiles_n * (grp + 1) / ngr - nb0;  // this group's N-tiles
+    const int64_t sub = (int64_t)tiles_m * tnk;
+    const int lo = (int)(sub * xs / xper), hi = (int)(sub * (xs + 1) / xper);
     const int first = lo + bid / ng;
     if (first >= hi) return;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -886,7 +527,7 @@ __global__ __launch_bounds__(512, 2) void gemm5_bf16_kernel(const __bf16* __rest
     const int wr = wid >> 2, wc = wid & 3;
     const int nk = K / GB_K;
 
-    // per-lane DMA geometry (see v4): piece pc = 2*wid + u of region half h
+    // per-lane DMA geometry: piece pc = 2*wid + u of region half h
     int rowA[2][2], kcA[2][2], offA[2][2], offW[2][2];
     uint32_t offAb[2][2], offWb[2][2];  // byte offsets from the tile's (row 0, k0) element
 #pragma unroll
@@ -914,8 +555,8 @@ __global__ __launch_bounds__(512, 2) void gemm5_bf16_kernel(const __bf16* __rest
     auto set_tile = [&](Pos& p, int tile) {
         p.tile = tile;
         p.kt = 0;
-        p.m0 = (int64_t)(tile / tiles_n) * G2_M;
-        p.n0 = (tile % tiles_n) * G2_N;
+        p.m0 = (int64_t)(tile / tnk) * G2_M;
+        p.n0 = (nb0 + tile % tnk) * G2_N;
         p.full = p.m0 + G2_M <= M;
     };
     auto advance = [&](Pos& p) {
@@ -923,28 +564,28 @@ __global__ __launch_bounds__(512, 2) void gemm5_bf16_kernel(const __bf16* __rest
     };
     // uniform tile base + per-lane 32-bit element offset (SGPR base + VGPR offset form)
     auto issue_a = [&](int stage, int h, const Pos& p) {
-        const __bf16* base = A + p.m0 * lda + p.kt * GB_K;
+        const _Float16* base = A + p.m0 * lda + p.kt * GB_K;
         if (p.full) {
 #pragma unroll
             for (int u = 0; u < 2; u++)
                 __builtin_amdgcn_global_load_lds((const char*)base + offAb[h][u],
-                                                 (lds_ptr_t)(lds5 + stage * G2_STAGE + offA[h][u]), 16, 0, 0);
+                                                 (lds_ptr_t)(lds + stage * G2_STAGE + offA[h][u]), 16, 0, 0);
         } else {  // partial last row tile: rows >= M read row M-1 (never stored)
             const int lim = (int)(M - p.m0);
 #pragma unroll
             for (int u = 0; u < 2; u++) {
                 const int r = rowA[h][u] < lim ? rowA[h][u] : lim - 1;
                 __builtin_amdgcn_global_load_lds((const char*)base + (uint32_t)(r * (int)lda + kcA[h][u]) * 2u,
-                                                 (lds_ptr_t)(lds5 + stage * G2_STAGE + offA[h][u]), 16, 0, 0);
+                                                 (lds_ptr_t)(lds + stage * G2_STAGE + offA[h][u]), 16, 0, 0);
             }
         }
     };
     auto issue_w = [&](int stage, int h, const Pos& p) {
-        const __bf16* base = W + (int64_t)p.n0 * ldw + p.kt * GB_K;
+        const _Float16* base = W + (int64_t)p.n0 * ldw + p.kt * GB_K;
 #pragma unroll
         for (int u = 0; u < 2; u++)
             __builtin_amdgcn_global_load_lds((const char*)base + offWb[h][u],
-                                             (lds_ptr_t)(lds5 + stage * G2_STAGE + offW[h][u]), 16, 0, 0);
+                                             (lds_ptr_t)(lds + stage * G2_STAGE + offW[h][u]), 16, 0, 0);
     };
 #define G5_BARRIER()                              \
     do {                                          \
@@ -954,21 +595,21 @@ __global__ __launch_bounds__(512, 2) void gemm5_bf16_kernel(const __bf16* __rest
     } while (0)
 #define G5_LDS_DONE() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
 
-    bf16x8 fa[4][2], fb[2][2];
+    f16x8 fa[4][2], fb[2][2];
     f32x4 acc[8][4];
-    auto load_a = [&](const __bf16* sA, int qm) {
+    auto load_a = [&](const _Float16* sA, int qm) {
 #pragma unroll
         for (int i = 0; i < 4; i++)
 #pragma unroll
             for (int ks = 0; ks < 2; ks++)
-                fa[i][ks] = *(const bf16x8*)(sA + swz(wr * 128 + qm * 64 + i * 16 + (lane & 15), ks * 4 + (lane >> 4)));
+                fa[i][ks] = *(const f16x8*)(sA + swz(wr * 128 + qm * 64 + i * 16 + (lane & 15), ks * 4 + (lane >> 4)));
     };
-    auto load_b = [&](const __bf16* sW, int qn) {
+    auto load_b = [&](const _Float16* sW, int qn) {
 #pragma unroll
         for (int j = 0; j < 2; j++)
 #pragma unroll
             for (int ks = 0; ks < 2; ks++)
-                fb[j][ks] = *(const bf16x8*)(sW + swz(wc * 64 + qn * 32 + j * 16 + (lane & 15), ks * 4 + (lane >> 4)));
+                fb[j][ks] = *(const f16x8*)(sW + swz(wc * 64 + qn * 32 + j * 16 + (lane & 15), ks * 4 + (lane >> 4)));
     };
     auto compute = [&](int qm, int qn) {
 #pragma unroll
@@ -977,18 +618,18 @@ __global__ __launch_bounds__(512, 2) void gemm5_bf16_kernel(const __bf16* __rest
             for (int i = 0; i < 4; i++)
 #pragma unroll
                 for (int j = 0; j < 2; j++)
-                    acc[qm * 4 + i][qn * 2 + j] = mfma16<F16>(fb[j][ks], fa[i][ks], acc[qm * 4 + i][qn * 2 + j]);
+                    acc[qm * 4 + i][qn * 2 + j] = mfma16(fb[j][ks], fa[i][ks], acc[qm * 4 + i][qn * 2 + j]);
     };
 
     // Bias of the current tile: one LDS-DMA per wave at the tile's first K-step into the
     // wave's own 1 KB slot (lane l -> bias[n0 + 4l .. 4l+3]); issued before that step's
     // B0 DMA, so the step's vmcnt(6) retires it.  The epilogue reads it with ds_read.
     const bool has_bias = EPI != EPI_PATCH && ea.bias != nullptr;
-    float* bias_slot = (float*)(lds5 + 2 * G2_STAGE) + wid * 256;
-    // Folded LayerNorm (F16): colsum of the tile's 256 columns and (rstd, -mean rstd) of the
+    float* bias_slot = (float*)(lds + 2 * G2_STAGE) + wid * 256;
+    // Folded LayerNorm: colsum of the tile's 256 columns and (rstd, -mean rstd) of the
     // wave's 128 rows go to LDS by the same DMA at the tile's first K-step (the rowstat
     // buffer is padded to whole 256-row tiles, gemm.h).
-    const bool fold = F16 && ea.rowstat != nullptr;
+    const bool fold = ea.rowstat != nullptr;
     float* cs_slot = bias_slot + 8 * 256;
     float* rs_slot = bias_slot + 16 * 256;
     // streams: p1 = step s+1 (region B0), p2 = step s+2 (A0, B1, A1); requires nk >= 2
@@ -1012,7 +653,7 @@ __global__ __launch_bounds__(512, 2) void gemm5_bf16_kernel(const __bf16* __rest
     __syncthreads();
     if (wr == 1) G5_BARRIER();
     int buf = 0;
-    constexpr bool CAN_DEFER = DEFER && EpiVm<EPI>::count > 0;
+    constexpr bool CAN_DEFER = EpiVm<EPI>::count > 0;
     bool deferred = false;  // the previous tile's epilogue stores may still be in flight
     for (int tile = first; tile < hi; tile += gx) {
 #pragma unroll
@@ -1022,22 +663,20 @@ __global__ __launch_bounds__(512, 2) void gemm5_bf16_kernel(const __bf16* __rest
         for (int kt = 0; kt < nk; ++kt) {
             const bool has1 = p1.tile < hi, has2 = p2.tile < hi;
             const bool b0_early = CAN_DEFER && kt == 0 && tile != first;  // issued before the epilogue
-            const __bf16* sA = lds5 + buf * G2_STAGE;
-            const __bf16* sW = sA + G2_M * GB_K;
+            const _Float16* sA = lds + buf * G2_STAGE;
+            const _Float16* sW = sA + G2_M * GB_K;
             // LOAD 0 / COMPUTE (0,0)
             load_a(sA, 0);
             load_b(sW, 0);
             if (kt == 0 && has_bias)
-                __builtin_amdgcn_global_load_lds(ea.bias + (tile % tiles_n) * G2_N + lane * 4, (lds_ptr_t)bias_slot,
+                __builtin_amdgcn_global_load_lds(ea.bias + (nb0 + tile % tnk) * G2_N + lane * 4, (lds_ptr_t)bias_slot,
                                                  16, 0, 0);
-            if constexpr (F16) {
-                if (kt == 0 && fold) {
-                    __builtin_amdgcn_global_load_lds(ea.colsum + (tile % tiles_n) * G2_N + lane * 4,
-                                                     (lds_ptr_t)cs_slot, 16, 0, 0);
-                    __builtin_amdgcn_global_load_lds((const float*)(ea.rowstat + (int64_t)(tile / tiles_n) * G2_M +
-                                                                    wr * 128) + lane * 4,
-                                                     (lds_ptr_t)rs_slot, 16, 0, 0);
-                }
+            if (kt == 0 && fold) {
+                __builtin_amdgcn_global_load_lds(ea.colsum + (nb0 + tile % tnk) * G2_N + lane * 4, (lds_ptr_t)cs_slot,
+                                                 16, 0, 0);
+                __builtin_amdgcn_global_load_lds((const float*)(ea.rowstat + (int64_t)(tile / tnk) * G2_M + wr * 128) +
+                                                     lane * 4,
+                                                 (lds_ptr_t)rs_slot, 16, 0, 0);
             }
             if (has1 && !b0_early) issue_w(buf ^ 1, 0, p1);
             G5_LDS_DONE();
@@ -1089,8 +728,8 @@ __global__ __launch_bounds__(512, 2) void gemm5_bf16_kernel(const __bf16* __rest
             advance(p2);
             buf ^= 1;
         }
-        const int64_t m0 = (int64_t)(tile / tiles_n) * G2_M;
-        const int n0 = (tile % tiles_n) * G2_N;
+        const int64_t m0 = (int64_t)(tile / tnk) * G2_M;
+        const int n0 = (nb0 + tile % tnk) * G2_N;
         if constexpr (CAN_DEFER) {
             deferred = false;
             if (p1.tile < hi) {  // a next tile exists: issue its K-step 1 B0 (skipped in its LOAD 0)
@@ -1101,302 +740,8 @@ __global__ __launch_bounds__(512, 2) void gemm5_bf16_kernel(const __bf16* __rest
         }
         if (has_bias) {
             float4 b[4];
-            if constexpr (DEFER) {
-                // inline ds_read: no compiler-inserted vmcnt(0) for the LDS-DMA'd slot (retired
-                // by the tile's first K-step wait)
-                const float* bp = bias_slot + wc * 64 + (lane >> 4) * 4;
-                const uint32_t ba = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)bp;
-                asm volatile("ds_read_b128 %0, %1" : "=v"(b[0]) : "v"(ba) : "memory");
-                asm volatile("ds_read_b128 %0, %1 offset:64" : "=v"(b[1]) : "v"(ba) : "memory");
-                asm volatile("ds_read_b128 %0, %1 offset:128" : "=v"(b[2]) : "v"(ba) : "memory");
-                asm volatile("ds_read_b128 %0, %1 offset:192" : "=v"(b[3]) : "v"(ba) : "memory");
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            } else {
-#pragma unroll
-                for (int j = 0; j < 4; j++) b[j] = *(const float4*)(bias_slot + wc * 64 + j * 16 + (lane >> 4) * 4);
-            }
-            if constexpr (F16) {
-                // acc <- rstd * acc + (-mean rstd * s_n + b'_n); without a fold (rstd, s) = (1, 0):
-                // fma(1, acc, fma(0, 0, b)) == acc + b exactly.  One branch-free update (a
-                // branch on acc would duplicate the 128 accumulators).
-                float4 sn[4];
-                float2 rs[8];
-                if (fold) {
-                    if constexpr (DEFER) {
-                        const uint32_t ca = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)(
-                            cs_slot + wc * 64 + (lane >> 4) * 4);
-                        const uint32_t ra = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)(
-                            rs_slot + (lane & 15) * 2);
-                        asm volatile("ds_read_b128 %0, %1" : "=v"(sn[0]) : "v"(ca) : "memory");
-                        asm volatile("ds_read_b128 %0, %1 offset:64" : "=v"(sn[1]) : "v"(ca) : "memory");
-                        asm volatile("ds_read_b128 %0, %1 offset:128" : "=v"(sn[2]) : "v"(ca) : "memory");
-                        asm volatile("ds_read_b128 %0, %1 offset:192" : "=v"(sn[3]) : "v"(ca) : "memory");
-                        asm volatile("ds_read_b64 %0, %1" : "=v"(rs[0]) : "v"(ra) : "memory");
-                        asm volatile("ds_read_b64 %0, %1 offset:128" : "=v"(rs[1]) : "v"(ra) : "memory");
-                        asm volatile("ds_read_b64 %0, %1 offset:256" : "=v"(rs[2]) : "v"(ra) : "memory");
-                        asm volatile("ds_read_b64 %0, %1 offset:384" : "=v"(rs[3]) : "v"(ra) : "memory");
-                        asm volatile("ds_read_b64 %0, %1 offset:512" : "=v"(rs[4]) : "v"(ra) : "memory");
-                        asm volatile("ds_read_b64 %0, %1 offset:640" : "=v"(rs[5]) : "v"(ra) : "memory");
-                        asm volatile("ds_read_b64 %0, %1 offset:768" : "=v"(rs[6]) : "v"(ra) : "memory");
-                        asm volatile("ds_read_b64 %0, %1 offset:896" : "=v"(rs[7]) : "v"(ra) : "memory");
-                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                    } else {
-#pragma unroll
-                        for (int j = 0; j < 4; j++) sn[j] = *(const float4*)(cs_slot + wc * 64 + j * 16 + (lane >> 4) * 4);
-#pragma unroll
-                        for (int i = 0; i < 8; i++) rs[i] = *(const float2*)(rs_slot + (i * 16 + (lane & 15)) * 2);
-                    }
-                } else {
-#pragma unroll
-                    for (int j = 0; j < 4; j++) sn[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-                    for (int i = 0; i < 8; i++) rs[i] = make_float2(1.f, 0.f);
-                }
-#pragma unroll
-                for (int i = 0; i < 8; i++)
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        acc[i][j][0] = __builtin_fmaf(rs[i].x, acc[i][j][0], __builtin_fmaf(rs[i].y, sn[j].x, b[j].x));
-                        acc[i][j][1] = __builtin_fmaf(rs[i].x, acc[i][j][1], __builtin_fmaf(rs[i].y, sn[j].y, b[j].y));
-                        acc[i][j][2] = __builtin_fmaf(rs[i].x, acc[i][j][2], __builtin_fmaf(rs[i].y, sn[j].z, b[j].z));
-                        acc[i][j][3] = __builtin_fmaf(rs[i].x, acc[i][j][3], __builtin_fmaf(rs[i].y, sn[j].w, b[j].w));
-                    }
-            } else {
-#pragma unroll
-                for (int i = 0; i < 8; i++)
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        acc[i][j][0] += b[j].x;
-                        acc[i][j][1] += b[j].y;
-                        acc[i][j][2] += b[j].z;
-                        acc[i][j][3] += b[j].w;
-                    }
-            }
-        }
-        epilogue_tile<EPI, 8, true, RNB>(ea, acc, m0 + wr * 128, n0 + wc * 64, M, N);
-    }
-    if (wr == 0) G5_BARRIER();
-#undef G5_BARRIER
-#undef G5_LDS_DONE
-}
-
-// v7: v5's persistent 256x256x64 tile and LDS-DMA streams with TWO sections per K-step
-// instead of four: LOAD X reads A quadrant 0 and both W quadrants (16 ds_read_b128), COMPUTE X
-// runs the 32 MFMAs of output quadrants (0,0),(0,1); LOAD Y reads A quadrant 1, COMPUTE Y
-// runs (1,0),(1,1).  Each compute section is 512 MFMA cycles (v5: 256), so the loading
-// partner's LDS latency, DMA issue and lgkmcnt drain fit inside it, at half the barriers.
-// Region refill: A0/W0/W1 of a stage are last read in LOAD X of step s (both halves, one
-// barrier apart) -> refilled for step s+2 in LOAD Y of step s; A1 last read in LOAD Y of
-// step s -> refilled for step s+2 in LOAD X of step s+1.  Every wait is vmcnt(8) (plus the
-// tile's bias/colsum/rowstat pieces at its first K-step).  Per accumulator the MFMA chain
-// (K ascending) is v5's, so results are bit-identical.
-template <int EPI, bool F16>
-__global__ __launch_bounds__(512, 2) void gemm7_bf16_kernel(const __bf16* __restrict__ A, int64_t lda,
-                                                            const __bf16* __restrict__ W, int64_t ldw, int64_t M,
-                                                            int N, int K, EpiArgs ea, int tiles_n, int ntiles) {
-    extern __shared__ __attribute__((aligned(16))) __bf16 lds5[];
-    const int G = gridDim.x;
-    const int bid = blockIdx.x;
-    const int ng = G < 8 ? G : 8;
-    const int xg = bid % ng, gx = G / ng + ((G % ng) > xg ? 1 : 0);
-    const int lo = (int)((int64_t)ntiles * xg / ng), hi = (int)((int64_t)ntiles * (xg + 1) / ng);
-    const int first = lo + bid / ng;
-    if (first >= hi) return;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wr = wid >> 2, wc = wid & 3;
-    const int nk = K / GB_K;
-
-    int rowA[2][2], kcA[2][2], offA[2][2], offW[2][2];
-    uint32_t offAb[2][2], offWb[2][2];
-#pragma unroll
-    for (int h = 0; h < 2; h++)
-#pragma unroll
-        for (int u = 0; u < 2; u++) {
-            const int pc = 2 * wid + u;
-            const int ra = 128 * (pc >> 3) + 64 * h + 8 * (pc & 7);
-            const int rb = 64 * (pc >> 2) + 32 * h + 8 * (pc & 3);
-            const int r1 = ra + (lane >> 3), r2 = rb + (lane >> 3);
-            rowA[h][u] = r1;
-            kcA[h][u] = ((lane & 7) ^ ((r1 >> 1) & 7)) * 8;
-            offAb[h][u] = (uint32_t)(r1 * (int)lda + kcA[h][u]) * 2u;
-            offWb[h][u] = (uint32_t)(r2 * (int)ldw + ((lane & 7) ^ ((r2 >> 1) & 7)) * 8) * 2u;
-            offA[h][u] = ra * GB_K;
-            offW[h][u] = G2_M * GB_K + rb * GB_K;
-        }
-    struct Pos {
-        int tile, kt;
-        int64_t m0;
-        int n0;
-        bool full;
-    };
-    auto set_tile = [&](Pos& p, int tile) {
-        p.tile = tile;
-        p.kt = 0;
-        p.m0 = (int64_t)(tile / tiles_n) * G2_M;
-        p.n0 = (tile % tiles_n) * G2_N;
-        p.full = p.m0 + G2_M <= M;
-    };
-    auto advance = [&](Pos& p) {
-        if (++p.kt == nk) set_tile(p, p.tile + gx);
-    };
-    auto issue_a = [&](int stage, int h, const Pos& p) {
-        const __bf16* base = A + p.m0 * lda + p.kt * GB_K;
-        if (p.full) {
-#pragma unroll
-            for (int u = 0; u < 2; u++)
-                __builtin_amdgcn_global_load_lds((const char*)base + offAb[h][u],
-                                                 (lds_ptr_t)(lds5 + stage * G2_STAGE + offA[h][u]), 16, 0, 0);
-        } else {
-            const int lim = (int)(M - p.m0);
-#pragma unroll
-            for (int u = 0; u < 2; u++) {
-                const int r = rowA[h][u] < lim ? rowA[h][u] : lim - 1;
-                __builtin_amdgcn_global_load_lds((const char*)base + (uint32_t)(r * (int)lda + kcA[h][u]) * 2u,
-                                                 (lds_ptr_t)(lds5 + stage * G2_STAGE + offA[h][u]), 16, 0, 0);
-            }
-        }
-    };
-    auto issue_w = [&](int stage, int h, const Pos& p) {
-        const __bf16* base = W + (int64_t)p.n0 * ldw + p.kt * GB_K;
-#pragma unroll
-        for (int u = 0; u < 2; u++)
-            __builtin_amdgcn_global_load_lds((const char*)base + offWb[h][u],
-                                             (lds_ptr_t)(lds5 + stage * G2_STAGE + offW[h][u]), 16, 0, 0);
-    };
-#define G7_BARRIER()                              \
-    do {                                          \
-        __builtin_amdgcn_sched_barrier(0);        \
-        __builtin_amdgcn_s_barrier();             \
-        __builtin_amdgcn_sched_barrier(0);        \
-    } while (0)
-#define G7_LDS_DONE() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
-#define G7_VM(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
-
-    bf16x8 fa[4][2], fb[4][2];
-    f32x4 acc[8][4];
-    auto load_a = [&](const __bf16* sA, int qm) {
-#pragma unroll
-        for (int i = 0; i < 4; i++)
-#pragma unroll
-            for (int ks = 0; ks < 2; ks++)
-                fa[i][ks] = *(const bf16x8*)(sA + swz(wr * 128 + qm * 64 + i * 16 + (lane & 15), ks * 4 + (lane >> 4)));
-    };
-    auto load_b = [&](const __bf16* sW) {
-#pragma unroll
-        for (int j = 0; j < 4; j++)
-#pragma unroll
-            for (int ks = 0; ks < 2; ks++)
-                fb[j][ks] = *(const bf16x8*)(sW + swz(wc * 64 + (j >> 1) * 32 + (j & 1) * 16 + (lane & 15),
-                                                      ks * 4 + (lane >> 4)));
-    };
-    auto compute = [&](int qm) {
-#pragma unroll
-        for (int ks = 0; ks < 2; ks++)
-#pragma unroll
-            for (int i = 0; i < 4; i++)
-#pragma unroll
-                for (int j = 0; j < 4; j++)
-                    acc[qm * 4 + i][j] = mfma16<F16>(fb[j][ks], fa[i][ks], acc[qm * 4 + i][j]);
-    };
-
-    const bool has_bias = EPI != EPI_PATCH && ea.bias != nullptr;
-    float* bias_slot = (float*)(lds5 + 2 * G2_STAGE) + wid * 256;
-    const bool fold = F16 && ea.rowstat != nullptr;
-    float* cs_slot = bias_slot + 8 * 256;
-    float* rs_slot = bias_slot + 16 * 256;
-    // streams: pX = step s+1 (A1, issued in LOAD X), pY = step s+2 (A0, W0, W1, LOAD Y)
-    Pos pX, pY;
-    {
-        Pos p0;
-        set_tile(p0, first);
-        issue_a(0, 0, p0);
-        issue_w(0, 0, p0);
-        issue_w(0, 1, p0);
-        issue_a(0, 1, p0);
-        pX = p0;
-        advance(pX);  // step 1: inside the first tile (nk >= 2)
-        issue_a(1, 0, pX);
-        issue_w(1, 0, pX);
-        issue_w(1, 1, pX);
-        pY = pX;
-        advance(pY);
-        G7_VM(8);  // step 0's A0/W0/W1 landed
-    }
-    __syncthreads();
-    if (wr == 1) G7_BARRIER();
-    int buf = 0;
-    for (int tile = first; tile < hi; tile += gx) {
-#pragma unroll
-        for (int i = 0; i < 8; i++)
-#pragma unroll
-            for (int j = 0; j < 4; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        for (int kt = 0; kt < nk; ++kt) {
-            const bool hasX = pX.tile < hi, hasY = pY.tile < hi;
-            const __bf16* sA = lds5 + buf * G2_STAGE;
-            const __bf16* sW = sA + G2_M * GB_K;
-            // LOAD X / COMPUTE X
-            load_a(sA, 0);
-            load_b(sW);
-            int nb = 0;  // tile-start pieces (bias, colsum, rowstat), issued before pX's
-            if (kt == 0 && has_bias) {
-                __builtin_amdgcn_global_load_lds(ea.bias + (tile % tiles_n) * G2_N + lane * 4, (lds_ptr_t)bias_slot,
-                                                 16, 0, 0);
-                nb = 1;
-            }
-            if constexpr (F16) {
-                if (kt == 0 && fold) {
-                    __builtin_amdgcn_global_load_lds(ea.colsum + (tile % tiles_n) * G2_N + lane * 4,
-                                                     (lds_ptr_t)cs_slot, 16, 0, 0);
-                    __builtin_amdgcn_global_load_lds((const float*)(ea.rowstat + (int64_t)(tile / tiles_n) * G2_M +
-                                                                    wr * 128) + lane * 4,
-                                                     (lds_ptr_t)rs_slot, 16, 0, 0);
-                    nb += 2;
-                }
-            }
-            nb = __builtin_amdgcn_readfirstlane(nb);
-            if (hasX) issue_a(buf ^ 1, 1, pX);
-            G7_LDS_DONE();
-            // A1 of this step (issued one LOAD X ago) landed
-            if (!hasX) G7_VM(0);
-            else if (nb == 0) G7_VM(8);
-            else if (nb == 1) G7_VM(9);
-            else G7_VM(11);
-            G7_BARRIER();
-            compute(0);
-            G7_BARRIER();
-            // LOAD Y / COMPUTE Y
-            load_a(sA, 1);
-            if (hasY) {
-                issue_a(buf, 0, pY);
-                issue_w(buf, 0, pY);
-                issue_w(buf, 1, pY);
-            }
-            G7_LDS_DONE();
-            // A0/W0/W1 of step s+1 (issued one LOAD Y ago) landed
-            if (hasY) {
-                if (nb == 0) G7_VM(8);
-                else if (nb == 1) G7_VM(9);
-                else G7_VM(11);
-            } else if (hasX) {
-                if (nb == 0) G7_VM(2);
-                else if (nb == 1) G7_VM(3);
-                else G7_VM(5);
-            } else {
-                G7_VM(0);
-            }
-            G7_BARRIER();
-            compute(1);
-            G7_BARRIER();
-            advance(pX);
-            advance(pY);
-            buf ^= 1;
-        }
-        const int64_t m0 = (int64_t)(tile / tiles_n) * G2_M;
-        const int n0 = (tile % tiles_n) * G2_N;
-        if (has_bias) {
-            // the tile-start pieces were retired by K-step 1's LOAD X wait (nk >= 2)
-            float4 b[4];
+            // inline ds_read: no compiler-inserted vmcnt(0) for the LDS-DMA'd slot (retired by
+            // the tile's first K-step wait)
             const float* bp = bias_slot + wc * 64 + (lane >> 4) * 4;
             const uint32_t ba = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)bp;
             asm volatile("ds_read_b128 %0, %1" : "=v"(b[0]) : "v"(ba) : "memory");
@@ -1404,186 +749,94 @@ __global__ __launch_bounds__(512, 2) void gemm7_bf16_kernel(const __bf16* __rest
             asm volatile("ds_read_b128 %0, %1 offset:128" : "=v"(b[2]) : "v"(ba) : "memory");
             asm volatile("ds_read_b128 %0, %1 offset:192" : "=v"(b[3]) : "v"(ba) : "memory");
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            if constexpr (F16) {
-                float4 sn[4];
-                float2 rs[8];
-                if (fold) {
-                    const uint32_t ca = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)(
-                        cs_slot + wc * 64 + (lane >> 4) * 4);
-                    const uint32_t ra = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)(
-                        rs_slot + (lane & 15) * 2);
-                    asm volatile("ds_read_b128 %0, %1" : "=v"(sn[0]) : "v"(ca) : "memory");
-                    asm volatile("ds_read_b128 %0, %1 offset:64" : "=v"(sn[1]) : "v"(ca) : "memory");
-                    asm volatile("ds_read_b128 %0, %1 offset:128" : "=v"(sn[2]) : "v"(ca) : "memory");
-                    asm volatile("ds_read_b128 %0, %1 offset:192" : "=v"(sn[3]) : "v"(ca) : "memory");
-                    asm volatile("ds_read_b64 %0, %1" : "=v"(rs[0]) : "v"(ra) : "memory");
-                    asm volatile("ds_read_b64 %0, %1 offset:128" : "=v"(rs[1]) : "v"(ra) : "memory");
-                    asm volatile("ds_read_b64 %0, %1 offset:256" : "=v"(rs[2]) : "v"(ra) : "memory");
-                    asm volatile("ds_read_b64 %0, %1 offset:384" : "=v"(rs[3]) : "v"(ra) : "memory");
-                    asm volatile("ds_read_b64 %0, %1 offset:512" : "=v"(rs[4]) : "v"(ra) : "memory");
-                    asm volatile("ds_read_b64 %0, %1 offset:640" : "=v"(rs[5]) : "v"(ra) : "memory");
-                    asm volatile("ds_read_b64 %0, %1 offset:768" : "=v"(rs[6]) : "v"(ra) : "memory");
-                    asm volatile("ds_read_b64 %0, %1 offset:896" : "=v"(rs[7]) : "v"(ra) : "memory");
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                } else {
-#pragma unroll
-                    for (int j = 0; j < 4; j++) sn[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-                    for (int i = 0; i < 8; i++) rs[i] = make_float2(1.f, 0.f);
-                }
-#pragma unroll
-                for (int i = 0; i < 8; i++)
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        acc[i][j][0] = __builtin_fmaf(rs[i].x, acc[i][j][0], __builtin_fmaf(rs[i].y, sn[j].x, b[j].x));
-                        acc[i][j][1] = __builtin_fmaf(rs[i].x, acc[i][j][1], __builtin_fmaf(rs[i].y, sn[j].y, b[j].y));
-                        acc[i][j][2] = __builtin_fmaf(rs[i].x, acc[i][j][2], __builtin_fmaf(rs[i].y, sn[j].z, b[j].z));
-                        acc[i][j][3] = __builtin_fmaf(rs[i].x, acc[i][j][3], __builtin_fmaf(rs[i].y, sn[j].w, b[j].w));
-                    }
+            // acc <- rstd * acc + (-mean rstd * s_n + b'_n); without a fold (rstd, s) = (1, 0):
+            // fma(1, acc, fma(0, 0, b)) == acc + b exactly.  One branch-free update (a branch on
+            // acc would duplicate the 128 accumulators).
+            float4 sn[4];
+            float2 rs[8];
+            if (fold) {
+                const uint32_t ca = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)(
+                    cs_slot + wc * 64 + (lane >> 4) * 4);
+                const uint32_t ra =
+                    (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)(rs_slot + (lane & 15) * 2);
+                asm volatile("ds_read_b128 %0, %1" : "=v"(sn[0]) : "v"(ca) : "memory");
+                asm volatile("ds_read_b128 %0, %1 offset:64" : "=v"(sn[1]) : "v"(ca) : "memory");
+                asm volatile("ds_read_b128 %0, %1 offset:128" : "=v"(sn[2]) : "v"(ca) : "memory");
+                asm volatile("ds_read_b128 %0, %1 offset:192" : "=v"(sn[3]) : "v"(ca) : "memory");
+                asm volatile("ds_read_b64 %0, %1" : "=v"(rs[0]) : "v"(ra) : "memory");
+                asm volatile("ds_read_b64 %0, %1 offset:128" : "=v"(rs[1]) : "v"(ra) : "memory");
+                asm volatile("ds_read_b64 %0, %1 offset:256" : "=v"(rs[2]) : "v"(ra) : "memory");
+                asm volatile("ds_read_b64 %0, %1 offset:384" : "=v"(rs[3]) : "v"(ra) : "memory");
+                asm volatile("ds_read_b64 %0, %1 offset:512" : "=v"(rs[4]) : "v"(ra) : "memory");
+                asm volatile("ds_read_b64 %0, %1 offset:640" : "=v"(rs[5]) : "v"(ra) : "memory");
+                asm volatile("ds_read_b64 %0, %1 offset:768" : "=v"(rs[6]) : "v"(ra) : "memory");
+                asm volatile("ds_read_b64 %0, %1 offset:896" : "=v"(rs[7]) : "v"(ra) : "memory");
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             } else {
 #pragma unroll
-                for (int i = 0; i < 8; i++)
+                for (int j = 0; j < 4; j++) sn[j] = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        acc[i][j][0] += b[j].x;
-                        acc[i][j][1] += b[j].y;
-                        acc[i][j][2] += b[j].z;
-                        acc[i][j][3] += b[j].w;
-                    }
+                for (int i = 0; i < 8; i++) rs[i] = make_float2(1.f, 0.f);
             }
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    acc[i][j][0] = __builtin_fmaf(rs[i].x, acc[i][j][0], __builtin_fmaf(rs[i].y, sn[j].x, b[j].x));
+                    acc[i][j][1] = __builtin_fmaf(rs[i].x, acc[i][j][1], __builtin_fmaf(rs[i].y, sn[j].y, b[j].y));
+                    acc[i][j][2] = __builtin_fmaf(rs[i].x, acc[i][j][2], __builtin_fmaf(rs[i].y, sn[j].z, b[j].z));
+                    acc[i][j][3] = __builtin_fmaf(rs[i].x, acc[i][j][3], __builtin_fmaf(rs[i].y, sn[j].w, b[j].w));
+                }
         }
         epilogue_tile<EPI, 8, true>(ea, acc, m0 + wr * 128, n0 + wc * 64, M, N);
     }
-    if (wr == 0) G7_BARRIER();
-#undef G7_BARRIER
-#undef G7_LDS_DONE
-#undef G7_VM
+    if (wr == 0) G5_BARRIER();
+#undef G5_BARRIER
+#undef G5_LDS_DONE
 }
 
-template <int EPI, bool F16>
+template <int EPI>
 static int launch(const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N, int64_t K,
                   const EpiArgs& ea, hipStream_t s) {
-    int var = variant();
-    if (F16 && var >= 2 && var <= 4) var = 0;  // fp16 operands: v1 / v5 / v6 / v7 only
     const int64_t tiles256 = (int64_t)ceil_div(M, G2_M) * (N / G2_N);
-    if (N % G2_N == 0 && K >= 2 * GB_K && lda * G2_M < (1ll << 31) && ldw * G2_N < (1ll << 31) &&
-        (var >= 5 || (var == 0 && tiles256 >= 256))) {
+    const bool fits = N % G2_N == 0 && K >= 2 * GB_K && lda * G2_M < (1ll << 31) && ldw * G2_N < (1ll << 31);
+    if (fits && (g_tile == 2 || (g_tile == 0 && tiles256 >= 256))) {
         const int tiles_m = ceil_div(M, G2_M), tiles_n = (int)(N / G2_N);
-        const int64_t ntiles = (int64_t)tiles_m * tiles_n;
-        RM_REQUIRE(ntiles < (1ll << 31), "gemm: grid too large");
-        const size_t lds = 2 * (size_t)G2_STAGE * 2 + (F16 ? 3 : 1) * 8 * 256 * sizeof(float);
-        static bool attr5 = false;
-        if (!attr5) {
-            RM_CHECK_HIP(hipFuncSetAttribute((const void*)gemm5_bf16_kernel<EPI, false, F16>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            RM_CHECK_HIP(hipFuncSetAttribute((const void*)gemm5_bf16_kernel<EPI, true, F16>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            attr5 = true;
-        }
-        const int grid = (int)(ntiles < 256 ? ntiles : 256);
-        if (var == 7) {
-            static bool attr7 = false;
-            if (!attr7) {
-                RM_CHECK_HIP(hipFuncSetAttribute((const void*)gemm7_bf16_kernel<EPI, F16>,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-                attr7 = true;
-            }
-            hipLaunchKernelGGL((gemm7_bf16_kernel<EPI, F16>), dim3((unsigned)grid), dim3(512), lds, s,
-                               (const __bf16*)A, lda, (const __bf16*)W, ldw, M, (int)N, (int)K, ea, tiles_n, (int)ntiles);
-        } else if (var == 8 || var == 9) {  // A/B: the residual epilogue's old load batches
-            static bool attr89 = false;
-            if (!attr89) {
-                RM_CHECK_HIP(hipFuncSetAttribute((const void*)gemm5_bf16_kernel<EPI, true, F16, 2>,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-                RM_CHECK_HIP(hipFuncSetAttribute((const void*)gemm5_bf16_kernel<EPI, true, F16, 4>,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-                attr89 = true;
-            }
-            if (var == 8)
-                hipLaunchKernelGGL((gemm5_bf16_kernel<EPI, true, F16, 2>), dim3((unsigned)grid), dim3(512), lds, s,
-                                   (const __bf16*)A, lda, (const __bf16*)W, ldw, M, (int)N, (int)K, ea, tiles_n,
-                                   (int)ntiles);
-            else
-                hipLaunchKernelGGL((gemm5_bf16_kernel<EPI, true, F16, 4>), dim3((unsigned)grid), dim3(512), lds, s,
-                                   (const __bf16*)A, lda, (const __bf16*)W, ldw, M, (int)N, (int)K, ea, tiles_n,
-                                   (int)ntiles);
-        } else if (var == 6 || var == 0)
-            hipLaunchKernelGGL((gemm5_bf16_kernel<EPI, true, F16>), dim3((unsigned)grid), dim3(512), lds, s,
-                               (const __bf16*)A, lda, (const __bf16*)W, ldw, M, (int)N, (int)K, ea, tiles_n, (int)ntiles);
-        else
-            hipLaunchKernelGGL((gemm5_bf16_kernel<EPI, false, F16>), dim3((unsigned)grid), dim3(512), lds, s,
-                               (const __bf16*)A, lda, (const __bf16*)W, ldw, M, (int)N, (int)K, ea, tiles_n, (int)ntiles);
-        RM_LAUNCHED();
-        return OK;
-    }
-    if (!F16 && N % G2_N == 0 && var == 4) {
-        const int tiles_m = ceil_div(M, G2_M), tiles_n = (int)(N / G2_N);
-        const int64_t nwg = (int64_t)tiles_m * tiles_n;
-        RM_REQUIRE(nwg < (1ll << 31), "gemm: grid too large");
-        const size_t lds = 2 * (size_t)G2_STAGE * 2;
-        static bool attr4 = false;
-        if (!attr4) {
-            RM_CHECK_HIP(hipFuncSetAttribute((const void*)gemm4_bf16_kernel<EPI>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            attr4 = true;
-        }
-        hipLaunchKernelGGL(gemm4_bf16_kernel<EPI>, dim3((unsigned)nwg), dim3(512), lds, s, (const __bf16*)A, lda,
-                           (const __bf16*)W, ldw, M, (int)N, (int)K, ea, tiles_n, (int)nwg);
-        RM_LAUNCHED();
-        return OK;
-    }
-    if (!F16 && N % G2_N == 0 && var == 3) {
-        const int tiles_m = ceil_div(M, G2_M), tiles_n = (int)(N / G2_N);
-        const int64_t ntiles = (int64_t)tiles_m * tiles_n;
-        RM_REQUIRE(ntiles < (1ll << 31), "gemm: grid too large");
-        const size_t lds = 2 * (size_t)G2_STAGE * 2;
-        static bool attr3 = false;
-        if (!attr3) {
-            RM_CHECK_HIP(hipFuncSetAttribute((const void*)gemm3_bf16_kernel<EPI>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            attr3 = true;
-        }
-        const int grid = (int)(ntiles < 256 ? ntiles : 256);
-        hipLaunchKernelGGL(gemm3_bf16_kernel<EPI>, dim3((unsigned)grid), dim3(512), lds, s, (const __bf16*)A, lda,
-                           (const __bf16*)W, ldw, M, (int)N, (int)K, ea, tiles_n, (int)ntiles);
-        RM_LAUNCHED();
-        return OK;
-    }
-    if (!F16 && N % G2_N == 0 && var != 1 && (var == 2 || (int64_t)ceil_div(M, G2_M) * (N / G2_N) >= 512)) {
-        const int tiles_m = ceil_div(M, G2_M), tiles_n = (int)(N / G2_N);
-        const int64_t nwg = (int64_t)tiles_m * tiles_n;
-        RM_REQUIRE(nwg < (1ll << 31), "gemm: grid too large");
-        const size_t lds = 2 * (size_t)G2_STAGE * 2;
+        RM_REQUIRE(tiles256 < (1ll << 31), "gemm: grid too large");
+        // two operand stages + bias / colsum / rowstat slots (8 waves x 1 KiB each)
+        const size_t lds = 2 * (size_t)G2_STAGE * 2 + 3 * 8 * 256 * sizeof(float);
         static bool attr = false;
         if (!attr) {
-            RM_CHECK_HIP(hipFuncSetAttribute((const void*)gemm2_bf16_kernel<EPI>,
+            RM_CHECK_HIP(hipFuncSetAttribute((const void*)gemm_persistent_kernel<EPI>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
             attr = true;
         }
-        hipLaunchKernelGGL(gemm2_bf16_kernel<EPI>, dim3((unsigned)nwg), dim3(512), lds, s, (const __bf16*)A, lda,
-                           (const __bf16*)W, ldw, M, (int)N, (int)K, ea, tiles_n, (int)nwg);
+        const int grid = (int)(tiles256 < 256 ? tiles256 : 256);
+        hipLaunchKernelGGL((gemm_persistent_kernel<EPI>), dim3((unsigned)grid), dim3(512), lds, s, (const _Float16*)A,
+                           lda, (const _Float16*)W, ldw, M, (int)N, (int)K, ea, tiles_m, tiles_n, g_ngroups);
         RM_LAUNCHED();
         return OK;
     }
     const int tiles_m = ceil_div(M, GB_M), tiles_n = (int)(N / GB_N);
     const int64_t nwg = (int64_t)tiles_m * tiles_n;
     RM_REQUIRE(nwg < (1ll << 31), "gemm: grid too large");
-    hipLaunchKernelGGL((gemm_bf16_kernel<EPI, F16>), dim3((unsigned)nwg), dim3(256), 0, s, (const __bf16*)A, lda,
-                       (const __bf16*)W, ldw, M, (int)N, (int)K, ea, tiles_n, (int)nwg);
+    hipLaunchKernelGGL((gemm_tile_kernel<EPI>), dim3((unsigned)nwg), dim3(256), 0, s, (const _Float16*)A, lda,
+                       (const _Float16*)W, ldw, M, (int)N, (int)K, ea, tiles_n, (int)nwg);
     RM_LAUNCHED();
     return OK;
 }
 
-template <bool F16>
-static int gemm_any(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N, int64_t K,
-                    const EpiArgs& ea, hipStream_t s) {
+int gemm_f16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N, int64_t K,
+             const EpiArgs& ea, hipStream_t s) {
     RM_REQUIRE(M >= 0 && N > 0 && K > 0, "gemm: bad shape");
     RM_REQUIRE((epi != EPI_QKV && epi != EPI_PATCH) || M < (1ll << 31), "gemm: head split / patch rows need M < 2^31");
     RM_REQUIRE(N % GB_N == 0 && K % GB_K == 0, "gemm: needs N % 128 == 0 and K % 64 == 0");
     RM_REQUIRE(lda % 8 == 0 && ldw % 8 == 0 && lda >= K && ldw >= K, "gemm: lda/ldw must be >= K and 16-byte rows");
-    RM_REQUIRE((epi != EPI_BF16 && epi != EPI_GELU_BF16 && epi != EPI_RESID_F16) ||
+    RM_REQUIRE((epi != EPI_H16 && epi != EPI_GELU_H16 && epi != EPI_RESID_F16) ||
                    (ea.ldc % 8 == 0 && ((uintptr_t)ea.out & 15) == 0),
-               "gemm: bf16/fp16 output needs ldc % 8 == 0 and a 16-byte aligned base");
+               "gemm: fp16 output needs ldc % 8 == 0 and a 16-byte aligned base");
+    RM_REQUIRE((ea.rowstat == nullptr) == (ea.colsum == nullptr), "gemm: rowstat and colsum go together");
+    RM_REQUIRE(ea.rowstat == nullptr || ea.bias != nullptr, "gemm: a folded LayerNorm needs the folded bias");
     if (M == 0) return OK;
     hipEvent_t ev_b = nullptr;
     if (prof::enabled) {
@@ -1600,49 +853,32 @@ static int gemm_any(int epi, const void* A, int64_t lda, const void* W, int64_t 
         ev_b = pr.second;
     }
     int rc;
-    if constexpr (F16) {
-        switch (epi) {
-            case EPI_BF16: rc = launch<EPI_BF16, true>(A, lda, W, ldw, M, N, K, ea, s); break;
-            case EPI_GELU_BF16: rc = launch<EPI_GELU_BF16, true>(A, lda, W, ldw, M, N, K, ea, s); break;
-            case EPI_QKV: rc = launch<EPI_QKV, true>(A, lda, W, ldw, M, N, K, ea, s); break;
-            default: return fail(EINVAL_, "gemm_f16: epilogue must be EPI_BF16, EPI_GELU_BF16 or EPI_QKV");
-        }
-    } else {
-        switch (epi) {
-            case EPI_BF16: rc = launch<EPI_BF16, false>(A, lda, W, ldw, M, N, K, ea, s); break;
-            case EPI_GELU_BF16: rc = launch<EPI_GELU_BF16, false>(A, lda, W, ldw, M, N, K, ea, s); break;
-            case EPI_RESID_F32: rc = launch<EPI_RESID_F32, false>(A, lda, W, ldw, M, N, K, ea, s); break;
-            case EPI_QKV: rc = launch<EPI_QKV, false>(A, lda, W, ldw, M, N, K, ea, s); break;
-            case EPI_PATCH: rc = launch<EPI_PATCH, false>(A, lda, W, ldw, M, N, K, ea, s); break;
-            case EPI_F32: rc = launch<EPI_F32, false>(A, lda, W, ldw, M, N, K, ea, s); break;
-            case EPI_RESID_F16: rc = launch<EPI_RESID_F16, false>(A, lda, W, ldw, M, N, K, ea, s); break;
-            default: return fail(EINVAL_, "gemm: unknown epilogue");
-        }
+    switch (epi) {
+        case EPI_H16: rc = launch<EPI_H16>(A, lda, W, ldw, M, N, K, ea, s); break;
+        case EPI_GELU_H16: rc = launch<EPI_GELU_H16>(A, lda, W, ldw, M, N, K, ea, s); break;
+        case EPI_QKV: rc = launch<EPI_QKV>(A, lda, W, ldw, M, N, K, ea, s); break;
+        case EPI_PATCH: rc = launch<EPI_PATCH>(A, lda, W, ldw, M, N, K, ea, s); break;
+        case EPI_F32: rc = launch<EPI_F32>(A, lda, W, ldw, M, N, K, ea, s); break;
+        case EPI_RESID_F16: rc = launch<EPI_RESID_F16>(A, lda, W, ldw, M, N, K, ea, s); break;
+        default: return fail(EINVAL_, "gemm: unknown epilogue");
     }
     if (ev_b) RM_CHECK_HIP(hipEventRecord(ev_b, s));
     return rc;
-}
-
-int gemm_bf16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N, int64_t K,
-              const EpiArgs& ea, hipStream_t s) {
-    return gemm_any<false>(epi, A, lda, W, ldw, M, N, K, ea, s);
-}
-
-int gemm_f16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N, int64_t K,
-             const EpiArgs& ea, hipStream_t s) {
-    RM_REQUIRE((ea.rowstat == nullptr) == (ea.colsum == nullptr), "gemm_f16: rowstat and colsum go together");
-    RM_REQUIRE(ea.rowstat == nullptr || ea.bias != nullptr, "gemm_f16: a folded LayerNorm needs the folded bias");
-    return gemm_any<true>(epi, A, lda, W, ldw, M, N, K, ea, s);
 }
 
 }  // namespace reidmi
 
 using namespace reidmi;
 
-REIDMI_API int reidmi_gemm_set_variant(int v) {
-    RM_REQUIRE(v >= 0 && v <= 9, "gemm variant: 0 auto, 1 128x128, 2 256x256, 3 256x256 persistent, 4 ping-pong, "
-                                 "5 persistent ping-pong, 6 = 5 with deferred epilogue-store waits, 7 = 5 with two sections per K-step, 8 / 9 = 6 with 2 / 4 (default 8) residual row groups per load batch");
-    g_variant = v;
+REIDMI_API int reidmi_gemm_set_tile(int t) {
+    RM_REQUIRE(t >= 0 && t <= 2, "gemm tile: 0 auto, 1 128x128, 2 persistent 256x256");
+    g_tile = t;
+    return OK;
+}
+
+REIDMI_API int reidmi_gemm_set_walk(int ngroups) {
+    RM_REQUIRE(ngroups == 1 || ngroups == 2 || ngroups == 4 || ngroups == 8, "gemm walk: ngroups in {1, 2, 4, 8}");
+    g_ngroups = ngroups;
     return OK;
 }
 
@@ -1655,7 +891,8 @@ REIDMI_API int reidmi_prof_enable(int on) {
 }
 
 // Sum of device time (ms), launch count and algorithmic FLOPs of the recorded GEMM launches
-// with epilogue `epi` (-1: all).  Waits for the recorded events; then clears the record.
+// with epilogue `epi` (-1: all) and at least `min_flops` each.  Waits for the recorded
+// events; then clears the record.
 REIDMI_API int reidmi_prof_collect_min(int epi, double min_flops, double* total_ms, int64_t* count, double* flops) {
     std::lock_guard<std::mutex> g(prof::mu);
     double t = 0, f = 0;
@@ -1685,7 +922,8 @@ REIDMI_API int reidmi_prof_collect(int epi, double* total_ms, int64_t* count, do
 REIDMI_API int reidmi_gemm_f16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N,
                                int64_t K, const float* bias, const void* rowstat, const float* colsum, void* out,
                                int64_t ldc, void* stream) {
-    RM_REQUIRE(epi == EPI_BF16 || epi == EPI_GELU_BF16, "reidmi_gemm_f16: epi must be 0 (bf16) or 1 (gelu bf16)");
+    RM_REQUIRE(epi == EPI_H16 || epi == EPI_GELU_H16 || epi == EPI_F32 || epi == EPI_RESID_F16,
+               "reidmi_gemm_f16: epi must be 0 (fp16), 1 (QuickGELU fp16), 5 (fp32) or 6 (fp16 residual)");
     EpiArgs ea{};
     ea.out = out;
     ea.ldc = ldc;
@@ -1693,15 +931,4 @@ REIDMI_API int reidmi_gemm_f16(int epi, const void* A, int64_t lda, const void* 
     ea.rowstat = (const float2*)rowstat;
     ea.colsum = colsum;
     return gemm_f16(epi, A, lda, W, ldw, M, N, K, ea, (hipStream_t)stream);
-}
-
-REIDMI_API int reidmi_gemm_bf16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N,
-                                int64_t K, const float* bias, void* out, int64_t ldc, void* stream) {
-    RM_REQUIRE(epi == EPI_BF16 || epi == EPI_GELU_BF16 || epi == EPI_RESID_F32 || epi == EPI_F32 || epi == EPI_RESID_F16,
-               "reidmi_gemm_bf16: epi must be 0 (bf16), 1 (gelu bf16), 2 (residual f32), 5 (f32) or 6 (residual f16)");
-    EpiArgs ea{};
-    ea.out = out;
-    ea.ldc = ldc;
-    ea.bias = bias;
-    return gemm_bf16(epi, A, lda, W, ldw, M, N, K, ea, (hipStream_t)stream);
 }

@@ -5,7 +5,7 @@
 //   R2 od = D / colmax, initial_rank[:, :K]      rowmax + topk (stable ties)           reranking.py:45-48
 //   R3 k-reciprocal expansion + V row            kreciprocal_kernel  (ELL, fp16)       reranking.py:51-71
 //   R4 query expansion V_qe = mean of k2 rows    qe_kernel            (ELL, fp16)      reranking.py:73-78
-//   R5 inverted index                            csc_count/scan/fill  (CSC)            reranking.py:80-82
+//   R5 inverted index                            csc_count/scan/fill(/sort) (CSC)      reranking.py:80-82
 //   R6+R7 Jaccard with sequential fp16 sums, blend with od, slice [:Q, Q:]  jaccard_kernel  reranking.py:84-100
 // Two drivers: one-call (reidmi_rerank*: N x N distance materialised, capacity-sized ELL
 // rows) and staged (reidmi_rr_*: row ranges over exactly sized CSR buffers, distance rows
@@ -17,7 +17,6 @@
 // (pinned against numpy 2.2.6), float32 pairwise sum, fp16 ufuncs = op in fp32 then RNE.
 #include "common.h"
 
-#include <hipcub/hipcub.hpp>
 
 namespace reidmi {
 
@@ -427,8 +426,8 @@ __global__ void rows_pack_kernel(Rows V, const int64_t* __restrict__ off, int32_
 }
 
 // ------------------------------------------------------------------ R5: CSC
-// invIndex[c] = rows r with V_qe[r, c] != 0 (reranking.py:80-82), rows ascending: the
-// row-major entry list is stably sorted by column (LSD radix sort is stable).
+// invIndex[c] = rows r with V_qe[r, c] != 0 (reranking.py:80-82): per-column counts, an
+// exclusive scan, an atomic fill, and (staged driver) a per-column sort by row.
 __global__ void csc_count_kernel(Rows V, int64_t N, int32_t* __restrict__ cnt) {
     const int64_t r = blockIdx.x;
     const int64_t s = V.beg(r);
@@ -436,24 +435,68 @@ __global__ void csc_count_kernel(Rows V, int64_t N, int32_t* __restrict__ cnt) {
     for (int t = threadIdx.x; t < n; t += blockDim.x) atomicAdd(&cnt[V.col[s + t]], 1);
 }
 
-// keys = column, payload = (row << 16) | fp16 bits, in row-major entry order
-__global__ void csc_keys_kernel(Rows V, int32_t* __restrict__ keys, int64_t* __restrict__ pay, const int64_t* __restrict__ dst) {
+// Unsorted inverted index by atomic fill (the one-call paths: sizes unknown on the host).
+__global__ void csc_fill_kernel(Rows V, int64_t N, const int64_t* __restrict__ off, int32_t* __restrict__ cur,
+                                int32_t* __restrict__ irow, uint16_t* __restrict__ ival) {
     const int64_t r = blockIdx.x;
-    const int64_t s = V.beg(r), d = dst ? dst[r] : s;
+    const int64_t s = V.beg(r);
     const int n = V.len(r);
     for (int t = threadIdx.x; t < n; t += blockDim.x) {
-        keys[d + t] = V.col[s + t];
-        pay[d + t] = (r << 16) | (int64_t)V.val[s + t];
+        const int32_t c = V.col[s + t];
+        const int64_t p = off[c] + atomicAdd(&cur[c], 1);
+        irow[p] = (int32_t)r;
+        ival[p] = V.val[s + t];
     }
 }
 
-__global__ void csc_split_kernel(const int64_t* __restrict__ pay, int64_t n, int32_t* __restrict__ irow,
-                                 uint16_t* __restrict__ ival) {
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= n) return;
-    const int64_t p = pay[e];
-    irow[e] = (int32_t)(p >> 16);
-    ival[e] = (uint16_t)(p & 0xffff);
+// Sort each inverted list by row (reranking.py:80-82 lists rows ascending; the staged
+// Jaccard kernel binary-searches a list for a chunk's row range).  One workgroup per column;
+// rows are unique within a column, so any sort is the stable one.  Lists of up to
+// CSC_LDS entries are bitonic-sorted in LDS; longer ones (hub items in very large galleries)
+// in a power-of-two padded slice of a global scratch at 2 * off[c] (>= the padded length,
+// since pow2_ceil(len) < 2 len).
+constexpr int CSC_LDS = 4096;
+
+__global__ __launch_bounds__(256) void csc_sort_kernel(const int64_t* __restrict__ off, int32_t* __restrict__ irow,
+                                                       uint16_t* __restrict__ ival, int32_t* __restrict__ sk,
+                                                       uint16_t* __restrict__ sv) {
+    __shared__ int32_t lk[CSC_LDS];
+    __shared__ uint16_t lv[CSC_LDS];
+    const int64_t c = blockIdx.x;
+    const int64_t b = off[c];
+    const int n = (int)(off[c + 1] - b);
+    if (n < 2) return;
+    int P = 1;
+    while (P < n) P <<= 1;
+    const bool in_lds = P <= CSC_LDS;
+    int32_t* K = in_lds ? lk : sk + 2 * b;
+    uint16_t* V = in_lds ? lv : sv + 2 * b;
+    for (int t = threadIdx.x; t < P; t += blockDim.x) {
+        K[t] = t < n ? irow[b + t] : 0x7fffffff;
+        V[t] = t < n ? ival[b + t] : 0;
+    }
+    __syncthreads();
+    for (int k = 2; k <= P; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int t = threadIdx.x; t < P; t += blockDim.x) {
+                const int o = t ^ j;
+                if (o > t) {
+                    const int32_t a = K[t], d = K[o];
+                    if ((d < a) == ((t & k) == 0)) {
+                        K[t] = d;
+                        K[o] = a;
+                        const uint16_t va = V[t];
+                        V[t] = V[o];
+                        V[o] = va;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    for (int t = threadIdx.x; t < n; t += blockDim.x) {
+        irow[b + t] = K[t];
+        ival[b + t] = V[t];
+    }
 }
 
 // ----------------------------------------------------------- R6 + R7: Jaccard
@@ -550,20 +593,6 @@ static void kr_depths(int k1, int64_t N, int& kf, int& kh1) {
     kf = (int)(k1 + 1 < N ? k1 + 1 : N);
     const int kh = (int)__builtin_nearbyint((double)k1 / 2.0);  // int(np.around(k1/2))
     kh1 = (int)(kh + 1 < N ? kh + 1 : N);
-}
-
-// Unsorted inverted index by atomic fill (the one-call paths: sizes unknown on the host).
-__global__ void csc_fill_kernel(Rows V, int64_t N, const int64_t* __restrict__ off, int32_t* __restrict__ cur,
-                                int32_t* __restrict__ irow, uint16_t* __restrict__ ival) {
-    const int64_t r = blockIdx.x;
-    const int64_t s = V.beg(r);
-    const int n = V.len(r);
-    for (int t = threadIdx.x; t < n; t += blockDim.x) {
-        const int32_t c = V.col[s + t];
-        const int64_t p = off[c] + atomicAdd(&cur[c], 1);
-        irow[p] = (int32_t)r;
-        ival[p] = V.val[s + t];
-    }
 }
 
 // Jaccard over unsorted inverted lists: every chunk scans whole lists and filters rows.
@@ -787,23 +816,15 @@ REIDMI_API int reidmi_rr_qe_rows(const int32_t* rank, int K, int k2, int64_t lo,
 
 namespace reidmi {
 struct CscPlan {
-    int64_t cnt, k0, k1, p0, p1, tmp, tmp_bytes, total;
+    int64_t cnt, cur, sk, sv, total;
 };
 static CscPlan csc_plan(int64_t N, int64_t nnz) {
     CscPlan p{};
     int64_t o = 0;
     p.cnt = o; o = al(o + N * 4);
-    p.k0 = o; o = al(o + nnz * 4);
-    p.k1 = o; o = al(o + nnz * 4);
-    p.p0 = o; o = al(o + nnz * 8);
-    p.p1 = o; o = al(o + nnz * 8);
-    size_t tb = 0;
-    hipcub::DoubleBuffer<int32_t> kb(nullptr, nullptr);
-    hipcub::DoubleBuffer<int64_t> pb(nullptr, nullptr);
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kb, pb, (int)(nnz > 0 ? nnz : 1), 0, 32, (hipStream_t)0);
-    p.tmp = o;
-    p.tmp_bytes = (int64_t)tb;
-    o = al(o + (int64_t)tb);
+    p.cur = o; o = al(o + N * 4);
+    p.sk = o; o = al(o + 2 * nnz * 4);  // padded sort scratch of long lists
+    p.sv = o; o = al(o + 2 * nnz * 2);
     p.total = o;
     return p;
 }
@@ -811,33 +832,30 @@ static CscPlan csc_plan(int64_t N, int64_t nnz) {
 
 REIDMI_API int64_t reidmi_rr_csc_workspace_bytes(int64_t N, int64_t nnz) { return csc_plan(N, nnz).total; }
 
+// R5 for the staged driver: count per column, exclusive scan, atomic fill, per-column sort
+// by row — the CSC of V_qe with every list in ascending row order (reranking.py:80-82).
 REIDMI_API int reidmi_rr_csc(int64_t N, const int64_t* qoff, const int32_t* qcol, const uint16_t* qval, int64_t nnz,
                              int64_t* coff, int32_t* irow, uint16_t* ival, void* ws_, int64_t ws_bytes, void* stream) {
-    RM_REQUIRE(N > 0 && nnz >= 0 && nnz < 0x7fffffff && qoff && coff, "rr_csc: bad arguments");
+    RM_REQUIRE(N > 0 && N < (1ll << 31) && nnz >= 0 && nnz < 0x7fffffff && qoff && coff, "rr_csc: bad arguments");
     const CscPlan P = csc_plan(N, nnz);
     RM_REQUIRE(ws_bytes >= P.total, "rr_csc: workspace too small");
     hipStream_t s = (hipStream_t)stream;
     char* ws = (char*)ws_;
     const Rows V{qoff, nullptr, 0, qcol, qval};
     int32_t* cnt = (int32_t*)(ws + P.cnt);
+    int32_t* cur = (int32_t*)(ws + P.cur);
     RM_CHECK_HIP(hipMemsetAsync(cnt, 0, N * 4, s));
+    RM_CHECK_HIP(hipMemsetAsync(cur, 0, N * 4, s));
     hipLaunchKernelGGL(csc_count_kernel, dim3((unsigned)N), dim3(256), 0, s, V, N, cnt);
     RM_LAUNCHED();
     hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, s, cnt, N, coff);
     RM_LAUNCHED();
     if (nnz == 0) return OK;
-    int32_t* k0 = (int32_t*)(ws + P.k0);
-    int64_t* p0 = (int64_t*)(ws + P.p0);
-    hipLaunchKernelGGL(csc_keys_kernel, dim3((unsigned)N), dim3(256), 0, s, V, k0, p0, (const int64_t*)nullptr);
+    hipLaunchKernelGGL(csc_fill_kernel, dim3((unsigned)N), dim3(256), 0, s, V, N, (const int64_t*)coff, cur, irow,
+                       ival);
     RM_LAUNCHED();
-    int bits = 1;
-    while (bits < 32 && ((int64_t)1 << bits) < N) bits++;
-    hipcub::DoubleBuffer<int32_t> kb(k0, (int32_t*)(ws + P.k1));
-    hipcub::DoubleBuffer<int64_t> pb(p0, (int64_t*)(ws + P.p1));
-    size_t tb = (size_t)P.tmp_bytes;
-    RM_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(ws + P.tmp, tb, kb, pb, (int)nnz, 0, bits, s));
-    hipLaunchKernelGGL(csc_split_kernel, dim3(ceil_div(nnz, 256)), dim3(256), 0, s, (const int64_t*)pb.Current(), nnz,
-                       irow, ival);
+    hipLaunchKernelGGL(csc_sort_kernel, dim3((unsigned)N), dim3(256), 0, s, (const int64_t*)coff, irow, ival,
+                       (int32_t*)(ws + P.sk), (uint16_t*)(ws + P.sv));
     RM_LAUNCHED();
     return OK;
 }

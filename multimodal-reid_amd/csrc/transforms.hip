@@ -72,7 +72,7 @@ struct PPArgs {
     int max_h, max_w;
     int kh_cap, kv_cap, rows_cap;
     float mean[3], stdv[3];
-    int out_bf16;
+    int out_f16;
     void* out;
 };
 
@@ -117,8 +117,8 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PPArgs a) {
         const int64_t e = ((int64_t)b * 3 + c) * plane + (int64_t)(y_lo + yi) * ow + x;
         const float v0 = lut[c * 256 + p[0][c]], v1 = lut[c * 256 + p[1][c]];
         const float v2 = lut[c * 256 + p[2][c]], v3 = lut[c * 256 + p[3][c]];
-        if (a.out_bf16)
-            *(u16x4*)((unsigned short*)a.out + e) = u16x4{f2bf_bits(v0), f2bf_bits(v1), f2bf_bits(v2), f2bf_bits(v3)};
+        if (a.out_f16)
+            *(u16x4*)((unsigned short*)a.out + e) = u16x4{f2h_bits(v0), f2h_bits(v1), f2h_bits(v2), f2h_bits(v3)};
         else
             *(float4*)((float*)a.out + e) = make_float4(v0, v1, v2, v3);
     };
@@ -262,7 +262,7 @@ REIDMI_API int reidmi_preprocess_u8(const uint8_t* pix, const int64_t* meta, int
                                     void* stream) {
     RM_REQUIRE(B >= 0 && oh > 0 && ow > 0 && max_h > 0 && max_w > 0, "preprocess: bad sizes");
     RM_REQUIRE(oh <= 65535 * PP_BAND && B <= 65535, "preprocess: grid too large (split the batch)");
-    RM_REQUIRE(out_dtype == 0 || out_dtype == 1, "preprocess: out_dtype must be 0 (fp32) or 1 (bf16)");
+    RM_REQUIRE(out_dtype == 0 || out_dtype == 1, "preprocess: out_dtype must be 0 (fp32) or 1 (fp16)");
     RM_REQUIRE(ow % 4 == 0, "preprocess: output width must be a multiple of 4");
     RM_REQUIRE(mean && stdv && out && (B == 0 || (pix && meta)), "preprocess: null pointer");
     if (B == 0) return OK;
@@ -281,7 +281,7 @@ REIDMI_API int reidmi_preprocess_u8(const uint8_t* pix, const int64_t* meta, int
         a.mean[c] = mean[c];
         a.stdv[c] = stdv[c];
     }
-    a.out_bf16 = out_dtype;
+    a.out_f16 = out_dtype;
     a.out = out;
     static size_t attr = 0;
     if (lds > 64 * 1024 && lds > attr) {

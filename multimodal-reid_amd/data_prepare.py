@@ -58,13 +58,13 @@ def pack_images(images):
     return buf, meta, max_h, max_w
 
 
-def preprocess(images, height=256, width=128, model_type="vit", dtype=torch.bfloat16, device=None, out=None):
+def preprocess(images, height=256, width=128, model_type="vit", dtype=torch.float16, device=None, out=None):
     """Resize((height, width)) -> ToTensor -> Normalize of a batch of decoded RGB images
     (PIL images or HxWx3 uint8 arrays of any sizes) -> device tensor [B, 3, height, width]
-    of `dtype` (torch.float32 = exactly the reference's tensor; torch.bfloat16 = that tensor
+    of `dtype` (torch.float32 = exactly the reference's tensor; torch.float16 = that tensor
     rounded to nearest-even, the encoder's input)."""
-    if dtype not in (torch.float32, torch.bfloat16):
-        raise ValueError("dtype must be torch.float32 or torch.bfloat16")
+    if dtype not in (torch.float32, torch.float16):
+        raise ValueError("dtype must be torch.float32 or torch.float16")
     device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
     buf, meta, max_h, max_w = pack_images(images)
     B = meta.shape[0]
@@ -90,7 +90,7 @@ def preprocess(images, height=256, width=128, model_type="vit", dtype=torch.bflo
 class EvalTransform:
     """Callable stand-in for data_prepare.get_loader's `transform_test` over a whole batch."""
 
-    def __init__(self, image_height=256, image_width=128, model_type="vit", dtype=torch.bfloat16):
+    def __init__(self, image_height=256, image_width=128, model_type="vit", dtype=torch.float16):
         self.h, self.w, self.model_type, self.dtype = image_height, image_width, model_type, dtype
 
     def __call__(self, images, device=None):

@@ -13,7 +13,8 @@ the vision keys of custom_clip_model.VisionTransformer (``conv1.weight``,
 ``transformer.resblocks.{i}.attn.in_proj_weight``, ... ``proj``; plus ``VPT`` /
 ``VPT_shallow`` for IVLP) and the text keys of CLIP (``token_embedding.weight``,
 ``transformer.resblocks.{i}...``, ``ln_final.*``, ``text_projection``).  Matrices are
-stored bf16 in HBM, vectors fp32.  All compute runs in libreidmi.so.
+stored fp16 in HBM (the reference's GPU dtype, utils.py:145-166), vectors fp32.  All compute
+runs in libreidmi.so.
 """
 import ctypes
 
@@ -81,8 +82,8 @@ class _Packer:
         self.keep.append(t)
         return t
 
-    def bf16(self, a):
-        t = _t(a).contiguous().to(torch.bfloat16).to(self.device)
+    def f16(self, a):
+        t = _t(a).contiguous().to(torch.float16).to(self.device)
         self.keep.append(t)
         return t
 
@@ -115,7 +116,7 @@ def _pack_blocks(sd, prefix, layers, pk):
         b.qkv_w = pk.keep_dev(wf).data_ptr()
         b.qkv_b = pk.keep_dev(bf).data_ptr()
         b.qkv_s = pk.keep_dev(cs).data_ptr()
-        b.out_w = pk.bf16(sd[p + "attn.out_proj.weight"]).data_ptr()
+        b.out_w = pk.f16(sd[p + "attn.out_proj.weight"]).data_ptr()
         b.out_b = pk.f32(sd[p + "attn.out_proj.bias"]).data_ptr()
         b.ln2_w = pk.f32(sd[p + "ln_2.weight"]).data_ptr()
         b.ln2_b = pk.f32(sd[p + "ln_2.bias"]).data_ptr()
@@ -124,7 +125,7 @@ def _pack_blocks(sd, prefix, layers, pk):
         b.fc1_w = pk.keep_dev(wf).data_ptr()
         b.fc1_b = pk.keep_dev(bf).data_ptr()
         b.fc1_s = pk.keep_dev(cs).data_ptr()
-        b.fc2_w = pk.bf16(sd[p + "mlp.c_proj.weight"]).data_ptr()
+        b.fc2_w = pk.f16(sd[p + "mlp.c_proj.weight"]).data_ptr()
         b.fc2_b = pk.f32(sd[p + "mlp.c_proj.bias"]).data_ptr()
         b.prompt = pk.f32(sd[p + "VPT_shallow"]).data_ptr() if (p + "VPT_shallow") in sd else None
     return arr
@@ -169,14 +170,14 @@ class VisionTransformer:
         w = self.weights = VitWeights()
         w.width, w.layers, w.heads, w.patch, w.stride = W, layers, W // 64, P, stride
         w.out_dim, w.grid_h, w.grid_w, w.n_ctx, w.kpad = self.out_dim, gh, gw, self.n_ctx, kpad
-        w.conv_w = pk.bf16(convp).data_ptr()
+        w.conv_w = pk.f16(convp).data_ptr()
         w.class_emb = pk.f32(sd["class_embedding"]).data_ptr()
         w.pos_emb = pk.f32(pos).data_ptr()
         w.ln_pre_w = pk.f32(sd["ln_pre.weight"]).data_ptr()
         w.ln_pre_b = pk.f32(sd["ln_pre.bias"]).data_ptr()
         w.ln_post_w = pk.f32(sd["ln_post.weight"]).data_ptr()
         w.ln_post_b = pk.f32(sd["ln_post.bias"]).data_ptr()
-        w.proj_t = pk.bf16(_t(sd["proj"]).t()).data_ptr()
+        w.proj_t = pk.f16(_t(sd["proj"]).t()).data_ptr()
         w.vpt = pk.f32(sd["VPT"]).data_ptr() if self.n_ctx else None
         self._blocks = _pack_blocks(sd, "", layers, pk)
         w.blocks = self._blocks
@@ -200,7 +201,7 @@ class VisionTransformer:
         if not isinstance(img, torch.Tensor):
             img = torch.from_numpy(np.asarray(img))
         img = img.to(self.device)
-        if img.dtype not in (torch.float32, torch.bfloat16):
+        if img.dtype not in (torch.float32, torch.float16):
             img = img.float()
         return img.contiguous()
 
@@ -212,7 +213,7 @@ class VisionTransformer:
         ws, nbytes = self._workspace(B, full)
         if tta is not None:
             tta = torch.as_tensor(tta, dtype=torch.int32).to(self.device).contiguous()
-        rc = _fn("reidmi_vit_forward")(ctypes.byref(self.weights), img.data_ptr(), int(img.dtype == torch.bfloat16),
+        rc = _fn("reidmi_vit_forward")(ctypes.byref(self.weights), img.data_ptr(), int(img.dtype == torch.float16),
                                        B, H, Wd, None if tta is None else tta.data_ptr(), int(full),
                                        x12.data_ptr(), proj.data_ptr(), None if x11 is None else x11.data_ptr(),
                                        ws.data_ptr(), nbytes, _lib.stream(self.device))
@@ -266,7 +267,7 @@ class TextTransformer:
         w.pos_emb = self.positional_embedding.data_ptr()
         w.ln_final_w = pk.f32(sd["ln_final.weight"]).data_ptr()
         w.ln_final_b = pk.f32(sd["ln_final.bias"]).data_ptr()
-        w.proj_t = pk.bf16(_t(sd["text_projection"]).t()).data_ptr()
+        w.proj_t = pk.f16(_t(sd["text_projection"]).t()).data_ptr()
         self._blocks = _pack_blocks(sd, "", layers, pk)
         w.blocks = self._blocks
         self._ws = None

@@ -6,13 +6,14 @@ over the same state-dict layout libreidmi packs.
 
 TEST INFRASTRUCTURE ONLY (tests/, smoke(), bench.py cpu_baseline leg).
 
-``bf16=True`` rounds exactly where the HIP kernels do — to bfloat16 for the out_proj /
-c_proj / patch / proj GEMM operands, q/k/v, softmax probabilities before P.V and the
-attention output, to float16 for the residual stream x (patch/CLS rows, ln_pre output,
-every residual add: the reference's own GPU dtype), and ln_1 / ln_2 folded into fp16 QKV /
-c_fc GEMMs on x (`_ln_linear`) — so tests can separate kernel bugs from the precision the
-MI355X path runs at.  With bf16=False it is the reference's fp32
-math, pinned to tests/golden/vit_b16.npz and text.npz (made by the reference modules).
+``f16=True`` rounds to float16 exactly where the HIP kernels do — the out_proj / c_proj /
+patch / proj GEMM operands, q/k/v, softmax probabilities before P.V, the attention and
+QuickGELU outputs, the residual stream x (patch/CLS rows, ln_pre output, every residual
+add) — and folds ln_1 / ln_2 into the fp16 QKV / c_fc GEMMs on x (`_ln_linear`), so tests
+can separate kernel bugs from the precision the MI355X path runs at (fp16 operands, fp32
+accumulation: the reference's own GPU dtype, utils.py:145-166).  With f16=False it is the
+reference's fp32 math, pinned to tests/golden/vit_b16.npz, text.npz and ivlp.npz (made by
+the reference modules).
 """
 import numpy as np
 import torch
@@ -23,12 +24,11 @@ def _t(a):
     return a.detach().float() if isinstance(a, torch.Tensor) else torch.from_numpy(np.asarray(a, np.float32))
 
 
-def _r(x, on):
-    return x.to(torch.bfloat16).float() if on else x
-
-
 def _h(x, on):
     return x.half().float() if on else x
+
+
+_r = _h  # every rounded GEMM / attention operand is fp16
 
 
 def _ln(x, w, b):
@@ -52,12 +52,12 @@ def _ln_linear(x, g, beta, w, b, emulate):
     return rstd * (x @ wf.float().t()) + (-mean * rstd) * s + bf
 
 
-def block(x, sd, p, heads, causal=False, bf16=False):
+def block(x, sd, p, heads, causal=False, f16=False):
     """ResidualAttentionBlock.forward (custom_clip_model.py:26-29) on x [B, L, W]."""
     B, L, W = x.shape
     qkv = _ln_linear(x, sd[p + "ln_1.weight"], sd[p + "ln_1.bias"], sd[p + "attn.in_proj_weight"],
-                     sd[p + "attn.in_proj_bias"], bf16)
-    qkv = _r(qkv, bf16).reshape(B, L, 3, heads, 64).permute(2, 0, 3, 1, 4)
+                     sd[p + "attn.in_proj_bias"], f16)
+    qkv = _r(qkv, f16).reshape(B, L, 3, heads, 64).permute(2, 0, 3, 1, 4)
     q, k, v = qkv[0], qkv[1], qkv[2]
     s = (q @ k.transpose(-1, -2)) * 0.125
     if causal:
@@ -65,13 +65,13 @@ def block(x, sd, p, heads, causal=False, bf16=False):
     m = s.amax(-1, keepdim=True)
     e = torch.exp(s - m)
     den = e.sum(-1, keepdim=True)
-    o = (_r(e, bf16) @ v) / den
-    o = _r(o.permute(0, 2, 1, 3).reshape(B, L, W), bf16)
-    x = _h(x + (o @ _r(_t(sd[p + "attn.out_proj.weight"]), bf16).t() + _t(sd[p + "attn.out_proj.bias"])), bf16)
+    o = (_r(e, f16) @ v) / den
+    o = _r(o.permute(0, 2, 1, 3).reshape(B, L, W), f16)
+    x = _h(x + (o @ _r(_t(sd[p + "attn.out_proj.weight"]), f16).t() + _t(sd[p + "attn.out_proj.bias"])), f16)
     u = _ln_linear(x, sd[p + "ln_2.weight"], sd[p + "ln_2.bias"], sd[p + "mlp.c_fc.weight"],
-                   sd[p + "mlp.c_fc.bias"], bf16)
-    u = _r(u * torch.sigmoid(1.702 * u), bf16)
-    return _h(x + (u @ _r(_t(sd[p + "mlp.c_proj.weight"]), bf16).t() + _t(sd[p + "mlp.c_proj.bias"])), bf16)
+                   sd[p + "mlp.c_fc.bias"], f16)
+    u = _r(u * torch.sigmoid(1.702 * u), f16)
+    return _h(x + (u @ _r(_t(sd[p + "mlp.c_proj.weight"]), f16).t() + _t(sd[p + "mlp.c_proj.bias"])), f16)
 
 
 def tta_view(img, offs):
@@ -83,7 +83,7 @@ def tta_view(img, offs):
                         for b in range(B)])
 
 
-def vit_forward(sd, img, stride=12, bf16=False, tta=None):
+def vit_forward(sd, img, stride=12, f16=False, tta=None):
     """(x11, x12, xproj) of the vision tower; img [B,3,H,W] fp32."""
     img = _t(img)
     if tta is not None:
@@ -93,38 +93,38 @@ def vit_forward(sd, img, stride=12, bf16=False, tta=None):
     B, _, H, Wd = img.shape
     gh, gw = (H - P) // stride + 1, (Wd - P) // stride + 1
     heads = W // 64
-    cols = F.unfold(_r(img, bf16), P, stride=stride).transpose(1, 2)  # [B, NP, 3PP] (c,ky,kx)
-    x = cols @ _r(conv.reshape(W, -1), bf16).t()
+    cols = F.unfold(_r(img, f16), P, stride=stride).transpose(1, 2)  # [B, NP, 3PP] (c,ky,kx)
+    x = cols @ _r(conv.reshape(W, -1), f16).t()
     pos = _t(sd["positional_embedding"])
     cls = (_t(sd["class_embedding"]) + pos[0]).expand(B, 1, W)
-    x = _h(torch.cat([cls, x + pos[1:1 + gh * gw]], 1), bf16)
+    x = _h(torch.cat([cls, x + pos[1:1 + gh * gw]], 1), f16)
     n_ctx = 0
     if "VPT" in sd:
         vpt = _t(sd["VPT"]).half().float()
         n_ctx = vpt.shape[0]
         x = torch.cat([x, vpt.expand(B, -1, -1)], 1)
-    x = _h(_ln(x, sd["ln_pre.weight"], sd["ln_pre.bias"]), bf16)
+    x = _h(_ln(x, sd["ln_pre.weight"], sd["ln_pre.bias"]), f16)
     L = x.shape[1]
     x11 = None
     for i in range(12):
         p = f"transformer.resblocks.{i}."
         if i > 0 and (p + "VPT_shallow") in sd:
             x = torch.cat([x[:, :L - n_ctx], _t(sd[p + "VPT_shallow"]).half().float().expand(B, -1, -1)], 1)
-        x = block(x, sd, p, heads, False, bf16)
+        x = block(x, sd, p, heads, False, f16)
         if i == 10:
             x11 = x
     x12 = _ln(x, sd["ln_post.weight"], sd["ln_post.bias"])
-    xp = _r(x12, bf16) @ _r(_t(sd["proj"]), bf16)
+    xp = _r(x12, f16) @ _r(_t(sd["proj"]), f16)
     return x11, x12, xp
 
 
-def text_forward(sd, tokens, prompts=None, bf16=False):
+def text_forward(sd, tokens, prompts=None, f16=False):
     """CLIP.encode_text(tokens) or TextEncoder(prompts, tokens): [N, E]."""
     tokens = torch.as_tensor(np.asarray(tokens)).long()
     W = _t(sd["ln_final.weight"]).shape[0]
     heads = W // 64
     x = _t(sd["token_embedding.weight"])[tokens] if prompts is None else _t(prompts)
-    x = _h(x + _t(sd["positional_embedding"]), bf16)
+    x = _h(x + _t(sd["positional_embedding"]), f16)
     N, L, _ = x.shape
     layers = len([k for k in sd if k.startswith("transformer.") and k.endswith(".attn.in_proj_weight")])
     for i in range(layers):
@@ -132,6 +132,6 @@ def text_forward(sd, tokens, prompts=None, bf16=False):
         if i > 0 and (p + "VPT_shallow") in sd:
             ctx = _t(sd[p + "VPT_shallow"]).half().float()
             x = torch.cat([x[:, :1], ctx.expand(N, -1, -1), x[:, 1 + ctx.shape[0]:]], 1)
-        x = block(x, sd, p, heads, True, bf16)
+        x = block(x, sd, p, heads, True, f16)
     x = _ln(x[torch.arange(N), tokens.argmax(-1)], sd["ln_final.weight"], sd["ln_final.bias"])
-    return _r(x, bf16) @ _r(_t(sd["text_projection"]), bf16)
+    return _r(x, f16) @ _r(_t(sd["text_projection"]), f16)

@@ -136,6 +136,27 @@ def test_eval_market_scale_rows_vs_oracle(gpu):
     assert np.array_equal(idx, oracle.topk_rows(dsub, 50))
 
 
+@pytest.mark.parametrize("G", [3001, 4099])
+def test_eval_many_positives_and_junk_vs_oracle(gpu, G):
+    """Queries whose positives (> 512) or junk items (> 256) exceed the wave kernel's LDS
+    lists go to the per-workgroup kernel; ragged row starts (ld = G) exercise the 16-byte
+    alignment head; quantised distances give exact ties.  Bit-exact against the oracle."""
+    r = np.random.default_rng(G)
+    Q = 9
+    gp = r.integers(1, 4, G).astype(np.int64)  # pids 1..3: ~G/3 positives per query
+    gc = r.integers(0, 3, G).astype(np.int64)
+    qp = np.array([1, 2, 3, 1, 2, 3, 7, 1, 2], np.int64)
+    qc = np.array([0, 1, 2, 5, 5, 5, 0, 1, 2], np.int64)
+    gp[::7] = 9  # some negatives for everyone
+    qp[7:], gp[:40] = 8, 8  # two queries with 40 items of their pid (wave kernel path)
+    gc[:40] = np.arange(40) % 3
+    dist = (np.round(r.random((Q, G)) * 64) / 64).astype(np.float32)
+    rows = _eval_rows_np(dist, qp, gp, qc, gc)
+    ref = oracle.eval_rows(dist, qp, gp, qc, gc)
+    for a, b in zip(rows, ref):
+        assert np.array_equal(a.astype(b.dtype), b)
+
+
 def test_eval_edge_cases(gpu):
     ev = _ev()
     r = np.random.default_rng(3)

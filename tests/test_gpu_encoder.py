@@ -2,9 +2,9 @@
 restatement (oracle/vit_ref.py, itself pinned to the reference's outputs) and the
 reference-generated fixtures.
 
-Tolerances (bf16 MFMA operands, fp32 accumulation; the reference runs fp16):
-  * kernels vs a torch fp32 reference on the same bf16-rounded operands: rel 2e-3
-  * towers vs oracle with bf16 rounding at the same points: cosine >= 0.99999
+Tolerances (fp16 MFMA operands, fp32 accumulation — the reference's own GPU dtype):
+  * kernels vs a torch fp32 reference on the same fp16 operands: rel 2e-3 (fp16 outputs)
+  * towers vs oracle with fp16 rounding at the same points: cosine >= 0.99999
   * towers vs the reference's fp32 outputs: cosine >= 0.9999, max |err| <= 0.05
     (the reference's own fp16 GPU dtype deviates 0.007 on the same inputs)
 """
@@ -30,67 +30,72 @@ def _cos(a, b):
     return (a * b).sum(1) / np.linalg.norm(a, axis=1) / np.linalg.norm(b, axis=1)
 
 
-@pytest.mark.parametrize("epi", [0, 1, 2, 5, 6])
+def _gemm(L, epi, A, W, bias, out, rowstat=None, colsum=None):
+    M, K = A.shape
+    N = W.shape[0]
+    L.call("reidmi_gemm_f16", epi, L.ptr(A), K, L.ptr(W), K, M, N, K, L.ptr(bias), L.ptr(rowstat), L.ptr(colsum),
+           L.ptr(out), out.shape[1], L.stream())
+
+
+@pytest.mark.parametrize("epi", [0, 1, 5, 6])
 @pytest.mark.parametrize("M,N,K", [(300, 256, 192), (1, 128, 64), (1000, 768, 768)])
 def test_gemm_epilogues(gpu, epi, M, N, K):
+    """fp16 operands, fp32 accumulation: against torch fp32 on the same fp16 values."""
     L = _lib()
     g = torch.Generator().manual_seed(M + N + K + epi)
-    A = torch.randn(M, K, generator=g).to(torch.bfloat16)
-    W = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16)
+    A = torch.randn(M, K, generator=g).half()
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).half()
     bias = torch.randn(N, generator=g)
     ref = A.float() @ W.float().t() + bias
-    dA, dW, db = A.cuda(), W.cuda(), bias.cuda()
-    if epi in (0, 1):
-        out = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    base = torch.randn(M, N, generator=g).half()
+    if epi == 6:
+        out = base.clone().cuda()
     else:
-        base = torch.randn(M, N, generator=g)
-        if epi == 6:
-            base = base.half()
-        out = base.clone().cuda() if epi in (2, 6) else torch.empty(M, N, device="cuda")
-    L.call("reidmi_gemm_bf16", epi, L.ptr(dA), K, L.ptr(dW), K, M, N, K, L.ptr(db), L.ptr(out), N, L.stream())
+        out = torch.empty(M, N, dtype=torch.float32 if epi == 5 else torch.float16, device="cuda")
+    _gemm(L, epi, A.cuda(), W.cuda(), bias.cuda(), out)
     got = out.float().cpu()
     if epi == 1:
         ref = ref * torch.sigmoid(1.702 * ref)
-    if epi in (2, 6):
+    if epi == 6:
         ref = ref + base.float()
-    tol = 1e-2 if epi in (0, 1) else (2e-3 if epi == 6 else 2e-3)  # bf16/fp16 outputs carry their own rounding
+    tol = 1e-5 if epi == 5 else 2e-3  # fp16 outputs carry their own rounding
     assert (got - ref).abs().max() <= tol * (ref.abs().max() + 1)
 
 
-@pytest.mark.parametrize("epi", [0, 1, 2, 5, 6])
-@pytest.mark.parametrize("M,N,K", [(54016, 768, 768), (1000, 2304, 768), (700, 512, 3072), (70000, 256, 192)])
-def test_gemm_v2_tile_bitexact_vs_v1(gpu, epi, M, N, K):
-    """The 256x256 LDS-DMA tiles (v2 plain, v3 persistent, v4 ping-pong, v5 persistent
-    ping-pong, v6 = v5 with deferred epilogue-store waits, v7 = v5 with two sections per K-step; odd K-step counts cross tiles with the stage parity flipped) and the 128x128
-    register-staged tile run the same MFMA
-    sequence per output element (k-steps ascending), so they agree bit for bit; rows
+@pytest.mark.parametrize("epi", [0, 1, 5, 6])
+@pytest.mark.parametrize("M,N,K", [(54016, 768, 768), (1000, 2304, 768), (700, 512, 3072), (70000, 256, 192),
+                                   (40000, 3072, 768)])
+def test_gemm_tiles_and_walks_bitexact(gpu, epi, M, N, K):
+    """The 128x128 register-staged tile and the persistent 256x256 LDS-DMA tile (every
+    XCD tile walk: 1, 2, 4, 8 N-groups; odd K-step counts cross tiles with the stage parity
+    flipped) run the same MFMA chain per output element, so they agree bit for bit; rows
     past M (clamped source rows) must not leak into the result."""
     L = _lib()
     g = torch.Generator().manual_seed(M + N + K + epi)
-    A = torch.randn(M, K, generator=g).to(torch.bfloat16).cuda()
-    W = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16).cuda()
+    A = torch.randn(M, K, generator=g).half().cuda()
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).half().cuda()
     bias = torch.randn(N, generator=g).cuda()
     outs = []
-    for v in (1, 2, 3, 4, 5, 6, 7, 8, 9):
-        L.call("reidmi_gemm_set_variant", v)
-        if epi in (0, 1):
-            out = torch.zeros(M, N, dtype=torch.bfloat16, device="cuda")
-        elif epi == 6:
+    for tile, walk in ((1, 1), (2, 1), (2, 2), (2, 4), (2, 8)):
+        L.call("reidmi_gemm_set_tile", tile)
+        L.call("reidmi_gemm_set_walk", walk)
+        if epi == 6:
             out = torch.ones(M, N, dtype=torch.float16, device="cuda")
         else:
-            out = torch.ones(M, N, device="cuda")
-        L.call("reidmi_gemm_bf16", epi, L.ptr(A), K, L.ptr(W), K, M, N, K, L.ptr(bias), L.ptr(out), N, L.stream())
+            out = torch.zeros(M, N, dtype=torch.float32 if epi == 5 else torch.float16, device="cuda")
+        _gemm(L, epi, A, W, bias, out)
         outs.append(out)
-    L.call("reidmi_gemm_set_variant", 0)
+    L.call("reidmi_gemm_set_tile", 0)
+    L.call("reidmi_gemm_set_walk", 1)
     for o in outs[1:]:
         assert torch.equal(outs[0], o)
     rows = torch.arange(0, M, max(1, M // 97), device="cuda")
     ref = A[rows].float() @ W.float().t() + bias
     if epi == 1:
         ref = ref * torch.sigmoid(1.702 * ref)
-    if epi in (2, 6):
+    if epi == 6:
         ref = ref + 1
-    assert (outs[1][rows].float() - ref).abs().max() <= 1e-2 * (ref.abs().max() + 1)
+    assert (outs[1][rows].float() - ref).abs().max() <= 2e-3 * (ref.abs().max() + 1)
 
 
 @pytest.mark.parametrize("epi", [0, 1])
@@ -98,7 +103,7 @@ def test_gemm_v2_tile_bitexact_vs_v1(gpu, epi, M, N, K):
 def test_gemm_f16_layernorm_fold(gpu, epi, M, N, K):
     """ln_1 / ln_2 folded into the fp16 QKV / c_fc GEMM (model.fold_layernorm + row statistics):
     epi(LN(x) W^T + b) against fp64 torch on the same fp16 x, rows with large means (the
-    cancellation the fold must survive); v1, v6 and v7 tiles bit-identical."""
+    cancellation the fold must survive); both tilings and the grouped walk bit-identical."""
     from multimodal_reid_amd.model import fold_layernorm
     L = _lib()
     g = torch.Generator().manual_seed(M + N + K)
@@ -117,18 +122,19 @@ def test_gemm_f16_layernorm_fold(gpu, epi, M, N, K):
         ref = ref * torch.sigmoid(1.702 * ref)
     dx, dw, dcs, dbf, drs = (t.cuda() for t in (x, wf, cs, bf, rs))
     outs = []
-    for v in (1, 6, 7):
-        L.call("reidmi_gemm_set_variant", v)
-        out = torch.zeros(M, N, dtype=torch.bfloat16, device="cuda")
-        L.call("reidmi_gemm_f16", epi, L.ptr(dx), K, L.ptr(dw), K, M, N, K, L.ptr(dbf), L.ptr(drs), L.ptr(dcs),
-               L.ptr(out), N, L.stream())
+    for tile, walk in ((1, 1), (2, 1), (2, 4)):
+        L.call("reidmi_gemm_set_tile", tile)
+        L.call("reidmi_gemm_set_walk", walk)
+        out = torch.zeros(M, N, dtype=torch.float16, device="cuda")
+        _gemm(L, epi, dx, dw, dbf, out, drs, dcs)
         outs.append(out)
-    L.call("reidmi_gemm_set_variant", 0)
+    L.call("reidmi_gemm_set_tile", 0)
+    L.call("reidmi_gemm_set_walk", 1)
     for o in outs[1:]:
         assert torch.equal(outs[0], o)
     got = outs[0].double().cpu()
-    assert (got - ref).abs().max() <= 1e-2 * (ref.abs().max() + 1)
-    assert _cos(got.numpy(), ref.numpy()).min() >= 0.9999
+    assert (got - ref).abs().max() <= 2e-3 * (ref.abs().max() + 1)
+    assert _cos(got.numpy(), ref.numpy()).min() >= 0.99999
 
 
 @pytest.mark.parametrize("W", [512, 768, 1024])
@@ -139,11 +145,11 @@ def test_layernorm(gpu, W):
     ref = torch.nn.functional.layer_norm(x, (W,), g, b, 1e-5)
     dx, dg, dbb = x.cuda(), g.cuda(), b.cuda()
     y32 = torch.empty(333, W, device="cuda")
-    y16 = torch.empty(333, W, device="cuda", dtype=torch.bfloat16)
+    y16 = torch.empty(333, W, device="cuda", dtype=torch.float16)
     L.call("reidmi_layernorm", L.ptr(dx), 333, W, None, W, L.ptr(dg), L.ptr(dbb), 1e-5, L.ptr(y32), W, L.ptr(y16), W,
            L.stream())
     assert (y32.cpu() - ref).abs().max() < 1e-4 * ref.abs().max()
-    assert (y16.float().cpu() - ref).abs().max() < 1e-2 * ref.abs().max()
+    assert (y16.float().cpu() - ref).abs().max() < 1e-3 * ref.abs().max()
 
 
 @pytest.mark.parametrize("L,causal", [(211, False), (213, False), (77, True), (50, False), (256, True), (128, False)])
@@ -152,15 +158,15 @@ def test_mhsa(gpu, L, causal):
     nseq, H = 3, 4
     lp = lib.load().reidmi_attn_lpad(L)
     g = torch.Generator().manual_seed(L)
-    q = (torch.randn(nseq * H, L, 64, generator=g) * 2).to(torch.bfloat16)
-    k = (torch.randn(nseq * H, L, 64, generator=g) * 2).to(torch.bfloat16)
-    v = torch.randn(nseq * H, L, 64, generator=g).to(torch.bfloat16)
-    vt = torch.zeros(nseq * H, 64, lp, dtype=torch.bfloat16)
+    q = (torch.randn(nseq * H, L, 64, generator=g) * 2).half()
+    k = (torch.randn(nseq * H, L, 64, generator=g) * 2).half()
+    v = torch.randn(nseq * H, L, 64, generator=g).half()
+    vt = torch.zeros(nseq * H, 64, lp, dtype=torch.float16)
     vt[:, :, :L] = v.transpose(1, 2)
     vt[:, :, L:] = float("nan")  # padding must never be read into the result
-    o = torch.empty(nseq * L, H * 64, dtype=torch.bfloat16, device="cuda")
+    o = torch.empty(nseq * L, H * 64, dtype=torch.float16, device="cuda")
     dq, dk, dvt = q.cuda(), k.cuda(), vt.cuda()
-    lib.call("reidmi_mhsa_bf16", lib.ptr(dq), lib.ptr(dk), lib.ptr(dvt), lib.ptr(o), nseq, L, H, int(causal),
+    lib.call("reidmi_mhsa_f16", lib.ptr(dq), lib.ptr(dk), lib.ptr(dvt), lib.ptr(o), nseq, L, H, int(causal),
              lib.stream())
     s = (q.float() @ k.float().transpose(1, 2)) * 0.125
     if causal:
@@ -169,7 +175,7 @@ def test_mhsa(gpu, L, causal):
     ref = (p @ v.float()).reshape(nseq, H, L, 64).permute(0, 2, 1, 3).reshape(nseq * L, H * 64)
     got = o.float().cpu()
     assert torch.isfinite(got).all()
-    assert (got - ref).abs().max() < 3e-2
+    assert (got - ref).abs().max() < 5e-3  # fp16 P and O (bf16 needed 3e-2)
 
 
 @pytest.fixture(scope="module")
@@ -190,7 +196,7 @@ def test_vit_b16_encode_image_vs_reference(vit_b16):
         assert _cos(got, ref).min() >= 0.9999
         assert np.abs(got - ref).max() <= 0.05
     with torch.no_grad():
-        b11, b12, bp = vit_ref.vit_forward(sd, imgs, bf16=True)
+        b11, b12, bp = vit_ref.vit_forward(sd, imgs, f16=True)
     assert _cos(x12[:, 0], b12[:, 0].numpy()).min() >= 0.99999
     assert _cos(xp[:, 0], bp[:, 0].numpy()).min() >= 0.99999
 
@@ -213,7 +219,7 @@ def test_vit_l14_encode_image_vs_reference(gpu):
     assert _cos(c12.cpu().numpy(), g["x12cls"]).min() >= 0.9999
     assert _cos(cp.cpu().numpy(), g["projcls"]).min() >= 0.9999
     with torch.no_grad():
-        _, b12, bp = vit_ref.vit_forward(sd, imgs, bf16=True)
+        _, b12, bp = vit_ref.vit_forward(sd, imgs, f16=True)
     assert _cos(x12[:, 0], b12[:, 0].numpy()).min() >= 0.99999
     assert _cos(xp[:, 0], bp[:, 0].numpy()).min() >= 0.99999
 
@@ -259,7 +265,7 @@ def test_vit_ivlp_prompts(gpu):
     imgs = syn.images(2, seed=4)
     _, x12, xp = m.encode_image(torch.from_numpy(imgs))
     with torch.no_grad():
-        _, r12, rp = vit_ref.vit_forward(sd, imgs, bf16=True)
+        _, r12, rp = vit_ref.vit_forward(sd, imgs, f16=True)
     assert _cos(x12[:, 0].cpu().numpy(), r12[:, 0].numpy()).min() >= 0.99999
     assert _cos(xp.cpu().numpy().reshape(-1, 512), rp.numpy().reshape(-1, 512)).min() >= 0.9999
 
@@ -272,7 +278,7 @@ def test_text_encoder_vs_reference(gpu):
     out = tm.encode_text(torch.from_numpy(g["tokens"])).cpu().numpy()
     assert _cos(out, g["text_feat"]).min() >= 0.9999
     with torch.no_grad():
-        ref = vit_ref.text_forward(sd, g["tokens"], bf16=True).numpy()
+        ref = vit_ref.text_forward(sd, g["tokens"], f16=True).numpy()
     assert _cos(out, ref).min() >= 0.99995  # 12 causal blocks: bf16 rounding flips compound
     # TextEncoder(prompts, tokenized) == encode_text when prompts = token_embedding(tokens)
     te = TextEncoder(tm)

@@ -64,7 +64,7 @@ def _cases():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
 def test_preprocess_kernel_bitexact(gpu, dtype):
     """One mixed-size batch per output size (Market crops, up/down/identity per axis, tall
     narrow sources, 1x1) through reidmi_preprocess_u8 vs the oracle."""
@@ -76,10 +76,10 @@ def test_preprocess_kernel_bitexact(gpu, dtype):
         got = data_prepare.preprocess(imgs, oh, ow, dtype=dtype).cpu()
         for i, img in enumerate(imgs):
             ref = torch.from_numpy(oracle.eval_transform(img, oh, ow))
-            if dtype == torch.bfloat16:
-                ref = ref.to(torch.bfloat16)
-            assert torch.equal(got[i].view(torch.int16 if dtype == torch.bfloat16 else torch.int32),
-                               ref.view(torch.int16 if dtype == torch.bfloat16 else torch.int32)), (img.shape, oh, ow)
+            if dtype == torch.float16:
+                ref = ref.to(torch.float16)
+            assert torch.equal(got[i].view(torch.int16 if dtype == torch.float16 else torch.int32),
+                               ref.view(torch.int16 if dtype == torch.float16 else torch.int32)), (img.shape, oh, ow)
 
 
 @pytest.mark.gpu
@@ -107,7 +107,7 @@ def test_preprocess_large_batch_matches_per_image(gpu):
     from multimodal_reid_amd import data_prepare
     r = np.random.default_rng(3)
     imgs = [source_image(int(r.integers(60, 500)), int(r.integers(30, 250)), 1000 + i) for i in range(300)]
-    batch = data_prepare.preprocess(imgs, dtype=torch.bfloat16)
+    batch = data_prepare.preprocess(imgs, dtype=torch.float16)
     for i in range(0, 300, 37):
-        one = data_prepare.preprocess([imgs[i]], dtype=torch.bfloat16)
+        one = data_prepare.preprocess([imgs[i]], dtype=torch.float16)
         assert torch.equal(batch[i], one[0])

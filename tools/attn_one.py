@@ -18,16 +18,16 @@ def main():
     lib = L.load()
     lp = lib.reidmi_attn_lpad(Lq)
     dev = torch.device("cuda")
-    q = (torch.randn(nseq * H, Lq, 64, device=dev) * 2).bfloat16()
-    k = (torch.randn(nseq * H, Lq, 64, device=dev) * 2).bfloat16()
-    vt = torch.randn(nseq * H, 64, lp, device=dev).bfloat16()
-    o = torch.empty(nseq * Lq, H * 64, dtype=torch.bfloat16, device=dev)
+    q = (torch.randn(nseq * H, Lq, 64, device=dev) * 2).half()
+    k = (torch.randn(nseq * H, Lq, 64, device=dev) * 2).half()
+    vt = torch.randn(nseq * H, 64, lp, device=dev).half()
+    o = torch.empty(nseq * Lq, H * 64, dtype=torch.float16, device=dev)
     args = (L.ptr(q), L.ptr(k), L.ptr(vt), L.ptr(o), nseq, Lq, H, 0, L.stream())
-    L.call("reidmi_mhsa_bf16", *args)
+    L.call("reidmi_mhsa_f16", *args)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(reps):
-        L.call("reidmi_mhsa_bf16", *args)
+        L.call("reidmi_mhsa_f16", *args)
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps

@@ -9,5 +9,5 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
   python bench.py ${BENCH_ARGS} > gpurun_out/bench_under_rocprof.json
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 90 rocprofv3 --pmc $c --kernel-trace --output-format csv -d gpurun_out/pmc_$c -o p -- \
-    python tools/gemm_one.py 216064 3072 768 1 0 5 fold > gpurun_out/pmc_$c.log 2>&1
+    python tools/gemm_one.py 216064 3072 768 1 5 fold > gpurun_out/pmc_$c.log 2>&1
 done

@@ -73,7 +73,7 @@ def embed_leg(dev, rank, world, n, batch, G):
     m = VisionTransformer(sd, device=dev)
     gen = torch.Generator(device=dev)
     gen.manual_seed(7 + rank)
-    imgs = (torch.rand((n, 3, 256, 128), generator=gen, device=dev) * 2 - 1).bfloat16()
+    imgs = (torch.rand((n, 3, 256, 128), generator=gen, device=dev) * 2 - 1).half()
     tta = torch.from_numpy(syn.tta_offsets(n, seed=3, offset=rank * n)).to(dev)
     emb = torch.empty((n, m.width + m.out_dim), device=dev)
 
@@ -91,7 +91,7 @@ def embed_leg(dev, rank, world, n, batch, G):
     rate = world * n / te
     tf = rate * 2 * VITL_GFLOP_PER_PASS / 1e3
     return {"sample_imgs_per_rank": n, "imgs_per_s": round(rate, 1), "TFLOPs": round(tf, 1),
-            "frac_of_bf16_peak": round(tf / (2500.0 * world), 4), "projected_gallery_embed_s": round(G / rate, 1)}
+            "frac_of_fp16_peak": round(tf / (2500.0 * world), 4), "projected_gallery_embed_s": round(G / rate, 1)}
 
 
 def main():
