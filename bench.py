@@ -40,6 +40,8 @@ from multimodal_reid_amd import zero_shot_learning as zsl  # noqa: E402
 from multimodal_reid_amd.model import VisionTransformer  # noqa: E402
 
 PEAK_F16_TFLOPS = 2500.0  # MI355X dense fp16/bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_F32_MATRIX_TFLOPS = 157.3  # MI355X fp32 matrix (v_mfma_f32_32x32x2_f32)
+PEAK_HBM_GBPS = 8000.0
 EPI_GELU = 1  # the c_fc GEMM (+QuickGELU epilogue): the largest single kernel per block
 # HBM-side bytes per c_fc launch (ln_2-folded fp16 GEMM, M = 1024*211 (the default batch),
 # N = 3072, K = 768) from rocprofv3 PMC passes (tools/prof_round.sh ->
@@ -113,8 +115,8 @@ class Workload:
         rows = gather_rows(rows, self.Q, self.world)
         torch.cuda.synchronize()
         rows = rows.cpu().numpy()
-        cmc, mAP = evaluate.aggregate_cmc_map(rows[:, 0] > 0, rows[:, 1].astype(np.int64), rows[:, 2],
-                                              rows[:, 3].astype(np.int64), self.G, 50, ovf.cpu().numpy())
+        cmc, mAP = evaluate.aggregate_cmc_map(rows[:, 0].astype(np.int64), rows[:, 1].astype(np.int64), rows[:, 2],
+                                              rows[:, 3].astype(np.int64), self.G, 50)
         t2 = time.perf_counter()
         return cmc, mAP, t1 - t0, t2 - t1
 
@@ -139,8 +141,8 @@ def msmt17_leg(model, dev, rank, world, batch):
             d, wl.q_pids[wl.qlo:wl.qhi], wl.g_pids, wl.q_cams[wl.qlo:wl.qhi], wl.g_cams)
         rows = gather_rows(torch.stack([valid.double(), first.double(), ap, nkept.double()], 1), Q, world)
         rows = rows.cpu().numpy()
-        return evaluate.aggregate_cmc_map(rows[:, 0] > 0, rows[:, 1].astype(np.int64), rows[:, 2],
-                                          rows[:, 3].astype(np.int64), G, 50, ovf.cpu().numpy())
+        return evaluate.aggregate_cmc_map(rows[:, 0].astype(np.int64), rows[:, 1].astype(np.int64), rows[:, 2],
+                                          rows[:, 3].astype(np.int64), G, 50)
 
     sync()
     t0 = time.perf_counter()
@@ -171,17 +173,22 @@ def msmt17_leg(model, dev, rank, world, batch):
             "mAP": round(float(mAP), 6), "mAP_rerank": round(float(mAP_rr), 6)}
 
 
-def rerank_leg(dev, cpu_n=1000, cpu=True):
+def rerank_leg(dev, cpu=True, threads=1):
     """configs[2]'s back end: DukeMTMC-size k-reciprocal re-rank (k1=50, k2=15, lambda=0.3;
     reranking.py:29-100, evaluate.py:124-132) + CMC/mAP on identity-clustered synthetic
-    features, timed on its own after the Market steps (not part of `value`)."""
+    features, timed on its own after the Market steps (not part of `value`).
+    Roofline: the stage chain is bound by the exact-fp32 N x N distance GEMM (2 N^2 D FLOP on
+    the 157 TF/s fp32 matrix peak) — far above its HBM floor (4 N^2 distance bytes + 4 Q G
+    final bytes at 8 TB/s); frac = max(floors) / wall.  cpu_port: the C restatement on the
+    full configuration, `threads` host threads."""
     from multimodal_reid_amd import reranking
     sp = syn.DATASET_SPLITS["dukemtmc"]
     Q, G = sp["num_query"], sp["num_gallery"]
     qp, gp, qc, gc = syn.labels(Q, G, sp["num_ids"], sp["num_cams"], seed=0, distractor_frac=0.1, junk_frac=0.02)
-    qf, gf = syn.features(qp, gp)
-    qf = evaluate.l2_normalize_device(torch.from_numpy(qf).to(dev))
-    gf = evaluate.l2_normalize_device(torch.from_numpy(gf).to(dev))
+    qf_np, gf_np = syn.features(qp, gp)
+    qf = evaluate.l2_normalize_device(torch.from_numpy(qf_np).to(dev))
+    gf = evaluate.l2_normalize_device(torch.from_numpy(gf_np).to(dev))
+    D = qf.shape[1]
 
     def run():
         d = reranking.re_ranking_device(qf, gf, 50, 15, 0.3)
@@ -196,24 +203,61 @@ def rerank_leg(dev, cpu_n=1000, cpu=True):
     cmc, mAP = run()
     wall = time.perf_counter() - t
     N = Q + G
-    out = {"config": f"DukeMTMC {Q}q x {G}g (N={N}) synthetic features D=1280, k1=50 k2=15 lambda=0.3, "
+    flop_floor = 2.0 * N * N * D / (PEAK_F32_MATRIX_TFLOPS * 1e12)
+    nbytes = 4 * N * N + 4 * Q * G
+    byte_floor = nbytes / (PEAK_HBM_GBPS * 1e9)
+    out = {"config": f"DukeMTMC {Q}q x {G}g (N={N}) synthetic features D={D}, k1=50 k2=15 lambda=0.3, "
                      "distance + re-rank + CMC/mAP on 1 GPU",
            "wall_s": round(wall, 4), "mAP": round(float(mAP), 6),
-           "algorithmic_bytes": 4 * N * N + 4 * Q * G,
+           "roofline": {"bound": "mfma-fp32 (exact N x N distance)", "flop_floor_s": round(flop_floor, 5),
+                        "hbm_floor_s": round(byte_floor, 5), "algorithmic_flop": 2.0 * N * N * D,
+                        "algorithmic_bytes": nbytes, "frac": round(max(flop_floor, byte_floor) / wall, 4)},
            "reference_cpu_s_survey": 122.0}
     if cpu:
         import oracle
-        q = int(cpu_n * Q / N)
-        sqp, sgp = qp[:q], gp[:cpu_n - q]
-        sqf, sgf = syn.features(sqp, sgp, seed=5)
+        oracle.set_threads(threads)
         t = time.perf_counter()
-        oracle.re_ranking(sqf, sgf, 50, 15, 0.3)
+        oracle.re_ranking(oracle.l2norm(qf_np), oracle.l2norm(gf_np), 50, 15, 0.3)
         tc = time.perf_counter() - t
-        out["cpu_port"] = {"sample": f"oracle C re-rank, {q}q x {cpu_n - q}g, 1 thread", "sample_s": round(tc, 3),
-                           "extrapolated_s": round(tc * (N / cpu_n) ** 2, 1), "kind": "port",
-                           "note": "quadratic extrapolation; the dense C restatement is slower than the "
-                                   "reference's numpy (SURVEY.md §6: 122 s for this config on 8 cores)"}
+        out["cpu_port"] = {"sample": f"oracle C re-rank (distance + R2-R7), full {Q}q x {G}g", "wall_s": round(tc, 2),
+                           "cores": threads, "kind": "port",
+                           "note": "not extrapolated; the reference's numpy took 122 s for this config on 8 cores "
+                                   "(SURVEY.md §6)"}
     return out
+
+
+def backend_rooflines(wl, reps=10):
+    """The retrieval kernels of the Market step on their own (HIP events on the launch
+    stream, the step's own buffers): exact-fp32 distance (MFMA fp32 bound: 2 Q G D FLOP)
+    and eval_rows (HBM bound: one read of the Q x G distances + the gallery labels once,
+    4 Q G + 16 G bytes); this rank's query and gallery shards (the whole split at N = 1)."""
+    qn = evaluate.l2_normalize_device(wl.q_emb)
+    gn = evaluate.l2_normalize_device(wl.g_emb)
+    Q, G, D = qn.shape[0], gn.shape[0], qn.shape[1]
+    qp, qc = wl.q_pids[wl.qlo:wl.qhi], wl.q_cams[wl.qlo:wl.qhi]
+
+    def timed(fn):
+        fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps * 1e-3
+
+    dist_buf = torch.empty(Q, G, device=wl.dev)
+    gp, gc = wl.g_pids[wl.glo:wl.ghi], wl.g_cams[wl.glo:wl.ghi]
+    td = timed(lambda: evaluate.euclidean_distance_device(qn, gn, out=dist_buf))
+    args = [torch.from_numpy(np.ascontiguousarray(a)).to(wl.dev) for a in (qp, gp, qc, gc)]
+    te = timed(lambda: evaluate.eval_rows_device(dist_buf, *args))
+    eb = 4.0 * Q * G + 16.0 * G
+    return {"distmat": {"bound": "mfma-fp32", "achieved": round(2.0 * Q * G * D / td / 1e12, 1),
+                        "peak": PEAK_F32_MATRIX_TFLOPS, "unit": "TFLOP/s",
+                        "frac": round(2.0 * Q * G * D / td / 1e12 / PEAK_F32_MATRIX_TFLOPS, 4), "ms": round(td * 1e3, 3)},
+            "eval_rows": {"bound": "hbm", "achieved": round(eb / te / 1e9, 1), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+                          "frac": round(eb / te / 1e9 / PEAK_HBM_GBPS, 4), "ms": round(te * 1e3, 3),
+                          "algorithmic_bytes": eb}}
 
 
 def preprocess_leg(dev, n=19281, reps=5):
@@ -249,35 +293,37 @@ def preprocess_leg(dev, n=19281, reps=5):
             "achieved_GBps": round(nbytes / (ms * 1e-3) / 1e9, 1), "peak_GBps": 8000.0}
 
 
-def cpu_baseline(wl, n_img=12, n_q=48):
-    """The oracle ("port") on this host: fp32 torch restatement of the encoder on a
-    bounded image sample (both TTA passes) + C restatement of distmat/eval on a query
-    subset against the full gallery; both extrapolated linearly to the Market split."""
+def cpu_baseline(wl, threads, n_img=64, bs=16):
+    """The oracle ("port") on this host: the fp32 torch restatement of the encoder on a
+    bounded image sample (both TTA passes, batches of `bs`), extrapolated linearly to the
+    split, plus the C restatement of L2-normalise + distance + eval_func on the FULL Market
+    split (not extrapolated), `threads` host threads for both."""
     import oracle
     from oracle import vit_ref
-    cores = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    oracle.set_threads(threads)
     imgs = syn.images(n_img, seed=3)
     offs = syn.tta_offsets(n_img, seed=3)
     with torch.no_grad():
-        vit_ref.vit_forward(wl.sd, imgs[:1])  # warm
+        vit_ref.vit_forward(wl.sd, imgs[:bs])  # warm
         t = time.perf_counter()
-        _, a12, ap = vit_ref.vit_forward(wl.sd, imgs)
-        _, b12, bp = vit_ref.vit_forward(wl.sd, imgs, tta=offs)
+        for s in range(0, n_img, bs):
+            vit_ref.vit_forward(wl.sd, imgs[s:s + bs])
+            vit_ref.vit_forward(wl.sd, imgs[s:s + bs], tta=offs[s:s + bs])
         t_img = (time.perf_counter() - t) / n_img
     r = np.random.default_rng(0)
     gf = r.standard_normal((wl.G, 1280)).astype(np.float32)
-    qf = r.standard_normal((n_q, 1280)).astype(np.float32)
+    qf = r.standard_normal((wl.Q, 1280)).astype(np.float32)
     t = time.perf_counter()
     qn, gn = oracle.l2norm(qf), oracle.l2norm(gf)
     d = oracle.distmat(qn, gn)
-    oracle.eval_rows(d, wl.q_pids[:n_q], wl.g_pids, wl.q_cams[:n_q], wl.g_cams)
-    t_q = (time.perf_counter() - t) / n_q
-    total = (wl.Q + wl.G) * t_img + wl.Q * t_q
-    return {"value": round((wl.Q + wl.G) / total, 3), "unit": "imgs/s", "cores": cores, "kind": "port",
-            "sample": f"oracle/vit_ref.py fp32 ViT-B/16 on {n_img} images x 2 TTA passes "
-                      f"({t_img:.3f} s/img, torch {cores} threads) + oracle C distmat+eval for {n_q} queries x "
-                      f"{wl.G} gallery ({t_q * 1e3:.1f} ms/query, 1 thread); extrapolated linearly to "
-                      f"{wl.Q}q x {wl.G}g"}
+    oracle.eval_rows(d, wl.q_pids, wl.g_pids, wl.q_cams, wl.g_cams)
+    t_eval = time.perf_counter() - t
+    total = (wl.Q + wl.G) * t_img + t_eval
+    return {"value": round((wl.Q + wl.G) / total, 3), "unit": "imgs/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/vit_ref.py fp32 ViT-B/16 on {n_img} images x 2 TTA passes, batches of {bs} "
+                      f"({t_img:.3f} s/img, extrapolated linearly to {wl.Q + wl.G} images) + oracle C "
+                      f"l2norm+distmat+eval on the full {wl.Q}q x {wl.G}g split ({t_eval:.2f} s)"}
 
 
 def main():
@@ -317,11 +363,11 @@ def main():
     elapsed = time.perf_counter() - t0
     import ctypes
     ms, cnt, fl = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
-    # persistent-tile c_fc launches only (>= half a full batch; the CLS-only last block's small
-    # c_fc runs a different kernel), so avg_launch_ms is comparable with that kernel's row
-    # in the rocprofv3 --stats summary
+    # full-batch c_fc launches only (the splits' partial last batches and the CLS-only last
+    # block's small c_fc are left out), so flops_per_launch / avg_launch_ms is the rate of the
+    # M = batch * 211 launch the PMC traffic below was measured on
     full = 2.0 * a.batch * 211 * 3072 * 768
-    L.reidmi_prof_collect_min(EPI_GELU, ctypes.c_double(0.5 * full), ctypes.byref(ms), ctypes.byref(cnt),
+    L.reidmi_prof_collect_min(EPI_GELU, ctypes.c_double(full), ctypes.byref(ms), ctypes.byref(cnt),
                               ctypes.byref(fl))
     L.reidmi_prof_enable(0)
     if world > 1:
@@ -362,11 +408,13 @@ def main():
         }
         if ms17 is not None:
             line["msmt17"] = ms17
+        line["backend"] = backend_rooflines(wl)
         line["preprocess"] = preprocess_leg(dev)
+        threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
         if not a.no_rerank:
-            line["rerank"] = rerank_leg(dev, cpu=not a.no_cpu_baseline)
+            line["rerank"] = rerank_leg(dev, cpu=not a.no_cpu_baseline, threads=threads)
         if not a.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(wl)
+            line["cpu_baseline"] = cpu_baseline(wl, threads)
         print(json.dumps(line))
     if world > 1:
         dist.barrier()

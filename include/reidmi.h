@@ -155,7 +155,8 @@ int reidmi_prof_collect_min(int epi, double min_flops, double* total_ms, int64_t
 int reidmi_gemm_set_tile(int t);
 
 /* Persistent tile walk: the XCDs are split into ngroups (1, 2, 4, 8) groups, each owning
- * 1/ngroups of the N-tiles (smaller weight share per XCD L2).  Bit-identical results. */
+ * 1/ngroups of the N-tiles (smaller weight share per XCD L2); 0 = auto (default).
+ * Bit-identical results. */
 int reidmi_gemm_set_walk(int ngroups);
 
 /* Key padding used for an L-token sequence by the attention kernel (rows of v^T). */

@@ -558,7 +558,8 @@ constexpr int EV_MAXP = 2048;
 // Fallback for the queries eval_rows_wave_kernel left (valid == 2: more than EVW_MAXP
 // positives or EVW_MAXJ junk items): one workgroup per query, up to EV_MAXP positives.
 // Positives are collected and sorted; every other kept gallery item is binned by how many
-// positives precede it (binary search).  Queries beyond EV_MAXP set *overflow.
+// positives precede it (binary search).  Queries beyond EV_MAXP set *overflow and
+// valid = -1 (the host refuses to aggregate them).
 __global__ __launch_bounds__(256) void eval_rows_kernel(
     const float* __restrict__ dist, int64_t G, int64_t ld, const int64_t* __restrict__ qp,
     const int64_t* __restrict__ gp, const int64_t* __restrict__ qc, const int64_t* __restrict__ gc,
@@ -588,7 +589,7 @@ __global__ __launch_bounds__(256) void eval_rows_kernel(
     __syncthreads();
     const int m = s_m;
     if (m > EV_MAXP) {
-        if (threadIdx.x == 0) { atomicExch(overflow, 1); valid[q] = 0; first[q] = -1; ap[q] = 0.0; nkept[q] = G - s_junk; }
+        if (threadIdx.x == 0) { atomicExch(overflow, 1); valid[q] = -1; first[q] = -1; ap[q] = 0.0; nkept[q] = G - s_junk; }
         return;
     }
     const int P = pow2_ceil(m < 2 ? 2 : m);

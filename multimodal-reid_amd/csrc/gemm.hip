@@ -39,8 +39,11 @@ static size_t used = 0;
 // the GEMM has >= 256 of them, else 128x128), 1 = force 128x128, 2 = force persistent.
 static int g_tile = 0;
 // Persistent tile walk (reidmi_gemm_set_walk; see gemm_persistent_kernel): N-groups the
-// XCDs are split into (1 = every XCD walks all N-tiles of its M range).
-static int g_ngroups = 1;
+// XCDs are split into (1 = every XCD walks all N-tiles of its M range); 0 = auto: 2 groups
+// when the N-tiles split evenly and there are >= 8 of them (c_fc: 12 tiles, +2 %, 15 % less
+// L2 fetch; an uneven split idles the XCDs of the smaller group), else 1
+// (profiles/r02/walk_ab.txt).
+static int g_ngroups = 0;
 
 constexpr int GB_M = 128, GB_N = 128, GB_K = 64;
 
@@ -812,8 +815,9 @@ static int launch(const void* A, int64_t lda, const void* W, int64_t ldw, int64_
             attr = true;
         }
         const int grid = (int)(tiles256 < 256 ? tiles256 : 256);
+        const int ngroups = g_ngroups > 0 ? g_ngroups : (tiles_n % 2 == 0 && tiles_n >= 8 ? 2 : 1);
         hipLaunchKernelGGL((gemm_persistent_kernel<EPI>), dim3((unsigned)grid), dim3(512), lds, s, (const _Float16*)A,
-                           lda, (const _Float16*)W, ldw, M, (int)N, (int)K, ea, tiles_m, tiles_n, g_ngroups);
+                           lda, (const _Float16*)W, ldw, M, (int)N, (int)K, ea, tiles_m, tiles_n, ngroups);
         RM_LAUNCHED();
         return OK;
     }
@@ -877,7 +881,8 @@ REIDMI_API int reidmi_gemm_set_tile(int t) {
 }
 
 REIDMI_API int reidmi_gemm_set_walk(int ngroups) {
-    RM_REQUIRE(ngroups == 1 || ngroups == 2 || ngroups == 4 || ngroups == 8, "gemm walk: ngroups in {1, 2, 4, 8}");
+    RM_REQUIRE(ngroups == 0 || ngroups == 1 || ngroups == 2 || ngroups == 4 || ngroups == 8,
+               "gemm walk: ngroups in {0 (auto), 1, 2, 4, 8}");
     g_ngroups = ngroups;
     return OK;
 }

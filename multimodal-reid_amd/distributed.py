@@ -87,7 +87,8 @@ def pack_rows(valid, first, ap, nkept):
 
 def unpack_rows(rows):
     rows = rows.cpu().numpy() if isinstance(rows, torch.Tensor) else rows
-    return rows[:, 0] > 0, rows[:, 1].astype(np.int64), rows[:, 2], rows[:, 3].astype(np.int64)
+    # valid keeps its sign: -1 = a query beyond eval_rows' capacity (aggregate_cmc_map raises)
+    return rows[:, 0].astype(np.int64), rows[:, 1].astype(np.int64), rows[:, 2], rows[:, 3].astype(np.int64)
 
 
 def sharded_eval(q_feat, g_feat, q_pids, g_pids, q_camids, g_camids, num_query, num_gallery, rows_fn, max_rank=50,

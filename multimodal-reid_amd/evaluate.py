@@ -74,7 +74,8 @@ def topk_rows_device(x, k, row_div=None, with_values=False):
 
 
 def eval_rows_device(dist, q_pids, g_pids, q_camids, g_camids):
-    """Per-query (valid, first_match_rank, AP, n_kept) for eval_func (evaluate.py:40-80)."""
+    """Per-query (valid, first_match_rank, AP, n_kept) for eval_func (evaluate.py:40-80);
+    valid = -1 marks a query beyond the kernel's positive-list capacity (aggregate refuses it)."""
     dist = _as_dev_f32(dist)
     Q, G = dist.shape
     qp, gp, qc, gc = (_as_dev_i64(a) for a in (q_pids, g_pids, q_camids, g_camids))
@@ -93,9 +94,11 @@ def eval_rows_device(dist, q_pids, g_pids, q_camids, g_camids):
 def aggregate_cmc_map(valid, first, ap, nkept, num_g, max_rank=50, overflow=None):
     """evaluate.py:37-39,82-88 on the per-query results, with numpy's exact arithmetic:
     CMC = float32 count / float32 num_valid, mAP = np.mean of the float64 APs in query order."""
-    if overflow is not None and int(np.asarray(overflow).reshape(-1)[0]):
+    valid = np.asarray(valid)
+    if (overflow is not None and int(np.asarray(overflow).reshape(-1)[0])) or \
+            (valid.dtype != bool and (valid < 0).any()):
         raise _lib.ReidmiError("eval_rows: a query has more than 2048 positives (kernel capacity)")
-    valid = np.asarray(valid).astype(bool)
+    valid = valid > 0
     first, ap, nkept = np.asarray(first), np.asarray(ap), np.asarray(nkept)
     if num_g < max_rank:
         max_rank = num_g

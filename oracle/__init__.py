@@ -36,6 +36,11 @@ def build():
     subprocess.run(["make", "-s", "-C", HERE], check=True)
 
 
+def set_threads(n):
+    """Worker threads of the C restatement's parallel loops (results do not depend on it)."""
+    lib().orc_set_threads(int(n))
+
+
 def lib():
     global _LIB
     if _LIB is None:

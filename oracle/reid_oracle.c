@@ -22,11 +22,63 @@
  *  - numpy float32 pairwise sum (PW_BLOCKSIZE 128, 8 accumulators).
  *  - numpy float16 ufuncs: op in float32 then round-to-nearest-even to half.
  * Build with -ffp-contract=off (no implicit FMA) — see oracle/Makefile.
+ *
+ * Threads (orc_set_threads, pthreads): rows / queries / column blocks are independent, so
+ * every parallel loop computes exactly what the serial one does (bench.py times the CPU
+ * baseline with the host's cores).  The distance kernel vectorises across gallery columns
+ * with AVX2 FMA (IEEE fused multiply-add == fmaf, same k order) when the CPU has it.
  */
+#include <immintrin.h>
 #include <math.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+
+/* ------------------------------------------------------------- threads ---- */
+static int g_threads = 1;
+void orc_set_threads(int n) { g_threads = n < 1 ? 1 : (n > 256 ? 256 : n); }
+int orc_get_threads(void) { return g_threads; }
+
+typedef void (*range_fn)(int64_t lo, int64_t hi, int tid, void* ctx);
+typedef struct {
+    range_fn fn;
+    void* ctx;
+    int64_t n, chunk;
+    int64_t* next;
+    int tid;
+} job_t;
+
+static void* run_job(void* p) {
+    job_t* j = (job_t*)p;
+    for (;;) {
+        int64_t lo = __atomic_fetch_add(j->next, j->chunk, __ATOMIC_RELAXED);
+        if (lo >= j->n) break;
+        int64_t hi = lo + j->chunk < j->n ? lo + j->chunk : j->n;
+        j->fn(lo, hi, j->tid, j->ctx);
+    }
+    return NULL;
+}
+
+/* fn(lo, hi, tid, ctx) over [0, n) in dynamic chunks; tid < orc_get_threads() */
+static void par_for(int64_t n, int64_t chunk, range_fn fn, void* ctx) {
+    int t = g_threads;
+    if (chunk < 1) chunk = 1;
+    if ((int64_t)t > (n + chunk - 1) / chunk) t = (int)((n + chunk - 1) / chunk);
+    if (t <= 1) {
+        if (n > 0) fn(0, n, 0, ctx);
+        return;
+    }
+    int64_t next = 0;
+    pthread_t th[256];
+    job_t jobs[256];
+    for (int i = 0; i < t; i++) {
+        jobs[i] = (job_t){fn, ctx, n, chunk, &next, i};
+        if (i > 0) pthread_create(&th[i], NULL, run_job, &jobs[i]);
+    }
+    run_job(&jobs[0]);
+    for (int i = 1; i < t; i++) pthread_join(th[i], NULL);
+}
 
 /* ---------------------------------------------------------------- fp16 ---- */
 uint16_t orc_f2h(float f) {
@@ -135,19 +187,90 @@ void orc_l2norm(const float* x, float* y, int64_t n, int64_t d) {
     }
 }
 
-/* ||q||^2 + ||g||^2 - 2 q.g   (evaluate.py:7-13; reranking.py:36-41) */
-void orc_distmat(const float* q, const float* g, int64_t Q, int64_t G, int64_t D, float* out) {
-    float* gg = (float*)malloc(sizeof(float) * (size_t)(G > 0 ? G : 1));
-    for (int64_t j = 0; j < G; j++) gg[j] = sqnorm(g + j * D, D);
-    for (int64_t i = 0; i < Q; i++) {
-        float qq = sqnorm(q + i * D, D);
-        for (int64_t j = 0; j < G; j++) {
+/* ||q||^2 + ||g||^2 - 2 q.g   (evaluate.py:7-13; reranking.py:36-41): per pair an fmaf chain
+ * over k ascending, then fmaf(-2, dot, qq + gg). */
+typedef struct {
+    const float *q, *g;
+    int64_t Q, G, D;
+    const float *qq, *gg;
+    float* out;
+} dist_ctx;
+
+static void sqnorm_rows(int64_t lo, int64_t hi, int tid, void* c) {
+    (void)tid;
+    float** a = (float**)c;
+    const float* x = a[0];
+    float* o = a[1];
+    int64_t d = (int64_t)(intptr_t)a[2];
+    for (int64_t i = lo; i < hi; i++) o[i] = sqnorm(x + i * d, d);
+}
+
+static void dist_scalar(int64_t lo, int64_t hi, int tid, void* c) {
+    (void)tid;
+    const dist_ctx* x = (const dist_ctx*)c;
+    for (int64_t i = lo; i < hi; i++)
+        for (int64_t j = 0; j < x->G; j++) {
             float acc = 0.0f;
-            const float* a = q + i * D; const float* b = g + j * D;
-            for (int64_t k = 0; k < D; k++) acc = fmaf(a[k], b[k], acc);
-            out[i * G + j] = fmaf(-2.0f, acc, qq + gg[j]);
+            const float* a = x->q + i * x->D; const float* b = x->g + j * x->D;
+            for (int64_t k = 0; k < x->D; k++) acc = fmaf(a[k], b[k], acc);
+            x->out[i * x->G + j] = fmaf(-2.0f, acc, x->qq[i] + x->gg[j]);
+        }
+}
+
+/* one block of DB gallery columns: transposed into gT [D][DB], then 4 query rows x 16
+ * columns per register tile (8 accumulators, k ascending: the fmaf chain of every pair) */
+#define DB 256
+__attribute__((target("avx2,fma"))) static void dist_avx2(int64_t lo, int64_t hi, int tid, void* c) {
+    (void)tid;
+    const dist_ctx* x = (const dist_ctx*)c;
+    const int64_t D = x->D, G = x->G, Q = x->Q;
+    float* gT = (float*)aligned_alloc(64, sizeof(float) * (size_t)(D * DB));
+    for (int64_t jb = lo; jb < hi; jb++) {
+        const int64_t j0 = jb * DB, nj = G - j0 < DB ? G - j0 : DB;
+        for (int64_t t = 0; t < DB; t++)
+            for (int64_t k = 0; k < D; k++) gT[k * DB + t] = t < nj ? x->g[(j0 + t) * D + k] : 0.0f;
+        for (int64_t i0 = 0; i0 < Q; i0 += 4) {
+            const int64_t ni = Q - i0 < 4 ? Q - i0 : 4;
+            const float* a[4];
+            for (int r = 0; r < 4; r++) a[r] = x->q + (i0 + (r < ni ? r : 0)) * D;
+            for (int64_t t0 = 0; t0 < nj; t0 += 16) {
+                __m256 acc[4][2];
+                for (int r = 0; r < 4; r++) acc[r][0] = acc[r][1] = _mm256_setzero_ps();
+                for (int64_t k = 0; k < D; k++) {
+                    const __m256 b0 = _mm256_load_ps(gT + k * DB + t0), b1 = _mm256_load_ps(gT + k * DB + t0 + 8);
+                    for (int r = 0; r < 4; r++) {
+                        const __m256 av = _mm256_set1_ps(a[r][k]);
+                        acc[r][0] = _mm256_fmadd_ps(av, b0, acc[r][0]);
+                        acc[r][1] = _mm256_fmadd_ps(av, b1, acc[r][1]);
+                    }
+                }
+                float tmp[16];
+                for (int r = 0; r < ni; r++) {
+                    _mm256_storeu_ps(tmp, acc[r][0]);
+                    _mm256_storeu_ps(tmp + 8, acc[r][1]);
+                    for (int64_t t = 0; t < 16 && t0 + t < nj; t++)
+                        x->out[(i0 + r) * G + j0 + t0 + t] = fmaf(-2.0f, tmp[t], x->qq[i0 + r] + x->gg[j0 + t0 + t]);
+                }
+            }
         }
     }
+    free(gT);
+}
+
+void orc_distmat(const float* q, const float* g, int64_t Q, int64_t G, int64_t D, float* out) {
+    float* qq = (float*)malloc(sizeof(float) * (size_t)(Q > 0 ? Q : 1));
+    float* gg = (float*)malloc(sizeof(float) * (size_t)(G > 0 ? G : 1));
+    void* a1[3] = {(void*)q, qq, (void*)(intptr_t)D};
+    void* a2[3] = {(void*)g, gg, (void*)(intptr_t)D};
+    par_for(Q, 256, sqnorm_rows, a1);
+    par_for(G, 256, sqnorm_rows, a2);
+    dist_ctx c = {q, g, Q, G, D, qq, gg, out};
+    __builtin_cpu_init();
+    if (__builtin_cpu_supports("avx2") && __builtin_cpu_supports("fma"))
+        par_for((G + DB - 1) / DB, 1, dist_avx2, &c);
+    else
+        par_for(Q, 4, dist_scalar, &c);
+    free(qq);
     free(gg);
 }
 
@@ -166,14 +289,39 @@ static void argsort_row(const float* row, int64_t n, kv_t* tmp, int32_t* idx) {
     for (int64_t j = 0; j < n; j++) idx[j] = tmp[j].i;
 }
 
-void orc_topk_rows(const float* dist, int64_t Q, int64_t G, int64_t k, int32_t* out) {
-    kv_t* tmp = (kv_t*)malloc(sizeof(kv_t) * (size_t)G);
-    int32_t* idx = (int32_t*)malloc(sizeof(int32_t) * (size_t)G);
-    for (int64_t i = 0; i < Q; i++) {
-        argsort_row(dist + i * G, G, tmp, idx);
-        memcpy(out + i * k, idx, sizeof(int32_t) * (size_t)k);
+/* first k of the stable argsort of each row: a sorted insertion buffer of the k smallest
+ * (value, index) keys (== the full stable sort's prefix) */
+typedef struct {
+    const float* x;
+    int64_t G, k;
+    int32_t* out;
+} topk_ctx;
+
+static int kv_less(float av, int32_t ai, float bv, int32_t bi) { return av < bv || (av == bv && ai < bi); }
+
+static void topk_part(int64_t lo, int64_t hi, int tid, void* c) {
+    (void)tid;
+    const topk_ctx* t = (const topk_ctx*)c;
+    kv_t* buf = (kv_t*)malloc(sizeof(kv_t) * (size_t)t->k);
+    for (int64_t i = lo; i < hi; i++) {
+        const float* row = t->x + i * t->G;
+        int64_t n = 0;
+        for (int64_t j = 0; j < t->G; j++) {
+            const float v = row[j];
+            if (n == t->k && !kv_less(v, (int32_t)j, buf[n - 1].v, buf[n - 1].i)) continue;
+            int64_t p = n < t->k ? n++ : n - 1;
+            while (p > 0 && kv_less(v, (int32_t)j, buf[p - 1].v, buf[p - 1].i)) { buf[p] = buf[p - 1]; p--; }
+            buf[p].v = v;
+            buf[p].i = (int32_t)j;
+        }
+        for (int64_t r = 0; r < t->k; r++) t->out[i * t->k + r] = buf[r].i;
     }
-    free(tmp); free(idx);
+    free(buf);
+}
+
+void orc_topk_rows(const float* dist, int64_t Q, int64_t G, int64_t k, int32_t* out) {
+    topk_ctx c = {dist, G, k, out};
+    par_for(Q, 16, topk_part, &c);
 }
 
 /* ------------------------------------------------------------- eval_func */
@@ -182,30 +330,47 @@ void orc_topk_rows(const float* dist, int64_t Q, int64_t G, int64_t k, int32_t* 
  *   first[q]  = 0-based position of the first match among kept items
  *   ap[q]     = AP exactly as numpy computes it (cumsum/arange*orig_cmc, pairwise sum / num_rel)
  *   nkept[q]  = number of kept gallery items (length of orig_cmc)            */
-void orc_eval_rows(const float* dist, int64_t Q, int64_t G, const int64_t* qp, const int64_t* gp,
-                   const int64_t* qc, const int64_t* gc, int32_t* valid, int64_t* first, double* ap,
-                   int64_t* nkept) {
+typedef struct {
+    const float* dist;
+    int64_t G;
+    const int64_t *qp, *gp, *qc, *gc;
+    int32_t* valid;
+    int64_t *first, *nkept;
+    double* ap;
+} eval_ctx;
+
+static void eval_part(int64_t lo, int64_t hi, int tid, void* c) {
+    (void)tid;
+    const eval_ctx* e = (const eval_ctx*)c;
+    const int64_t G = e->G;
     kv_t* tmp = (kv_t*)malloc(sizeof(kv_t) * (size_t)G);
     int32_t* idx = (int32_t*)malloc(sizeof(int32_t) * (size_t)G);
     double* t = (double*)malloc(sizeof(double) * (size_t)G);
-    for (int64_t q = 0; q < Q; q++) {
-        argsort_row(dist + q * G, G, tmp, idx);
+    for (int64_t q = lo; q < hi; q++) {
+        argsort_row(e->dist + q * G, G, tmp, idx);
         int64_t n = 0, hits = 0, f = -1;
         for (int64_t j = 0; j < G; j++) {
             int32_t g = idx[j];
-            if (gp[g] == qp[q] && gc[g] == qc[q]) continue; /* remove */
-            int m = gp[g] == qp[q];
+            if (e->gp[g] == e->qp[q] && e->gc[g] == e->qc[q]) continue; /* remove */
+            int m = e->gp[g] == e->qp[q];
             if (m) { hits++; if (f < 0) f = n; }
             /* tmp_cmc = cumsum / arange(1..) ; * orig_cmc  (evaluate.py:74-78) */
             t[n] = m ? (double)hits / (double)(n + 1) : 0.0;
             n++;
         }
-        nkept[q] = n;
-        valid[q] = hits > 0;
-        first[q] = f;
-        ap[q] = hits > 0 ? orc_pairwise_f64(t, n) / (double)hits : 0.0;
+        e->nkept[q] = n;
+        e->valid[q] = hits > 0;
+        e->first[q] = f;
+        e->ap[q] = hits > 0 ? orc_pairwise_f64(t, n) / (double)hits : 0.0;
     }
     free(tmp); free(idx); free(t);
+}
+
+void orc_eval_rows(const float* dist, int64_t Q, int64_t G, const int64_t* qp, const int64_t* gp,
+                   const int64_t* qc, const int64_t* gc, int32_t* valid, int64_t* first, double* ap,
+                   int64_t* nkept) {
+    eval_ctx c = {dist, G, qp, gp, qc, gc, valid, first, nkept, ap};
+    par_for(Q, 4, eval_part, &c);
 }
 
 /* ------------------------------------------------------------- re_ranking */
@@ -232,88 +397,129 @@ static int kreciprocal(const int32_t* R, int64_t ldr, int32_t i, int kk1, int32_
  * numpy weak-scalar conversions of reranking.py:95 (the caller makes them with numpy).
  * final: Q x (N-Q) float32.  Optional debug outputs (may be NULL):
  * rank_out N x K int32 (K = min(max(k1+1,k2), N)), vqe_out N x N fp16 bits, jac_out Q x N fp16 bits. */
-int orc_rerank_from_dist(const float* D, int64_t N, int64_t Q, int k1, int k2, uint16_t one_minus_lambda_h,
-                         float lambda_f, float* final_out, int32_t* rank_out, uint16_t* vqe_out, uint16_t* jac_out) {
-    int64_t G = N - Q;
-    /* R2: od = transpose(D / max(D, axis=0))  (reranking.py:46) */
-    float* colmax = (float*)malloc(sizeof(float) * (size_t)N);
-    for (int64_t c = 0; c < N; c++) colmax[c] = D[c];
-    for (int64_t r = 1; r < N; r++)
-        for (int64_t c = 0; c < N; c++) if (D[r * N + c] > colmax[c]) colmax[c] = D[r * N + c];
-    float* od = (float*)malloc(sizeof(float) * (size_t)(N * N));
-    for (int64_t i = 0; i < N; i++)
-        for (int64_t j = 0; j < N; j++) od[i * N + j] = D[j * N + i] / colmax[i];
-    /* initial_rank = argsort(od) (stable), first K columns (reranking.py:48) */
-    int64_t K = k1 + 1 > k2 ? k1 + 1 : k2; if (K > N) K = N;
-    int32_t* R = (int32_t*)malloc(sizeof(int32_t) * (size_t)(N * K));
-    orc_topk_rows(od, N, N, K, R);
-    if (rank_out) memcpy(rank_out, R, sizeof(int32_t) * (size_t)(N * K));
-    int kf = (int)(k1 + 1 < N ? k1 + 1 : N);
-    int kh = (int)nearbyint((double)k1 / 2.0); /* int(np.around(k1/2)) (round half even) */
-    int kh1 = kh + 1 < N ? kh + 1 : (int)N;
-    /* R3: V (dense fp16 bits) */
-    uint16_t* V = (uint16_t*)calloc((size_t)(N * N), sizeof(uint16_t));
+typedef struct {
+    const float* D;
+    float* od;
+    float* colmax;
+    float* part;  /* [nchunk][N] partial column maxima */
+    int64_t N, Q, K, nchunk;
+    const int32_t* R;
+    int kf, kh1, k2;
+    uint16_t *V, *Vq;
+    int64_t *ccnt, *cnt;  /* [nchunk][N+1] per-chunk column counts / positions; cnt [N+1] */
+    int32_t* inv;
+    uint16_t lam16;
+    float lam_f;
+    float* final_out;
+    uint16_t* jac_out;
+    uint16_t* tmin;  /* [threads][N] */
+} rr_ctx;
+
+static void rr_colmax(int64_t lo, int64_t hi, int tid, void* c) {
+    (void)tid;
+    rr_ctx* x = (rr_ctx*)c;
+    const int64_t N = x->N;
+    for (int64_t ch = lo; ch < hi; ch++) {
+        float* m = x->part + ch * N;
+        const int64_t r0 = N * ch / x->nchunk, r1 = N * (ch + 1) / x->nchunk;
+        for (int64_t cc = 0; cc < N; cc++) m[cc] = x->D[r0 * N + cc];
+        for (int64_t r = r0 + 1; r < r1; r++)
+            for (int64_t cc = 0; cc < N; cc++) if (x->D[r * N + cc] > m[cc]) m[cc] = x->D[r * N + cc];
+    }
+}
+
+static void rr_od(int64_t lo, int64_t hi, int tid, void* c) {
+    (void)tid;
+    rr_ctx* x = (rr_ctx*)c;
+    const int64_t N = x->N;
+    for (int64_t i = lo; i < hi; i++)
+        for (int64_t j = 0; j < N; j++) x->od[i * N + j] = x->D[j * N + i] / x->colmax[i];
+}
+
+static void rr_v(int64_t lo, int64_t hi, int tid, void* c) {
+    (void)tid;
+    rr_ctx* x = (rr_ctx*)c;
+    const int64_t N = x->N, K = x->K;
+    const int kf = x->kf, kh1 = x->kh1;
     int32_t* kr = (int32_t*)malloc(sizeof(int32_t) * (size_t)kf);
     int32_t* ckr = (int32_t*)malloc(sizeof(int32_t) * (size_t)kh1);
     int32_t* exp_idx = (int32_t*)malloc(sizeof(int32_t) * (size_t)(kf + (int64_t)kf * kh1));
     float* w = (float*)malloc(sizeof(float) * (size_t)(kf + (int64_t)kf * kh1));
-    for (int64_t i = 0; i < N; i++) {
-        int nk = kreciprocal(R, K, (int32_t)i, kf, kr);
+    for (int64_t i = lo; i < hi; i++) {
+        int nk = kreciprocal(x->R, K, (int32_t)i, kf, kr);
         int ne = 0;
         for (int a = 0; a < nk; a++) exp_idx[ne++] = kr[a];
         for (int a = 0; a < nk; a++) {
-            int nc = kreciprocal(R, K, kr[a], kh1, ckr);
+            int nc = kreciprocal(x->R, K, kr[a], kh1, ckr);
             int inter = 0;
             for (int b = 0; b < nc; b++)
-                for (int c = 0; c < nk; c++) if (ckr[b] == kr[c]) { inter++; break; }
+                for (int cc = 0; cc < nk; cc++) if (ckr[b] == kr[cc]) { inter++; break; }
             if ((double)inter > 2.0 / 3.0 * (double)nc)
                 for (int b = 0; b < nc; b++) exp_idx[ne++] = ckr[b];
         }
         qsort(exp_idx, (size_t)ne, sizeof(int32_t), cmp_i32);
         int nu = 0;
         for (int a = 0; a < ne; a++) if (nu == 0 || exp_idx[a] != exp_idx[nu - 1]) exp_idx[nu++] = exp_idx[a];
-        for (int a = 0; a < nu; a++) w[a] = orc_np_expf(-od[i * N + exp_idx[a]]);
+        for (int a = 0; a < nu; a++) w[a] = orc_np_expf(-x->od[i * N + exp_idx[a]]);
         float s = orc_pairwise_f32(w, nu);
-        for (int a = 0; a < nu; a++) V[i * N + exp_idx[a]] = orc_f2h(w[a] / s);
+        for (int a = 0; a < nu; a++) x->V[i * N + exp_idx[a]] = orc_f2h(w[a] / s);
     }
-    /* R4: query expansion (reranking.py:73-78) */
-    if (k2 != 1) {
-        uint16_t* Vq = (uint16_t*)malloc(sizeof(uint16_t) * (size_t)(N * N));
-        float* acc = (float*)malloc(sizeof(float) * (size_t)N);
-        for (int64_t i = 0; i < N; i++) {
-            for (int64_t c = 0; c < N; c++) acc[c] = 0.0f;
-            for (int r = 0; r < k2; r++) {
-                const uint16_t* row = V + (int64_t)R[i * K + r] * N;
-                for (int64_t c = 0; c < N; c++) acc[c] += orc_h2f(row[c]);
-            }
-            for (int64_t c = 0; c < N; c++) Vq[i * N + c] = orc_f2h(acc[c] / (float)k2);
+    free(kr); free(ckr); free(exp_idx); free(w);
+}
+
+static void rr_qe(int64_t lo, int64_t hi, int tid, void* c) {
+    (void)tid;
+    rr_ctx* x = (rr_ctx*)c;
+    const int64_t N = x->N;
+    float* acc = (float*)malloc(sizeof(float) * (size_t)N);
+    for (int64_t i = lo; i < hi; i++) {
+        for (int64_t cc = 0; cc < N; cc++) acc[cc] = 0.0f;
+        for (int r = 0; r < x->k2; r++) {
+            const uint16_t* row = x->V + (int64_t)x->R[i * x->K + r] * N;
+            for (int64_t cc = 0; cc < N; cc++) acc[cc] += orc_h2f(row[cc]);
         }
-        free(acc); free(V); V = Vq;
+        for (int64_t cc = 0; cc < N; cc++) x->Vq[i * N + cc] = orc_f2h(acc[cc] / (float)x->k2);
     }
-    if (vqe_out) memcpy(vqe_out, V, sizeof(uint16_t) * (size_t)(N * N));
-    /* R5: invIndex (reranking.py:80-82) as column lists, rows ascending */
-    int64_t* cnt = (int64_t*)calloc((size_t)N + 1, sizeof(int64_t));
-    for (int64_t r = 0; r < N; r++)
-        for (int64_t c = 0; c < N; c++) if (V[r * N + c] & 0x7fffu) cnt[c + 1]++;
-    for (int64_t c = 0; c < N; c++) cnt[c + 1] += cnt[c];
-    int32_t* inv = (int32_t*)malloc(sizeof(int32_t) * (size_t)(cnt[N] > 0 ? cnt[N] : 1));
-    int64_t* pos = (int64_t*)malloc(sizeof(int64_t) * (size_t)N);
-    for (int64_t c = 0; c < N; c++) pos[c] = cnt[c];
-    for (int64_t r = 0; r < N; r++)
-        for (int64_t c = 0; c < N; c++) if (V[r * N + c] & 0x7fffu) inv[pos[c]++] = (int32_t)r;
-    /* R6: Jaccard (reranking.py:84-93) with fp16 sequential accumulation */
-    uint16_t* tmin = (uint16_t*)malloc(sizeof(uint16_t) * (size_t)N);
-    uint16_t lam16 = one_minus_lambda_h;
-    float lam_f = lambda_f;
-    for (int64_t i = 0; i < Q; i++) {
+    free(acc);
+}
+
+static void rr_count(int64_t lo, int64_t hi, int tid, void* c) {
+    (void)tid;
+    rr_ctx* x = (rr_ctx*)c;
+    const int64_t N = x->N;
+    for (int64_t ch = lo; ch < hi; ch++) {
+        int64_t* cn = x->ccnt + ch * (N + 1);
+        for (int64_t cc = 0; cc <= N; cc++) cn[cc] = 0;
+        for (int64_t r = N * ch / x->nchunk; r < N * (ch + 1) / x->nchunk; r++)
+            for (int64_t cc = 0; cc < N; cc++) if (x->V[r * N + cc] & 0x7fffu) cn[cc]++;
+    }
+}
+
+static void rr_fill(int64_t lo, int64_t hi, int tid, void* c) {
+    (void)tid;
+    rr_ctx* x = (rr_ctx*)c;
+    const int64_t N = x->N;
+    for (int64_t ch = lo; ch < hi; ch++) {
+        int64_t* pos = x->ccnt + ch * (N + 1);  /* positions of this chunk's first entry per column */
+        for (int64_t r = N * ch / x->nchunk; r < N * (ch + 1) / x->nchunk; r++)
+            for (int64_t cc = 0; cc < N; cc++) if (x->V[r * N + cc] & 0x7fffu) x->inv[pos[cc]++] = (int32_t)r;
+    }
+}
+
+static void rr_jaccard(int64_t lo, int64_t hi, int tid, void* c) {
+    rr_ctx* x = (rr_ctx*)c;
+    const int64_t N = x->N, Q = x->Q, G = N - Q;
+    const uint16_t* V = x->V;
+    uint16_t* tmin = x->tmin + (int64_t)tid * N;
+    for (int64_t i = lo; i < hi; i++) {
         for (int64_t r = 0; r < N; r++) tmin[r] = 0;
-        for (int64_t c = 0; c < N; c++) {
-            uint16_t vi = V[i * N + c];
+        for (int64_t cc = 0; cc < N; cc++) {
+            uint16_t vi = V[i * N + cc];
             if (!(vi & 0x7fffu)) continue;
             float fvi = orc_h2f(vi);
-            for (int64_t p = cnt[c]; p < cnt[c + 1]; p++) {
-                int32_t r = inv[p];
-                float fvr = orc_h2f(V[(int64_t)r * N + c]);
+            for (int64_t p = x->cnt[cc]; p < x->cnt[cc + 1]; p++) {
+                int32_t r = x->inv[p];
+                float fvr = orc_h2f(V[(int64_t)r * N + cc]);
                 float mn = fvr < fvi ? fvr : fvi;               /* np.minimum (fp16) */
                 tmin[r] = orc_f2h(orc_h2f(tmin[r]) + mn);        /* fp16 + fp16 -> fp16 */
             }
@@ -323,17 +529,80 @@ int orc_rerank_from_dist(const float* D, int64_t N, int64_t Q, int k1, int k2, u
             uint16_t den = orc_f2h(2.0f - t);                       /* 2 - temp_min   */
             uint16_t qt = orc_f2h(t / orc_h2f(den));                /* temp_min / (.) */
             uint16_t jac = orc_f2h(1.0f - orc_h2f(qt));             /* 1 - (.)        */
-            if (jac_out) jac_out[i * N + r] = jac;
+            if (x->jac_out) x->jac_out[i * N + r] = jac;
             if (r >= Q) {
                 /* R7: jaccard*(1-lambda) [fp16] + original_dist*lambda [fp32] (reranking.py:95) */
-                float a = orc_h2f(orc_f2h(orc_h2f(jac) * orc_h2f(lam16)));
-                float b = od[i * N + r] * lam_f;
-                final_out[i * G + (r - Q)] = a + b;
+                float a = orc_h2f(orc_f2h(orc_h2f(jac) * orc_h2f(x->lam16)));
+                float b = x->od[i * N + r] * x->lam_f;
+                x->final_out[i * G + (r - Q)] = a + b;
             }
         }
     }
-    free(colmax); free(od); free(R); free(V); free(kr); free(ckr); free(exp_idx); free(w);
-    free(cnt); free(inv); free(pos); free(tmin);
+}
+
+int orc_rerank_from_dist(const float* D, int64_t N, int64_t Q, int k1, int k2, uint16_t one_minus_lambda_h,
+                         float lambda_f, float* final_out, int32_t* rank_out, uint16_t* vqe_out, uint16_t* jac_out) {
+    rr_ctx x;
+    memset(&x, 0, sizeof(x));
+    x.D = D; x.N = N; x.Q = Q; x.k2 = k2; x.lam16 = one_minus_lambda_h; x.lam_f = lambda_f;
+    x.final_out = final_out; x.jac_out = jac_out;
+    x.nchunk = g_threads < N ? g_threads : N;
+    /* R2: od = transpose(D / max(D, axis=0))  (reranking.py:46) */
+    x.part = (float*)malloc(sizeof(float) * (size_t)(x.nchunk * N));
+    par_for(x.nchunk, 1, rr_colmax, &x);
+    x.colmax = (float*)malloc(sizeof(float) * (size_t)N);
+    for (int64_t cc = 0; cc < N; cc++) {
+        float m = x.part[cc];
+        for (int64_t ch = 1; ch < x.nchunk; ch++) if (x.part[ch * N + cc] > m) m = x.part[ch * N + cc];
+        x.colmax[cc] = m;
+    }
+    free(x.part);
+    x.od = (float*)malloc(sizeof(float) * (size_t)(N * N));
+    par_for(N, 64, rr_od, &x);
+    /* initial_rank = argsort(od) (stable), first K columns (reranking.py:48) */
+    int64_t K = k1 + 1 > k2 ? k1 + 1 : k2; if (K > N) K = N;
+    x.K = K;
+    int32_t* R = (int32_t*)malloc(sizeof(int32_t) * (size_t)(N * K));
+    orc_topk_rows(x.od, N, N, K, R);
+    x.R = R;
+    if (rank_out) memcpy(rank_out, R, sizeof(int32_t) * (size_t)(N * K));
+    x.kf = (int)(k1 + 1 < N ? k1 + 1 : N);
+    int kh = (int)nearbyint((double)k1 / 2.0); /* int(np.around(k1/2)) (round half even) */
+    x.kh1 = kh + 1 < N ? kh + 1 : (int)N;
+    /* R3: V (dense fp16 bits), reranking.py:51-71 */
+    x.V = (uint16_t*)calloc((size_t)(N * N), sizeof(uint16_t));
+    par_for(N, 16, rr_v, &x);
+    /* R4: query expansion (reranking.py:73-78) */
+    if (k2 != 1) {
+        x.Vq = (uint16_t*)malloc(sizeof(uint16_t) * (size_t)(N * N));
+        par_for(N, 16, rr_qe, &x);
+        free(x.V);
+        x.V = x.Vq;
+    }
+    if (vqe_out) memcpy(vqe_out, x.V, sizeof(uint16_t) * (size_t)(N * N));
+    /* R5: invIndex (reranking.py:80-82) as column lists, rows ascending (row chunks in order) */
+    x.ccnt = (int64_t*)malloc(sizeof(int64_t) * (size_t)(x.nchunk * (N + 1)));
+    par_for(x.nchunk, 1, rr_count, &x);
+    x.cnt = (int64_t*)calloc((size_t)N + 1, sizeof(int64_t));
+    for (int64_t cc = 0; cc < N; cc++) {
+        int64_t tot = 0;
+        for (int64_t ch = 0; ch < x.nchunk; ch++) tot += x.ccnt[ch * (N + 1) + cc];
+        x.cnt[cc + 1] = x.cnt[cc] + tot;
+    }
+    for (int64_t cc = 0; cc < N; cc++) {
+        int64_t p = x.cnt[cc];
+        for (int64_t ch = 0; ch < x.nchunk; ch++) {
+            const int64_t n = x.ccnt[ch * (N + 1) + cc];
+            x.ccnt[ch * (N + 1) + cc] = p;
+            p += n;
+        }
+    }
+    x.inv = (int32_t*)malloc(sizeof(int32_t) * (size_t)(x.cnt[N] > 0 ? x.cnt[N] : 1));
+    par_for(x.nchunk, 1, rr_fill, &x);
+    /* R6 + R7: Jaccard (reranking.py:84-100) with fp16 sequential accumulation */
+    x.tmin = (uint16_t*)malloc(sizeof(uint16_t) * (size_t)(g_threads * N));
+    par_for(Q, 4, rr_jaccard, &x);
+    free(x.colmax); free(x.od); free(R); free(x.V); free(x.ccnt); free(x.cnt); free(x.inv); free(x.tmin);
     return 0;
 }
 

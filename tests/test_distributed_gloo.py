@@ -79,3 +79,16 @@ def test_shard_partition():
             assert all(parts[i][1] == parts[i + 1][0] for i in range(w - 1))
             sizes = [b - a for a, b in parts]
             assert max(sizes) - min(sizes) <= 1
+
+
+def test_aggregate_refuses_overflowed_queries():
+    """valid = -1 (a query beyond eval_rows' positive-list capacity) travels through the
+    gathered per-query rows and makes the aggregation raise instead of reporting a wrong AP."""
+    from multimodal_reid_amd import _lib
+    from multimodal_reid_amd.distributed import pack_rows, unpack_rows
+    from multimodal_reid_amd.evaluate import aggregate_cmc_map
+    rows = pack_rows(np.array([1, -1, 1]), np.array([0, -1, 3]), np.array([1.0, 0.0, 0.25]), np.array([90, 90, 90]))
+    with pytest.raises(_lib.ReidmiError):
+        aggregate_cmc_map(*unpack_rows(rows), 100, 50)
+    cmc, mAP = aggregate_cmc_map(*unpack_rows(rows[[0, 2]]), 100, 50)
+    assert mAP == np.mean([1.0, 0.25]) and cmc[0] == 0.5 and cmc[3] == 1.0

@@ -86,7 +86,7 @@ def test_gemm_tiles_and_walks_bitexact(gpu, epi, M, N, K):
         _gemm(L, epi, A, W, bias, out)
         outs.append(out)
     L.call("reidmi_gemm_set_tile", 0)
-    L.call("reidmi_gemm_set_walk", 1)
+    L.call("reidmi_gemm_set_walk", 0)
     for o in outs[1:]:
         assert torch.equal(outs[0], o)
     rows = torch.arange(0, M, max(1, M // 97), device="cuda")
@@ -129,7 +129,7 @@ def test_gemm_f16_layernorm_fold(gpu, epi, M, N, K):
         _gemm(L, epi, dx, dw, dbf, out, drs, dcs)
         outs.append(out)
     L.call("reidmi_gemm_set_tile", 0)
-    L.call("reidmi_gemm_set_walk", 1)
+    L.call("reidmi_gemm_set_walk", 0)
     for o in outs[1:]:
         assert torch.equal(outs[0], o)
     got = outs[0].double().cpu()

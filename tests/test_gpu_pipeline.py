@@ -177,10 +177,11 @@ def _topk_agree(rank_a, rank_b, k):
 
 def test_end_to_end_accuracy_vs_reference(gpu):
     """North-star claim on identity-structured crops (128 q x 512 g, 2 passes each).
-    The reference ran its own pipeline twice, in its GPU dtype (fp16) and in fp32; the two
-    differ by dmAP_ref.  Ours must sit within max(1e-3, dmAP_ref) of BOTH reference runs'
-    mAP (plain and re-ranked), match their rank-1, and agree with the fp32 run's top-10
-    lists at least as often as the reference's fp16 run does (minus one query)."""
+    The reference ran its own pipeline twice, in fp32 (its exact arithmetic) and in its GPU
+    dtype (fp16); the two differ by dmAP_ref (~1e-3 here).  Ours must be within 1e-3 of the
+    fp32 run's mAP and within dmAP_ref + 1e-3 of the fp16 run's (plain and re-ranked), match
+    their rank-1, and agree with the fp32 run's top-10 lists at least as often as the
+    reference's fp16 run does (minus one query)."""
     from multimodal_reid_amd import evaluate, utils
     from multimodal_reid_amd import zero_shot_learning as zsl
     g = golden("e2e.npz")
@@ -195,8 +196,7 @@ def test_end_to_end_accuracy_vs_reference(gpu):
     cmc, mAP = zsl.get_cmc_map(feats[Q:], feats[:Q], torch.from_numpy(gp), torch.from_numpy(qp),
                                torch.from_numpy(gc), torch.from_numpy(qc))
     d_ref = abs(float(g["map_fp16"]) - float(g["map_fp32"]))
-    tol = max(1e-3, d_ref)
-    for tag in ("fp32", "fp16"):
+    for tag, tol in (("fp32", 1e-3), ("fp16", d_ref + 1e-3)):
         assert abs(mAP - float(g[f"map_{tag}"])) <= tol, (tag, mAP, float(g[f"map_{tag}"]), tol)
         assert cmc[0] == g[f"cmc_{tag}"][0]
     assert cmc.shape == (50,)
@@ -211,8 +211,8 @@ def test_end_to_end_accuracy_vs_reference(gpu):
     rcmc, rmap = zsl.get_cmc_map(feats[Q:], feats[:Q], torch.from_numpy(gp), torch.from_numpy(qp),
                                  torch.from_numpy(gc), torch.from_numpy(qc), reranking=True)
     d_rr = abs(float(g["map_rr_fp16"]) - float(g["map_rr_fp32"]))
-    for tag in ("fp32", "fp16"):
-        assert abs(rmap - float(g[f"map_rr_{tag}"])) <= max(1e-3, d_rr), (tag, rmap)
+    for tag, tol in (("fp32", 1e-3), ("fp16", d_rr + 1e-3)):
+        assert abs(rmap - float(g[f"map_rr_{tag}"])) <= tol, (tag, rmap, float(g[f"map_rr_{tag}"]), tol)
     print(f"e2e: mAP {mAP:.5f} (ref fp32 {float(g['map_fp32']):.5f}, fp16 {float(g['map_fp16']):.5f}); "
           f"top-10 agreement with ref fp32 {a_ours:.3f} (ref fp16 {a_ref:.3f}); "
           f"re-rank mAP {rmap:.5f} (ref {float(g['map_rr_fp32']):.5f} / {float(g['map_rr_fp16']):.5f})")

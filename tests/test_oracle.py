@@ -178,3 +178,19 @@ def test_ivlp_oracle_vs_reference_build_model():
     for got, ref in ((x12[:, 0], g["x12cls"]), (x11[:, 0], g["x11cls"]), (xp[:, 0], g["projcls"]),
                      (x12[1, -2:], g["x12_prompt"]), (xp[0, 100:103], g["proj_tok"]), (t, g["text_feat"])):
         assert np.abs(got.numpy() - ref).max() < 2e-5
+
+
+def test_threaded_oracle_is_deterministic():
+    """The C restatement's parallel loops (bench.py's CPU baseline runs them on the host's
+    cores) give bit-identical results for any thread count."""
+    qp, gp, qc, gc = syn.labels(90, 410, num_ids=50, num_cams=5, seed=8)
+    qf, gf = syn.features(qp, gp, dim=256, seed=8)
+    outs = []
+    for th in (1, 5):
+        oracle.set_threads(th)
+        d = oracle.distmat(qf, gf)
+        outs.append((d, *oracle.eval_rows(d, qp, gp, qc, gc), oracle.re_ranking(qf, gf, 20, 6, 0.3),
+                     oracle.topk_rows(d, 33)))
+    oracle.set_threads(1)
+    for a, b in zip(*outs):
+        assert np.array_equal(np.asarray(a).view(np.uint8), np.asarray(b).view(np.uint8))

@@ -64,8 +64,8 @@ def cmc_map(d, qp, gp, qc, gc, Q, G):
     valid, first, ap, nkept, ovf = evaluate.eval_rows_device(d, qp, gp, qc, gc)
     rows = rd.gather_rows(torch.stack([valid.double(), first.double(), ap, nkept.double()], 1), Q)
     rows = rows.cpu().numpy()
-    return evaluate.aggregate_cmc_map(rows[:, 0] > 0, rows[:, 1].astype(np.int64), rows[:, 2],
-                                      rows[:, 3].astype(np.int64), G, 50, ovf.cpu().numpy())
+    return evaluate.aggregate_cmc_map(rows[:, 0].astype(np.int64), rows[:, 1].astype(np.int64), rows[:, 2],
+                                      rows[:, 3].astype(np.int64), G, 50)
 
 
 def embed_leg(dev, rank, world, n, batch, G):
