@@ -44,14 +44,13 @@ PEAK_F32_MATRIX_TFLOPS = 157.3  # MI355X fp32 matrix (v_mfma_f32_32x32x2_f32)
 PEAK_HBM_GBPS = 8000.0
 EPI_GELU = 1  # the c_fc GEMM (+QuickGELU epilogue): the largest single kernel per block
 # HBM-side bytes per c_fc launch (ln_2-folded fp16 GEMM, M = 1024*211 (the default batch),
-# N = 3072, K = 768) from rocprofv3 PMC passes (tools/prof_round.sh ->
-# profiles/r01/pmc_c_fc_fold_b1024_{FETCH,WRITE}_SIZE.csv, mean of the 5 timed launches):
-# FETCH_SIZE 1 103 090 KiB doubled (gfx950 reports half of 16-B/lane streaming reads,
-# MI355X_MICROARCH.md "HBM") + WRITE_SIZE 1 296 384 KiB.  FETCH_SIZE also counts
-# Infinity-Cache hits: the 4.7 MB weight (393 KB per 256-column panel) is re-read by every
-# one of the 10 128 tiles and does not stay in a 4 MB XCD L2.
+# N = 3072, K = 768, auto tile walk = 2 N-groups) from rocprofv3 PMC passes (tools/prof_round.sh
+# -> profiles/r02/pmc_c_fc_fp16_walk2_{FETCH,WRITE}_SIZE.csv, 6 launches): FETCH_SIZE
+# 736 400 KiB doubled (gfx950 reports half of 16-B/lane streaming reads, MI355X_MICROARCH.md
+# "HBM") + WRITE_SIZE 1 296 384 KiB.  FETCH_SIZE also counts Infinity-Cache hits: A panels
+# are re-read by the 2 XCD groups and W panels by the rounds of an XCD (4 MB L2).
 # Algorithmic: A 332 MB + W 4.7 MB + out 1 327 MB = 1.66 GB.
-C_FC_TRAFFIC_BYTES = (2 * 1103090 + 1296384) * 1024
+C_FC_TRAFFIC_BYTES = (2 * 736400 + 1296384) * 1024
 
 
 def shard(n, rank, world):
