@@ -10,6 +10,8 @@
 // result is bit-for-bit that chain (one rounding per product, k-pairs in order).
 #include "common.h"
 
+#include <algorithm>
+
 namespace reidmi {
 
 // --------------------------------------------------------------------------- norms
@@ -339,10 +341,18 @@ __device__ int lower_pos(POS pos, int lo, int hi, int64_t x) {
     return lo;
 }
 
+// The walk's stack lives in LDS (`st`, PW_DEPTH frames, one walker lane): a private
+// array indexed at run time would sit in scratch memory, one HBM round trip per access.
+struct PwFrame {
+    int64_t off, n, n2;
+    int lo, hi, mid, stage;
+    double left;
+};
+constexpr int PW_DEPTH = 48;
+
 template <typename POS, typename VAL>
-__device__ double pairwise_sparse(POS pos, VAL val, int m, int64_t n) {
-    struct Frame { int64_t off, n, n2; int lo, hi, mid, stage; double left; };
-    Frame st[48];
+__device__ double pairwise_sparse(POS pos, VAL val, int m, int64_t n, PwFrame* st) {
+    using Frame = PwFrame;
     int sp = 0;
     st[sp++] = Frame{0, n, 0, 0, m, 0, 0, 0.0};
     double ret = 0.0;
@@ -350,6 +360,7 @@ __device__ double pairwise_sparse(POS pos, VAL val, int m, int64_t n) {
         Frame& f = st[sp - 1];
         if (f.stage == 0) {
             if (f.lo == f.hi) { ret = 0.0; sp--; continue; }
+            if (f.hi - f.lo == 1) { ret = val(f.lo); sp--; continue; }  // x + zeros == x in any order
             if (f.n <= 128) { ret = leaf_sum(pos, val, f.lo, f.hi, f.off, f.n); sp--; continue; }
             int64_t n2 = f.n / 2;
             n2 -= n2 % 8;
@@ -371,6 +382,72 @@ __device__ double pairwise_sparse(POS pos, VAL val, int m, int64_t n) {
     return ret;
 }
 
+// The same sum as pairwise_sparse, for one wave: the m nonzeros' leaves of numpy's split tree
+// (blocks of <= 128 elements; halving split rounded down to a multiple of 8) are found by
+// the lanes in parallel (path bits + depth per nonzero), each leaf is summed by leaf_sum,
+// and the leaves are combined in tree order by operator-precedence evaluation on the depth
+// of each adjacent pair's lowest common split (the first differing path bit): O(m) serial
+// steps instead of a walk over every split node.  Scratch (LDS, one wave): path[m], dep[m]
+// ints, vals/ops stacks of AP_STACK entries.  Returns the sum on lane 0.
+constexpr int AP_STACK = 34;
+
+template <typename VAL>
+__device__ double pairwise_tree_wave(const int* rk, VAL val, int m, int64_t n, uint32_t* path, int* dep,
+                                     double* vals, int* ops) {
+    const int lane = threadIdx.x & 63;
+    for (int t = lane; t < m; t += 64) {
+        int64_t off = 0, len = n;
+        uint32_t pb = 0;
+        int d = 0;
+        while (len > 128) {
+            int64_t n2 = len / 2;
+            n2 -= n2 % 8;
+            if ((int64_t)rk[t] - off < n2) len = n2;
+            else { off += n2; len -= n2; pb |= 1u << d; }
+            d++;
+        }
+        path[t] = pb;
+        dep[t] = d;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    double res = 0.0;
+    if (lane == 0) {
+        int sp = 0, op = 0;
+        int t = 0;
+        while (t < m) {
+            // leaf group [t, u): same path and depth
+            int u = t + 1;
+            while (u < m && path[u] == path[t] && dep[u] == dep[t]) u++;
+            int64_t off = 0, len = n;
+            for (int d = 0; d < dep[t]; d++) {  // the leaf's [off, off + len)
+                int64_t n2 = len / 2;
+                n2 -= n2 % 8;
+                if ((path[t] >> d) & 1u) { off += n2; len -= n2; } else len = n2;
+            }
+            const double v = leaf_sum([&](int k) { return (int64_t)rk[k]; }, val, t, u, off, len);
+            if (t > 0) {
+                const int c = __builtin_ctz(path[t - 1] ^ path[t]);  // depth of the split between the leaves
+                while (op > 0 && ops[op - 1] > c) {
+                    const double b = vals[--sp];
+                    vals[sp - 1] = vals[sp - 1] + b;
+                    op--;
+                }
+                ops[op++] = c;
+            }
+            vals[sp++] = v;
+            t = u;
+        }
+        while (op > 0) {
+            const double b = vals[--sp];
+            vals[sp - 1] = vals[sp - 1] + b;
+            op--;
+        }
+        res = vals[0];
+    }
+    return res;
+}
+
 // Per query (evaluate.py:40-80): positives = gallery items with the query's pid and another
 // camera, junk = same pid and same camera (removed, :55-56), everything else a kept
 // negative.  With the positives sorted by (distance, index) — np.argsort(kind="stable") —
@@ -381,134 +458,224 @@ __device__ double pairwise_sparse(POS pos, VAL val, int m, int64_t n) {
 // ranks; AP = numpy's pairwise sum of (k+1)/(rank_k+1) at positions rank_k over the kept
 // length, / m (:73-79); first = rank_0 (the CMC step, :65-68).
 //
-// eval_rows_wave_kernel: one wave per query, 4 queries per 256-thread workgroup, ~8 KiB of
-// LDS per wave (so ~16 waves per CU keep loads in flight).  Pass 1 streams the gallery
-// labels (int64 pid / camera, L2-resident: every query reads the same 2 x 8 B per item) and
-// compacts the positives' and junk items' indices with ballots; their distances are then
-// gathered and the positives bitonic-sorted in LDS.  Pass 2 reads the distance row once
-// (16-byte loads after a scalar head to 16-byte alignment), skipping items beyond the last
-// positive, and bins the rest by binary search into an LDS histogram.  A wave-wide scan
-// turns the histogram into ranks; lane 0 does the AP sum.  Queries with more than
-// EVW_MAXP positives or EVW_MAXJ junk items are left to eval_rows_kernel (valid = 2).
-constexpr int EVW_MAXP = 512, EVW_MAXJ = 256, EVW_WAVES = 4;
-
-struct EvWaveLds {
-    float pv[EVW_MAXP];
-    int pi[EVW_MAXP];
-    int hist[EVW_MAXP + 1];
-    float jv[EVW_MAXJ];
-    int ji[EVW_MAXJ];
+// Gallery labels packed once per eval_rows call: when the gallery pids span < 65535 values
+// (every ReID benchmark), pid - min as uint16 (padded to a multiple of 8 with 0xFFFF), so
+// each query's label pass reads 2 B per item instead of 8 (it is L2 traffic repeated by
+// every query).  Otherwise the kernel reads the int64 pids.
+struct EvLabels {
+    int64_t lo, hi;  // min / max gallery pid, biased to unsigned order for the atomics
 };
 
-#define EVW_SYNC()                                          \
-    do {                                                    \
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
-        __builtin_amdgcn_wave_barrier();                    \
-    } while (0)
+__device__ __forceinline__ uint64_t ord64(int64_t v) { return (uint64_t)v ^ 0x8000000000000000ull; }
+__device__ __forceinline__ int64_t unord64(uint64_t v) { return (int64_t)(v ^ 0x8000000000000000ull); }
 
-__global__ __launch_bounds__(256) void eval_rows_wave_kernel(
-    const float* __restrict__ dist, int64_t Q, int64_t G, int64_t ld, const int64_t* __restrict__ qp,
+__global__ void ev_minmax_init_kernel(unsigned long long* mm) {
+    mm[0] = ~0ull;
+    mm[1] = 0ull;
+}
+
+__global__ __launch_bounds__(256) void ev_minmax_kernel(const int64_t* __restrict__ gp, int64_t G,
+                                                        unsigned long long* mm) {
+    uint64_t lo = ~0ull, hi = 0;
+    for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < G; j += (int64_t)gridDim.x * 256) {
+        const uint64_t o = ord64(gp[j]);
+        lo = o < lo ? o : lo;
+        hi = o > hi ? o : hi;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t a = __shfl_xor(lo, off, 64), b = __shfl_xor(hi, off, 64);
+        lo = a < lo ? a : lo;
+        hi = b > hi ? b : hi;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMin(&mm[0], (unsigned long long)lo);
+        atomicMax(&mm[1], (unsigned long long)hi);
+    }
+}
+
+__global__ void ev_pack_kernel(const int64_t* __restrict__ gp, int64_t G, int64_t G8,
+                               const unsigned long long* __restrict__ mm, uint16_t* __restrict__ pk) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= G8) return;
+    const int64_t lo = unord64(mm[0]), hi = unord64(mm[1]);
+    if ((uint64_t)(hi - lo) >= 0xFFFFull) return;  // wide pid range: the int64 path
+    pk[j] = j < G ? (uint16_t)(gp[j] - lo) : (uint16_t)0xFFFF;
+}
+
+// eval_rows_wg_kernel: one 256-thread workgroup (4 waves) per query, ~8 KiB of LDS, so
+// ~8 workgroups per CU keep loads in flight.  Pass 1 streams the gallery labels (int64 pid /
+// camera, L2-resident: every query reads the same 2 x 8 B per item) and compacts the
+// positives' and junk items' indices (ballot + one LDS atomic per wave and step); their
+// distances are then gathered and the positives bitonic-sorted in LDS.  Pass 2 reads the
+// distance row once (16-byte loads after a scalar head to 16-byte alignment), skipping items
+// beyond the last positive, and bins the rest into an LDS histogram through a bucket table
+// of the positives (no per-item binary search: that search was 2/3 of the kernel).  Wave 0
+// scans the histogram into ranks; lane 0 does the AP sum.  Queries with more than EVW_MAXP
+// positives or EVW_MAXJ junk items are left to eval_rows_kernel (valid = 2).
+constexpr int EVW_MAXP = 512, EVW_MAXJ = 256, EVW_T = 1024;
+
+__global__ __launch_bounds__(256) void eval_rows_wg_kernel(
+    const float* __restrict__ dist, int64_t G, int64_t ld, const int64_t* __restrict__ qp,
     const int64_t* __restrict__ gp, const int64_t* __restrict__ qc, const int64_t* __restrict__ gc,
-    int32_t* __restrict__ valid, int64_t* __restrict__ first, double* __restrict__ ap,
-    int64_t* __restrict__ nkept) {
-    __shared__ EvWaveLds sm[EVW_WAVES];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int64_t q = (int64_t)blockIdx.x * EVW_WAVES + w;
-    if (q >= Q) return;  // whole waves only: no workgroup barrier below
-    EvWaveLds& L = sm[w];
+    const unsigned long long* __restrict__ mm, const uint16_t* __restrict__ pk, int32_t* __restrict__ valid,
+    int64_t* __restrict__ first, double* __restrict__ ap, int64_t* __restrict__ nkept) {
+    __shared__ float pv[EVW_MAXP];
+    __shared__ int pi[EVW_MAXP];
+    __shared__ int hist[EVW_MAXP + 1];
+    __shared__ float jv[EVW_MAXJ];
+    __shared__ int ji[EVW_MAXJ];
+    __shared__ int s_m, s_nj;
+    __shared__ double tvals[AP_STACK];
+    __shared__ int tops[AP_STACK];
+    __shared__ int2 bucket[EVW_T];  // [S[t], S[t+1]): the positives whose bucket is t
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int64_t q = blockIdx.x;
     const float* row = dist + q * ld;
     const int64_t qpid = qp[q], qcam = qc[q];
     const uint64_t below = (1ull << lane) - 1;
-    // ---- pass 1: labels -> positive / junk index lists
-    int m = 0, nj = 0;
-    constexpr int U1 = 4;
-    for (int64_t j0 = 0; j0 < G; j0 += 64 * U1) {
-        int64_t pid[U1], cam[U1];
-#pragma unroll
-        for (int u = 0; u < U1; u++) {
-            const int64_t j = j0 + u * 64 + lane;
-            pid[u] = j < G ? gp[j] : qpid + 1;
-            cam[u] = j < G ? gc[j] : 0;
+    if (tid == 0) { s_m = 0; s_nj = 0; }
+    __syncthreads();
+    // ---- pass 1: labels -> positive / junk index lists (ballot compaction + one LDS atomic
+    // per wave and step).  Every workgroup reads the same label lines, so each starts at its
+    // own chunk; the camera is loaded only for items of the query's pid.
+    auto take = [&](bool same, int64_t j) {
+        const bool samecam = same && gc[j] == qcam;
+        const bool pos = same && !samecam, junk = samecam;
+        const uint64_t mp = __ballot(pos), mj = __ballot(junk);
+        if (mp) {
+            int base = 0;
+            if (lane == 0) base = atomicAdd(&s_m, __popcll(mp));
+            base = __shfl(base, 0, 64);
+            const int sl = base + __popcll(mp & below);
+            if (pos && sl < EVW_MAXP) pi[sl] = (int)j;
         }
+        if (mj) {
+            int base = 0;
+            if (lane == 0) base = atomicAdd(&s_nj, __popcll(mj));
+            base = __shfl(base, 0, 64);
+            const int sl = base + __popcll(mj & below);
+            if (junk && sl < EVW_MAXJ) ji[sl] = (int)j;
+        }
+    };
+    const int64_t plo = unord64(mm[0]), phi = unord64(mm[1]);
+    if ((uint64_t)(phi - plo) < 0xFFFFull) {  // packed uint16 labels, 8 per 16-byte load
+        if (qpid >= plo && qpid <= phi) {
+            const uint16_t key = (uint16_t)(qpid - plo);
+            constexpr int U1 = 2, CH = 2048 * U1;
+            const int64_t nch = (G + CH - 1) / CH;
+            const int64_t c0 = (q * 37) % nch;
+            const int64_t n8 = (G + 7) / 8;
+            for (int64_t c = 0; c < nch; c++) {
+                int64_t v0 = ((c0 + c) % nch) * (CH / 8);
+                uint4 w[U1];
 #pragma unroll
-        for (int u = 0; u < U1; u++) {
-            const int64_t j = j0 + u * 64 + lane;
-            const bool same = pid[u] == qpid;
-            const bool pos = same && cam[u] != qcam, junk = same && cam[u] == qcam;
-            const uint64_t mp = __ballot(pos), mj = __ballot(junk);
-            if (pos) {
-                const int s = m + __popcll(mp & below);
-                if (s < EVW_MAXP) L.pi[s] = (int)j;
+                for (int u = 0; u < U1; u++) {
+                    const int64_t v = v0 + u * 256 + tid;
+                    w[u] = v < n8 ? ((const uint4*)pk)[v] : make_uint4(~0u, ~0u, ~0u, ~0u);
+                }
+#pragma unroll
+                for (int u = 0; u < U1; u++) {
+                    const int64_t jb = (v0 + u * 256 + tid) * 8;
+                    const uint32_t d[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
+#pragma unroll
+                    for (int e = 0; e < 8; e++) {
+                        const uint16_t lab = (uint16_t)(d[e >> 1] >> (16 * (e & 1)));
+                        const bool same = lab == key;  // padding 0xFFFF never equals a key
+                        if (__ballot(same)) take(same, jb + e);
+                    }
+                }
             }
-            if (junk) {
-                const int s = nj + __popcll(mj & below);
-                if (s < EVW_MAXJ) L.ji[s] = (int)j;
+        }
+    } else {
+        constexpr int U1 = 4, CH = 256 * U1;
+        const int64_t nch = (G + CH - 1) / CH;
+        const int64_t c0 = (q * 37) % nch;
+        for (int64_t c = 0; c < nch; c++) {
+            const int64_t j0 = ((c0 + c) % nch) * CH;
+            int64_t pid[U1];
+#pragma unroll
+            for (int u = 0; u < U1; u++) {
+                const int64_t j = j0 + u * 256 + tid;
+                pid[u] = j < G ? gp[j] : qpid + 1;
             }
-            m += __popcll(mp);
-            nj += __popcll(mj);
+#pragma unroll
+            for (int u = 0; u < U1; u++) take(pid[u] == qpid, j0 + u * 256 + tid);
         }
     }
-    if (lane == 0) nkept[q] = G - nj;
+    __syncthreads();
+    const int m = s_m, nj = s_nj;
+    if (tid == 0) nkept[q] = G - nj;
     if (m == 0) {
-        if (lane == 0) { valid[q] = 0; first[q] = -1; ap[q] = 0.0; }
+        if (tid == 0) { valid[q] = 0; first[q] = -1; ap[q] = 0.0; }
         return;
     }
-    if (m > EVW_MAXP || nj > EVW_MAXJ) {  // eval_rows_kernel (one workgroup per query) takes it
-        if (lane == 0) valid[q] = 2;
+    if (m > EVW_MAXP || nj > EVW_MAXJ) {  // eval_rows_kernel (large lists) takes it
+        if (tid == 0) valid[q] = 2;
         return;
     }
-    EVW_SYNC();
     // ---- gather the positives' / junk distances, sort the positives by (value, index)
     int P = 1;
     while (P < m) P <<= 1;
-    for (int t = lane; t < P; t += 64) {
-        if (t < m) L.pv[t] = row[L.pi[t]];
-        else { L.pv[t] = __builtin_inff(); L.pi[t] = 0x7fffffff; }
+    for (int t = tid; t < P; t += 256) {
+        if (t < m) pv[t] = row[pi[t]];
+        else { pv[t] = __builtin_inff(); pi[t] = 0x7fffffff; }
     }
-    for (int t = lane; t < nj; t += 64) L.jv[t] = row[L.ji[t]];
-    for (int t = lane; t <= m; t += 64) L.hist[t] = 0;
-    EVW_SYNC();
-    for (int k = 2; k <= P; k <<= 1)
-        for (int jj = k >> 1; jj > 0; jj >>= 1) {
-            for (int t = lane; t < P; t += 64) {
-                const int o = t ^ jj;
-                if (o > t) {
-                    const bool up = (t & k) == 0;
-                    const float av = L.pv[t], bv = L.pv[o];
-                    const int ai = L.pi[t], bi = L.pi[o];
-                    if (key_less(bv, bi, av, ai) == up) { L.pv[t] = bv; L.pv[o] = av; L.pi[t] = bi; L.pi[o] = ai; }
-                }
-            }
-            EVW_SYNC();
-        }
-    // ---- pass 2: bin every item of the row by the number of positives before it
-    const float lv = L.pv[m - 1];
-    const int li = L.pi[m - 1];
-    auto bin = [&](float v, int j) {
-        if (key_less(lv, li, v, j)) return;  // after the last positive: b = m, not needed
+    for (int t = tid; t < nj; t += 256) jv[t] = row[ji[t]];
+    for (int t = tid; t <= m; t += 256) hist[t] = 0;
+    __syncthreads();
+    bitonic_sort_kv(pv, pi, P);
+    // ---- pass 2: bin every item of the row by the number of positives before it.  A
+    // bucket table narrows each item's candidates: t(x) = clamp(floor((x - v_0) * T /
+    // (v_last - v_0)), 0, T-1) is monotone in x (the same float operations for every x), so
+    // positives in buckets below t(x) are all smaller, those above all larger, and only the
+    // positives of bucket t(x) (usually none or one) need the exact (value, index) compare.
+    const float lv = pv[m - 1];
+    const int li = pi[m - 1];
+    const float v0 = pv[0];
+    const int T = 8 * P < EVW_T ? (8 * P > 64 ? 8 * P : 64) : EVW_T;  // ~8 buckets per positive
+    const float scale = (float)T / (lv - v0);  // inf / NaN when the positives tie: clamped
+    auto bucket_of = [&](float x) {
+        const float f = __builtin_floorf((x - v0) * scale);
+        return (int)__builtin_fminf(__builtin_fmaxf(f, 0.0f), (float)(T - 1));
+    };
+    for (int t = tid; t < T; t += 256) {  // S[t] = #{k : t(pv_k) < t}
         int lo = 0, hi = m;
         while (lo < hi) {
             const int mid = (lo + hi) >> 1;
-            if (key_less(L.pv[mid], L.pi[mid], v, j)) lo = mid + 1; else hi = mid;
+            if (bucket_of(pv[mid]) < t) lo = mid + 1; else hi = mid;
         }
-        __hip_atomic_fetch_add(&L.hist[lo], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        int lo2 = lo, hi2 = m;
+        while (lo2 < hi2) {
+            const int mid = (lo2 + hi2) >> 1;
+            if (bucket_of(pv[mid]) <= t) lo2 = mid + 1; else hi2 = mid;
+        }
+        bucket[t] = make_int2(lo, lo2);
+    }
+    __syncthreads();
+    auto bin = [&](float v, int j) {
+        // after the last positive (b = m, not needed); NaN sorts last (np.argsort)
+        if (key_less(lv, li, v, j) || v != v) return;
+        const int2 se = bucket[bucket_of(v)];
+        int b = se.x;
+        while (b < se.y && key_less(pv[b], pi[b], v, j)) b++;
+        atomicAdd(&hist[b], 1);
     };
     const int head = (int)(((16 - ((uintptr_t)row & 15)) & 15) >> 2);  // scalar items before 16-B alignment
     const int h = head < G ? head : (int)G;
-    if (lane < h) bin(row[lane], lane);
+    if (tid < h) bin(row[tid], tid);
     const int64_t nv = (G - h) >> 2;  // float4 groups
     const float4* r4 = (const float4*)(row + h);
     constexpr int U2 = 4;
-    for (int64_t g0 = 0; g0 < nv; g0 += 64 * U2) {
+    for (int64_t g0 = 0; g0 < nv; g0 += 256 * U2) {
         float4 v[U2];
 #pragma unroll
         for (int u = 0; u < U2; u++) {
-            const int64_t g = g0 + u * 64 + lane;
-            v[u] = g < nv ? r4[g] : make_float4(__builtin_inff(), 0.f, 0.f, 0.f);
+            const int64_t g = g0 + u * 256 + tid;
+            v[u] = g < nv ? r4[g] : make_float4(0.f, 0.f, 0.f, 0.f);
         }
 #pragma unroll
         for (int u = 0; u < U2; u++) {
-            const int64_t g = g0 + u * 64 + lane;
+            const int64_t g = g0 + u * 256 + tid;
             if (g < nv) {
                 const int j = h + (int)g * 4;
                 bin(v[u].x, j);
@@ -518,61 +685,72 @@ __global__ __launch_bounds__(256) void eval_rows_wave_kernel(
             }
         }
     }
-    for (int64_t j = h + nv * 4 + lane; j < G; j += 64) bin(row[j], (int)j);
-    EVW_SYNC();
-    // ---- ranks: inclusive scan of hist, minus the item itself and the junk before it
-    int carry = 0;
-    for (int c0 = 0; c0 < m; c0 += 64) {
-        const int k = c0 + lane;
-        int v = k < m ? L.hist[k] : 0;
+    for (int64_t j = h + nv * 4 + tid; j < G; j += 256) bin(row[j], (int)j);
+    __syncthreads();
+    // ---- ranks (wave 0): inclusive scan of hist, minus the item itself and the junk before it
+    if (tid < 64) {
+        int carry = 0;
+        for (int c0 = 0; c0 < m; c0 += 64) {
+            const int k = c0 + lane;
+            int v = k < m ? hist[k] : 0;
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int t = __shfl_up(v, o, 64);
-            if (lane >= o) v += t;
+            for (int o = 1; o < 64; o <<= 1) {
+                const int t = __shfl_up(v, o, 64);
+                if (lane >= o) v += t;
+            }
+            const int incl = v + carry;
+            carry = __shfl(incl, 63, 64);
+            if (k < m) {
+                const float pvk = pv[k];
+                const int pik = pi[k];
+                int jb = 0;
+                for (int t = 0; t < nj; t++) jb += key_less(jv[t], ji[t], pvk, pik);
+                hist[k] = incl - 1 - jb;  // rank_k (0-based position among the kept items)
+            }
         }
-        const int incl = v + carry;
-        carry = __shfl(incl, 63, 64);
-        if (k < m) {
-            const float pvk = L.pv[k];
-            const int pik = L.pi[k];
-            int jb = 0;
-            for (int t = 0; t < nj; t++) jb += key_less(L.jv[t], L.ji[t], pvk, pik);
-            L.hist[k] = incl - 1 - jb;  // rank_k (0-based position among the kept items)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        const int* rk = hist;
+        const double sum = pairwise_tree_wave(rk, [&](int t) { return (double)(t + 1) / (double)(rk[t] + 1); }, m,
+                                              G - nj, (uint32_t*)pv, pi, tvals, tops);  // pv / pi are free now
+        if (lane == 0) {
+            valid[q] = 1;
+            first[q] = rk[0];
+            ap[q] = sum / (double)m;
         }
-    }
-    EVW_SYNC();
-    if (lane == 0) {
-        const int* rk = L.hist;
-        const int64_t n = G - nj;
-        valid[q] = 1;
-        first[q] = rk[0];
-        ap[q] = pairwise_sparse([&](int t) { return (int64_t)rk[t]; },
-                                [&](int t) { return (double)(t + 1) / (double)(rk[t] + 1); }, m, n) /
-                (double)m;
     }
 }
-#undef EVW_SYNC
 
 constexpr int EV_MAXP = 2048;
 
-// Fallback for the queries eval_rows_wave_kernel left (valid == 2: more than EVW_MAXP
+// Fallback for the queries eval_rows_wg_kernel left (valid == 2: more than EVW_MAXP
 // positives or EVW_MAXJ junk items): one workgroup per query, up to EV_MAXP positives.
 // Positives are collected and sorted; every other kept gallery item is binned by how many
 // positives precede it (binary search).  Queries beyond EV_MAXP set *overflow and
 // valid = -1 (the host refuses to aggregate them).
-__global__ __launch_bounds__(256) void eval_rows_kernel(
-    const float* __restrict__ dist, int64_t G, int64_t ld, const int64_t* __restrict__ qp,
-    const int64_t* __restrict__ gp, const int64_t* __restrict__ qc, const int64_t* __restrict__ gc,
-    int32_t* __restrict__ valid, int64_t* __restrict__ first, double* __restrict__ ap,
-    int64_t* __restrict__ nkept, int32_t* __restrict__ overflow) {
-    __shared__ float pv[EV_MAXP];
-    __shared__ int pi[EV_MAXP];
-    __shared__ int hist[EV_MAXP + 1];
-    __shared__ int64_t rk[EV_MAXP];
-    __shared__ double rv[EV_MAXP];
-    __shared__ int s_m, s_junk;
-    const int64_t q = blockIdx.x;
-    if (valid[q] != 2) return;
+struct EvLargeLds {
+    float pv[EV_MAXP];
+    int pi[EV_MAXP];
+    int hist[EV_MAXP + 1];
+    int64_t rk[EV_MAXP];
+    double rv[EV_MAXP];
+    int s_m, s_junk;
+    PwFrame pw[PW_DEPTH];
+};
+
+__device__ void eval_row_large(int64_t q, const float* __restrict__ dist, int64_t G, int64_t ld,
+                               const int64_t* __restrict__ qp, const int64_t* __restrict__ gp,
+                               const int64_t* __restrict__ qc, const int64_t* __restrict__ gc,
+                               int32_t* __restrict__ valid, int64_t* __restrict__ first, double* __restrict__ ap,
+                               int64_t* __restrict__ nkept, int32_t* __restrict__ overflow, EvLargeLds& L) {
+    float* pv = L.pv;
+    int* pi = L.pi;
+    int* hist = L.hist;
+    int64_t* rk = L.rk;
+    double* rv = L.rv;
+    int& s_m = L.s_m;
+    int& s_junk = L.s_junk;
+    PwFrame* pw = L.pw;
     const float* row = dist + q * ld;
     const int64_t qpid = qp[q], qcam = qc[q];
     if (threadIdx.x == 0) { s_m = 0; s_junk = 0; }
@@ -619,7 +797,21 @@ __global__ __launch_bounds__(256) void eval_rows_kernel(
             rv[k] = (double)(k + 1) / (double)(rk[k] + 1);
         }
         first[q] = rk[0];
-        ap[q] = pairwise_sparse([&](int t) { return rk[t]; }, [&](int t) { return rv[t]; }, m, n) / (double)m;
+        ap[q] = pairwise_sparse([&](int t) { return rk[t]; }, [&](int t) { return rv[t]; }, m, n, pw) / (double)m;
+    }
+}
+
+// Grid-stride over the queries (a few workgroups per CU instead of one launch-slot per query).
+__global__ __launch_bounds__(256) void eval_rows_kernel(
+    const float* __restrict__ dist, int64_t Q, int64_t G, int64_t ld, const int64_t* __restrict__ qp,
+    const int64_t* __restrict__ gp, const int64_t* __restrict__ qc, const int64_t* __restrict__ gc,
+    int32_t* __restrict__ valid, int64_t* __restrict__ first, double* __restrict__ ap,
+    int64_t* __restrict__ nkept, int32_t* __restrict__ overflow) {
+    __shared__ EvLargeLds L;
+    for (int64_t q = blockIdx.x; q < Q; q += gridDim.x) {
+        if (valid[q] != 2) continue;  // uniform per workgroup
+        eval_row_large(q, dist, G, ld, qp, gp, qc, gc, valid, first, ap, nkept, overflow, L);
+        __syncthreads();
     }
 }
 
@@ -738,20 +930,38 @@ REIDMI_API int reidmi_topk_rows_f32(const float* x, int64_t rows, int64_t cols, 
     return topk_launch(x, rows, cols, ldx, row_div, k, out_idx, out_val, ldo, (hipStream_t)stream);
 }
 
+static int64_t ev_ws_bytes(int64_t G) { return 256 + ((G + 7) / 8 * 8) * 2; }
+
+REIDMI_API int64_t reidmi_eval_rows_workspace_bytes(int64_t G) { return G > 0 ? ev_ws_bytes(G) : -1; }
+
 REIDMI_API int reidmi_eval_rows(const float* dist, int64_t Q, int64_t G, int64_t ldd, const int64_t* q_pids,
                                 const int64_t* g_pids, const int64_t* q_cams, const int64_t* g_cams, int32_t* valid,
-                                int64_t* first, double* ap, int64_t* nkept, int32_t* overflow, void* stream) {
+                                int64_t* first, double* ap, int64_t* nkept, int32_t* overflow, void* ws_,
+                                int64_t ws_bytes, void* stream) {
     RM_REQUIRE(Q >= 0 && G > 0 && ldd >= G && G < 0x7fffffff, "eval_rows: bad shape");
     RM_REQUIRE(overflow != nullptr, "eval_rows: overflow flag pointer required");
     RM_REQUIRE(((uintptr_t)dist & 3) == 0, "eval_rows: dist must be 4-byte aligned");
+    RM_REQUIRE(ws_ != nullptr && ((uintptr_t)ws_ & 15) == 0 && ws_bytes >= ev_ws_bytes(G),
+               "eval_rows: workspace (reidmi_eval_rows_workspace_bytes, 16-byte aligned) required");
     if (Q == 0) return OK;
+    RM_REQUIRE(Q < (1ll << 31), "eval_rows: too many queries");
     hipStream_t s = (hipStream_t)stream;
-    RM_REQUIRE(ceil_div(Q, EVW_WAVES) < (1ll << 31), "eval_rows: too many queries");
-    hipLaunchKernelGGL(eval_rows_wave_kernel, dim3((unsigned)ceil_div(Q, EVW_WAVES)), dim3(64 * EVW_WAVES), 0, s,
-                       dist, Q, G, ldd, q_pids, g_pids, q_cams, g_cams, valid, first, ap, nkept);
+    unsigned long long* mm = (unsigned long long*)ws_;
+    uint16_t* pk = (uint16_t*)((char*)ws_ + 256);
+    const int64_t G8 = (G + 7) / 8 * 8;
+    hipLaunchKernelGGL(ev_minmax_init_kernel, dim3(1), dim3(1), 0, s, mm);
     RM_LAUNCHED();
-    hipLaunchKernelGGL(eval_rows_kernel, dim3((unsigned)Q), dim3(256), 0, s, dist, G, ldd, q_pids, g_pids, q_cams,
-                       g_cams, valid, first, ap, nkept, overflow);
+    hipLaunchKernelGGL(ev_minmax_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(G, 256), 1024)), dim3(256), 0, s,
+                       g_pids, G, mm);
+    RM_LAUNCHED();
+    hipLaunchKernelGGL(ev_pack_kernel, dim3(ceil_div(G8, 256)), dim3(256), 0, s, g_pids, G, G8,
+                       (const unsigned long long*)mm, pk);
+    RM_LAUNCHED();
+    hipLaunchKernelGGL(eval_rows_wg_kernel, dim3((unsigned)Q), dim3(256), 0, s, dist, G, ldd, q_pids, g_pids, q_cams,
+                       g_cams, (const unsigned long long*)mm, (const uint16_t*)pk, valid, first, ap, nkept);
+    RM_LAUNCHED();
+    hipLaunchKernelGGL(eval_rows_kernel, dim3((unsigned)std::min<int64_t>(Q, 512)), dim3(256), 0, s, dist, Q, G, ldd,
+                       q_pids, g_pids, q_cams, g_cams, valid, first, ap, nkept, overflow);
     RM_LAUNCHED();
     return OK;
 }

@@ -136,10 +136,11 @@ def test_eval_market_scale_rows_vs_oracle(gpu):
     assert np.array_equal(idx, oracle.topk_rows(dsub, 50))
 
 
-@pytest.mark.parametrize("G", [3001, 4099])
-def test_eval_many_positives_and_junk_vs_oracle(gpu, G):
-    """Queries whose positives (> 512) or junk items (> 256) exceed the wave kernel's LDS
-    lists go to the per-workgroup kernel; ragged row starts (ld = G) exercise the 16-byte
+@pytest.mark.parametrize("G,pid_shift,pid_scale", [(3001, 0, 1), (4099, 0, 1), (3001, -(1 << 40), 1),
+                                                   (2053, (1 << 62) - 9, 1), (3001, 0, 100003), (4099, -5, 1 << 40)])
+def test_eval_many_positives_and_junk_vs_oracle(gpu, G, pid_shift, pid_scale):
+    """Queries whose positives (> 512) or junk items (> 256) exceed the main kernel's LDS
+    lists go to the large-list kernel; ragged row starts (ld = G) exercise the 16-byte
     alignment head; quantised distances give exact ties.  Bit-exact against the oracle."""
     r = np.random.default_rng(G)
     Q = 9
@@ -150,6 +151,8 @@ def test_eval_many_positives_and_junk_vs_oracle(gpu, G):
     gp[::7] = 9  # some negatives for everyone
     qp[7:], gp[:40] = 8, 8  # two queries with 40 items of their pid (wave kernel path)
     gc[:40] = np.arange(40) % 3
+    # arbitrary int64 pids: packed 16-bit labels when the gallery's pid range allows, else int64
+    qp, gp = qp * pid_scale + pid_shift, gp * pid_scale + pid_shift
     dist = (np.round(r.random((Q, G)) * 64) / 64).astype(np.float32)
     rows = _eval_rows_np(dist, qp, gp, qc, gc)
     ref = oracle.eval_rows(dist, qp, gp, qc, gc)
