@@ -178,6 +178,13 @@ int reidmi_layernorm(const float* x, int64_t rows, int64_t ldx, const int32_t* r
                      const float* gamma, const float* beta, float eps, float* y32, int64_t ldy32, void* y16,
                      int64_t ldy16, void* stream);
 
+/* Prompt construction — coop.PromptLearner.forward (coop.py:95-110) /
+ * maple.VLPromptLearner.construct_prompts (maple.py:57-90): out [B][P+C+S][W] fp32 with
+ * out[b] = cat(prefix [P][W], ctx[label[b]] [C][W] of ctx [ncls][C][W], suffix [S][W]).
+ * W % 4 == 0.  bad_label (nullable device int32) is set to 1 for a label outside [0, ncls). */
+int reidmi_prompt_build(const float* prefix, int P, const float* ctx, int C, const int64_t* label, int64_t ncls,
+                        const float* suffix, int S, int64_t B, int W, float* out, int32_t* bad_label, void* stream);
+
 /* Per-block weights of a CLIP transformer block (ResidualAttentionBlock,
  * custom_clip_model.py:8-29 / ResidualAttentionBlock_IVLP, maple.py:579-644).
  * Matrices in PyTorch [out][in] layout, vectors fp32.  ln_1 / ln_2 are folded into the

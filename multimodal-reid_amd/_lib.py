@@ -53,6 +53,7 @@ SIGNATURES = {
     "reidmi_feature_tta_avg": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _i64, _vp],
     "reidmi_feature_tta_mm": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _vp, _i64, _vp],
     "reidmi_class_mean_normalize": [_vp, _vp, _i64, _i64, _vp, _vp],
+    "reidmi_prompt_build": [_vp, _i32, _vp, _i32, _vp, _i64, _vp, _i32, _i64, _i32, _vp, _vp, _vp],
     "reidmi_preprocess_u8": [_vp, _vp, _i64, _i32, _i32, _i32, _i32, _vp, _vp, _i32, _vp, _vp],
     "reidmi_preprocess_lds_size": [_i32, _i32, _i32, _i32, _vp],
 }

@@ -109,9 +109,49 @@ __global__ __launch_bounds__(256) void class_mean_norm_kernel(const float* __res
     for (int64_t k = threadIdx.x; k < E; k += blockDim.x) out[c * E + k] = acc[k] * inv;
 }
 
+// Prompt construction (T3): coop.PromptLearner.forward (coop.py:95-110) and
+// maple.VLPromptLearner.construct_prompts (maple.py:57-90): for each label b,
+// prompts[b] = cat(prefix [P][W], ctx[label[b]] [C][W], suffix [S][W]) along the tokens.
+// One float4 per thread; prefix / suffix rows are shared by every label.
+__global__ void prompt_build_kernel(const float* __restrict__ prefix, int P, const float* __restrict__ ctx, int C,
+                                    const int64_t* __restrict__ label, int64_t ncls, const float* __restrict__ suffix,
+                                    int S, int64_t B, int W, float* __restrict__ out, int32_t* __restrict__ bad) {
+    const int L = P + C + S, W4 = W / 4;
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= B * L * W4) return;
+    const int c4 = (int)(e % W4);
+    const int64_t bt = e / W4;
+    const int t = (int)(bt % L);
+    const int64_t b = bt / L;
+    const float* src;
+    if (t < P) src = prefix + (int64_t)t * W;
+    else if (t < P + C) {
+        int64_t lb = label[b];
+        if (lb < 0 || lb >= ncls) {  // an out-of-range label: flagged, row 0 used
+            if (bad) *bad = 1;
+            lb = 0;
+        }
+        src = ctx + (lb * C + (t - P)) * (int64_t)W;
+    } else src = suffix + (int64_t)(t - P - C) * W;
+    ((float4*)(out + bt * W))[c4] = ((const float4*)src)[c4];
+}
+
 }  // namespace reidmi
 
 using namespace reidmi;
+
+REIDMI_API int reidmi_prompt_build(const float* prefix, int P, const float* ctx, int C, const int64_t* label,
+                                   int64_t ncls, const float* suffix, int S, int64_t B, int W, float* out,
+                                   int32_t* bad_label, void* stream) {
+    RM_REQUIRE(P >= 0 && C >= 0 && S >= 0 && P + C + S > 0 && B >= 0 && W > 0 && W % 4 == 0 && ncls > 0,
+               "prompt_build: bad shape");
+    if (B == 0) return OK;
+    const int64_t n = B * (P + C + S) * (W / 4);
+    hipLaunchKernelGGL(prompt_build_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, (hipStream_t)stream, prefix, P, ctx,
+                       C, label, ncls, suffix, S, B, W, out, bad_label);
+    RM_LAUNCHED();
+    return OK;
+}
 
 REIDMI_API int reidmi_class_mean_normalize(const float* feats, const int64_t* offsets, int64_t ncls, int64_t E,
                                            float* out, void* stream) {

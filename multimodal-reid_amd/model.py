@@ -305,7 +305,12 @@ class TextEncoder:
         self.dtype = torch.float32
 
     def __call__(self, prompts, tokenized_prompts):
-        return self.text._forward(tokenized_prompts, prompts)
+        tok = torch.as_tensor(tokenized_prompts)
+        if tok.dim() == 2 and tok.shape[0] == 1 and prompts.shape[0] > 1:
+            # one template's token row for every prompt: the reference's
+            # x[arange(B), tokenized_prompts.argmax(-1)] broadcasts it (text_encoder.py:23)
+            tok = tok.expand(prompts.shape[0], -1)
+        return self.text._forward(tok, prompts)
 
     forward = __call__
 

@@ -301,3 +301,14 @@ def round_like_convert_weights(sd):
 def glue_cls_features(n, dim, seed=0):
     """[n, dim] fp32 stand-in CLS features for the inference() glue fixtures."""
     return _normal(f"glue{dim}", (n, dim), 1.0, seed)
+
+
+# Synthetic token row standing in for clip.tokenize("A photo of X X X X X person.") (the BPE
+# vocabulary is absent): SOT, 10 body ids, EOT (the row's maximum, argmax -> EOT), zero pad.
+CTX_INIT_TOKENS = [49406, 320, 1125, 539, 343, 343, 343, 343, 343, 2533, 269, 49407]
+
+
+def ctx_init_tokens(ctx=77):
+    out = np.zeros((1, ctx), np.int64)
+    out[0, :len(CTX_INIT_TOKENS)] = CTX_INIT_TOKENS
+    return out

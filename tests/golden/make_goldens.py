@@ -468,12 +468,42 @@ def e2e_fixtures(out):
     np.savez_compressed(os.path.join(out, "e2e.npz"), **res)
 
 
+def prompt_fixtures(out):
+    """T3 + T2: coop.PromptLearner (coop.py:62-110) and maple.VLPromptLearner (maple.py:21-90)
+    built on the reference maple.CLIP text tower, forward(label) -> prompts, then
+    text_encoder.TextEncoder(prompts, tokenized_prompts) (text_encoder.py:14-24).  The learned
+    context vectors (torch RNG) are stored; prompts are pinned by a float64 checksum."""
+    _, maple, _, _ = _stubbed()
+    import clip
+    import coop
+    sentence = "A photo of X X X X X person."
+    clip.TOKENS[sentence] = syn.ctx_init_tokens()[0]
+    model = _small_clip(maple, syn.text_state_dict(seed=30))
+    label = torch.tensor([2, 0, 3, 2])
+    res = {"label": label.numpy()}
+    with _cpu_cuda(), torch.no_grad():
+        torch.manual_seed(31)
+        pl = coop.PromptLearner(4, model, "market1501")
+        p = pl(label)
+        te = ref_te.TextEncoder(model)
+        res.update(coop_ctx=pl.cls_ctx.detach().numpy(), coop_prompts_sum=np.float64(p.double().sum()),
+                   coop_prompts_abs=np.float64(p.double().abs().sum()), coop_feat=te(p, pl.tokenized_prompts).numpy())
+        torch.manual_seed(32)
+        vl = maple.VLPromptLearner(4, model, "market1501")
+        p2 = vl(label)
+        res.update(vl_ctx=vl.ctx.detach().numpy(), vl_prompts_sum=np.float64(p2.double().sum()),
+                   vl_prompts_abs=np.float64(p2.double().abs().sum()), vl_feat=te(p2, vl.tokenized_prompts).numpy())
+    assert p.shape == (4, 77, 512) and p2.shape == (4, 77, 512)
+    np.savez_compressed(os.path.join(out, "prompts.npz"), **res)
+    print("prompt fixtures ok")
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=HERE)
     ap.add_argument("--only", default="")
     a = ap.parse_args()
     todo = a.only.split(",") if a.only else ["backend", "rerank", "vit", "vitl", "text", "ivlp", "glue",
-                                              "adaptor", "e2e"]
+                                              "adaptor", "e2e", "prompt"]
     for t in todo:
         globals()[f"{t}_fixtures"](a.out)

@@ -216,3 +216,28 @@ def test_end_to_end_accuracy_vs_reference(gpu):
     print(f"e2e: mAP {mAP:.5f} (ref fp32 {float(g['map_fp32']):.5f}, fp16 {float(g['map_fp16']):.5f}); "
           f"top-10 agreement with ref fp32 {a_ours:.3f} (ref fp16 {a_ref:.3f}); "
           f"re-rank mAP {rmap:.5f} (ref {float(g['map_rr_fp32']):.5f} / {float(g['map_rr_fp16']):.5f})")
+
+
+@pytest.mark.parametrize("kind", ["coop", "vl"])
+def test_prompt_learners_vs_reference(gpu, kind):
+    """T3 + T2: coop.PromptLearner / maple.VLPromptLearner forward(label) on the device kernel
+    (prefix | learned context rows | suffix) with the reference's learned vectors, then
+    TextEncoder(prompts, tokenized_prompts): prompts equal the reference's (float64 checksums
+    of the exact fp32 concatenation), features within the encoder tolerance."""
+    from multimodal_reid_amd.model import TextTransformer, TextEncoder
+    from multimodal_reid_amd import prompts as pr
+    g = golden("prompts.npz")
+    tm = TextTransformer(syn.text_state_dict(seed=30))
+    cls = pr.PromptLearner if kind == "coop" else pr.VLPromptLearner
+    learner = cls(4, tm, "market1501", syn.ctx_init_tokens(), g[f"{kind}_ctx"])
+    p = learner(torch.from_numpy(g["label"]))
+    assert p.shape == (4, 77, 512)
+    assert float(p.double().sum()) == float(g[f"{kind}_prompts_sum"])
+    assert float(p.double().abs().sum()) == float(g[f"{kind}_prompts_abs"])
+    ref = torch.cat([learner.token_prefix.expand(4, -1, -1), learner.ctx[torch.from_numpy(g["label"]).cuda()],
+                     learner.token_suffix.expand(4, -1, -1)], 1)
+    assert torch.equal(p, ref)
+    feat = TextEncoder(tm)(p, learner.tokenized_prompts).cpu().numpy()
+    _close(feat, g[f"{kind}_feat"], atol=5e-3)
+    with pytest.raises(IndexError):
+        learner(torch.tensor([4]))
