@@ -312,3 +312,27 @@ def ctx_init_tokens(ctx=77):
     out = np.zeros((1, ctx), np.int64)
     out[0, :len(CTX_INIT_TOKENS)] = CTX_INIT_TOKENS
     return out
+
+
+MARKET_ATTRIBUTE_FIELDS = (["age", "backpack", "bag", "handbag", "clothes", "down", "up", "hair", "hat", "gender"]
+                           + ["up" + c for c in ("black", "white", "red", "purple", "yellow", "gray", "blue", "green")]
+                           + ["down" + c for c in ("black", "white", "pink", "purple", "yellow", "gray", "blue",
+                                                   "green", "brown")]
+                           + ["image_index"])
+
+
+def write_market_attribute_mat(path, n_ids=24, seed=0):
+    """A synthetic Market-1501_Attribute/market_attribute.mat (the submodule is absent
+    offline) with the layout data_prepare.get_prompts reads (data_prepare.py:296-309):
+    market_attribute.{test,train} structs of 28 1 x n fields — age in 1..4, the other 26
+    attributes in {1, 2}, image_index the identity strings."""
+    import scipy.io as sio
+    r = _rng("market_attribute", seed)
+    d = {}
+    for f in MARKET_ATTRIBUTE_FIELDS[:-1]:
+        d[f] = r.integers(1, 5 if f == "age" else 3, (1, n_ids))
+    idx = np.empty((1, n_ids), dtype=object)
+    for i in range(n_ids):
+        idx[0, i] = f"{i + 1:04d}"
+    d["image_index"] = idx
+    sio.savemat(path, {"market_attribute": {"test": d, "train": d}})

@@ -498,12 +498,31 @@ def prompt_fixtures(out):
     print("prompt fixtures ok")
 
 
+def template_fixtures(out):
+    """data_prepare.get_prompts / get_prompts_augmented / get_prompts_simple
+    (data_prepare.py:287-537) on a synthetic market_attribute.mat (regenerated from its seed
+    by the test)."""
+    import tempfile
+    _stubbed()
+    import data_prepare as ref_dp
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "attr.mat")
+        syn.write_market_attribute_mat(path, n_ids=24, seed=5)
+        ids, plain = ref_dp.get_prompts(path)
+        ids2, aug = ref_dp.get_prompts_augmented(path)
+    _, simple = ref_dp.get_prompts_simple(ids, 24)
+    assert ids == ids2
+    np.savez_compressed(os.path.join(out, "templates.npz"), ids=np.array(ids), plain=np.array([plain[i] for i in ids]),
+                        augmented=np.array([aug[i] for i in ids]), simple=np.array([simple[i] for i in ids]))
+    print("template fixtures ok", len(aug[ids[0]]))
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=HERE)
     ap.add_argument("--only", default="")
     a = ap.parse_args()
     todo = a.only.split(",") if a.only else ["backend", "rerank", "vit", "vitl", "text", "ivlp", "glue",
-                                              "adaptor", "e2e", "prompt"]
+                                              "adaptor", "e2e", "prompt", "template"]
     for t in todo:
         globals()[f"{t}_fixtures"](a.out)
