@@ -15,10 +15,12 @@ Total work is fixed as N grows ("strong").
 Extra legs in the same JSON line (not part of `value`): "msmt17" = configs[3] / the north
 star's target, MSMT17 end to end on all ranks (sharded embed, all-gather, distmat + CMC/mAP,
 sharded k-reciprocal re-rank + CMC/mAP, wall seconds max over ranks); "rerank" = configs[2]'s
-Duke-size re-rank on rank 0 with the C port timed on a sample; "cpu_baseline".
+Duke-size re-rank on rank 0 with the C port timed on the full config; "text" = the --mm
+zero-shot classifier's text side at Market size (750 x 56 token rows, TF/s); "backend" /
+"preprocess" = retrieval-kernel and transform rooflines; "cpu_baseline".
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B (default 1024)] [--no-cpu-baseline] [--no-rerank]
-                    [--no-msmt17]
+                    [--no-msmt17] [--no-text]
 """
 import argparse
 import json
@@ -292,6 +294,62 @@ def preprocess_leg(dev, n=19281, reps=5):
             "achieved_GBps": round(nbytes / (ms * 1e-3) / 1e9, 1), "peak_GBps": 8000.0}
 
 
+def text_leg(dev, n_cls=750, n_tpl=56, reps=3, cpu=True, threads=1, n_cpu=32):
+    """the --mm zero-shot classifier's text side at Market size
+    (zero_shot_learning.py:37-49): n_cls identities x n_tpl augmented templates = 42 000 token
+    rows of 77 through the CLIP text tower (width 512, 12 layers, causal), EOT rows ->
+    ln_final -> text_projection, then per-class L2-normalise / mean / L2-normalise.  Synthetic
+    token rows of 30-50 tokens (the augmented sentences' length) and random-init weights.
+    FLOP per row = layers * (24 L W^2 + 4 L^2 W) (the reference's dense causal attention
+    included) + 2 W E for the projection; rate against the dense fp16 MFMA peak."""
+    from multimodal_reid_amd.model import TextTransformer
+    sd = syn.text_state_dict(seed=0)
+    tm = TextTransformer(sd, device=dev)
+    N = n_cls * n_tpl
+    tokens = torch.from_numpy(syn.token_ids(N, seed=5, min_len=30, max_len=50)).to(dev)
+    counts = [n_tpl] * n_cls
+    L, W, E, layers = tm.ctx, tm.width, tm.out_dim, tm.layers
+    flop = N * (layers * (24.0 * L * W * W + 4.0 * L * L * W) + 2.0 * W * E)
+
+    def run():  # zero_shot_learning.zeroshot_classifier on device-resident token rows
+        return _classifier(tm, tokens, counts)
+
+    run()  # warm: sizes the workspace
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    s = e0.elapsed_time(e1) / reps * 1e-3
+    out = {"config": f"{n_cls} classes x {n_tpl} augmented templates = {N} x {L} tokens, CLIP text tower "
+                     f"(width {W}, {layers} layers), fp16 operands, + class mean/normalise",
+           "wall_s": round(s, 4), "seqs_per_s": round(N / s, 1), "gflop_per_seq": round(flop / N / 1e9, 3),
+           "achieved": round(flop / s / 1e12, 1), "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
+           "frac": round(flop / s / 1e12 / PEAK_F16_TFLOPS, 4)}
+    del tm
+    torch.cuda.empty_cache()
+    if cpu:
+        from oracle import vit_ref
+        torch.set_num_threads(threads)
+        tk = syn.token_ids(n_cpu, seed=5, min_len=30, max_len=50)
+        with torch.no_grad():
+            vit_ref.text_forward(sd, tk[:4])
+            t = time.perf_counter()
+            vit_ref.text_forward(sd, tk)
+            tc = (time.perf_counter() - t) / n_cpu
+        out["cpu_port"] = {"sample": f"oracle/vit_ref.py fp32 text tower on {n_cpu} rows ({tc * 1e3:.1f} ms/row), "
+                                     f"extrapolated to {N} rows", "wall_s": round(tc * N, 1), "cores": threads,
+                           "kind": "port"}
+    return out
+
+
+def _classifier(tm, tokens, counts):
+    from multimodal_reid_amd.ops import class_mean_normalize_device
+    return class_mean_normalize_device(tm.encode_text(tokens), counts)
+
+
 def cpu_baseline(wl, threads, n_img=64, bs=16):
     """The oracle ("port") on this host: the fp32 torch restatement of the encoder on a
     bounded image sample (both TTA passes, batches of `bs`), extrapolated linearly to the
@@ -334,6 +392,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-rerank", action="store_true")
     ap.add_argument("--no-msmt17", action="store_true")
+    ap.add_argument("--no-text", action="store_true")
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -412,6 +471,8 @@ def main():
         threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
         if not a.no_rerank:
             line["rerank"] = rerank_leg(dev, cpu=not a.no_cpu_baseline, threads=threads)
+        if not a.no_text:
+            line["text"] = text_leg(dev, cpu=not a.no_cpu_baseline, threads=threads)
         if not a.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(wl, threads)
         print(json.dumps(line))

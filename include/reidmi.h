@@ -178,6 +178,16 @@ int reidmi_layernorm(const float* x, int64_t rows, int64_t ldx, const int32_t* r
                      const float* gamma, const float* beta, float eps, float* y32, int64_t ldy32, void* y16,
                      int64_t ldy16, void* stream);
 
+/* The encoder's LayerNorm-fold pieces, exported for tests.  row_stats_f16: st [rows] float2 =
+ * (rstd, -mean*rstd) (eps 1e-5) of fp16 rows x [rows][ldx] (W = 512 | 768 | 1024), from a
+ * pass over x (pst == NULL) or combined from 64-column partials pst [W/64][rows] float2.
+ * gemm_f16_resid_partials: the residual GEMM (epi 6: out = half(out + A W^T + bias)) that
+ * also writes those partials of the updated rows, pst[n/64 * M + m] (N % 64 == 0). */
+int reidmi_row_stats_f16(const void* x, int64_t rows, int64_t ldx, int64_t W, const void* pst, void* st,
+                         void* stream);
+int reidmi_gemm_f16_resid_partials(const void* A, int64_t lda, const void* Wt, int64_t ldw, int64_t M, int64_t N,
+                                   int64_t K, const float* bias, void* out, int64_t ldc, void* pst, void* stream);
+
 /* Prompt construction — coop.PromptLearner.forward (coop.py:95-110) /
  * maple.VLPromptLearner.construct_prompts (maple.py:57-90): out [B][P+C+S][W] fp32 with
  * out[b] = cat(prefix [P][W], ctx[label[b]] [C][W] of ctx [ncls][C][W], suffix [S][W]).
@@ -259,12 +269,16 @@ typedef struct reidmi_text_weights {
     const reidmi_block_weights* blocks;
 } reidmi_text_weights;
 
+/* Workspace for N rows at the full ctx (an upper bound for any ctx_used). */
 int64_t reidmi_text_workspace_bytes(const reidmi_text_weights* w, int64_t N);
 
 /* tokens: device int64 [N][ctx] (always needed: the EOT row is tokens.argmax(-1)).
- * prompts: device fp32 [N][ctx][W] or NULL (then x = tok_emb[tokens]).  out [N][E] fp32. */
+ * prompts: device fp32 [N][ctx][W] or NULL (then x = tok_emb[tokens]).  out [N][E] fp32.
+ * ctx_used: 0 = all ctx positions; else run on the first ctx_used positions only, which
+ * gives the same output when every row's EOT position (argmax) and IVLP prompt rows are
+ * < ctx_used (causal mask: rows past the EOT never reach it); n_ctx < ctx_used <= ctx. */
 int reidmi_text_forward(const reidmi_text_weights* w, const int64_t* tokens, const float* prompts, int64_t N,
-                        float* out, void* ws, int64_t ws_bytes, void* stream);
+                        int ctx_used, float* out, void* ws, int64_t ws_bytes, void* stream);
 
 /* -------------------------------------------------------- inference glue (G1) */
 

@@ -268,19 +268,21 @@ __global__ void prompt_rows_kernel(_Float16* __restrict__ x, int64_t nseq, int L
     x[(b * L + row0 + r) * W + n] = (_Float16)prompt[r * W + n];
 }
 
-// x[n*L+t] = (prompts ? prompts[n,t] : tok_emb[tokens[n,t]]) + pos[t]   (maple.py:972-974)
+// x[n*L+t] = (prompts ? prompts[n,t] : tok_emb[tokens[n,t]]) + pos[t]   (maple.py:972-974),
+// t < L; tokens / prompts rows have Lt >= L positions (the first L are used).
 __global__ void text_embed_kernel(_Float16* __restrict__ x, const int64_t* __restrict__ tokens,
                                   const float* __restrict__ prompts, const float* __restrict__ tok_emb,
-                                  const float* __restrict__ pos, int64_t N, int L, int W, int64_t vocab) {
+                                  const float* __restrict__ pos, int64_t N, int L, int Lt, int W, int64_t vocab) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= N * L * (W / 4)) return;
     const int c4 = (int)(e % (W / 4));
     const int64_t nt = e / (W / 4);
     const int t = (int)(nt % L);
+    const int64_t src = (nt / L) * Lt + t;
     float4 v;
-    if (prompts) v = ((const float4*)(prompts + nt * W))[c4];
+    if (prompts) v = ((const float4*)(prompts + src * W))[c4];
     else {
-        int64_t id = tokens[nt];
+        int64_t id = tokens[src];
         id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
         v = ((const float4*)(tok_emb + id * W))[c4];
     }
@@ -289,16 +291,18 @@ __global__ void text_embed_kernel(_Float16* __restrict__ x, const int64_t* __res
     ((f16x4*)(x + nt * W))[c4] = h;
 }
 
-// row index of tokens[n].argmax() (first maximum, torch semantics) in the [N*L] row space
-__global__ void eot_rows_kernel(const int64_t* __restrict__ tokens, int64_t N, int L, int32_t* __restrict__ rows) {
+// row index of tokens[n].argmax() over all Lt positions (first maximum, torch semantics) in
+// the [N*L] row space (clamped to L-1: the caller's ctx_used covers every EOT position)
+__global__ void eot_rows_kernel(const int64_t* __restrict__ tokens, int64_t N, int L, int Lt,
+                                int32_t* __restrict__ rows) {
     const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (n >= N) return;
-    const int64_t* t = tokens + n * L;
+    const int64_t* t = tokens + n * Lt;
     int best = 0;
     int64_t bv = t[0];
-    for (int i = 1; i < L; i++)
+    for (int i = 1; i < Lt; i++)
         if (t[i] > bv) { bv = t[i]; best = i; }
-    rows[n] = (int32_t)(n * L + best);
+    rows[n] = (int32_t)(n * L + (best < L ? best : L - 1));
 }
 
 // --------------------------------------------------------------- workspace plan
@@ -573,11 +577,17 @@ REIDMI_API int64_t reidmi_text_workspace_bytes(const reidmi_text_weights* w, int
 }
 
 REIDMI_API int reidmi_text_forward(const reidmi_text_weights* w, const int64_t* tokens, const float* prompts,
-                                   int64_t N, float* out, void* ws_, int64_t ws_bytes, void* stream) {
+                                   int64_t N, int ctx_used, float* out, void* ws_, int64_t ws_bytes, void* stream) {
     RM_REQUIRE(w && w->blocks && tokens && out, "text: null argument");
     RM_REQUIRE(w->width == w->heads * 64 && w->width % 256 == 0, "text: width");
     hipStream_t s = (hipStream_t)stream;
-    const int W = w->width, L = w->ctx, E = w->out_dim;
+    const int W = w->width, Lt = w->ctx, E = w->out_dim;
+    // Causal mask: row t of every block reads rows <= t only, so the rows past the last EOT
+    // position never reach the output (x[n, argmax(tokens[n])], maple.py:981); ctx_used > 0
+    // runs the tower on the first ctx_used positions (the caller guarantees every EOT and
+    // every IVLP prompt row lies below it) - the same values for the rows it keeps.
+    const int L = ctx_used > 0 ? ctx_used : Lt;
+    RM_REQUIRE(L <= Lt && L > w->n_ctx, "text: ctx_used must be in (n_ctx, ctx]");
     RM_REQUIRE(attn_lpad(L) > 0, "text: context too long");
     const Plan P = plan(N, L, W, attn_lpad(L), N);
     RM_REQUIRE(ws_bytes >= P.total, "text: workspace too small");
@@ -588,7 +598,7 @@ REIDMI_API int reidmi_text_forward(const reidmi_text_weights* w, const int64_t* 
     int32_t* rows = (int32_t*)(ws + P.rows);
     const int64_t te = N * L * (W / 4);
     hipLaunchKernelGGL(text_embed_kernel, dim3(ceil_div(te, 256)), dim3(256), 0, s, x, tokens, prompts, w->tok_emb,
-                       w->pos_emb, N, L, W, (int64_t)w->vocab);
+                       w->pos_emb, N, L, Lt, W, (int64_t)w->vocab);
     RM_LAUNCHED();
     int rc;
     for (int i = 0; i < w->layers; i++) {
@@ -602,11 +612,38 @@ REIDMI_API int reidmi_text_forward(const reidmi_text_weights* w, const int64_t* 
         const bool x_pst = i > 0 && !(bw.prompt && w->n_ctx > 0);
         if ((rc = run_block(bw, ws, P, N, L, W, w->heads, true, x_pst, s))) return rc;
     }
-    hipLaunchKernelGGL(eot_rows_kernel, dim3(ceil_div(N, 256)), dim3(256), 0, s, tokens, N, L, rows);
+    hipLaunchKernelGGL(eot_rows_kernel, dim3(ceil_div(N, 256)), dim3(256), 0, s, tokens, N, L, Lt, rows);
     RM_LAUNCHED();
     if ((rc = layernorm(x, N, W, rows, W, w->ln_final_w, w->ln_final_b, 1e-5f, nullptr, 0, h, W, s))) return rc;
     EpiArgs eo{};
     eo.out = out;
     eo.ldc = E;
     return gemm_f16(EPI_F32, h, W, w->proj_t, W, N, E, W, eo, s);
+}
+
+// LayerNorm row statistics as the encoder computes them (test entry points): st[r] =
+// (rstd, -mean * rstd) of the fp16 rows x, from a pass over x (pst == NULL) or combined from
+// the residual epilogue's 64-column partials pst [W/64][rows] (run_block's ln_1 / ln_2).
+REIDMI_API int reidmi_row_stats_f16(const void* x, int64_t rows, int64_t ldx, int64_t W, const void* pst, void* st,
+                                    void* stream) {
+    RM_REQUIRE(st && (x || pst), "row stats: null argument");
+    if (pst) return row_stats_from_partials((const float2*)pst, rows, (int)W, (float2*)st, (hipStream_t)stream);
+    return row_stats((const _Float16*)x, rows, ldx, W, (float2*)st, (hipStream_t)stream);
+}
+
+// The residual GEMM of run_block with its LayerNorm partials: out[m][n] = half(out[m][n] +
+// (A W^T)[m][n] + bias[n]) and pst[n/64 * M + m] = (sum, centred sum of squares) of the 64
+// updated values of row m in column block n/64 (N % 64 == 0).
+REIDMI_API int reidmi_gemm_f16_resid_partials(const void* A, int64_t lda, const void* Wt, int64_t ldw, int64_t M,
+                                              int64_t N, int64_t K, const float* bias, void* out, int64_t ldc,
+                                              void* pst, void* stream) {
+    RM_REQUIRE(A && Wt && out && pst && N % 64 == 0, "resid partials: null argument or N % 64 != 0");
+    EpiArgs e{};
+    e.out = out;
+    e.ldc = ldc;
+    e.bias = bias;
+    e.pstat = (float2*)pst;
+    e.ldp = M;
+    return gemm_f16(EPI_RESID_F16, (const _Float16*)A, lda, (const _Float16*)Wt, ldw, M, (int)N, (int)K, e,
+                    (hipStream_t)stream);
 }

@@ -50,8 +50,8 @@ _SIG = {
     "reidmi_vit_forward": ([ctypes.POINTER(VitWeights), _vp, ctypes.c_int, ctypes.c_int64, ctypes.c_int,
                             ctypes.c_int, _vp, ctypes.c_int, _vp, _vp, _vp, _vp, ctypes.c_int64, _vp], ctypes.c_int),
     "reidmi_text_workspace_bytes": ([ctypes.POINTER(TextWeights), ctypes.c_int64], ctypes.c_int64),
-    "reidmi_text_forward": ([ctypes.POINTER(TextWeights), _vp, _vp, ctypes.c_int64, _vp, _vp, ctypes.c_int64, _vp],
-                            ctypes.c_int),
+    "reidmi_text_forward": ([ctypes.POINTER(TextWeights), _vp, _vp, ctypes.c_int64, ctypes.c_int, _vp, _vp,
+                             ctypes.c_int64, _vp], ctypes.c_int),
 }
 
 
@@ -271,13 +271,28 @@ class TextTransformer:
         self._blocks = _pack_blocks(sd, "", layers, pk)
         w.blocks = self._blocks
         self._ws = None
+        # run on the positions up to the last EOT of the batch only (exact: causal mask,
+        # reidmi_text_forward's ctx_used); False = all ctx positions, as the reference does
+        self.trim_context = True
 
     def token_embedding(self, tokens):
         """nn.Embedding lookup (device) — used by prompt learners to build prompts."""
         return self.token_embedding_weight[torch.as_tensor(tokens, device=self.device).long()]
 
+    def ctx_used(self, tokens):
+        """Positions the batch needs: 1 + the largest EOT position (tokens.argmax(-1), the
+        row text_encoder.py:23 / maple.py:981 reads), and at least the IVLP prompt rows."""
+        if not self.trim_context or tokens.shape[0] == 0:
+            return 0
+        last = int(tokens.argmax(-1).max())  # one host sync when tokens are on the device
+        return max(last + 1, self.n_ctx + 1)
+
     def _forward(self, tokens, prompts):
-        tokens = torch.as_tensor(tokens).to(self.device, torch.int64).contiguous()
+        tokens = torch.as_tensor(tokens)
+        if tokens.dim() != 2 or tokens.shape[1] != self.ctx:
+            raise ValueError(f"tokens must be [N, {self.ctx}]")
+        used = self.ctx_used(tokens)
+        tokens = tokens.to(self.device, torch.int64).contiguous()
         N = tokens.shape[0]
         nbytes = _fn("reidmi_text_workspace_bytes")(ctypes.byref(self.weights), N)
         if self._ws is None or self._ws.numel() < nbytes:
@@ -286,7 +301,7 @@ class TextTransformer:
         if prompts is not None:
             prompts = prompts.to(self.device, torch.float32).contiguous()
         rc = _fn("reidmi_text_forward")(ctypes.byref(self.weights), tokens.data_ptr(),
-                                        None if prompts is None else prompts.data_ptr(), N, out.data_ptr(),
+                                        None if prompts is None else prompts.data_ptr(), N, used, out.data_ptr(),
                                         self._ws.data_ptr(), nbytes, _lib.stream(self.device))
         if rc != 0:
             raise _lib.ReidmiError(f"reidmi_text_forward: {_lib.load().reidmi_last_error().decode()}")

@@ -138,6 +138,42 @@ def test_gemm_f16_layernorm_fold(gpu, epi, M, N, K):
 
 
 @pytest.mark.parametrize("W", [512, 768, 1024])
+@pytest.mark.parametrize("M,K_mult", [(300, 1), (1037, 4), (13, 1)])
+def test_residual_partials_rowstats(gpu, W, M, K_mult):
+    """The residual epilogue's 64-column LayerNorm partials (EpiArgs::pstat) combined by
+    rowstat_combine_kernel (run_block's ln_1 / ln_2 statistics) equal a statistics pass over
+    the same fp16 rows within a few ulp, for every width and ragged M."""
+    L = _lib()
+    g = torch.Generator(device="cuda").manual_seed(W + M)
+    K = W * K_mult
+    A = (torch.randn(M, K, device="cuda", generator=g) * 0.5).half()
+    Wt = (torch.randn(W, K, device="cuda", generator=g) * K ** -0.5).half()
+    bias = torch.randn(W, device="cuda", generator=g) * 0.1
+    x = (torch.randn(M, W, device="cuda", generator=g) * 3 + 0.7).half()
+    pst = torch.full((W // 64, M, 2), float("nan"), device="cuda")
+    L.call("reidmi_gemm_f16_resid_partials", L.ptr(A), K, L.ptr(Wt), K, M, W, K, L.ptr(bias), L.ptr(x), W,
+           L.ptr(pst), L.stream())
+    st_p = torch.empty(M, 2, device="cuda")
+    st_x = torch.empty(M + 256, 2, device="cuda")
+    L.call("reidmi_row_stats_f16", None, M, W, W, L.ptr(pst), L.ptr(st_p), L.stream())
+    L.call("reidmi_row_stats_f16", L.ptr(x), M, W, W, None, L.ptr(st_x), L.stream())
+    torch.cuda.synchronize()
+    assert torch.isfinite(pst).all()
+    xf = x.double()  # the rows the residual GEMM updated in place
+    mean, var = xf.mean(1), xf.var(1, unbiased=False)
+    rstd = (var + 1e-5).rsqrt()
+    want = torch.stack([rstd, -mean * rstd], 1).float()
+    assert torch.allclose(st_p, st_x[:M], rtol=1e-5, atol=1e-6)
+    assert torch.allclose(st_p, want, rtol=2e-5, atol=2e-6)
+    # the partials themselves: per 64-column block sum and centred sum of squares
+    blk = xf.view(M, W // 64, 64)
+    s = blk.sum(2)
+    m2 = ((blk - blk.mean(2, keepdim=True)) ** 2).sum(2)
+    assert torch.allclose(pst[..., 0].double(), s.t(), rtol=1e-5, atol=1e-3)
+    assert torch.allclose(pst[..., 1].double(), m2.t(), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("W", [512, 768, 1024])
 def test_layernorm(gpu, W):
     L = _lib()
     x = torch.randn(333, W) * 3 + 1
@@ -285,6 +321,30 @@ def test_text_encoder_vs_reference(gpu):
     prompts = tm.token_embedding(g["tokens"])
     out2 = te(prompts, torch.from_numpy(g["tokens"])).cpu().numpy()
     assert np.array_equal(out, out2)
+
+
+@pytest.mark.parametrize("text_ctx", [0, 4])
+def test_text_trimmed_context_bitexact(gpu, text_ctx):
+    """ctx_used (the causal-mask trim to 1 + the batch's last EOT position) changes no bit of
+    encode_text / TextEncoder, for token rows and for IVLP text prompts (maple.py:630-640);
+    a row encoded alone (its own, shorter trim) equals the same row inside the batch."""
+    from multimodal_reid_amd.model import TextTransformer, TextEncoder
+    sd = syn.text_state_dict(seed=3, layers=4, text_ctx=text_ctx)
+    tm = TextTransformer(sd)
+    tok = syn.token_ids(24, seed=3, min_len=8, max_len=60)
+    assert tm.ctx_used(torch.from_numpy(tok)) == int(tok.argmax(-1).max()) + 1 < 77
+    trimmed = tm.encode_text(tok)
+    tm.trim_context = False
+    full = tm.encode_text(tok)
+    assert torch.equal(trimmed, full)
+    prompts = tm.token_embedding(tok)
+    te = TextEncoder(tm)
+    pf = te(prompts, torch.from_numpy(tok))
+    tm.trim_context = True
+    pt = te(prompts, torch.from_numpy(tok))
+    assert torch.equal(pf, pt) and torch.equal(pt, trimmed)
+    for i in (0, 5, 17):
+        assert torch.equal(tm.encode_text(tok[i:i + 1])[0], trimmed[i])
 
 
 def test_inference_glue(vit_b16):
