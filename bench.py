@@ -38,6 +38,7 @@ import reidmi_boot  # noqa: E402
 
 reidmi_boot.load()
 from multimodal_reid_amd import _lib, evaluate, synthetic as syn  # noqa: E402
+from multimodal_reid_amd.distributed import gather_rows, shard  # noqa: E402
 from multimodal_reid_amd import zero_shot_learning as zsl  # noqa: E402
 from multimodal_reid_amd.model import VisionTransformer  # noqa: E402
 
@@ -53,24 +54,6 @@ EPI_GELU = 1  # the c_fc GEMM (+QuickGELU epilogue): the largest single kernel p
 # are re-read by the 2 XCD groups and W panels by the rounds of an XCD (4 MB L2).
 # Algorithmic: A 332 MB + W 4.7 MB + out 1 327 MB = 1.66 GB.
 C_FC_TRAFFIC_BYTES = (2 * 736400 + 1296384) * 1024
-
-
-def shard(n, rank, world):
-    lo = n * rank // world
-    return lo, n * (rank + 1) // world
-
-
-def gather_rows(x, n_total, world):
-    """all_gather of row shards (sizes differ by <= 1) into [n_total, D]."""
-    if world == 1:
-        return x
-    sizes = [shard(n_total, r, world)[1] - shard(n_total, r, world)[0] for r in range(world)]
-    mx = max(sizes)
-    pad = torch.zeros((mx,) + tuple(x.shape[1:]), device=x.device, dtype=x.dtype)
-    pad[:x.shape[0]] = x
-    out = torch.empty((world * mx,) + tuple(x.shape[1:]), device=x.device, dtype=x.dtype)
-    dist.all_gather_into_tensor(out, pad)
-    return torch.cat([out[r * mx:r * mx + sizes[r]] for r in range(world)])
 
 
 class Workload:
@@ -106,14 +89,14 @@ class Workload:
         self.embed(self.q_img, self.q_tta, self.q_emb)
         self.embed(self.g_img, self.g_tta, self.g_emb)
         qn = evaluate.l2_normalize_device(self.q_emb)
-        gn = gather_rows(evaluate.l2_normalize_device(self.g_emb), self.G, self.world)
+        gn = gather_rows(evaluate.l2_normalize_device(self.g_emb), self.G)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         evaluate.euclidean_distance_device(qn, gn, out=self.dist)
         valid, first, ap, nkept, ovf = evaluate.eval_rows_device(
             self.dist, self.q_pids[self.qlo:self.qhi], self.g_pids, self.q_cams[self.qlo:self.qhi], self.g_cams)
         rows = torch.stack([valid.double(), first.double(), ap, nkept.double()], 1)
-        rows = gather_rows(rows, self.Q, self.world)
+        rows = gather_rows(rows, self.Q)
         torch.cuda.synchronize()
         rows = rows.cpu().numpy()
         cmc, mAP = evaluate.aggregate_cmc_map(rows[:, 0].astype(np.int64), rows[:, 1].astype(np.int64), rows[:, 2],
@@ -140,7 +123,7 @@ def msmt17_leg(model, dev, rank, world, batch):
     def rows_to_map(d):
         valid, first, ap, nkept, ovf = evaluate.eval_rows_device(
             d, wl.q_pids[wl.qlo:wl.qhi], wl.g_pids, wl.q_cams[wl.qlo:wl.qhi], wl.g_cams)
-        rows = gather_rows(torch.stack([valid.double(), first.double(), ap, nkept.double()], 1), Q, world)
+        rows = gather_rows(torch.stack([valid.double(), first.double(), ap, nkept.double()], 1), Q)
         rows = rows.cpu().numpy()
         return evaluate.aggregate_cmc_map(rows[:, 0].astype(np.int64), rows[:, 1].astype(np.int64), rows[:, 2],
                                           rows[:, 3].astype(np.int64), G, 50)
@@ -149,8 +132,8 @@ def msmt17_leg(model, dev, rank, world, batch):
     t0 = time.perf_counter()
     wl.embed(wl.q_img, wl.q_tta, wl.q_emb)
     wl.embed(wl.g_img, wl.g_tta, wl.g_emb)
-    qn = gather_rows(evaluate.l2_normalize_device(wl.q_emb), Q, world)
-    gn = gather_rows(evaluate.l2_normalize_device(wl.g_emb), G, world)
+    qn = gather_rows(evaluate.l2_normalize_device(wl.q_emb), Q)
+    gn = gather_rows(evaluate.l2_normalize_device(wl.g_emb), G)
     sync()
     t1 = time.perf_counter()
     evaluate.euclidean_distance_device(qn[wl.qlo:wl.qhi], gn, out=wl.dist)

@@ -21,9 +21,13 @@ import torch.distributed as dist
 
 
 def world():
-    if dist.is_available() and dist.is_initialized():
+    if _initialized():
         return dist.get_rank(), dist.get_world_size()
     return 0, 1
+
+
+def _initialized():
+    return dist.is_available() and dist.is_initialized()
 
 
 def shard(n, rank, world_size):
@@ -33,9 +37,10 @@ def shard(n, rank, world_size):
 
 def gather_rows(x, n_total):
     """All-gather row shards produced by `shard(n_total, r, W)` into one [n_total, ...] tensor
-    (same device as x).  RCCL path: one padded all_gather_into_tensor."""
+    (same device as x).  RCCL path: one padded all_gather_into_tensor (also run at world
+    size 1 when a process group exists, so a 1-GPU box exercises the RCCL path)."""
     rank, W = world()
-    if W == 1:
+    if not _initialized():
         return x
     sizes = [shard(n_total, r, W)[1] - shard(n_total, r, W)[0] for r in range(W)]
     mx = max(sizes)
@@ -62,7 +67,7 @@ def gather_var(x):
     """All-gather 1-D pieces of different lengths; returns their concatenation in rank order
     (same device as x).  Used for the CSR payloads of the sharded re-ranking."""
     rank, W = world()
-    if W == 1:
+    if not _initialized():
         return x
     dev = _collective_device(x)
     dtype = x.dtype
