@@ -202,14 +202,13 @@ __global__ __launch_bounds__(512) void mhsa_kernel(const _Float16* __restrict__ 
     }
 }
 
-// V^T row stride (elements): >= LP, == 2 dwords mod 64 dwords, so the 32 rows of one
-// half-wave ds_read_b64 cover all 64 banks exactly once.  The QKV epilogue writes V^T with
-// this same stride in HBM, so one head's V^T is a contiguous blob for the LDS-DMA copy.
-static int vt_stride(int lp) {
-    int dw = lp / 2;
-    int pad = ((2 - dw) % 64 + 64) % 64;
-    return (dw + pad) * 2;
-}
+// V^T row stride (elements): LP + 4, i.e. LP/2 + 2 dwords, which is 2 mod 4 dwords (LP is a
+// multiple of 32): the 32 rows of one half-wave ds_read_b64 then start on 32 distinct even
+// banks (row r at bank 2 * (r * odd mod 32)), so they cover all 64 banks exactly once.  (The
+// stride 2 mod 64 used before padded V^T by up to 60 elements per row: 23 % of V at L = 211.)
+// The QKV epilogue writes V^T with this same stride in HBM, so one head's V^T is a contiguous
+// blob for the LDS-DMA copy; 64 * (LP + 4) * 2 bytes is a multiple of 512.
+static int vt_stride(int lp) { return lp + 4; }
 
 static int g_num_cu = 0;
 static int num_cu() {

@@ -1,4 +1,4 @@
-"""Run the encoder's attention kernel on the bench shape (512 images x 12 heads, L = 211)
+"""Run the encoder's attention kernel on the bench shape (NSEQ (default 1024) images x 12 heads, L = 211)
 REPS times, for rocprofv3 --pmc / --kernel-trace passes:  python tools/attn_one.py [REPS]"""
 import os
 import sys
@@ -14,7 +14,7 @@ from multimodal_reid_amd import _lib as L  # noqa: E402
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
-    nseq, H, Lq = 512, 12, 211
+    nseq, H, Lq = int(os.environ.get("NSEQ", "1024")), 12, 211
     lib = L.load()
     lp = lib.reidmi_attn_lpad(Lq)
     dev = torch.device("cuda")
