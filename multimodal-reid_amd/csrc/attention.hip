@@ -238,7 +238,19 @@ static int launch_mhsa(const void* q, const void* k, const void* vt, void* o, in
     }
     const int64_t nbh = nseq * H;
     const int waves = (L + 31) / 32;
-    const int64_t grid = nbh < num_cu() ? nbh : num_cu();
+    // Persistent grid: as many workgroups per CU as fit (LDS, VGPRs).  Vision (L = 211: 7
+    // waves, 2 x 57 KB LDS) fits one; short text rows (L <= 64: 2 waves, 2 x 17 KB) fit four,
+    // which a single workgroup per CU would leave latency-bound on its K/V loads.
+    static int occ_waves = -1, occ = 1;
+    if (occ_waves != waves) {
+        int n = 0;
+        RM_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)mhsa_kernel<NKB, CAUSAL>,
+                                                                  64 * waves, lds));
+        occ = n > 0 ? n : 1;
+        occ_waves = waves;
+    }
+    const int64_t slots = (int64_t)num_cu() * occ;
+    const int64_t grid = nbh < slots ? nbh : slots;
     hipLaunchKernelGGL((mhsa_kernel<NKB, CAUSAL>), dim3((unsigned)grid), dim3(64 * waves), lds, s,
                        (const _Float16*)q, (const _Float16*)k, (const _Float16*)vt, (_Float16*)o, L, H, vs, nbh,
                        scale_log2);
