@@ -320,12 +320,17 @@ __device__ double leaf_sum(POS pos, VAL val, int lo, int hi, int64_t off, int64_
         for (int t = lo; t < hi; t++) res += val(t);
         return res;
     }
+    // r[] indexed only by constants (a run-time index would put it in scratch memory, one
+    // memory round trip per access): each accumulator adds v or +0.0, and r + 0.0 == r for
+    // every r reachable here (all accumulators start at +0.0 and the values are positive)
     double r[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const int64_t main_end = n - (n % 8);
     int t = lo;
     for (; t < hi && pos(t) - off < main_end; t++) {
-        int64_t p = pos(t) - off;
-        r[p & 7] += val(t);
+        const int p = (int)((pos(t) - off) & 7);
+        const double v = val(t);
+#pragma unroll
+        for (int k = 0; k < 8; k++) r[k] += p == k ? v : 0.0;
     }
     double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
     for (; t < hi; t++) res += val(t);
@@ -446,6 +451,72 @@ __device__ double pairwise_tree_wave(const int* rk, VAL val, int m, int64_t n, u
         res = vals[0];
     }
     return res;
+}
+
+// pairwise_tree_wave for m <= 64 without LDS on the serial chain: lane t holds rk[t] (in
+// rk_l); the leaf-by-leaf combination runs on every lane with wave-uniform values (readlane),
+// and its two stacks keep entry i in lane i (writelane / readlane).  The LDS variant waited
+// one LDS round trip per step of that dependent chain (a third of a Market query's time).
+// VAL: (t, rk[t]) -> double.  Same additions in the same order: bit-identical.
+template <typename VAL>
+__device__ double pairwise_tree_regs(int rk_l, VAL val, int m, int64_t n) {
+    const int lane = threadIdx.x & 63;
+    uint32_t pb = 0;
+    int d = 0;
+    if (lane < m) {
+        int64_t off = 0, len = n;
+        while (len > 128) {
+            int64_t n2 = len / 2;
+            n2 -= n2 % 8;
+            if ((int64_t)rk_l - off < n2) len = n2;
+            else { off += n2; len -= n2; pb |= 1u << d; }
+            d++;
+        }
+    }
+    auto rd = [](int v, int t) { return __builtin_amdgcn_readlane(v, t); };
+    auto wr = [&](int x, int i, int old) { return lane == i ? x : old; };  // writelane
+    int sv_lo = 0, sv_hi = 0, so = 0;
+    int sp = 0, op = 0, t = 0;
+    auto push_val = [&](double x) {
+        const uint64_t b = __builtin_bit_cast(uint64_t, x);
+        sv_lo = wr((int)(uint32_t)b, sp, sv_lo);
+        sv_hi = wr((int)(uint32_t)(b >> 32), sp, sv_hi);
+        sp++;
+    };
+    auto get_val = [&](int i) {
+        const uint32_t lo = (uint32_t)rd(sv_lo, i), hi = (uint32_t)rd(sv_hi, i);
+        return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+    };
+    auto reduce_top = [&]() {  // vals[sp-2] += vals[sp-1]
+        const double b = get_val(sp - 1), a = get_val(sp - 2);
+        sp -= 2;
+        push_val(a + b);
+        op--;
+    };
+    while (t < m) {
+        const uint32_t pt = (uint32_t)rd((int)pb, t);
+        const int dt = rd(d, t);
+        int u = t + 1;
+        while (u < m && (uint32_t)rd((int)pb, u) == pt && rd(d, u) == dt) u++;
+        int64_t off = 0, len = n;
+        for (int e = 0; e < dt; e++) {
+            int64_t n2 = len / 2;
+            n2 -= n2 % 8;
+            if ((pt >> e) & 1u) { off += n2; len -= n2; } else len = n2;
+        }
+        const double v = leaf_sum([&](int k) { return (int64_t)rd(rk_l, k); },
+                                  [&](int k) { return val(k, rd(rk_l, k)); }, t, u, off, len);
+        if (t > 0) {
+            const int c = __builtin_ctz((uint32_t)rd((int)pb, t - 1) ^ pt);
+            while (op > 0 && rd(so, op - 1) > c) reduce_top();
+            so = wr(c, op, so);
+            op++;
+        }
+        push_val(v);
+        t = u;
+    }
+    while (op > 0) reduce_top();
+    return get_val(0);
 }
 
 // Per query (evaluate.py:40-80): positives = gallery items with the query's pid and another
@@ -711,8 +782,11 @@ __global__ __launch_bounds__(256) void eval_rows_wg_kernel(
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();
         const int* rk = hist;
-        const double sum = pairwise_tree_wave(rk, [&](int t) { return (double)(t + 1) / (double)(rk[t] + 1); }, m,
-                                              G - nj, (uint32_t*)pv, pi, tvals, tops);  // pv / pi are free now
+        const double sum =
+            m <= 64 ? pairwise_tree_regs(lane < m ? rk[lane] : 0,
+                                         [](int t, int r) { return (double)(t + 1) / (double)(r + 1); }, m, G - nj)
+                    : pairwise_tree_wave(rk, [&](int t) { return (double)(t + 1) / (double)(rk[t] + 1); }, m, G - nj,
+                                         (uint32_t*)pv, pi, tvals, tops);  // pv / pi are free now
         if (lane == 0) {
             valid[q] = 1;
             first[q] = rk[0];
