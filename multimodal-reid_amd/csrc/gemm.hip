@@ -479,8 +479,9 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 // Persistent: grid = min(#tiles, 256) (one workgroup per CU).  The two DMA streams — "+1"
 // (region B0 of the next K-step) and "+2" (A0, B1, A1 of the K-step after) — run over the
 // workgroup's concatenated (tile, K-step) sequence, so while a tile's epilogue runs, the next
-// tile's first two K-steps are already landing.  The epilogue needs no barrier: group A runs
-// it in the slot where group B computes the tile's last quadrant.
+// tile's first two K-steps are already landing.  Both groups run the epilogue in one barrier
+// slot (their store tails overlap: +1 % c_fc, +2-6 % out_proj over running them back to
+// back, profiles/r02/gemm_epilogue_sync_ab.txt).
 //
 // Tile walk (XCD-aware): workgroup b runs on XCD b % 8.  The XCDs are split into `ngroups`
 // groups; group k owns the N-tiles [k T_n / ngroups, (k+1) T_n / ngroups), and each XCD of
@@ -731,6 +732,10 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
             advance(p2);
             buf ^= 1;
         }
+        // both wave groups run the epilogue in the same barrier slot (group A, one barrier ahead
+        // in the K-loop, waits here for group B's last COMPUTE; B catches up after it), so the
+        // two groups' store tails overlap instead of running back to back
+        if (wr == 0) G5_BARRIER();
         const int64_t m0 = (int64_t)(tile / tnk) * G2_M;
         const int n0 = (nb0 + tile % tnk) * G2_N;
         if constexpr (CAN_DEFER) {
@@ -792,6 +797,7 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
                 }
         }
         epilogue_tile<EPI, 8, true>(ea, acc, m0 + wr * 128, n0 + wc * 64, M, N);
+        if (wr == 1) G5_BARRIER();
     }
     if (wr == 0) G5_BARRIER();
 #undef G5_BARRIER
