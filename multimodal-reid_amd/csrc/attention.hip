@@ -18,6 +18,96 @@ int attn_lpad(int L);
 
 __device__ __forceinline__ int kswz(int r, int kc) { return r * 64 + ((kc ^ ((r >> 1) & 7)) << 3); }
 
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+
+// One wave's block of 32 queries (row qi = block * 32 + (lane & 31)) against the head's K
+// [LP][64] and V^T [64][vstride] in LDS:
+//   S^T[key][q] = K Q^T on v_mfma_f32_32x32x16_f16; lane (q = lane&31, h = lane>>5) holds
+//     keys kb*32 + (r&3) + 8(r>>2) + 4h in s[kb][r];
+//   P stays in registers: registers 8s'..8s'+7 of block kb are the B fragment of key-step s'
+//     of O^T = V^T P^T (accumulator-as-operand), V^T read with the same key permutation;
+//   O^T[d][q] comes out as 4 runs of 4 consecutive d per lane -> 8 8-byte stores (the wave's
+//     only vector-memory ops here; lanes with qi >= L store nothing).
+template <int NKB, bool CAUSAL>
+__device__ __forceinline__ void attn_block(const _Float16* sK, const _Float16* sV, int vstride, const f16x8 (&qf)[4],
+                                           int qi, int L, int64_t bh, int H, _Float16* __restrict__ o,
+                                           float scale_log2) {
+    const int lane = threadIdx.x & 63;
+    const int hh = lane >> 5, ql = lane & 31;
+    f32x16 s[NKB];
+#pragma unroll
+    for (int kb = 0; kb < NKB; kb++) {
+        f32x16 a = f32x16{};
+#pragma unroll
+        for (int ks = 0; ks < 4; ks++) {
+            const f16x8 kf = *(const f16x8*)(sK + kswz(kb * 32 + ql, 2 * ks + hh));
+            a = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[ks], a, 0, 0, 0);
+        }
+        s[kb] = a;
+    }
+    float mx = -__builtin_inff();
+#pragma unroll
+    for (int kb = 0; kb < NKB; kb++)
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            if (CAUSAL || kb == NKB - 1) {
+                const int key = kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+                const bool ok = key < L && (!CAUSAL || key <= qi);
+                s[kb][r] = ok ? s[kb][r] : -__builtin_inff();
+            }
+            mx = fmaxf(mx, s[kb][r]);
+        }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    // exponent argument and running sums on packed-fp32 VALU (v_pk_fma_f32 /
+    // v_pk_add_f32: two elements per instruction); two partial sums (even / odd r).
+    const float mb = -mx * scale_log2;
+    const f32x2v sc2 = {scale_log2, scale_log2}, mb2 = {mb, mb};
+    f32x2v sum2 = {0.f, 0.f};
+#pragma unroll
+    for (int kb = 0; kb < NKB; kb++)
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+            const f32x2v t = __builtin_elementwise_fma(f32x2v{s[kb][r], s[kb][r + 1]}, sc2, mb2);
+            const f32x2v p = {__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
+            s[kb][r] = p.x;
+            s[kb][r + 1] = p.y;
+            sum2 += p;
+        }
+    float sum = sum2.x + sum2.y;
+    sum += __shfl_xor(sum, 32, 64);
+    const float inv = 1.0f / sum;
+    f32x16 oacc[2] = {f32x16{}, f32x16{}};
+#pragma unroll
+    for (int kb = 0; kb < NKB; kb++)
+#pragma unroll
+        for (int sp = 0; sp < 2; sp++) {
+            f16x8 pf;
+#pragma unroll
+            for (int j = 0; j < 8; j++) pf[j] = (_Float16)s[kb][8 * sp + j];
+#pragma unroll
+            for (int db = 0; db < 2; db++) {
+                const _Float16* vr = sV + (db * 32 + ql) * vstride + kb * 32 + 16 * sp + 4 * hh;
+                const f16x4 v0 = *(const f16x4*)(vr);
+                const f16x4 v1 = *(const f16x4*)(vr + 8);
+                const f16x8 vf = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+                oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, pf, oacc[db], 0, 0, 0);
+            }
+        }
+    if (qi < L) {
+        const int64_t b = bh / H, hd = bh % H;
+        _Float16* orow = o + (b * L + qi) * (int64_t)(H * 64) + hd * 64;
+#pragma unroll
+        for (int db = 0; db < 2; db++)
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                f16x4 w = {(_Float16)(oacc[db][4 * g] * inv), (_Float16)(oacc[db][4 * g + 1] * inv),
+                            (_Float16)(oacc[db][4 * g + 2] * inv), (_Float16)(oacc[db][4 * g + 3] * inv)};
+                *(f16x4*)(orow + db * 32 + 8 * g + 4 * hh) = w;
+            }
+    }
+}
+
 // Persistent: gridDim.x workgroups (one per CU) walk the (sequence, head) pairs; one wave
 // per 32-query block (ceil(L/32) waves).  NKB = number of 32-key blocks (Lp = 32 * NKB).
 // K of the next head is copied into the other LDS stage by global_load_lds (8 rows per 1-KiB
@@ -29,8 +119,6 @@ __device__ __forceinline__ int kswz(int r, int kc) { return r * 64 + ((kc ^ ((r 
 //   P stays in registers: registers 8s'..8s'+7 of block kb are the B fragment of key-step s'
 //     of O^T = V^T P^T (accumulator-as-operand), V^T read with the same key permutation;
 //   O^T[d][q] comes out as 4 runs of 4 consecutive d per lane -> 8-byte stores.
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
-typedef float f32x2v __attribute__((ext_vector_type(2)));
 
 template <int NKB, bool CAUSAL>
 __global__ __launch_bounds__(512) void mhsa_kernel(const _Float16* __restrict__ q, const _Float16* __restrict__ k,
@@ -106,79 +194,7 @@ __global__ __launch_bounds__(512) void mhsa_kernel(const _Float16* __restrict__ 
         }
         const _Float16* sK = lds + stage * stage_elems;
         const _Float16* sV = sK + LP * 64;
-        if (wid * 32 < L) {
-            f32x16 s[NKB];
-#pragma unroll
-            for (int kb = 0; kb < NKB; kb++) {
-                f32x16 a = f32x16{};
-#pragma unroll
-                for (int ks = 0; ks < 4; ks++) {
-                    const f16x8 kf = *(const f16x8*)(sK + kswz(kb * 32 + ql, 2 * ks + hh));
-                    a = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[ks], a, 0, 0, 0);
-                }
-                s[kb] = a;
-            }
-            float mx = -__builtin_inff();
-#pragma unroll
-            for (int kb = 0; kb < NKB; kb++)
-#pragma unroll
-                for (int r = 0; r < 16; r++) {
-                    if (CAUSAL || kb == NKB - 1) {
-                        const int key = kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-                        const bool ok = key < L && (!CAUSAL || key <= qi);
-                        s[kb][r] = ok ? s[kb][r] : -__builtin_inff();
-                    }
-                    mx = fmaxf(mx, s[kb][r]);
-                }
-            mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-            // exponent argument and running sums on packed-fp32 VALU (v_pk_fma_f32 /
-            // v_pk_add_f32: two elements per instruction); two partial sums (even / odd r).
-            const float mb = -mx * scale_log2;
-            const f32x2v sc2 = {scale_log2, scale_log2}, mb2 = {mb, mb};
-            f32x2v sum2 = {0.f, 0.f};
-#pragma unroll
-            for (int kb = 0; kb < NKB; kb++)
-#pragma unroll
-                for (int r = 0; r < 16; r += 2) {
-                    const f32x2v t = __builtin_elementwise_fma(f32x2v{s[kb][r], s[kb][r + 1]}, sc2, mb2);
-                    const f32x2v p = {__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
-                    s[kb][r] = p.x;
-                    s[kb][r + 1] = p.y;
-                    sum2 += p;
-                }
-            float sum = sum2.x + sum2.y;
-            sum += __shfl_xor(sum, 32, 64);
-            const float inv = 1.0f / sum;
-            f32x16 oacc[2] = {f32x16{}, f32x16{}};
-#pragma unroll
-            for (int kb = 0; kb < NKB; kb++)
-#pragma unroll
-                for (int sp = 0; sp < 2; sp++) {
-                    f16x8 pf;
-#pragma unroll
-                    for (int j = 0; j < 8; j++) pf[j] = (_Float16)s[kb][8 * sp + j];
-#pragma unroll
-                    for (int db = 0; db < 2; db++) {
-                        const _Float16* vr = sV + (db * 32 + ql) * vstride + kb * 32 + 16 * sp + 4 * hh;
-                        const f16x4 v0 = *(const f16x4*)(vr);
-                        const f16x4 v1 = *(const f16x4*)(vr + 8);
-                        const f16x8 vf = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-                        oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, pf, oacc[db], 0, 0, 0);
-                    }
-                }
-            if (qi < L) {
-                const int64_t b = bh / H, hd = bh % H;
-                _Float16* orow = o + (b * L + qi) * (int64_t)(H * 64) + hd * 64;
-#pragma unroll
-                for (int db = 0; db < 2; db++)
-#pragma unroll
-                    for (int g = 0; g < 4; g++) {
-                        f16x4 w = {(_Float16)(oacc[db][4 * g] * inv), (_Float16)(oacc[db][4 * g + 1] * inv),
-                                    (_Float16)(oacc[db][4 * g + 2] * inv), (_Float16)(oacc[db][4 * g + 3] * inv)};
-                        *(f16x4*)(orow + db * 32 + 8 * g + 4 * hh) = w;
-                    }
-            }
-        }
+        if (wid * 32 < L) attn_block<NKB, CAUSAL>(sK, sV, vstride, qf, qi, L, bh, H, o, scale_log2);
         // Wait for the next head's K/V DMA and Q loads only: the 8 O stores this wave just
         // issued (when it owns queries) are the youngest vector-memory ops and stay in flight
         // (vmcnt retires in issue order).
