@@ -704,10 +704,14 @@ __global__ __launch_bounds__(256) void eval_rows_wg_kernel(
     const int li = pi[m - 1];
     const float v0 = pv[0];
     const int T = 8 * P < EVW_T ? (8 * P > 64 ? 8 * P : 64) : EVW_T;  // ~8 buckets per positive
-    const float scale = (float)T / (lv - v0);  // inf / NaN when the positives tie: clamped
+    // t(x) = floor(med3(x * scale - v_0 * scale, 0, T-1)): one fma, one med3, one floor-convert
+    // per item; when the positives tie (scale inf / NaN) every item goes to bucket 0 and the
+    // exact compares decide
+    float scale = (float)T / (lv - v0);
+    if (!(scale <= 3.0e38f)) scale = 0.0f;
+    const float c0 = -v0 * scale, tmax = (float)(T - 1);
     auto bucket_of = [&](float x) {
-        const float f = __builtin_floorf((x - v0) * scale);
-        return (int)__builtin_fminf(__builtin_fmaxf(f, 0.0f), (float)(T - 1));
+        return (int)__builtin_floorf(__builtin_amdgcn_fmed3f(__builtin_fmaf(x, scale, c0), 0.0f, tmax));
     };
     for (int t = tid; t < T; t += 256) {  // S[t] = #{k : t(pv_k) < t}
         int lo = 0, hi = m;
@@ -724,8 +728,9 @@ __global__ __launch_bounds__(256) void eval_rows_wg_kernel(
     }
     __syncthreads();
     auto bin = [&](float v, int j) {
-        // after the last positive (b = m, not needed); NaN sorts last (np.argsort)
-        if (key_less(lv, li, v, j) || v != v) return;
+        // after the last positive (b = m, not needed); NaN sorts last (np.argsort):
+        // key_less(lv, li, v, j) || v != v, with the NaN test folded into !(v <= lv)
+        if (!(v <= lv) || (v == lv && j > li)) return;
         const int2 se = bucket[bucket_of(v)];
         int b = se.x;
         while (b < se.y && key_less(pv[b], pi[b], v, j)) b++;
