@@ -317,6 +317,34 @@ int reidmi_preprocess_u8(const uint8_t* pix, const int64_t* meta, int64_t B, int
  * (the call fails above 160 KiB: resize such images on the host first). */
 int reidmi_preprocess_lds_size(int oh, int ow, int max_h, int max_w, int64_t* bytes);
 
+/* ---------------------------------------------------------------- JPEG decode (§8f) */
+
+/* Image.open(path).convert("RGB") — data_prepare.py:87-92 (reidDataset.__getitem__, run in the
+ * DataLoader workers of data_prepare.py:275-283) — for a batch of JPEG files, bit-exact with
+ * Pillow 12.2 / libjpeg-turbo defaults (islow IDCT, fancy upsampling).  Supported: baseline /
+ * extended-sequential Huffman, 8-bit, one scan, grayscale or 3 components at 4:4:4, 4:2:2,
+ * 4:2:0.  Two steps:
+ *
+ * reidmi_jpeg_plan (HOST only, no GPU): parses the headers of files[offsets[i] .. offsets[i+1])
+ * (host bytes, offsets int64 [B+1]) and writes
+ *   status int32 [B]  0 ok, 1 not a JPEG / truncated, 2 progressive / lossless / arithmetic /
+ *                     12-bit / multi-scan, 3 component layout, 4 bad tables;
+ *   meta int64 [B][3] (byte offset in the decoded batch, h, w) — the `meta` of
+ *                     reidmi_preprocess_u8; zeros for images with status != 0;
+ *   info int64 [7]    plan bytes, workspace bytes, decoded bytes, max h, max w, images with
+ *                     status != 0, coefficient count;
+ *   plan              when plan != NULL and plan_capacity >= info[0]: a position-independent
+ *                     blob the caller copies to the device (call once with plan = NULL to size it).
+ *
+ * reidmi_jpeg_decode (stream-ordered): files = the same bytes on the DEVICE, plan = the plan on
+ * the device, info = the HOST info[7] of the plan call; ws >= info[1] bytes; pix >= info[2]
+ * bytes receives the HWC uint8 images; err int32 [B] (device) = the plan status, or 5 where the
+ * entropy-coded data does not decode. */
+int reidmi_jpeg_plan(const uint8_t* files, const int64_t* offsets, int64_t B, void* plan, int64_t plan_capacity,
+                     int64_t* meta, int32_t* status, int64_t* info);
+int reidmi_jpeg_decode(const uint8_t* files, const void* plan, const int64_t* info, int64_t B, void* ws,
+                       int64_t ws_bytes, uint8_t* pix, int32_t* err, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

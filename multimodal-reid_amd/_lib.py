@@ -58,6 +58,8 @@ SIGNATURES = {
     "reidmi_prompt_build": [_vp, _i32, _vp, _i32, _vp, _i64, _vp, _i32, _i64, _i32, _vp, _vp, _vp],
     "reidmi_preprocess_u8": [_vp, _vp, _i64, _i32, _i32, _i32, _i32, _vp, _vp, _i32, _vp, _vp],
     "reidmi_preprocess_lds_size": [_i32, _i32, _i32, _i32, _vp],
+    "reidmi_jpeg_plan": [_vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp],
+    "reidmi_jpeg_decode": [_vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp],
 }
 # entry points with struct arguments are typed in model.py (reidmi_vit_*, reidmi_text_*)
 STRUCT_ENTRY_POINTS = ("reidmi_vit_workspace_bytes", "reidmi_vit_forward", "reidmi_text_workspace_bytes",

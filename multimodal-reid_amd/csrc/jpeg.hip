@@ -1,0 +1,357 @@
+// jpeg.hip — JPEG decode of the reference's loaders on the GPU:
+// reidDataset.__getitem__ opens every crop with `Image.open(path).convert("RGB")`
+// (data_prepare.py:87-92) in 4 DataLoader workers (data_prepare.py:275-283).  Here a batch of
+// baseline JPEG files is decoded on the device, bit-exact with Pillow / libjpeg-turbo, into the
+// packed HWC uint8 layout reidmi_preprocess_u8 (transforms.hip) consumes.
+//
+// Split (the arithmetic lives in jpeg_core.h):
+//   host   reidmi_jpeg_plan    — marker parse of each file's headers (a few hundred bytes):
+//                                quantisers, Huffman tables (derived once per distinct table),
+//                                geometry, workspace / output offsets -> one plan blob;
+//   device jpeg_entropy_kernel — one lane per image: the serial Huffman decode (the only
+//                                sequential part of JPEG) into int16 coefficient blocks;
+//          jpeg_pixels_kernel  — one workgroup per image: islow IDCT of every block into its
+//                                component plane (L2-resident), then fancy upsampling +
+//                                YCbCr->RGB per output pixel.
+// Supported: baseline / extended-sequential Huffman, 8-bit, one scan, grayscale or three
+// components at 4:4:4, 4:2:2 or 4:2:0 (every ReID benchmark's crops).  Anything else gets a
+// per-image status and is left to the caller (the Python mirror raises).
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "jpeg_core.h"
+
+namespace reidmi {
+namespace jpeg {
+
+// ------------------------------------------------------------------ host: header parse
+
+static void build_huff(const uint8_t* counts, const uint8_t* syms, int nsym, JpegHuff& t) {
+    // jdhuff.c jpeg_make_d_derived_tbl: canonical codes by length, then the lookahead table
+    memset(&t, 0, sizeof(t));
+    int p = 0;
+    int32_t code = 0;
+    for (int l = 1; l <= 16; ++l) {
+        const int n = counts[l - 1];
+        if (n) {
+            t.valoff[l] = p - code;
+            for (int i = 0; i < n; ++i, ++p, ++code) {
+                if (l <= 9) {
+                    const int shift = 9 - l;
+                    for (int e = 0; e < (1 << shift); ++e)
+                        t.lut[(code << shift) | e] = (uint16_t)((l << 8) | syms[p]);
+                }
+            }
+            t.maxcode[l] = code - 1;
+        } else {
+            t.maxcode[l] = -1;
+        }
+        code <<= 1;
+    }
+    t.maxcode[17] = 0x7FFFFFFF;
+    for (int i = 0; i < nsym && i < 256; ++i) t.val[i] = syms[i];
+}
+
+struct Pools {
+    std::vector<JpegHuff> huff;
+    std::map<std::string, int> huff_ix;
+    std::vector<int16_t> quant;   // [n][64]
+    std::map<std::string, int> quant_ix;
+
+    int add_huff(const std::string& raw) {   // raw = 16 counts + symbols
+        auto it = huff_ix.find(raw);
+        if (it != huff_ix.end()) return it->second;
+        JpegHuff t;
+        build_huff((const uint8_t*)raw.data(), (const uint8_t*)raw.data() + 16, (int)raw.size() - 16, t);
+        huff.push_back(t);
+        return huff_ix[raw] = (int)huff.size() - 1;
+    }
+    int add_quant(const int16_t* q) {
+        std::string key((const char*)q, 128);
+        auto it = quant_ix.find(key);
+        if (it != quant_ix.end()) return it->second;
+        quant.insert(quant.end(), q, q + 64);
+        return quant_ix[key] = (int)(quant.size() / 64) - 1;
+    }
+};
+
+static inline int u16be(const uint8_t* p) { return (p[0] << 8) | p[1]; }
+
+// jdmarker.c read_markers up to the first SOS, restricted to what the device decodes.
+static int32_t parse_one(const uint8_t* f, int64_t n, int64_t base, JpegImage& im, Pools& pools) {
+    memset(&im, 0, sizeof(im));
+    if (n < 4 || f[0] != 0xFF || f[1] != 0xD8) return J_NOT_JPEG;
+    int64_t p = 2;
+    bool jfif = false, adobe = false, sof = false;
+    int adobe_t = -1;
+    bool qdef[4] = {false, false, false, false};
+    int16_t qt[4][64];
+    std::string hdc[4], hac[4];
+    int cid[3] = {0, 0, 0}, tq[3] = {0, 0, 0};
+    for (;;) {
+        while (p < n && f[p] != 0xFF) ++p;   // extraneous bytes (libjpeg warns and skips)
+        while (p < n && f[p] == 0xFF) ++p;   // fill bytes
+        if (p >= n) return J_NOT_JPEG;
+        const int m = f[p++];
+        if (m == 0x01 || m == 0xD8 || (m >= 0xD0 && m <= 0xD7)) continue;
+        if (m == 0xD9) return J_NOT_JPEG;   // EOI before any scan
+        if (p + 2 > n) return J_NOT_JPEG;
+        const int len = u16be(f + p);
+        if (len < 2 || p + len > n) return J_NOT_JPEG;
+        const uint8_t* s = f + p + 2;
+        const int sl = len - 2;
+        if (m == 0xC0 || m == 0xC1) {   // SOF0 baseline / SOF1 extended sequential, Huffman
+            if (sl < 6 || s[0] != 8) return J_UNSUPPORTED;
+            im.h = u16be(s + 1);
+            im.w = u16be(s + 3);
+            im.ncomp = s[5];
+            if (im.h == 0 || im.w == 0) return J_UNSUPPORTED;   // DNL-defined height
+            if (im.ncomp != 1 && im.ncomp != 3) return J_LAYOUT;
+            if (sl < 6 + 3 * im.ncomp) return J_NOT_JPEG;
+            for (int c = 0; c < im.ncomp; ++c) {
+                cid[c] = s[6 + 3 * c];
+                im.hs[c] = s[7 + 3 * c] >> 4;
+                im.vs[c] = s[7 + 3 * c] & 15;
+                tq[c] = s[8 + 3 * c] & 3;
+            }
+            sof = true;
+        } else if ((m >= 0xC2 && m <= 0xCF) && m != 0xC4 && m != 0xC8 && m != 0xCC) {
+            return J_UNSUPPORTED;   // progressive, lossless, hierarchical, arithmetic
+        } else if (m == 0xC4) {     // DHT
+            int i = 0;
+            while (i + 17 <= sl) {
+                const int tc = s[i] >> 4, th = s[i] & 15;
+                int tot = 0;
+                for (int l = 0; l < 16; ++l) tot += s[i + 1 + l];
+                if (tc > 1 || th > 3 || tot > 256 || i + 17 + tot > sl) return J_BAD_TABLE;
+                std::string raw((const char*)s + i + 1, 16 + tot);
+                (tc ? hac : hdc)[th] = raw;
+                i += 17 + tot;
+            }
+        } else if (m == 0xDB) {     // DQT
+            int i = 0;
+            while (i < sl) {
+                const int pq = s[i] >> 4, t = s[i] & 15;
+                if (pq > 1 || t > 3 || i + 1 + 64 * (pq + 1) > sl) return J_BAD_TABLE;
+                for (int k = 0; k < 64; ++k)   // kept in zig-zag order; libjpeg's quantval is
+                    qt[t][k] = (int16_t)(pq ? u16be(s + i + 1 + 2 * k) : s[i + 1 + k]);   // read as-is
+                qdef[t] = true;
+                i += 1 + 64 * (pq + 1);
+            }
+        } else if (m == 0xDD) {     // DRI
+            if (sl < 2) return J_NOT_JPEG;
+            im.ri = u16be(s);
+        } else if (m == 0xE0) {
+            if (sl >= 5 && memcmp(s, "JFIF\0", 5) == 0) jfif = true;
+        } else if (m == 0xEE) {
+            if (sl >= 12 && memcmp(s, "Adobe", 5) == 0) {
+                adobe = true;
+                adobe_t = s[11];
+            }
+        } else if (m == 0xDA) {     // SOS
+            if (!sof) return J_NOT_JPEG;
+            const int ns = sl > 0 ? s[0] : 0;
+            if (ns != im.ncomp || sl < 4 + 2 * ns) return J_UNSUPPORTED;   // one interleaved scan only
+            for (int j = 0; j < ns; ++j) {
+                if (s[1 + 2 * j] != cid[j]) return J_UNSUPPORTED;   // scan order = frame order
+                const int td = s[2 + 2 * j] >> 4, ta = s[2 + 2 * j] & 15;
+                if (td > 3 || ta > 3 || hdc[td].empty() || hac[ta].empty()) return J_BAD_TABLE;
+                im.dc[j] = pools.add_huff(hdc[td]);
+                im.ac[j] = pools.add_huff(hac[ta]);
+            }
+            const uint8_t* e = s + 1 + 2 * ns;
+            if (e[0] != 0 || e[1] != 63 || e[2] != 0) return J_UNSUPPORTED;   // Ss, Se, Ah/Al
+            im.src_off = base + p + len;
+            im.src_len = n - (p + len);
+            break;
+        }
+        p += len;
+    }
+    for (int c = 0; c < im.ncomp; ++c) {
+        if (!qdef[tq[c]]) return J_BAD_TABLE;
+        im.quant[c] = pools.add_quant(qt[tq[c]]);
+    }
+    // geometry (jdinput.c initial_setup, per_scan_setup)
+    if (im.ncomp == 1) {
+        im.hs[0] = im.vs[0] = 1;
+        im.mcux = (im.w + 7) / 8;
+        im.mcuy = (im.h + 7) / 8;
+        im.bw[0] = im.mcux;
+        im.bh[0] = im.mcuy;
+        im.dw[0] = im.w;
+        im.dh[0] = im.h;
+        im.cspace = CS_GRAY;
+    } else {
+        const int h0 = im.hs[0], v0 = im.vs[0];
+        for (int c = 1; c < 3; ++c)
+            if (im.hs[c] != 1 || im.vs[c] != 1) return J_LAYOUT;
+        if (!((h0 == 1 && v0 == 1) || (h0 == 2 && v0 == 1) || (h0 == 2 && v0 == 2))) return J_LAYOUT;
+        im.mcux = (im.w + 8 * h0 - 1) / (8 * h0);
+        im.mcuy = (im.h + 8 * v0 - 1) / (8 * v0);
+        for (int c = 0; c < 3; ++c) {
+            im.bw[c] = im.mcux * im.hs[c];
+            im.bh[c] = im.mcuy * im.vs[c];
+            im.dw[c] = (int)(((int64_t)im.w * im.hs[c] + h0 - 1) / h0);
+            im.dh[c] = (int)(((int64_t)im.h * im.vs[c] + v0 - 1) / v0);
+        }
+        // jdapimin.c default_decompress_parms (3 components)
+        if (jfif) im.cspace = CS_YCC;
+        else if (adobe) im.cspace = adobe_t == 0 ? CS_RGB : CS_YCC;
+        else if (cid[0] == 82 && cid[1] == 71 && cid[2] == 66) im.cspace = CS_RGB;
+        else im.cspace = CS_YCC;
+    }
+    if ((int64_t)im.w * im.h > (int64_t)1 << 26) return J_UNSUPPORTED;   // > 64 Mpixel
+    return J_OK;
+}
+
+static inline int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
+
+// ------------------------------------------------------------------ device
+
+__global__ __launch_bounds__(64) void jpeg_entropy_kernel(const uint8_t* __restrict__ src,
+                                                          const uint8_t* __restrict__ plan, int64_t B,
+                                                          int16_t* __restrict__ coef, int32_t* __restrict__ err) {
+    const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    if (i >= B) return;
+    const JpegPlan* P = (const JpegPlan*)plan;
+    const JpegImage im = ((const JpegImage*)(plan + P->img_off))[i];
+    int32_t st = im.status;
+    if (st == J_OK) st = entropy_decode(src, im, (const JpegHuff*)(plan + P->huff_off), coef);
+    err[i] = st;
+}
+
+__global__ __launch_bounds__(256) void jpeg_pixels_kernel(const uint8_t* __restrict__ plan,
+                                                          const int16_t* __restrict__ coef,
+                                                          uint8_t* __restrict__ planes, uint8_t* __restrict__ out) {
+    const JpegPlan* P = (const JpegPlan*)plan;
+    const JpegImage im = ((const JpegImage*)(plan + P->img_off))[blockIdx.x];
+    if (im.status != J_OK) return;
+    const int16_t* qbase = (const int16_t*)(plan + P->quant_off);
+    const int nc = im.ncomp;
+    const int64_t n0 = (int64_t)im.bw[0] * im.bh[0];
+    const int64_t n1 = nc > 1 ? (int64_t)im.bw[1] * im.bh[1] : 0;
+    const int64_t nblk = n0 + (nc > 1 ? 2 * n1 : 0);
+    for (int64_t t = threadIdx.x; t < nblk; t += 256) {
+        int c;
+        int64_t local;
+        if (t < n0) {
+            c = 0;
+            local = t;
+        } else {
+            c = t < n0 + n1 ? 1 : 2;
+            local = t - n0 - (c == 2 ? n1 : 0);
+        }
+        const int bw = c == 0 ? im.bw[0] : (c == 1 ? im.bw[1] : im.bw[2]);
+        const int64_t by = local / bw, bx = local - by * bw;
+        const int64_t pitch = (int64_t)bw * 8;
+        const int qi = c == 0 ? im.quant[0] : (c == 1 ? im.quant[1] : im.quant[2]);
+        const int64_t cc = c == 0 ? im.comp_coef[0] : (c == 1 ? im.comp_coef[1] : im.comp_coef[2]);
+        const int64_t cp = c == 0 ? im.comp_plane[0] : (c == 1 ? im.comp_plane[1] : im.comp_plane[2]);
+        idct_islow(coef + im.coef_off + cc + local * 64, qbase + (int64_t)qi * 64,
+                   planes + im.plane_off + cp + by * 8 * pitch + bx * 8, pitch);
+    }
+    __syncthreads();
+    const int64_t npx = (int64_t)im.w * im.h;
+    uint8_t* o = out + im.out_off;
+    for (int64_t p = threadIdx.x; p < npx; p += 256) {
+        const int y = (int)(p / im.w);
+        const int x = (int)(p - (int64_t)y * im.w);
+        uint8_t rgb[3];
+        pixel_rgb(im, planes, x, y, rgb);
+        o[p * 3 + 0] = rgb[0];
+        o[p * 3 + 1] = rgb[1];
+        o[p * 3 + 2] = rgb[2];
+    }
+}
+
+}  // namespace jpeg
+}  // namespace reidmi
+
+using namespace reidmi;
+using namespace reidmi::jpeg;
+
+REIDMI_API int reidmi_jpeg_plan(const uint8_t* files, const int64_t* offsets, int64_t B, void* plan,
+                                int64_t plan_capacity, int64_t* meta, int32_t* status, int64_t* info) {
+    RM_REQUIRE(B >= 0 && info != nullptr && (B == 0 || (files && offsets && meta && status)),
+               "reidmi_jpeg_plan: bad arguments");
+    std::vector<JpegImage> imgs((size_t)B);
+    Pools pools;
+    int64_t coef = 0, plane = 0, outb = 0, max_h = 0, max_w = 0, bad = 0;
+    for (int64_t i = 0; i < B; ++i) {
+        const int64_t a = offsets[i], n = offsets[i + 1] - offsets[i];
+        RM_REQUIRE(a >= 0 && n >= 0, "reidmi_jpeg_plan: offsets must be non-decreasing from 0");
+        JpegImage& im = imgs[(size_t)i];
+        const int32_t st = parse_one(files + a, n, a, im, pools);
+        im.status = st;
+        status[i] = st;
+        if (st != J_OK) {
+            meta[3 * i] = meta[3 * i + 1] = meta[3 * i + 2] = 0;
+            ++bad;
+            continue;
+        }
+        im.coef_off = coef;
+        im.plane_off = plane;
+        int64_t cc = 0;
+        for (int c = 0; c < im.ncomp; ++c) {
+            im.comp_coef[c] = cc;
+            im.comp_plane[c] = cc;   // one byte per coefficient slot: the same relative layout
+            cc += (int64_t)im.bw[c] * im.bh[c] * 64;
+        }
+        coef += cc;
+        plane += cc;
+        im.out_off = outb;
+        meta[3 * i] = outb;
+        meta[3 * i + 1] = im.h;
+        meta[3 * i + 2] = im.w;
+        outb += (int64_t)im.w * im.h * 3;
+        max_h = im.h > max_h ? im.h : max_h;
+        max_w = im.w > max_w ? im.w : max_w;
+    }
+    JpegPlan hdr;
+    hdr.B = B;
+    hdr.n_huff = (int64_t)pools.huff.size();
+    hdr.n_quant = (int64_t)pools.quant.size() / 64;
+    hdr.img_off = align_up(sizeof(JpegPlan), 64);
+    hdr.huff_off = align_up(hdr.img_off + B * (int64_t)sizeof(JpegImage), 64);
+    hdr.quant_off = align_up(hdr.huff_off + hdr.n_huff * (int64_t)sizeof(JpegHuff), 64);
+    hdr.coef_elems = coef;
+    hdr.plane_bytes = plane;
+    hdr.out_bytes = outb;
+    const int64_t plan_bytes = hdr.quant_off + hdr.n_quant * 128;
+    info[0] = plan_bytes;
+    info[1] = align_up(coef * 2, 256) + plane;   // workspace: int16 coefficients, then planes
+    info[2] = outb;
+    info[3] = max_h;
+    info[4] = max_w;
+    info[5] = bad;
+    info[6] = coef;
+    if (plan == nullptr || plan_capacity < plan_bytes) return OK;   // sizing call
+    uint8_t* pb = (uint8_t*)plan;
+    memset(pb, 0, (size_t)plan_bytes);
+    memcpy(pb, &hdr, sizeof(hdr));
+    if (B) memcpy(pb + hdr.img_off, imgs.data(), (size_t)B * sizeof(JpegImage));
+    if (hdr.n_huff) memcpy(pb + hdr.huff_off, pools.huff.data(), pools.huff.size() * sizeof(JpegHuff));
+    if (hdr.n_quant) memcpy(pb + hdr.quant_off, pools.quant.data(), pools.quant.size() * sizeof(int16_t));
+    return OK;
+}
+
+REIDMI_API int reidmi_jpeg_decode(const uint8_t* files, const void* plan, const int64_t* info, int64_t B, void* ws,
+                                  int64_t ws_bytes, uint8_t* pix, int32_t* err, void* stream) {
+    RM_REQUIRE(info != nullptr && B >= 0, "reidmi_jpeg_decode: bad arguments");
+    if (B == 0) return OK;
+    RM_REQUIRE(files && plan && ws && err && (pix || info[2] == 0), "reidmi_jpeg_decode: null pointer");
+    RM_REQUIRE(ws_bytes >= info[1], "reidmi_jpeg_decode: workspace smaller than info[1]");
+    hipStream_t s = (hipStream_t)stream;
+    int16_t* coef = (int16_t*)ws;
+    uint8_t* planes = (uint8_t*)ws + align_up(info[6] * 2, 256);
+    if (info[6]) RM_CHECK_HIP(hipMemsetAsync(coef, 0, (size_t)info[6] * 2, s));
+    jpeg_entropy_kernel<<<dim3((unsigned)((B + 63) / 64)), dim3(64), 0, s>>>(files, (const uint8_t*)plan, B, coef,
+                                                                             err);
+    RM_LAUNCHED();
+    jpeg_pixels_kernel<<<dim3((unsigned)B), dim3(256), 0, s>>>((const uint8_t*)plan, coef, planes, pix);
+    RM_LAUNCHED();
+    return OK;
+}

@@ -1,0 +1,401 @@
+// jpeg_core.h — baseline-JPEG decode arithmetic shared by the device kernels (jpeg.hip) and
+// the host-side check tool (tools/jpeg_host_check.hip).  What it reproduces, bit for bit, is
+// the decoder behind the reference's `Image.open(path).convert("RGB")` (data_prepare.py:89):
+// Pillow 12.2 on libjpeg-turbo (jpeg 6.2 API) with its defaults — Huffman sequential decode,
+// the "islow" integer IDCT (LL&M, 13-bit constants, 2 extra bits between passes), "fancy"
+// triangular chroma upsampling for 2x1 and 2x2 subsampling, and the 16-bit fixed-point
+// YCbCr -> RGB tables.  The published algorithm is restated here; the GPU tests pin it
+// against Pillow's own output.
+//
+// A decode plan (built on the host by reidmi_jpeg_plan from the file headers) is one
+// position-independent blob: JpegPlan | JpegImage[B] | JpegHuff[n_huff] | int16 quant[n_quant][64]
+// (quantisers, like the coefficients, in zig-zag order).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace reidmi {
+namespace jpeg {
+
+// per-image status (reidmi_jpeg_plan / reidmi_jpeg_decode)
+enum : int32_t {
+    J_OK = 0,
+    J_NOT_JPEG = 1,        // no SOI / truncated headers
+    J_UNSUPPORTED = 2,     // progressive, lossless, arithmetic-coded, 12-bit, multi-scan
+    J_LAYOUT = 3,          // component count / sampling factors outside 1, 3 x {4:4:4, 4:2:2, 4:2:0}
+    J_BAD_TABLE = 4,       // missing or malformed DQT / DHT
+    J_BAD_DATA = 5,        // entropy-coded data does not decode (set by the device pass)
+};
+
+enum : int32_t { CS_GRAY = 0, CS_YCC = 1, CS_RGB = 2 };
+
+struct JpegHuff {          // jdhuff.c-style derived table
+    uint16_t lut[512];     // 9-bit lookahead: (code length << 8) | symbol, 0 = longer code
+    int32_t maxcode[18];   // largest code of each length (-1 if none); [17] sentinel
+    int32_t valoff[18];    // symbol index of a length-l code = code + valoff[l]
+    uint8_t val[256];
+};
+
+struct JpegImage {
+    int64_t src_off, src_len;   // entropy-coded data (after SOS) in the file batch
+    int64_t coef_off;           // int16 elements into the coefficient workspace
+    int64_t plane_off;          // bytes into the plane workspace
+    int64_t out_off;            // bytes into the RGB output (HWC uint8)
+    int64_t comp_coef[3];       // per component, relative to coef_off
+    int64_t comp_plane[3];      // per component, relative to plane_off
+    int32_t w, h, ncomp, cspace;
+    int32_t mcux, mcuy, ri, status;   // MCUs per row / column, restart interval (MCUs)
+    int32_t hs[3], vs[3];       // sampling factors (1 or 2)
+    int32_t bw[3], bh[3];       // blocks per row / column (whole MCUs)
+    int32_t dw[3], dh[3];       // downsampled component size (libjpeg downsampled_width/height)
+    int32_t quant[3], dc[3], ac[3];   // pool indices
+};
+
+struct JpegPlan {
+    int64_t B, n_huff, n_quant;
+    int64_t img_off, huff_off, quant_off;   // bytes from the plan start
+    int64_t coef_elems, plane_bytes, out_bytes;
+};
+
+// natural (row-major) index -> zig-zag position.  Coefficients and quantisers are kept in
+// zig-zag (stream) order; the IDCT's fully unrolled loads apply this permutation at compile time.
+constexpr uint8_t kZz[64] = {0,  1,  5,  6,  14, 15, 27, 28, 2,  4,  7,  13, 16, 26, 29, 42,
+                             3,  8,  12, 17, 25, 30, 41, 43, 9,  11, 18, 24, 31, 40, 44, 53,
+                             10, 19, 23, 32, 39, 45, 52, 54, 20, 22, 33, 38, 46, 51, 55, 60,
+                             21, 34, 37, 47, 50, 56, 59, 61, 35, 36, 48, 49, 57, 58, 62, 63};
+
+// ---------------------------------------------------------------- entropy decode (one image)
+// jdhuff.c decode_mcu for a single interleaved (or single-component) baseline scan, written as
+// one flat loop over Huffman symbols so that the lanes of a wave (one image each) stay
+// converged: one iteration = one DC or AC symbol.  Bits are read MSB first from a 64-bit
+// window; 0xFF00 is a stuffed 0xFF; any other marker stops the stream (zeros are fed, as
+// libjpeg does) until the restart logic skips an RSTn.
+struct BitReader {
+    const uint8_t* p;
+    const uint8_t* end;
+    uint64_t acc;
+    int bits;
+    bool marker;
+
+    __host__ __device__ inline void refill() {
+        while (bits <= 56) {
+            uint32_t b = 0;
+            if (!marker) {
+                if (p >= end) {
+                    marker = true;
+                } else {
+                    b = p[0];
+                    if (b == 0xFF) {
+                        const uint32_t n = (p + 1 < end) ? p[1] : 0xD9;
+                        if (n == 0) {
+                            p += 2;
+                        } else {
+                            marker = true;
+                            b = 0;
+                        }
+                    } else {
+                        ++p;
+                    }
+                }
+            }
+            acc |= (uint64_t)b << (56 - bits);
+            bits += 8;
+        }
+    }
+    __host__ __device__ inline uint32_t take(int n) {   // n in [1, 16]
+        const uint32_t v = (uint32_t)(acc >> (64 - n));
+        acc <<= n;
+        bits -= n;
+        return v;
+    }
+    // jpeg_huff_decode: returns the symbol or -1 for an invalid code
+    __host__ __device__ inline int decode(const JpegHuff* t) {
+        const uint32_t e = t->lut[acc >> 55];
+        if (e >> 8) {
+            const int l = (int)(e >> 8);
+            acc <<= l;
+            bits -= l;
+            return (int)(e & 0xFF);
+        }
+        const uint32_t code16 = (uint32_t)(acc >> 48);
+        int l = 10;
+        int32_t c = (int32_t)(code16 >> 6);
+        while (l <= 16 && c > t->maxcode[l]) {
+            ++l;
+            c = (int32_t)(code16 >> (16 - l));
+        }
+        if (l > 16) return -1;
+        acc <<= l;
+        bits -= l;
+        return t->val[(c + t->valoff[l]) & 0xFF];
+    }
+    // skip to just past the next RSTn (jdmarker.c read_restart_marker on a valid stream)
+    __host__ __device__ inline void restart() {
+        acc = 0;
+        bits = 0;
+        marker = false;
+        while (p + 1 < end && !(p[0] == 0xFF && p[1] >= 0xD0 && p[1] <= 0xD7)) ++p;
+        if (p + 1 < end) p += 2;
+    }
+};
+
+__host__ __device__ inline int32_t huff_extend(uint32_t v, int s) {   // HUFF_EXTEND
+    return (v < (1u << (s - 1))) ? (int32_t)v - (1 << s) + 1 : (int32_t)v;
+}
+
+// Decodes one image's scan into zig-zag-order int16 coefficient blocks (the caller zeroed
+// them).  Returns J_OK or J_BAD_DATA.
+__host__ __device__ inline int32_t entropy_decode(const uint8_t* src, const JpegImage& im, const JpegHuff* huff,
+                                                  int16_t* coef) {
+    BitReader br{src + im.src_off, src + im.src_off + im.src_len, 0, 0, false};
+    const int n0 = im.ncomp == 1 ? 1 : im.hs[0] * im.vs[0];   // Y blocks per MCU
+    const int nb = im.ncomp == 1 ? 1 : n0 + 2;                // blocks per MCU
+    const int64_t nmcu = (int64_t)im.mcux * im.mcuy;
+    const JpegHuff* dct0 = huff + im.dc[0];
+    const JpegHuff* dct1 = huff + im.dc[im.ncomp > 1 ? 1 : 0];
+    const JpegHuff* dct2 = huff + im.dc[im.ncomp > 2 ? 2 : 0];
+    const JpegHuff* act0 = huff + im.ac[0];
+    const JpegHuff* act1 = huff + im.ac[im.ncomp > 1 ? 1 : 0];
+    const JpegHuff* act2 = huff + im.ac[im.ncomp > 2 ? 2 : 0];
+    int16_t* base0 = coef + im.coef_off + im.comp_coef[0];
+    int16_t* base1 = coef + im.coef_off + im.comp_coef[1];
+    int16_t* base2 = coef + im.coef_off + im.comp_coef[2];
+    int32_t pred0 = 0, pred1 = 0, pred2 = 0;
+    int64_t mcu = 0;
+    int mx = 0, my = 0, b = 0, k = 0;
+    int togo = im.ri;   // MCUs left in this restart interval
+    int16_t* blk = base0;
+    int comp = 0;
+    const JpegHuff* tbl = dct0;
+    while (mcu < nmcu) {
+        br.refill();
+        const int sym = br.decode(tbl);
+        if (sym < 0) return J_BAD_DATA;
+        if (k == 0) {
+            int32_t diff = 0;
+            if (sym) {
+                if (sym > 15) return J_BAD_DATA;
+                diff = huff_extend(br.take(sym), sym);
+            }
+            int32_t dc;
+            if (comp == 0) dc = pred0 += diff;
+            else if (comp == 1) dc = pred1 += diff;
+            else dc = pred2 += diff;
+            blk[0] = (int16_t)dc;
+            k = 1;
+            tbl = comp == 0 ? act0 : comp == 1 ? act1 : act2;
+        } else {
+            const int r = sym >> 4, s = sym & 15;
+            if (s) {
+                k += r;
+                if (k > 63) return J_BAD_DATA;
+                blk[k] = (int16_t)huff_extend(br.take(s), s);
+                ++k;
+            } else if (r == 15) {
+                k += 16;
+            } else {
+                k = 64;
+            }
+        }
+        if (k >= 64) {   // block done: advance to the next block of the MCU (or MCU)
+            k = 0;
+            if (++b == nb) {
+                b = 0;
+                ++mcu;
+                if (++mx == im.mcux) {
+                    mx = 0;
+                    ++my;
+                }
+                if (im.ri && mcu < nmcu && --togo == 0) {
+                    togo = im.ri;
+                    pred0 = pred1 = pred2 = 0;
+                    br.restart();
+                }
+            }
+            int bx, by;
+            if (b < n0) {
+                comp = 0;
+                const int dx = im.hs[0] == 2 ? (b & 1) : 0;
+                const int dy = im.hs[0] == 2 ? (b >> 1) : b;
+                if (im.ncomp == 1) {
+                    bx = mx;
+                    by = my;
+                } else {
+                    bx = mx * im.hs[0] + dx;
+                    by = my * im.vs[0] + dy;
+                }
+                blk = base0 + ((int64_t)by * im.bw[0] + bx) * 64;
+                tbl = dct0;
+            } else {
+                comp = b - n0 + 1;
+                bx = mx;
+                by = my;
+                blk = (comp == 1 ? base1 + ((int64_t)by * im.bw[1] + bx) * 64
+                                 : base2 + ((int64_t)by * im.bw[2] + bx) * 64);
+                tbl = comp == 1 ? dct1 : dct2;
+            }
+        }
+    }
+    return J_OK;
+}
+
+// ---------------------------------------------------------------- islow IDCT (jidctint.c)
+constexpr int CB = 13, P1 = 2;   // CONST_BITS, PASS1_BITS
+constexpr int32_t F0298 = 2446, F0390 = 3196, F0541 = 4433, F0765 = 6270, F0899 = 7373, F1175 = 9633,
+                  F1501 = 12299, F1847 = 15137, F1961 = 16069, F2053 = 16819, F2562 = 20995, F3072 = 25172;
+
+__host__ __device__ inline int32_t descale(int32_t x, int n) { return (x + (1 << (n - 1))) >> n; }
+
+// IDCT_range_limit[x & RANGE_MASK] of jdmaster.c prepare_range_limit_table (8-bit samples)
+__host__ __device__ inline uint8_t idct_limit(int32_t x) {
+    const int32_t v = x & 1023;
+    if (v < 128) return (uint8_t)(v + 128);
+    if (v < 512) return 255;
+    if (v < 896) return 0;
+    return (uint8_t)(v - 896);
+}
+
+// one 1-D 8-point pass of the LL&M butterfly on d[0..7] (stride st), dequantised inputs
+struct Idct8 {
+    int32_t t10, t11, t12, t13, o0, o1, o2, o3;
+    __host__ __device__ inline void run(int32_t d0, int32_t d1, int32_t d2, int32_t d3, int32_t d4, int32_t d5,
+                                        int32_t d6, int32_t d7) {
+        int32_t z1 = (d2 + d6) * F0541;
+        const int32_t tmp2 = z1 + d6 * (-F1847);
+        const int32_t tmp3 = z1 + d2 * F0765;
+        const int32_t tmp0 = (d0 + d4) * (1 << CB);
+        const int32_t tmp1 = (d0 - d4) * (1 << CB);
+        t10 = tmp0 + tmp3;
+        t13 = tmp0 - tmp3;
+        t11 = tmp1 + tmp2;
+        t12 = tmp1 - tmp2;
+        int32_t a0 = d7, a1 = d5, a2 = d3, a3 = d1;
+        z1 = a0 + a3;
+        int32_t z2 = a1 + a2, z3 = a0 + a2, z4 = a1 + a3;
+        const int32_t z5 = (z3 + z4) * F1175;
+        a0 *= F0298;
+        a1 *= F2053;
+        a2 *= F3072;
+        a3 *= F1501;
+        z1 *= -F0899;
+        z2 *= -F2562;
+        z3 *= -F1961;
+        z4 *= -F0390;
+        z3 += z5;
+        z4 += z5;
+        o0 = a0 + z1 + z3;
+        o1 = a1 + z2 + z4;
+        o2 = a2 + z2 + z3;
+        o3 = a3 + z1 + z4;
+    }
+};
+
+// coef: 64 zig-zag-order int16, q: 64 zig-zag-order quantisers (both 16-byte aligned);
+// out: 8 rows of 8 samples (8-byte aligned rows, pitch `stride`)
+__host__ __device__ inline void idct_islow(const int16_t* coef, const int16_t* q, uint8_t* out, int64_t stride) {
+    struct V16 { uint32_t w[4]; };
+    union Blk { V16 v[8]; int16_t s[64]; } cz, qz;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        cz.v[i] = ((const V16*)coef)[i];
+        qz.v[i] = ((const V16*)q)[i];
+    }
+    int32_t ws[64];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {   // pass 1: columns
+        int32_t d[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) d[r] = (int32_t)cz.s[kZz[r * 8 + c]] * qz.s[kZz[r * 8 + c]];
+        Idct8 t;
+        t.run(d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7]);
+        ws[0 * 8 + c] = descale(t.t10 + t.o3, CB - P1);
+        ws[7 * 8 + c] = descale(t.t10 - t.o3, CB - P1);
+        ws[1 * 8 + c] = descale(t.t11 + t.o2, CB - P1);
+        ws[6 * 8 + c] = descale(t.t11 - t.o2, CB - P1);
+        ws[2 * 8 + c] = descale(t.t12 + t.o1, CB - P1);
+        ws[5 * 8 + c] = descale(t.t12 - t.o1, CB - P1);
+        ws[3 * 8 + c] = descale(t.t13 + t.o0, CB - P1);
+        ws[4 * 8 + c] = descale(t.t13 - t.o0, CB - P1);
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {   // pass 2: rows
+        const int32_t* w = ws + r * 8;
+        Idct8 t;
+        t.run(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7]);
+        constexpr int S = CB + P1 + 3;
+        const uint32_t o0 = idct_limit(descale(t.t10 + t.o3, S)), o7 = idct_limit(descale(t.t10 - t.o3, S));
+        const uint32_t o1 = idct_limit(descale(t.t11 + t.o2, S)), o6 = idct_limit(descale(t.t11 - t.o2, S));
+        const uint32_t o2 = idct_limit(descale(t.t12 + t.o1, S)), o5 = idct_limit(descale(t.t12 - t.o1, S));
+        const uint32_t o3 = idct_limit(descale(t.t13 + t.o0, S)), o4 = idct_limit(descale(t.t13 - t.o0, S));
+        const uint64_t row = (uint64_t)(o0 | (o1 << 8) | (o2 << 16) | (o3 << 24)) |
+                             ((uint64_t)(o4 | (o5 << 8) | (o6 << 16) | (o7 << 24)) << 32);
+        *(uint64_t*)(out + r * stride) = row;
+    }
+}
+
+// ---------------------------------------------------------------- upsampling + colour
+__host__ __device__ inline int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+__host__ __device__ inline uint8_t clamp8(int v) { return (uint8_t)clampi(v, 0, 255); }
+
+// One chroma sample of output pixel (x, y), component c with plane `pl` (pitch bw*8):
+// jdsample.c h2v2_fancy_upsample / h2v1_fancy_upsample, or a plain copy at full resolution.
+// Beyond the last downsampled column the triangle filter repeats the edge sample (libjpeg's
+// special-cased first / last columns); rows above / below the component repeat the edge row
+// (jdmainct.c context pointers).
+__host__ __device__ inline int chroma_at(const JpegImage& im, const uint8_t* pl, int c, int x, int y) {
+    const int64_t pitch = (int64_t)im.bw[c] * 8;
+    const int hx = im.hs[0] / im.hs[c], vy = im.vs[0] / im.vs[c];
+    if (hx == 1 && vy == 1) return pl[(int64_t)y * pitch + x];
+    const int cx = x >> 1;
+    const int dw = im.dw[c];
+    // libjpeg-turbo's jinit_upsampler takes the fancy path only for downsampled_width > 2;
+    // narrower components are replicated (h2v1_upsample / h2v2_upsample)
+    if (dw <= 2) return pl[(int64_t)(vy == 2 ? y >> 1 : y) * pitch + cx];
+    const int xn = (x & 1) ? (cx + 1 < dw ? cx + 1 : cx) : (cx > 0 ? cx - 1 : 0);
+    if (vy == 1) {   // h2v1: (3 * this + neighbour + 1 or 2) >> 2
+        const uint8_t* row = pl + (int64_t)y * pitch;
+        return (3 * row[cx] + row[xn] + ((x & 1) ? 2 : 1)) >> 2;
+    }
+    // h2v2: column sums 3 * this row + nearer neighbouring row, then (3 * this + neighbour + 8 or 7) >> 4
+    const int cy = y >> 1;
+    const int yn = (y & 1) ? (cy + 1 < im.dh[c] ? cy + 1 : cy) : (cy > 0 ? cy - 1 : 0);
+    const uint8_t* r0 = pl + (int64_t)cy * pitch;
+    const uint8_t* r1 = pl + (int64_t)yn * pitch;
+    const int s_this = 3 * r0[cx] + r1[cx];
+    const int s_next = 3 * r0[xn] + r1[xn];
+    return (3 * s_this + s_next + ((x & 1) ? 7 : 8)) >> 4;
+}
+
+// jdcolor.c ycc_rgb_convert with build_ycc_rgb_table's 16-bit fixed-point factors
+__host__ __device__ inline void ycc_to_rgb(int yy, int cb, int cr, uint8_t* rgb) {
+    constexpr int SB = 16;
+    constexpr int32_t HALF = 1 << (SB - 1);
+    const int32_t xb = cb - 128, xr = cr - 128;
+    const int32_t r_off = (91881 * xr + HALF) >> SB;      // FIX(1.40200)
+    const int32_t b_off = (116130 * xb + HALF) >> SB;     // FIX(1.77200)
+    const int32_t g_off = ((-22554) * xb + HALF + (-46802) * xr) >> SB;   // FIX(0.34414), FIX(0.71414)
+    rgb[0] = clamp8(yy + r_off);
+    rgb[1] = clamp8(yy + g_off);
+    rgb[2] = clamp8(yy + b_off);
+}
+
+__host__ __device__ inline void pixel_rgb(const JpegImage& im, const uint8_t* planes, int x, int y, uint8_t* rgb) {
+    const uint8_t* p0 = planes + im.plane_off + im.comp_plane[0];
+    const int yy = p0[(int64_t)y * im.bw[0] * 8 + x];
+    if (im.ncomp == 1) {
+        rgb[0] = rgb[1] = rgb[2] = (uint8_t)yy;
+        return;
+    }
+    const int c1 = chroma_at(im, planes + im.plane_off + im.comp_plane[1], 1, x, y);
+    const int c2 = chroma_at(im, planes + im.plane_off + im.comp_plane[2], 2, x, y);
+    if (im.cspace == CS_RGB) {
+        rgb[0] = (uint8_t)yy;
+        rgb[1] = (uint8_t)c1;
+        rgb[2] = (uint8_t)c2;
+    } else {
+        ycc_to_rgb(yy, c1, c2, rgb);
+    }
+}
+
+}  // namespace jpeg
+}  // namespace reidmi

@@ -12,9 +12,14 @@ RGB images of a whole batch go to the device as one packed uint8 buffer and
 PIL.Image.resize(BILINEAR) + ToTensor + Normalize (oracle/transforms_oracle.c pins the
 arithmetic against Pillow).  The augmented view's flip / pad / crop commute with ToTensor
 and Normalize, so they are not materialised: the encoder's im2col applies them from per-image
-crop offsets (`tta_offsets`, `zero_shot_learning.embed_pair(tta=...)`).  JPEG decode stays on
-the host (PIL), as in the reference's DataLoader workers.
+crop offsets (`tta_offsets`, `zero_shot_learning.embed_pair(tta=...)`).
+
+The JPEG files themselves (data_prepare.py:89 `Image.open(path).convert("RGB")`) decode on the
+device too: `decode_jpeg` parses the headers on the host (`reidmi_jpeg_plan`), ships the file
+bytes and the plan to the GPU once, and `reidmi_jpeg_decode` produces the same packed HWC
+batch `preprocess` builds from PIL images — bit-exact with Pillow's decoder.
 """
+import os
 import ctypes
 
 import numpy as np
@@ -95,6 +100,102 @@ class EvalTransform:
 
     def __call__(self, images, device=None):
         return preprocess(images, self.h, self.w, self.model_type, self.dtype, device)
+
+
+def read_files(files):
+    """Concatenate JPEG files (paths or bytes objects): (uint8 buffer, int64 offsets [B+1])."""
+    blobs = []
+    for f in files:
+        if isinstance(f, (bytes, bytearray, memoryview)):
+            blobs.append(bytes(f))
+        else:
+            with open(os.fspath(f), "rb") as fh:
+                blobs.append(fh.read())
+    offsets = np.zeros(len(blobs) + 1, np.int64)
+    offsets[1:] = np.cumsum([len(b) for b in blobs], dtype=np.int64)
+    buf = np.frombuffer(b"".join(blobs), np.uint8) if blobs else np.zeros(0, np.uint8)
+    return buf, offsets
+
+
+JPEG_STATUS = {1: "not a JPEG or truncated", 2: "progressive / lossless / arithmetic-coded / 12-bit / multi-scan",
+               3: "component layout other than grayscale or 3 x {4:4:4, 4:2:2, 4:2:0}",
+               4: "missing or malformed quantisation / Huffman tables", 5: "entropy-coded data does not decode"}
+
+
+class JpegBatch:
+    """Host side of a JPEG batch: the file bytes, the decode plan (reidmi_jpeg_plan) and the
+    per-image status / (offset, h, w) of the decoded layout.  Host only: needs no GPU."""
+
+    def __init__(self, files):
+        self.buf, self.offsets = read_files(files)
+        B = len(self.offsets) - 1
+        self.B = B
+        self.meta = np.zeros((B, 3), np.int64)
+        self.status = np.zeros(B, np.int32)
+        self.info = np.zeros(7, np.int64)
+        args = (self.buf.ctypes.data_as(ctypes.c_void_p), self.offsets.ctypes.data_as(ctypes.c_void_p), B)
+        out = (self.meta.ctypes.data_as(ctypes.c_void_p), self.status.ctypes.data_as(ctypes.c_void_p),
+               self.info.ctypes.data_as(ctypes.c_void_p))
+        _lib.call("reidmi_jpeg_plan", *args, None, 0, *out)
+        self.plan = np.zeros(int(self.info[0]), np.uint8)
+        _lib.call("reidmi_jpeg_plan", *args, self.plan.ctypes.data_as(ctypes.c_void_p), int(self.info[0]), *out)
+        self.ws_bytes, self.out_bytes = int(self.info[1]), int(self.info[2])
+        self.max_h, self.max_w = max(int(self.info[3]), 1), max(int(self.info[4]), 1)
+
+    def raise_for_status(self, status=None):
+        st = self.status if status is None else status
+        bad = np.nonzero(st)[0]
+        if bad.size:
+            i = int(bad[0])
+            raise ValueError(f"{bad.size} of {self.B} JPEG files cannot be decoded on the device; file {i}: "
+                             f"{JPEG_STATUS.get(int(st[i]), int(st[i]))}")
+
+
+def decode_jpeg(files, device=None, check=True):
+    """Image.open(f).convert("RGB") of every file (data_prepare.py:89), on the GPU.
+    Returns (pix uint8 device tensor of the packed HWC images, meta int64 device tensor [B][3]
+    = (offset, h, w), JpegBatch) — the input reidmi_preprocess_u8 takes.  With check=True an
+    unsupported or undecodable file raises (there is no host fallback)."""
+    device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    jb = files if isinstance(files, JpegBatch) else JpegBatch(files)
+    if check:
+        jb.raise_for_status()
+    dev_files = torch.from_numpy(jb.buf).to(device, non_blocking=True) if jb.buf.size else \
+        torch.zeros(1, dtype=torch.uint8, device=device)
+    dplan = torch.from_numpy(jb.plan).to(device, non_blocking=True)
+    ws = torch.empty(max(jb.ws_bytes, 1), dtype=torch.uint8, device=device)
+    pix = torch.empty(max(jb.out_bytes, 1), dtype=torch.uint8, device=device)
+    err = torch.empty(max(jb.B, 1), dtype=torch.int32, device=device)
+    _lib.require_cuda(pix)
+    info = jb.info.copy()
+    _lib.call("reidmi_jpeg_decode", _lib.ptr(dev_files), _lib.ptr(dplan), info.ctypes.data_as(ctypes.c_void_p), jb.B,
+              _lib.ptr(ws), ws.numel(), _lib.ptr(pix), _lib.ptr(err), _lib.stream(device))
+    if check and jb.B:
+        jb.raise_for_status(err[:jb.B].cpu().numpy())
+    meta = torch.from_numpy(jb.meta).to(device, non_blocking=True)
+    return pix, meta, jb
+
+
+def preprocess_jpeg(files, height=256, width=128, model_type="vit", dtype=torch.float16, device=None, out=None):
+    """reidDataset.__getitem__ + transform_test for a batch of JPEG files, all on the GPU:
+    decode_jpeg -> Resize -> ToTensor -> Normalize -> [B, 3, height, width]."""
+    if dtype not in (torch.float32, torch.float16):
+        raise ValueError("dtype must be torch.float32 or torch.float16")
+    device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    pix, meta, jb = decode_jpeg(files, device)
+    B = jb.B
+    if out is None:
+        out = torch.empty((B, 3, height, width), dtype=dtype, device=device)
+    elif tuple(out.shape) != (B, 3, height, width) or out.dtype != dtype or not out.is_contiguous():
+        raise ValueError("out must be a contiguous [B, 3, height, width] tensor of `dtype`")
+    if B == 0:
+        return out
+    mean, std = norm_stats(model_type)
+    mean_c = (ctypes.c_float * 3)(*mean)
+    std_c = (ctypes.c_float * 3)(*std)
+    _lib.call("reidmi_preprocess_u8", _lib.ptr(pix), _lib.ptr(meta), B, jb.max_h, jb.max_w, height, width, mean_c,
+              std_c, 0 if dtype == torch.float32 else 1, _lib.ptr(out), _lib.stream(device))
+    return out
 
 
 def tta_offsets(n, generator=None):

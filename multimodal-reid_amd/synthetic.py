@@ -235,6 +235,34 @@ def identity_crops(pids, cams, seed=0, noise=0.6, detail=0.3, cast=0.02, shift=1
     return out
 
 
+def crop_rgb(h, w, seed=0, key=0, noise=12.0):
+    """A decoded-photo-like RGB crop, uint8 [h][w][3]: a smooth random colour field (a coarse
+    grid linearly upsampled), a few hard-edged rectangles and per-pixel noise."""
+    r = _rng(f"crop{key}", seed)
+    gh, gw = max(2, h // 24 + 2), max(2, w // 24 + 2)
+    img = _upsample_rows_cols(r.uniform(0, 255, (3, gh, gw)), max(h, 2), max(w, 2))[:, :h, :w]
+    for _ in range(3):
+        y0, x0 = int(r.integers(0, h)), int(r.integers(0, w))
+        img[:, y0:y0 + int(r.integers(1, h + 1)), x0:x0 + int(r.integers(1, w + 1))] = r.uniform(0, 255, (3, 1, 1))
+    img = img + noise * r.standard_normal((3, h, w))
+    return np.ascontiguousarray(np.clip(np.rint(img), 0, 255).astype(np.uint8).transpose(1, 2, 0))
+
+
+def jpeg_files(n, h=128, w=64, seed=0, quality=90, subsampling=2, offset=0, **save_kw):
+    """n JPEG files (bytes) of synthetic crops encoded by Pillow (libjpeg-turbo): Market-1501
+    crops are 128 x 64 baseline JPEGs with 4:2:0 chroma (subsampling=2)."""
+    import io
+
+    from PIL import Image
+    out = []
+    for k in range(n):
+        b = io.BytesIO()
+        Image.fromarray(crop_rgb(h, w, seed, offset + k)).save(b, "JPEG", quality=quality, subsampling=subsampling,
+                                                               **save_kw)
+        out.append(b.getvalue())
+    return out
+
+
 def token_ids(n, ctx=77, vocab=49408, seed=0, min_len=4, max_len=20):
     """Synthetic CLIP token rows: SOT 49406, random body, EOT 49407 (the max id, so
     ``argmax`` finds it, text_encoder.py:23), zero padding."""
