@@ -16,9 +16,10 @@
 // Supported: baseline / extended-sequential Huffman, 8-bit, one scan, grayscale or three
 // components at 4:4:4, 4:2:2 or 4:2:0 (every ReID benchmark's crops).  Anything else gets a
 // per-image status and is left to the caller (the Python mirror raises).
+#include <algorithm>
 #include <cstring>
-#include <map>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "common.h"
@@ -57,24 +58,25 @@ static void build_huff(const uint8_t* counts, const uint8_t* syms, int nsym, Jpe
 
 struct Pools {
     std::vector<JpegHuff> huff;
-    std::map<std::string, int> huff_ix;
-    std::vector<int16_t> quant;   // [n][64]
-    std::map<std::string, int> quant_ix;
+    std::vector<std::string> huff_raw;   // 16 counts + symbols of each pooled table
+    std::vector<int16_t> quant;          // [n][64]
 
-    int add_huff(const std::string& raw) {   // raw = 16 counts + symbols
-        auto it = huff_ix.find(raw);
-        if (it != huff_ix.end()) return it->second;
+    // Tables repeat across a dataset (one encoder setting: 4 Huffman + 2 quantisation tables),
+    // so the lookup is a scan of the few pooled ones, newest first.
+    int add_huff(const uint8_t* raw, int len) {
+        for (int i = (int)huff_raw.size() - 1; i >= 0; --i)
+            if ((int)huff_raw[i].size() == len && memcmp(huff_raw[i].data(), raw, len) == 0) return i;
         JpegHuff t;
-        build_huff((const uint8_t*)raw.data(), (const uint8_t*)raw.data() + 16, (int)raw.size() - 16, t);
+        build_huff(raw, raw + 16, len - 16, t);
         huff.push_back(t);
-        return huff_ix[raw] = (int)huff.size() - 1;
+        huff_raw.emplace_back((const char*)raw, len);
+        return (int)huff.size() - 1;
     }
     int add_quant(const int16_t* q) {
-        std::string key((const char*)q, 128);
-        auto it = quant_ix.find(key);
-        if (it != quant_ix.end()) return it->second;
+        for (int i = (int)(quant.size() / 64) - 1; i >= 0; --i)
+            if (memcmp(quant.data() + 64 * i, q, 128) == 0) return i;
         quant.insert(quant.end(), q, q + 64);
-        return quant_ix[key] = (int)(quant.size() / 64) - 1;
+        return (int)(quant.size() / 64) - 1;
     }
 };
 
@@ -82,14 +84,16 @@ static inline int u16be(const uint8_t* p) { return (p[0] << 8) | p[1]; }
 
 // jdmarker.c read_markers up to the first SOS, restricted to what the device decodes.
 static int32_t parse_one(const uint8_t* f, int64_t n, int64_t base, JpegImage& im, Pools& pools) {
-    memset(&im, 0, sizeof(im));
+    memset(&im, 0, sizeof(im));   // (status is set by the caller from the return value)
     if (n < 4 || f[0] != 0xFF || f[1] != 0xD8) return J_NOT_JPEG;
     int64_t p = 2;
     bool jfif = false, adobe = false, sof = false;
     int adobe_t = -1;
     bool qdef[4] = {false, false, false, false};
     int16_t qt[4][64];
-    std::string hdc[4], hac[4];
+    const uint8_t* hdc[4] = {nullptr, nullptr, nullptr, nullptr};
+    const uint8_t* hac[4] = {nullptr, nullptr, nullptr, nullptr};
+    int hdc_len[4] = {0, 0, 0, 0}, hac_len[4] = {0, 0, 0, 0};
     int cid[3] = {0, 0, 0}, tq[3] = {0, 0, 0};
     for (;;) {
         while (p < n && f[p] != 0xFF) ++p;   // extraneous bytes (libjpeg warns and skips)
@@ -127,8 +131,8 @@ static int32_t parse_one(const uint8_t* f, int64_t n, int64_t base, JpegImage& i
                 int tot = 0;
                 for (int l = 0; l < 16; ++l) tot += s[i + 1 + l];
                 if (tc > 1 || th > 3 || tot > 256 || i + 17 + tot > sl) return J_BAD_TABLE;
-                std::string raw((const char*)s + i + 1, 16 + tot);
-                (tc ? hac : hdc)[th] = raw;
+                (tc ? hac : hdc)[th] = s + i + 1;
+                (tc ? hac_len : hdc_len)[th] = 16 + tot;
                 i += 17 + tot;
             }
         } else if (m == 0xDB) {     // DQT
@@ -158,9 +162,9 @@ static int32_t parse_one(const uint8_t* f, int64_t n, int64_t base, JpegImage& i
             for (int j = 0; j < ns; ++j) {
                 if (s[1 + 2 * j] != cid[j]) return J_UNSUPPORTED;   // scan order = frame order
                 const int td = s[2 + 2 * j] >> 4, ta = s[2 + 2 * j] & 15;
-                if (td > 3 || ta > 3 || hdc[td].empty() || hac[ta].empty()) return J_BAD_TABLE;
-                im.dc[j] = pools.add_huff(hdc[td]);
-                im.ac[j] = pools.add_huff(hac[ta]);
+                if (td > 3 || ta > 3 || !hdc[td] || !hac[ta]) return J_BAD_TABLE;
+                im.dc[j] = pools.add_huff(hdc[td], hdc_len[td]);
+                im.ac[j] = pools.add_huff(hac[ta], hac_len[ta]);
             }
             const uint8_t* e = s + 1 + 2 * ns;
             if (e[0] != 0 || e[1] != 63 || e[2] != 0) return J_UNSUPPORTED;   // Ss, Se, Ah/Al
@@ -277,20 +281,50 @@ REIDMI_API int reidmi_jpeg_plan(const uint8_t* files, const int64_t* offsets, in
                                 int64_t plan_capacity, int64_t* meta, int32_t* status, int64_t* info) {
     RM_REQUIRE(B >= 0 && info != nullptr && (B == 0 || (files && offsets && meta && status)),
                "reidmi_jpeg_plan: bad arguments");
+    for (int64_t i = 0; i < B; ++i)
+        RM_REQUIRE(offsets[i] >= 0 && offsets[i + 1] >= offsets[i], "reidmi_jpeg_plan: offsets must be non-decreasing from 0");
     std::vector<JpegImage> imgs((size_t)B);
+    // headers parse independently: chunks on host threads, each with its own table pool, merged after
+    const int nt = (int)std::max<int64_t>(1, std::min<int64_t>({16, (int64_t)std::thread::hardware_concurrency(),
+                                                               B / 2048}));
+    std::vector<Pools> local((size_t)nt);
+    auto work = [&](int t) {
+        for (int64_t i = B * t / nt; i < B * (t + 1) / nt; ++i) {
+            const int64_t a = offsets[i];
+            imgs[(size_t)i].status = parse_one(files + a, offsets[i + 1] - a, a, imgs[(size_t)i], local[(size_t)t]);
+        }
+    };
+    if (nt == 1) {
+        work(0);
+    } else {
+        std::vector<std::thread> th;
+        for (int t = 0; t < nt; ++t) th.emplace_back(work, t);
+        for (auto& x : th) x.join();
+    }
     Pools pools;
+    std::vector<std::vector<int>> hmap((size_t)nt), qmap((size_t)nt);
+    for (int t = 0; t < nt; ++t) {
+        const Pools& L = local[(size_t)t];
+        for (size_t j = 0; j < L.huff_raw.size(); ++j)
+            hmap[(size_t)t].push_back(pools.add_huff((const uint8_t*)L.huff_raw[j].data(), (int)L.huff_raw[j].size()));
+        for (size_t j = 0; j < L.quant.size() / 64; ++j) qmap[(size_t)t].push_back(pools.add_quant(L.quant.data() + 64 * j));
+    }
     int64_t coef = 0, plane = 0, outb = 0, max_h = 0, max_w = 0, bad = 0;
     for (int64_t i = 0; i < B; ++i) {
-        const int64_t a = offsets[i], n = offsets[i + 1] - offsets[i];
-        RM_REQUIRE(a >= 0 && n >= 0, "reidmi_jpeg_plan: offsets must be non-decreasing from 0");
         JpegImage& im = imgs[(size_t)i];
-        const int32_t st = parse_one(files + a, n, a, im, pools);
-        im.status = st;
+        const int32_t st = im.status;
         status[i] = st;
         if (st != J_OK) {
             meta[3 * i] = meta[3 * i + 1] = meta[3 * i + 2] = 0;
             ++bad;
             continue;
+        }
+        int t = 0;
+        while (t + 1 < nt && i >= B * (t + 1) / nt) ++t;
+        for (int c = 0; c < im.ncomp; ++c) {
+            im.dc[c] = hmap[(size_t)t][(size_t)im.dc[c]];
+            im.ac[c] = hmap[(size_t)t][(size_t)im.ac[c]];
+            im.quant[c] = qmap[(size_t)t][(size_t)im.quant[c]];
         }
         im.coef_off = coef;
         im.plane_off = plane;

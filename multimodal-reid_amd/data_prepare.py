@@ -19,8 +19,9 @@ device too: `decode_jpeg` parses the headers on the host (`reidmi_jpeg_plan`), s
 bytes and the plan to the GPU once, and `reidmi_jpeg_decode` produces the same packed HWC
 batch `preprocess` builds from PIL images — bit-exact with Pillow's decoder.
 """
-import os
 import ctypes
+import os
+import warnings
 
 import numpy as np
 import torch
@@ -106,15 +107,23 @@ def read_files(files):
     """Concatenate JPEG files (paths or bytes objects): (uint8 buffer, int64 offsets [B+1])."""
     blobs = []
     for f in files:
-        if isinstance(f, (bytes, bytearray, memoryview)):
+        if isinstance(f, bytes):
+            blobs.append(f)
+        elif isinstance(f, (bytearray, memoryview)):
             blobs.append(bytes(f))
         else:
             with open(os.fspath(f), "rb") as fh:
                 blobs.append(fh.read())
     offsets = np.zeros(len(blobs) + 1, np.int64)
-    offsets[1:] = np.cumsum([len(b) for b in blobs], dtype=np.int64)
-    buf = np.frombuffer(b"".join(blobs), np.uint8) if blobs else np.zeros(0, np.uint8)
-    return buf, offsets
+    offsets[1:] = np.cumsum(np.fromiter(map(len, blobs), np.int64, len(blobs)))
+    return np.frombuffer(b"".join(blobs), np.uint8), offsets   # read-only view of one joined copy
+
+
+def _to_device(a, device):
+    """Host numpy array -> device tensor; read-only buffers are only read by the copy."""
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", UserWarning)
+        return torch.from_numpy(a).to(device)
 
 
 JPEG_STATUS = {1: "not a JPEG or truncated", 2: "progressive / lossless / arithmetic-coded / 12-bit / multi-scan",
@@ -136,9 +145,14 @@ class JpegBatch:
         args = (self.buf.ctypes.data_as(ctypes.c_void_p), self.offsets.ctypes.data_as(ctypes.c_void_p), B)
         out = (self.meta.ctypes.data_as(ctypes.c_void_p), self.status.ctypes.data_as(ctypes.c_void_p),
                self.info.ctypes.data_as(ctypes.c_void_p))
-        _lib.call("reidmi_jpeg_plan", *args, None, 0, *out)
-        self.plan = np.zeros(int(self.info[0]), np.uint8)
-        _lib.call("reidmi_jpeg_plan", *args, self.plan.ctypes.data_as(ctypes.c_void_p), int(self.info[0]), *out)
+        # one parse when the tables fit the first guess (a dataset has a handful of distinct ones)
+        cap = 4096 + B * 256 + 64 * 1536
+        self.plan = np.zeros(cap, np.uint8)
+        _lib.call("reidmi_jpeg_plan", *args, self.plan.ctypes.data_as(ctypes.c_void_p), cap, *out)
+        if int(self.info[0]) > cap:
+            self.plan = np.zeros(int(self.info[0]), np.uint8)
+            _lib.call("reidmi_jpeg_plan", *args, self.plan.ctypes.data_as(ctypes.c_void_p), int(self.info[0]), *out)
+        self.plan = self.plan[:int(self.info[0])]
         self.ws_bytes, self.out_bytes = int(self.info[1]), int(self.info[2])
         self.max_h, self.max_w = max(int(self.info[3]), 1), max(int(self.info[4]), 1)
 
@@ -160,9 +174,8 @@ def decode_jpeg(files, device=None, check=True):
     jb = files if isinstance(files, JpegBatch) else JpegBatch(files)
     if check:
         jb.raise_for_status()
-    dev_files = torch.from_numpy(jb.buf).to(device, non_blocking=True) if jb.buf.size else \
-        torch.zeros(1, dtype=torch.uint8, device=device)
-    dplan = torch.from_numpy(jb.plan).to(device, non_blocking=True)
+    dev_files = _to_device(jb.buf, device) if jb.buf.size else torch.zeros(1, dtype=torch.uint8, device=device)
+    dplan = _to_device(jb.plan, device)
     ws = torch.empty(max(jb.ws_bytes, 1), dtype=torch.uint8, device=device)
     pix = torch.empty(max(jb.out_bytes, 1), dtype=torch.uint8, device=device)
     err = torch.empty(max(jb.B, 1), dtype=torch.int32, device=device)

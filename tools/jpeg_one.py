@@ -33,8 +33,8 @@ def main():
     jb = data_prepare.JpegBatch(files)
     t_plan = time.perf_counter() - t
     dev = torch.device("cuda")
-    dfiles = torch.from_numpy(jb.buf).to(dev)
-    dplan = torch.from_numpy(jb.plan).to(dev)
+    dfiles = data_prepare._to_device(jb.buf, dev)
+    dplan = data_prepare._to_device(jb.plan, dev)
     ws = torch.empty(jb.ws_bytes, dtype=torch.uint8, device=dev)
     pix = torch.empty(jb.out_bytes, dtype=torch.uint8, device=dev)
     err = torch.empty(n, dtype=torch.int32, device=dev)
