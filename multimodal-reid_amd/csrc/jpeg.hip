@@ -34,25 +34,21 @@ static void build_huff(const uint8_t* counts, const uint8_t* syms, int nsym, Jpe
     // jdhuff.c jpeg_make_d_derived_tbl: canonical codes by length, then the lookahead table
     memset(&t, 0, sizeof(t));
     int p = 0;
-    int32_t code = 0;
+    uint32_t code = 0;
     for (int l = 1; l <= 16; ++l) {
         const int n = counts[l - 1];
-        if (n) {
-            t.valoff[l] = p - code;
-            for (int i = 0; i < n; ++i, ++p, ++code) {
-                if (l <= 9) {
-                    const int shift = 9 - l;
-                    for (int e = 0; e < (1 << shift); ++e)
-                        t.lut[(code << shift) | e] = (uint16_t)((l << 8) | syms[p]);
-                }
+        t.valoff[l] = p - (int32_t)code;
+        for (int i = 0; i < n; ++i, ++p, ++code) {
+            if (l <= kLookahead) {
+                const int shift = kLookahead - l;
+                for (int e = 0; e < (1 << shift) && (code << shift | e) < (1u << kLookahead); ++e)
+                    t.lut[(code << shift) | e] = (uint16_t)((l << 8) | syms[p]);
             }
-            t.maxcode[l] = code - 1;
-        } else {
-            t.maxcode[l] = -1;
         }
+        t.lim[l] = code << (16 - l);
         code <<= 1;
     }
-    t.maxcode[17] = 0x7FFFFFFF;
+    t.lim[17] = 0xFFFFFFFFu;
     for (int i = 0; i < nsym && i < 256; ++i) t.val[i] = syms[i];
 }
 
@@ -215,24 +211,81 @@ static inline int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * 
 
 // ------------------------------------------------------------------ device
 
+constexpr int kLdsTables = 8;   // Huffman tables staged in LDS per workgroup (4 per encoder setting)
+
+// kLds: the plan's table pool (n_huff <= kLdsTables, the usual case) is copied to LDS and every
+// lookup is a ds_read (a generic pointer would compile to flat loads, whose waits also drain
+// the lane's outstanding global loads and stores).
+// Each lane assembles its current block in LDS (ds_write per coefficient) and stores it whole
+// (8 x 16 bytes) when the block ends, so no global store sits between a refill's word load
+// and its use, and the coefficient workspace needs no clearing.
+struct LdsSink {
+    int16_t* buf;   // this lane's 64 slots in LDS
+    int16_t* dst;
+    __device__ inline void begin(int16_t* b) {
+        dst = b;
+        uint4* q = (uint4*)buf;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) q[j] = make_uint4(0, 0, 0, 0);
+    }
+    __device__ inline void put(int k, int32_t v) { buf[k] = (int16_t)v; }
+    __device__ inline void end() {
+        const uint4* q = (const uint4*)buf;
+        uint4* d = (uint4*)dst;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d[j] = q[j];
+    }
+};
+
+// kLds: the plan's table pool (n_huff <= kLdsTables, the usual case) is copied to LDS and every
+// lookup is a ds_read (a generic pointer would compile to flat loads, whose waits also drain
+// the lane's outstanding global loads and stores).
+template <bool kLds>
 __global__ __launch_bounds__(64) void jpeg_entropy_kernel(const uint8_t* __restrict__ src,
                                                           const uint8_t* __restrict__ plan, int64_t B,
                                                           int16_t* __restrict__ coef, int32_t* __restrict__ err) {
+    __shared__ JpegHuff lds[kLds ? kLdsTables : 1];
+    __shared__ __attribute__((aligned(16))) int16_t blocks[64][64];
+    const JpegPlan* P = (const JpegPlan*)plan;
+    const JpegHuff* gh = (const JpegHuff*)(plan + P->huff_off);
+    if constexpr (kLds) {
+        const uint4* g = (const uint4*)gh;
+        uint4* l = (uint4*)lds;
+        const int n16 = (int)(P->n_huff * (int64_t)sizeof(JpegHuff) / 16);
+        for (int j = threadIdx.x; j < n16; j += 64) l[j] = g[j];
+        __syncthreads();
+    }
     const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
     if (i >= B) return;
-    const JpegPlan* P = (const JpegPlan*)plan;
     const JpegImage im = ((const JpegImage*)(plan + P->img_off))[i];
     int32_t st = im.status;
-    if (st == J_OK) st = entropy_decode(src, im, (const JpegHuff*)(plan + P->huff_off), coef);
+    if (st == J_OK) {
+        LdsSink sink{blocks[threadIdx.x], nullptr};
+        if constexpr (kLds) st = entropy_decode(src, im, lds, coef, sink);
+        else st = entropy_decode(src, im, gh, coef, sink);
+        if (st != J_OK) {   // undecodable data: the image's coefficients are defined as zero
+            int64_t n = 0;
+            for (int c = 0; c < im.ncomp; ++c) n += (int64_t)im.bw[c] * im.bh[c] * 64;
+            uint4* d = (uint4*)(coef + im.coef_off);
+            for (int64_t j = 0; j < n / 8; ++j) d[j] = make_uint4(0, 0, 0, 0);
+        }
+    }
     err[i] = st;
 }
 
+constexpr int64_t kPlaneLds = 64 << 10;   // images whose planes fit stage them in LDS
+
+// kLds: the image's component planes live in (dynamic) LDS between the IDCT and the colour
+// pass; otherwise in the plane workspace (L2-resident at these sizes).
+template <bool kLds>
 __global__ __launch_bounds__(256) void jpeg_pixels_kernel(const uint8_t* __restrict__ plan,
                                                           const int16_t* __restrict__ coef,
                                                           uint8_t* __restrict__ planes, uint8_t* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t jpeg_planes_lds[];
     const JpegPlan* P = (const JpegPlan*)plan;
     const JpegImage im = ((const JpegImage*)(plan + P->img_off))[blockIdx.x];
     if (im.status != J_OK) return;
+    uint8_t* ip = kLds ? jpeg_planes_lds : planes + im.plane_off;
     const int16_t* qbase = (const int16_t*)(plan + P->quant_off);
     const int nc = im.ncomp;
     const int64_t n0 = (int64_t)im.bw[0] * im.bh[0];
@@ -254,20 +307,30 @@ __global__ __launch_bounds__(256) void jpeg_pixels_kernel(const uint8_t* __restr
         const int qi = c == 0 ? im.quant[0] : (c == 1 ? im.quant[1] : im.quant[2]);
         const int64_t cc = c == 0 ? im.comp_coef[0] : (c == 1 ? im.comp_coef[1] : im.comp_coef[2]);
         const int64_t cp = c == 0 ? im.comp_plane[0] : (c == 1 ? im.comp_plane[1] : im.comp_plane[2]);
-        idct_islow(coef + im.coef_off + cc + local * 64, qbase + (int64_t)qi * 64,
-                   planes + im.plane_off + cp + by * 8 * pitch + bx * 8, pitch);
+        idct_islow(coef + im.coef_off + cc + local * 64, qbase + (int64_t)qi * 64, ip + cp + by * 8 * pitch + bx * 8,
+                   pitch);
     }
     __syncthreads();
-    const int64_t npx = (int64_t)im.w * im.h;
+    // pixels in raster order, 256 apart per thread: (x, y) advances by (256 mod w, 256 / w)
+    // without a division per pixel
+    const int w = im.w;
+    const int sy = 256 / w, sx = 256 - sy * w;
+    int y = (int)threadIdx.x / w;
+    int x = (int)threadIdx.x - y * w;
     uint8_t* o = out + im.out_off;
-    for (int64_t p = threadIdx.x; p < npx; p += 256) {
-        const int y = (int)(p / im.w);
-        const int x = (int)(p - (int64_t)y * im.w);
+    while (y < im.h) {
         uint8_t rgb[3];
-        pixel_rgb(im, planes, x, y, rgb);
-        o[p * 3 + 0] = rgb[0];
-        o[p * 3 + 1] = rgb[1];
-        o[p * 3 + 2] = rgb[2];
+        pixel_rgb(im, ip, x, y, rgb);
+        uint8_t* d = o + ((int64_t)y * w + x) * 3;
+        d[0] = rgb[0];
+        d[1] = rgb[1];
+        d[2] = rgb[2];
+        x += sx;
+        y += sy;
+        if (x >= w) {
+            x -= w;
+            ++y;
+        }
     }
 }
 
@@ -309,7 +372,7 @@ REIDMI_API int reidmi_jpeg_plan(const uint8_t* files, const int64_t* offsets, in
             hmap[(size_t)t].push_back(pools.add_huff((const uint8_t*)L.huff_raw[j].data(), (int)L.huff_raw[j].size()));
         for (size_t j = 0; j < L.quant.size() / 64; ++j) qmap[(size_t)t].push_back(pools.add_quant(L.quant.data() + 64 * j));
     }
-    int64_t coef = 0, plane = 0, outb = 0, max_h = 0, max_w = 0, bad = 0;
+    int64_t coef = 0, plane = 0, outb = 0, max_h = 0, max_w = 0, bad = 0, max_plane = 0;
     for (int64_t i = 0; i < B; ++i) {
         JpegImage& im = imgs[(size_t)i];
         const int32_t st = im.status;
@@ -336,6 +399,7 @@ REIDMI_API int reidmi_jpeg_plan(const uint8_t* files, const int64_t* offsets, in
         }
         coef += cc;
         plane += cc;
+        max_plane = cc > max_plane ? cc : max_plane;
         im.out_off = outb;
         meta[3 * i] = outb;
         meta[3 * i + 1] = im.h;
@@ -362,6 +426,8 @@ REIDMI_API int reidmi_jpeg_plan(const uint8_t* files, const int64_t* offsets, in
     info[4] = max_w;
     info[5] = bad;
     info[6] = coef;
+    info[7] = hdr.n_huff;
+    info[8] = max_plane;
     if (plan == nullptr || plan_capacity < plan_bytes) return OK;   // sizing call
     uint8_t* pb = (uint8_t*)plan;
     memset(pb, 0, (size_t)plan_bytes);
@@ -381,11 +447,17 @@ REIDMI_API int reidmi_jpeg_decode(const uint8_t* files, const void* plan, const 
     hipStream_t s = (hipStream_t)stream;
     int16_t* coef = (int16_t*)ws;
     uint8_t* planes = (uint8_t*)ws + align_up(info[6] * 2, 256);
-    if (info[6]) RM_CHECK_HIP(hipMemsetAsync(coef, 0, (size_t)info[6] * 2, s));
-    jpeg_entropy_kernel<<<dim3((unsigned)((B + 63) / 64)), dim3(64), 0, s>>>(files, (const uint8_t*)plan, B, coef,
-                                                                             err);
+    const dim3 eg((unsigned)((B + 63) / 64));
+    if (info[7] <= kLdsTables)
+        jpeg_entropy_kernel<true><<<eg, dim3(64), 0, s>>>(files, (const uint8_t*)plan, B, coef, err);
+    else
+        jpeg_entropy_kernel<false><<<eg, dim3(64), 0, s>>>(files, (const uint8_t*)plan, B, coef, err);
     RM_LAUNCHED();
-    jpeg_pixels_kernel<<<dim3((unsigned)B), dim3(256), 0, s>>>((const uint8_t*)plan, coef, planes, pix);
+    if (info[8] <= kPlaneLds)
+        jpeg_pixels_kernel<true><<<dim3((unsigned)B), dim3(256), (size_t)info[8], s>>>((const uint8_t*)plan, coef,
+                                                                                       planes, pix);
+    else
+        jpeg_pixels_kernel<false><<<dim3((unsigned)B), dim3(256), 0, s>>>((const uint8_t*)plan, coef, planes, pix);
     RM_LAUNCHED();
     return OK;
 }

@@ -30,11 +30,13 @@ enum : int32_t {
 enum : int32_t { CS_GRAY = 0, CS_YCC = 1, CS_RGB = 2 };
 
 struct JpegHuff {          // jdhuff.c-style derived table
-    uint16_t lut[512];     // 9-bit lookahead: (code length << 8) | symbol, 0 = longer code
-    int32_t maxcode[18];   // largest code of each length (-1 if none); [17] sentinel
+    uint16_t lut[1 << 10]; // 10-bit lookahead: (code length << 8) | symbol, 0 = longer code
+    uint32_t lim[18];      // left-justified 16-bit bound of all codes of length <= l
     int32_t valoff[18];    // symbol index of a length-l code = code + valoff[l]
     uint8_t val[256];
 };
+
+static_assert(sizeof(JpegHuff) % 16 == 0, "JpegHuff is staged to LDS in 16-byte words");
 
 struct JpegImage {
     int64_t src_off, src_len;   // entropy-coded data (after SOS) in the file batch
@@ -70,37 +72,96 @@ constexpr uint8_t kZz[64] = {0,  1,  5,  6,  14, 15, 27, 28, 2,  4,  7,  13, 16,
 // converged: one iteration = one DC or AC symbol.  Bits are read MSB first from a 64-bit
 // window; 0xFF00 is a stuffed 0xFF; any other marker stops the stream (zeros are fed, as
 // libjpeg does) until the restart logic skips an RSTn.
+constexpr int kLookahead = 10;
+
 struct BitReader {
     const uint8_t* p;
     const uint8_t* end;
-    uint64_t acc;
-    int bits;
-    bool marker;
+    uint64_t acc;   // MSB-aligned bit window
+    int bits;       // valid bits in acc
+    bool marker;    // a marker (or the end) was reached: zeros are fed from here on
+    bool nw_ok;     // nw0/nw1: the aligned words covering >= 5 stream bytes at p, loaded one
+    int nmis;       // refill ahead and first read at the next refill, so the load's latency
+    uint32_t nw0, nw1;   // hides behind the symbols decoded in between
 
+    __host__ __device__ inline void fetch() {
+        nw_ok = !marker && p + 8 <= end;
+        if (nw_ok) {
+            nmis = (int)((uintptr_t)p & 3);
+            const uint32_t* w = (const uint32_t*)(p - nmis);   // (pointer arithmetic keeps it a global load)
+            nw0 = w[0];
+            nw1 = w[1];
+        }
+    }
+    __host__ __device__ inline void start(const uint8_t* b, const uint8_t* e) {
+        p = b;
+        end = e;
+        acc = 0;
+        bits = 0;
+        marker = false;
+        fetch();
+    }
+    // Keeps >= 32 bits in the window (a symbol plus its extra bits is at most 16 + 15).  The
+    // next 4 stream bytes come from the prefetched words: all four at once when none is 0xFF,
+    // else one at a time in registers (0xFF 0x00 is a stuffed 0xFF, 0xFF + anything else a
+    // marker) — no memory access either way.  Only the last 8 bytes of a stream go byte by byte.
     __host__ __device__ inline void refill() {
-        while (bits <= 56) {
-            uint32_t b = 0;
+        if (bits >= 32) return;
+        if (nw_ok) {
+            const uint64_t win = (((uint64_t)nw1 << 32) | nw0) >> (nmis * 8);   // stream bytes, LSB first
+            const uint32_t x = ~(uint32_t)win;
+            if (((x - 0x01010101u) & ~x & 0x80808080u) == 0) {
+                const uint32_t v = (uint32_t)win;
+                const uint32_t be = (v >> 24) | ((v >> 8) & 0xFF00u) | ((v << 8) & 0xFF0000u) | (v << 24);
+                acc |= (uint64_t)be << (32 - bits);
+                bits += 32;
+                p += 4;
+            } else {
+                int pos = 0;
+                while (pos < 4 && bits < 32) {
+                    const uint32_t c = (uint32_t)(win >> (8 * pos)) & 0xFF;
+                    if (c == 0xFF) {
+                        if (((win >> (8 * pos + 8)) & 0xFF) != 0) {
+                            marker = true;
+                            break;
+                        }
+                        pos += 2;
+                    } else {
+                        pos += 1;
+                    }
+                    acc |= (uint64_t)c << (56 - bits);
+                    bits += 8;
+                }
+                p += pos;
+                if (marker) bits = 32 > bits ? 32 : bits;   // zeros from here on
+            }
+            fetch();
+            return;
+        }
+        while (bits < 32) {
+            uint32_t c = 0;
             if (!marker) {
                 if (p >= end) {
                     marker = true;
                 } else {
-                    b = p[0];
-                    if (b == 0xFF) {
+                    c = p[0];
+                    if (c == 0xFF) {
                         const uint32_t n = (p + 1 < end) ? p[1] : 0xD9;
                         if (n == 0) {
                             p += 2;
                         } else {
                             marker = true;
-                            b = 0;
+                            c = 0;
                         }
                     } else {
                         ++p;
                     }
                 }
             }
-            acc |= (uint64_t)b << (56 - bits);
+            acc |= (uint64_t)c << (56 - bits);
             bits += 8;
         }
+        fetch();
     }
     __host__ __device__ inline uint32_t take(int n) {   // n in [1, 16]
         const uint32_t v = (uint32_t)(acc >> (64 - n));
@@ -108,9 +169,11 @@ struct BitReader {
         bits -= n;
         return v;
     }
-    // jpeg_huff_decode: returns the symbol or -1 for an invalid code
+    // jpeg_huff_decode: returns the symbol or -1 for an invalid code.  Codes longer than the
+    // lookahead: the length is K+1 + #{l in K+1..16 : lim[l] <= code} (lim is monotone),
+    // evaluated without a loop so that the lanes of a wave do not diverge on it.
     __host__ __device__ inline int decode(const JpegHuff* t) {
-        const uint32_t e = t->lut[acc >> 55];
+        const uint32_t e = t->lut[acc >> (64 - kLookahead)];
         if (e >> 8) {
             const int l = (int)(e >> 8);
             acc <<= l;
@@ -118,24 +181,19 @@ struct BitReader {
             return (int)(e & 0xFF);
         }
         const uint32_t code16 = (uint32_t)(acc >> 48);
-        int l = 10;
-        int32_t c = (int32_t)(code16 >> 6);
-        while (l <= 16 && c > t->maxcode[l]) {
-            ++l;
-            c = (int32_t)(code16 >> (16 - l));
-        }
+        int l = kLookahead + 1;
+#pragma unroll
+        for (int j = kLookahead + 1; j <= 16; ++j) l += code16 >= t->lim[j] ? 1 : 0;
         if (l > 16) return -1;
+        const int32_t c = (int32_t)(code16 >> (16 - l));
         acc <<= l;
         bits -= l;
         return t->val[(c + t->valoff[l]) & 0xFF];
     }
     // skip to just past the next RSTn (jdmarker.c read_restart_marker on a valid stream)
     __host__ __device__ inline void restart() {
-        acc = 0;
-        bits = 0;
-        marker = false;
         while (p + 1 < end && !(p[0] == 0xFF && p[1] >= 0xD0 && p[1] <= 0xD7)) ++p;
-        if (p + 1 < end) p += 2;
+        start(p + 1 < end ? p + 2 : p, end);
     }
 };
 
@@ -143,68 +201,85 @@ __host__ __device__ inline int32_t huff_extend(uint32_t v, int s) {   // HUFF_EX
     return (v < (1u << (s - 1))) ? (int32_t)v - (1 << s) + 1 : (int32_t)v;
 }
 
-// Decodes one image's scan into zig-zag-order int16 coefficient blocks (the caller zeroed
-// them).  Returns J_OK or J_BAD_DATA.
+// Where decoded coefficients go.  DirectSink writes them into zeroed blocks in place (host
+// check); the device kernel stages each block in LDS and writes it out whole (jpeg.hip).
+struct DirectSink {
+    int16_t* blk;
+    __host__ __device__ inline void begin(int16_t* b) { blk = b; }
+    __host__ __device__ inline void put(int k, int32_t v) { blk[k] = (int16_t)v; }
+    __host__ __device__ inline void end() {}
+};
+
+// Decodes one image's scan into zig-zag-order int16 coefficient blocks.  Returns J_OK or
+// J_BAD_DATA (then the blocks not yet ended are left as they were).
+template <class Sink>
 __host__ __device__ inline int32_t entropy_decode(const uint8_t* src, const JpegImage& im, const JpegHuff* huff,
-                                                  int16_t* coef) {
-    BitReader br{src + im.src_off, src + im.src_off + im.src_len, 0, 0, false};
-    const int n0 = im.ncomp == 1 ? 1 : im.hs[0] * im.vs[0];   // Y blocks per MCU
-    const int nb = im.ncomp == 1 ? 1 : n0 + 2;                // blocks per MCU
+                                                  int16_t* coef, Sink& sink) {
+    // One iteration = one symbol, with the DC and AC cases folded into the same arithmetic
+    // (DC: run 0, size = symbol, value added to the component's predictor) and the block
+    // position kept as running per-component MCU origins, so that lanes at different points
+    // of their streams execute nearly the same instructions.
+    BitReader br;
+    br.start(src + im.src_off, src + im.src_off + im.src_len);
+    const bool gray = im.ncomp == 1;
+    const int h0 = gray ? 1 : im.hs[0];
+    const int n0 = gray ? 1 : im.hs[0] * im.vs[0];   // Y blocks per MCU
+    const int nb = gray ? 1 : n0 + 2;                // blocks per MCU
     const int64_t nmcu = (int64_t)im.mcux * im.mcuy;
     const JpegHuff* dct0 = huff + im.dc[0];
-    const JpegHuff* dct1 = huff + im.dc[im.ncomp > 1 ? 1 : 0];
-    const JpegHuff* dct2 = huff + im.dc[im.ncomp > 2 ? 2 : 0];
+    const JpegHuff* dct1 = huff + im.dc[gray ? 0 : 1];
+    const JpegHuff* dct2 = huff + im.dc[gray ? 0 : 2];
     const JpegHuff* act0 = huff + im.ac[0];
-    const JpegHuff* act1 = huff + im.ac[im.ncomp > 1 ? 1 : 0];
-    const JpegHuff* act2 = huff + im.ac[im.ncomp > 2 ? 2 : 0];
-    int16_t* base0 = coef + im.coef_off + im.comp_coef[0];
-    int16_t* base1 = coef + im.coef_off + im.comp_coef[1];
-    int16_t* base2 = coef + im.coef_off + im.comp_coef[2];
+    const JpegHuff* act1 = huff + im.ac[gray ? 0 : 1];
+    const JpegHuff* act2 = huff + im.ac[gray ? 0 : 2];
+    const int64_t bw0 = im.bw[0];
+    int16_t* org0 = coef + im.coef_off + im.comp_coef[0];   // MCU origins per component
+    int16_t* org1 = coef + im.coef_off + im.comp_coef[1];
+    int16_t* org2 = coef + im.coef_off + im.comp_coef[2];
+    const int64_t row_skip0 = gray ? 0 : (int64_t)(im.vs[0] - 1) * bw0 * 64;   // Y rows of an MCU beyond the first
     int32_t pred0 = 0, pred1 = 0, pred2 = 0;
     int64_t mcu = 0;
-    int mx = 0, my = 0, b = 0, k = 0;
+    int mx = 0, b = 0, k = 0;
     int togo = im.ri;   // MCUs left in this restart interval
-    int16_t* blk = base0;
     int comp = 0;
+    sink.begin(org0);
     const JpegHuff* tbl = dct0;
     while (mcu < nmcu) {
         br.refill();
         const int sym = br.decode(tbl);
         if (sym < 0) return J_BAD_DATA;
-        if (k == 0) {
-            int32_t diff = 0;
-            if (sym) {
-                if (sym > 15) return J_BAD_DATA;
-                diff = huff_extend(br.take(sym), sym);
-            }
-            int32_t dc;
-            if (comp == 0) dc = pred0 += diff;
-            else if (comp == 1) dc = pred1 += diff;
-            else dc = pred2 += diff;
-            blk[0] = (int16_t)dc;
-            k = 1;
-            tbl = comp == 0 ? act0 : comp == 1 ? act1 : act2;
-        } else {
-            const int r = sym >> 4, s = sym & 15;
-            if (s) {
-                k += r;
-                if (k > 63) return J_BAD_DATA;
-                blk[k] = (int16_t)huff_extend(br.take(s), s);
-                ++k;
-            } else if (r == 15) {
-                k += 16;
-            } else {
-                k = 64;
-            }
+        const bool dc = k == 0;
+        const int r = dc ? 0 : sym >> 4;
+        const int s = dc ? sym : sym & 15;
+        if (s > 15) return J_BAD_DATA;
+        int32_t v = s ? huff_extend(br.take(s), s) : 0;
+        if (dc) {
+            v += comp == 0 ? pred0 : (comp == 1 ? pred1 : pred2);
+            pred0 = comp == 0 ? v : pred0;
+            pred1 = comp == 1 ? v : pred1;
+            pred2 = comp == 2 ? v : pred2;
+            tbl = comp == 0 ? act0 : (comp == 1 ? act1 : act2);
         }
-        if (k >= 64) {   // block done: advance to the next block of the MCU (or MCU)
+        k += r;
+        if (s || dc) {
+            if (k > 63) return J_BAD_DATA;
+            sink.put(k, v);
+            k += 1;
+        } else {
+            k = r == 15 ? k + 1 : 64;   // ZRL: 16 zeros; EOB
+        }
+        if (k >= 64) {   // block done: the next block of the MCU, or the next MCU
+            sink.end();
             k = 0;
             if (++b == nb) {
                 b = 0;
                 ++mcu;
+                org0 += h0 * 64;
+                org1 += 64;
+                org2 += 64;
                 if (++mx == im.mcux) {
                     mx = 0;
-                    ++my;
+                    org0 += row_skip0;
                 }
                 if (im.ri && mcu < nmcu && --togo == 0) {
                     togo = im.ri;
@@ -212,28 +287,10 @@ __host__ __device__ inline int32_t entropy_decode(const uint8_t* src, const Jpeg
                     br.restart();
                 }
             }
-            int bx, by;
-            if (b < n0) {
-                comp = 0;
-                const int dx = im.hs[0] == 2 ? (b & 1) : 0;
-                const int dy = im.hs[0] == 2 ? (b >> 1) : b;
-                if (im.ncomp == 1) {
-                    bx = mx;
-                    by = my;
-                } else {
-                    bx = mx * im.hs[0] + dx;
-                    by = my * im.vs[0] + dy;
-                }
-                blk = base0 + ((int64_t)by * im.bw[0] + bx) * 64;
-                tbl = dct0;
-            } else {
-                comp = b - n0 + 1;
-                bx = mx;
-                by = my;
-                blk = (comp == 1 ? base1 + ((int64_t)by * im.bw[1] + bx) * 64
-                                 : base2 + ((int64_t)by * im.bw[2] + bx) * 64);
-                tbl = comp == 1 ? dct1 : dct2;
-            }
+            comp = b < n0 ? 0 : b - n0 + 1;
+            int16_t* y = org0 + ((b & (h0 - 1)) + (int64_t)(b >> (h0 - 1)) * bw0) * 64;
+            sink.begin(comp == 0 ? y : (comp == 1 ? org1 : org2));
+            tbl = comp == 0 ? dct0 : (comp == 1 ? dct1 : dct2);
         }
     }
     return J_OK;
@@ -379,15 +436,16 @@ __host__ __device__ inline void ycc_to_rgb(int yy, int cb, int cr, uint8_t* rgb)
     rgb[2] = clamp8(yy + b_off);
 }
 
-__host__ __device__ inline void pixel_rgb(const JpegImage& im, const uint8_t* planes, int x, int y, uint8_t* rgb) {
-    const uint8_t* p0 = planes + im.plane_off + im.comp_plane[0];
+// img_planes: this image's component planes (comp_plane[] relative to it)
+__host__ __device__ inline void pixel_rgb(const JpegImage& im, const uint8_t* img_planes, int x, int y, uint8_t* rgb) {
+    const uint8_t* p0 = img_planes + im.comp_plane[0];
     const int yy = p0[(int64_t)y * im.bw[0] * 8 + x];
     if (im.ncomp == 1) {
         rgb[0] = rgb[1] = rgb[2] = (uint8_t)yy;
         return;
     }
-    const int c1 = chroma_at(im, planes + im.plane_off + im.comp_plane[1], 1, x, y);
-    const int c2 = chroma_at(im, planes + im.plane_off + im.comp_plane[2], 2, x, y);
+    const int c1 = chroma_at(im, img_planes + im.comp_plane[1], 1, x, y);
+    const int c2 = chroma_at(im, img_planes + im.comp_plane[2], 2, x, y);
     if (im.cspace == CS_RGB) {
         rgb[0] = (uint8_t)yy;
         rgb[1] = (uint8_t)c1;

@@ -23,7 +23,8 @@ extern "C" int jpeg_host_decode(const uint8_t* files, const uint8_t* plan, const
         const JpegImage& im = imgs[i];
         err[i] = im.status;
         if (im.status != J_OK) continue;
-        err[i] = entropy_decode(files, im, huff, coef.data());
+        DirectSink sink;
+        err[i] = entropy_decode(files, im, huff, coef.data(), sink);
         for (int c = 0; c < im.ncomp; ++c) {
             const int64_t pitch = (int64_t)im.bw[c] * 8;
             for (int by = 0; by < im.bh[c]; ++by)
@@ -34,7 +35,7 @@ extern "C" int jpeg_host_decode(const uint8_t* files, const uint8_t* plan, const
                                pitch);
         }
         for (int y = 0; y < im.h; ++y)
-            for (int x = 0; x < im.w; ++x) pixel_rgb(im, planes.data(), x, y, out + im.out_off + ((int64_t)y * im.w + x) * 3);
+            for (int x = 0; x < im.w; ++x) pixel_rgb(im, planes.data() + im.plane_off, x, y, out + im.out_off + ((int64_t)y * im.w + x) * 3);
     }
     return 0;
 }
