@@ -17,10 +17,11 @@ star's target, MSMT17 end to end on all ranks (sharded embed, all-gather, distma
 sharded k-reciprocal re-rank + CMC/mAP, wall seconds max over ranks); "rerank" = configs[2]'s
 Duke-size re-rank on rank 0 with the C port timed on the full config; "text" = the --mm
 zero-shot classifier's text side at Market size (750 x 56 token rows, TF/s); "backend" /
-"preprocess" = retrieval-kernel and transform rooflines; "cpu_baseline".
+"preprocess" = retrieval-kernel and transform rooflines; "jpeg" = the loaders' JPEG decode of
+a Market split of files on the device (and + transform), Pillow timed beside it; "cpu_baseline".
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B (default 1024)] [--no-cpu-baseline] [--no-rerank]
-                    [--no-msmt17] [--no-text]
+                    [--no-msmt17] [--no-text] [--no-jpeg]
 """
 import argparse
 import json
@@ -277,6 +278,78 @@ def preprocess_leg(dev, n=19281, reps=5):
             "achieved_GBps": round(nbytes / (ms * 1e-3) / 1e9, 1), "peak_GBps": 8000.0}
 
 
+def jpeg_leg(dev, n=19281, reps=5, unique=2048, cpu=True, n_cpu=2000):
+    """`Image.open(path).convert("RGB")` of the loaders
+    (data_prepare.py:87-92) for the Market split's worth of 128x64 4:2:0 JPEG files (Pillow-
+    encoded synthetic crops, `unique` distinct files cycled), file bytes and plan resident in
+    HBM: reidmi_jpeg_decode alone, and decode + reidmi_preprocess_u8 to fp16 [n, 3, 256, 128].
+    The Huffman pass is serial per image (one lane each; latency-bound), so the bound named is
+    that pass, with the file + RGB bytes' HBM rate reported beside it.  CPU: Pillow itself (the
+    reference's decoder) on one thread over n_cpu files."""
+    import ctypes
+    import io
+    from multimodal_reid_amd import data_prepare
+    u = syn.jpeg_files(min(n, unique), 128, 64, seed=0, quality=90)
+    files = [u[i % len(u)] for i in range(n)]
+    t = time.perf_counter()
+    jb = data_prepare.JpegBatch(files)
+    t_plan = time.perf_counter() - t
+    jb.raise_for_status()
+    dfiles = data_prepare._to_device(jb.buf, dev)
+    dplan = data_prepare._to_device(jb.plan, dev)
+    ws = torch.empty(jb.ws_bytes, dtype=torch.uint8, device=dev)
+    pix = torch.empty(jb.out_bytes, dtype=torch.uint8, device=dev)
+    err = torch.empty(n, dtype=torch.int32, device=dev)
+    meta = torch.from_numpy(jb.meta).to(dev)
+    out = torch.empty((n, 3, 256, 128), dtype=torch.float16, device=dev)
+    info = jb.info.copy()
+    half = (ctypes.c_float * 3)(0.5, 0.5, 0.5)
+    s = _lib.stream(dev)
+
+    def decode():
+        _lib.call("reidmi_jpeg_decode", _lib.ptr(dfiles), _lib.ptr(dplan), info.ctypes.data_as(ctypes.c_void_p), n,
+                  _lib.ptr(ws), ws.numel(), _lib.ptr(pix), _lib.ptr(err), s)
+
+    def both():
+        decode()
+        _lib.call("reidmi_preprocess_u8", _lib.ptr(pix), _lib.ptr(meta), n, jb.max_h, jb.max_w, 256, 128, half, half,
+                  1, _lib.ptr(out), s)
+
+    res = {}
+    for name, fn in (("decode", decode), ("decode_preprocess", both)):
+        fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        res[name] = e0.elapsed_time(e1) / reps
+    assert not err.any().item(), "jpeg decode reported undecodable files"
+    fb = int(jb.buf.size)
+    line = {"config": f"{n} Pillow-encoded 128x64 4:2:0 q90 JPEG files ({fb / n:.0f} B avg) in HBM -> RGB; "
+                      "+ Resize/ToTensor/Normalize -> fp16 [n,3,256,128]",
+            "imgs_per_s": round(n / (res["decode"] * 1e-3), 1), "ms": round(res["decode"], 3),
+            "decode_preprocess_ms": round(res["decode_preprocess"], 3),
+            "decode_preprocess_imgs_per_s": round(n / (res["decode_preprocess"] * 1e-3), 1),
+            "host_plan_ms": round(t_plan * 1e3, 2),
+            "roofline": {"bound": "latency (serial Huffman decode, one lane per image)",
+                         "achieved_GBps": round((fb + jb.out_bytes) / (res["decode"] * 1e-3) / 1e9, 1),
+                         "peak_GBps": PEAK_HBM_GBPS}}
+    if cpu:
+        from PIL import Image
+        k = min(n_cpu, n)
+        t = time.perf_counter()
+        for f in files[:k]:
+            np.asarray(Image.open(io.BytesIO(f)).convert("RGB"))
+        dt = time.perf_counter() - t
+        line["cpu_reference"] = {"sample": f"Pillow Image.open(...).convert('RGB') of {k} of these files, 1 thread "
+                                           "(the reference decodes in 4 DataLoader workers, data_prepare.py:275-283)",
+                                 "imgs_per_s": round(k / dt, 1), "cores": 1, "kind": "reference"}
+    del dfiles, ws, pix, out
+    return line
+
+
 def text_leg(dev, n_cls=750, n_tpl=56, reps=3, cpu=True, threads=1, n_cpu=32):
     """the --mm zero-shot classifier's text side at Market size
     (zero_shot_learning.py:37-49): n_cls identities x n_tpl augmented templates = 42 000 token
@@ -384,6 +457,7 @@ def main():
     ap.add_argument("--no-rerank", action="store_true")
     ap.add_argument("--no-msmt17", action="store_true")
     ap.add_argument("--no-text", action="store_true")
+    ap.add_argument("--no-jpeg", action="store_true")
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -459,6 +533,8 @@ def main():
             line["msmt17"] = ms17
         line["backend"] = backend_rooflines(wl)
         line["preprocess"] = preprocess_leg(dev)
+        if not a.no_jpeg:
+            line["jpeg"] = jpeg_leg(dev, cpu=not a.no_cpu_baseline)
         threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
         if not a.no_rerank:
             line["rerank"] = rerank_leg(dev, cpu=not a.no_cpu_baseline, threads=threads)
