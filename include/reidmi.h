@@ -331,16 +331,17 @@ int reidmi_preprocess_lds_size(int oh, int ow, int max_h, int max_w, int64_t* by
  *                     12-bit / multi-scan, 3 component layout, 4 bad tables;
  *   meta int64 [B][3] (byte offset in the decoded batch, h, w) — the `meta` of
  *                     reidmi_preprocess_u8; zeros for images with status != 0;
- *   info int64 [9]    plan bytes, workspace bytes, decoded bytes, max h, max w, images with
+ *   info int64 [10]   plan bytes, workspace bytes, decoded bytes, max h, max w, images with
  *                     status != 0, coefficient count, distinct Huffman tables, largest
- *                     per-image plane bytes;
+ *                     per-image plane bytes, B;
  *   plan              when plan != NULL and plan_capacity >= info[0]: a position-independent
  *                     blob the caller copies to the device (call once with plan = NULL to size it).
  *
  * reidmi_jpeg_decode (stream-ordered): files = the same bytes on the DEVICE, plan = the plan on
- * the device, info = the HOST info[9] of the plan call; ws >= info[1] bytes; pix >= info[2]
- * bytes receives the HWC uint8 images; err int32 [B] (device) = the plan status, or 5 where the
- * entropy-coded data does not decode. */
+ * the device, info = the HOST info[10] of the plan call (B must equal info[9]); ws >= info[1]
+ * bytes; pix >= info[2] bytes receives the HWC uint8 images; err int32 [B] (device) = the plan
+ * status, or 5 where the entropy-coded data does not decode (that image's coefficients are
+ * then zero). */
 int reidmi_jpeg_plan(const uint8_t* files, const int64_t* offsets, int64_t B, void* plan, int64_t plan_capacity,
                      int64_t* meta, int32_t* status, int64_t* info);
 int reidmi_jpeg_decode(const uint8_t* files, const void* plan, const int64_t* info, int64_t B, void* ws,

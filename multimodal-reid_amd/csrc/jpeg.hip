@@ -251,7 +251,8 @@ __global__ __launch_bounds__(64) void jpeg_entropy_kernel(const uint8_t* __restr
     if constexpr (kLds) {
         const uint4* g = (const uint4*)gh;
         uint4* l = (uint4*)lds;
-        const int n16 = (int)(P->n_huff * (int64_t)sizeof(JpegHuff) / 16);
+        const int64_t nh = P->n_huff < kLdsTables ? P->n_huff : kLdsTables;   // (the host checked n_huff)
+        const int n16 = (int)(nh * (int64_t)sizeof(JpegHuff) / 16);
         for (int j = threadIdx.x; j < n16; j += 64) l[j] = g[j];
         __syncthreads();
     }
@@ -428,6 +429,7 @@ REIDMI_API int reidmi_jpeg_plan(const uint8_t* files, const int64_t* offsets, in
     info[6] = coef;
     info[7] = hdr.n_huff;
     info[8] = max_plane;
+    info[9] = B;
     if (plan == nullptr || plan_capacity < plan_bytes) return OK;   // sizing call
     uint8_t* pb = (uint8_t*)plan;
     memset(pb, 0, (size_t)plan_bytes);
@@ -444,6 +446,7 @@ REIDMI_API int reidmi_jpeg_decode(const uint8_t* files, const void* plan, const 
     if (B == 0) return OK;
     RM_REQUIRE(files && plan && ws && err && (pix || info[2] == 0), "reidmi_jpeg_decode: null pointer");
     RM_REQUIRE(ws_bytes >= info[1], "reidmi_jpeg_decode: workspace smaller than info[1]");
+    RM_REQUIRE(info[9] == B, "reidmi_jpeg_decode: B differs from the plan's (info[9])");
     hipStream_t s = (hipStream_t)stream;
     int16_t* coef = (int16_t*)ws;
     uint8_t* planes = (uint8_t*)ws + align_up(info[6] * 2, 256);

@@ -141,7 +141,7 @@ class JpegBatch:
         self.B = B
         self.meta = np.zeros((B, 3), np.int64)
         self.status = np.zeros(B, np.int32)
-        self.info = np.zeros(9, np.int64)
+        self.info = np.zeros(10, np.int64)
         args = (self.buf.ctypes.data_as(ctypes.c_void_p), self.offsets.ctypes.data_as(ctypes.c_void_p), B)
         out = (self.meta.ctypes.data_as(ctypes.c_void_p), self.status.ctypes.data_as(ctypes.c_void_p),
                self.info.ctypes.data_as(ctypes.c_void_p))
