@@ -453,17 +453,23 @@ __device__ double pairwise_tree_wave(const int* rk, VAL val, int m, int64_t n, u
     return res;
 }
 
-// pairwise_tree_wave for m <= 64 without LDS on the serial chain: lane t holds rk[t] (in
-// rk_l); the leaf-by-leaf combination runs on every lane with wave-uniform values (readlane),
-// and its two stacks keep entry i in lane i (writelane / readlane).  The LDS variant waited
-// one LDS round trip per step of that dependent chain (a third of a Market query's time).
-// VAL: (t, rk[t]) -> double.  Same additions in the same order: bit-identical.
+// pairwise_tree_wave's sum for m <= 64 with the leaves combined lane-parallel: lane t < m holds
+// rk[t] (rk_l; rk is the same array in LDS, read for leaves holding several nonzeros).  Each
+// leaf group's first lane sums its leaf (one nonzero: the value itself, x + zeros == x; more:
+// leaf_sum over the group), then the splits are applied deepest first: at depth D every
+// segment whose left boundary is a depth-D split adds itself into the segment on its left.
+// Two depth-D boundaries never border the same segment (a shallower split lies between
+// them), so this is pairwise_tree_wave's precedence evaluation step for step — the same
+// additions, bit-identical — in (tree depth) wave steps instead of a serial chain over the
+// leaves (that chain, even in registers, was ~27 % of a Market query:
+// profiles/r02/eval_rows_phase_stamps.txt).
 template <typename VAL>
-__device__ double pairwise_tree_regs(int rk_l, VAL val, int m, int64_t n) {
+__device__ double pairwise_tree_par(int rk_l, const int* rk, VAL val, int m, int64_t n) {
     const int lane = threadIdx.x & 63;
+    const bool live = lane < m;
     uint32_t pb = 0;
     int d = 0;
-    if (lane < m) {
+    if (live) {
         int64_t off = 0, len = n;
         while (len > 128) {
             int64_t n2 = len / 2;
@@ -473,50 +479,47 @@ __device__ double pairwise_tree_regs(int rk_l, VAL val, int m, int64_t n) {
             d++;
         }
     }
-    auto rd = [](int v, int t) { return __builtin_amdgcn_readlane(v, t); };
-    auto wr = [&](int x, int i, int old) { return lane == i ? x : old; };  // writelane
-    int sv_lo = 0, sv_hi = 0, so = 0;
-    int sp = 0, op = 0, t = 0;
-    auto push_val = [&](double x) {
-        const uint64_t b = __builtin_bit_cast(uint64_t, x);
-        sv_lo = wr((int)(uint32_t)b, sp, sv_lo);
-        sv_hi = wr((int)(uint32_t)(b >> 32), sp, sv_hi);
-        sp++;
-    };
-    auto get_val = [&](int i) {
-        const uint32_t lo = (uint32_t)rd(sv_lo, i), hi = (uint32_t)rd(sv_hi, i);
-        return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
-    };
-    auto reduce_top = [&]() {  // vals[sp-2] += vals[sp-1]
-        const double b = get_val(sp - 1), a = get_val(sp - 2);
-        sp -= 2;
-        push_val(a + b);
-        op--;
-    };
-    while (t < m) {
-        const uint32_t pt = (uint32_t)rd((int)pb, t);
-        const int dt = rd(d, t);
-        int u = t + 1;
-        while (u < m && (uint32_t)rd((int)pb, u) == pt && rd(d, u) == dt) u++;
-        int64_t off = 0, len = n;
-        for (int e = 0; e < dt; e++) {
-            int64_t n2 = len / 2;
-            n2 -= n2 % 8;
-            if ((pt >> e) & 1u) { off += n2; len -= n2; } else len = n2;
+    const uint32_t ppb = (uint32_t)__shfl_up((int)pb, 1, 64);
+    const int pd = __shfl_up(d, 1, 64);
+    const bool head = live && (lane == 0 || ppb != pb || pd != d);
+    const uint64_t heads = __ballot(head);
+    double s = 0.0;
+    int c = -1;  // depth of the split between the previous leaf and this one
+    if (head) {
+        const uint64_t above = (heads >> lane) >> 1;
+        const int u = above ? lane + 1 + __builtin_ctzll(above) : m;
+        if (u == lane + 1) {
+            s = val(lane, rk_l);
+        } else {
+            int64_t off = 0, len = n;
+            for (int e = 0; e < d; e++) {
+                int64_t n2 = len / 2;
+                n2 -= n2 % 8;
+                if ((pb >> e) & 1u) { off += n2; len -= n2; } else len = n2;
+            }
+            s = leaf_sum([&](int k) { return (int64_t)rk[k]; }, [&](int k) { return val(k, rk[k]); }, lane, u, off,
+                         len);
         }
-        const double v = leaf_sum([&](int k) { return (int64_t)rd(rk_l, k); },
-                                  [&](int k) { return val(k, rd(rk_l, k)); }, t, u, off, len);
-        if (t > 0) {
-            const int c = __builtin_ctz((uint32_t)rd((int)pb, t - 1) ^ pt);
-            while (op > 0 && rd(so, op - 1) > c) reduce_top();
-            so = wr(c, op, so);
-            op++;
-        }
-        push_val(v);
-        t = u;
+        if (lane > 0) c = __builtin_ctz(ppb ^ pb);
     }
-    while (op > 0) reduce_top();
-    return get_val(0);
+    int maxc = c;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const int t = __shfl_xor(maxc, o, 64);
+        maxc = t > maxc ? t : maxc;
+    }
+    uint64_t act = heads;
+    for (int D = maxc; D >= 0; D--) {
+        const bool on = (act >> lane) & 1;
+        const uint64_t mrg = __ballot(on && c == D);
+        if (!mrg) continue;
+        const uint64_t nxt = lane < 63 ? act >> (lane + 1) : 0;
+        const int R = nxt ? lane + 1 + __builtin_ctzll(nxt) : lane;
+        const double sr = __shfl(s, R, 64);
+        if (on && nxt && ((mrg >> R) & 1)) s = s + sr;
+        act &= ~mrg;
+    }
+    return __shfl(s, 0, 64);
 }
 
 // Per query (evaluate.py:40-80): positives = gallery items with the query's pid and another
@@ -540,9 +543,45 @@ struct EvLabels {
 __device__ __forceinline__ uint64_t ord64(int64_t v) { return (uint64_t)v ^ 0x8000000000000000ull; }
 __device__ __forceinline__ int64_t unord64(uint64_t v) { return (int64_t)(v ^ 0x8000000000000000ull); }
 
-__global__ void ev_minmax_init_kernel(unsigned long long* mm) {
+__global__ void ev_minmax_init_kernel(unsigned long long* mm, int32_t* overflow) {
     mm[0] = ~0ull;
     mm[1] = 0ull;
+    *overflow = 0;
+}
+
+// min / max and the uint16 packing in ONE workgroup for galleries up to EV_PREP1_MAX (every
+// ReID benchmark): one launch instead of three (each ~4-7 us at Market size, the kernel
+// itself ~130 us).  Same outputs as ev_minmax_init/ev_minmax/ev_pack.
+constexpr int64_t EV_PREP1_MAX = 1 << 18;
+
+__global__ __launch_bounds__(1024) void ev_prep1_kernel(const int64_t* __restrict__ gp, int64_t G, int64_t G8,
+                                                        unsigned long long* __restrict__ mm, uint16_t* __restrict__ pk,
+                                                        int32_t* __restrict__ overflow) {
+    __shared__ uint64_t slo[16], shi[16];
+    const int tid = threadIdx.x;
+    uint64_t lo = ~0ull, hi = 0;
+    for (int64_t j = tid; j < G; j += 1024) {
+        const uint64_t o = ord64(gp[j]);
+        lo = o < lo ? o : lo;
+        hi = o > hi ? o : hi;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t a = __shfl_xor(lo, off, 64), b = __shfl_xor(hi, off, 64);
+        lo = a < lo ? a : lo;
+        hi = b > hi ? b : hi;
+    }
+    if ((tid & 63) == 0) { slo[tid >> 6] = lo; shi[tid >> 6] = hi; }
+    __syncthreads();
+    lo = slo[0];
+    hi = shi[0];
+    for (int w = 1; w < 16; w++) {
+        lo = slo[w] < lo ? slo[w] : lo;
+        hi = shi[w] > hi ? shi[w] : hi;
+    }
+    if (tid == 0) { mm[0] = lo; mm[1] = hi; *overflow = 0; }
+    const int64_t plo = unord64(lo), phi = unord64(hi);
+    if ((uint64_t)(phi - plo) >= 0xFFFFull) return;  // wide pid range: the int64 path
+    for (int64_t j = tid; j < G8; j += 1024) pk[j] = j < G ? (uint16_t)(gp[j] - plo) : (uint16_t)0xFFFF;
 }
 
 __global__ __launch_bounds__(256) void ev_minmax_kernel(const int64_t* __restrict__ gp, int64_t G,
@@ -573,19 +612,20 @@ __global__ void ev_pack_kernel(const int64_t* __restrict__ gp, int64_t G, int64_
     pk[j] = j < G ? (uint16_t)(gp[j] - lo) : (uint16_t)0xFFFF;
 }
 
-// eval_rows_wg_kernel: one 256-thread workgroup (4 waves) per query, ~8 KiB of LDS, so
-// ~8 workgroups per CU keep loads in flight.  Pass 1 streams the gallery labels (int64 pid /
-// camera, L2-resident: every query reads the same 2 x 8 B per item) and compacts the
-// positives' and junk items' indices (ballot + one LDS atomic per wave and step); their
-// distances are then gathered and the positives bitonic-sorted in LDS.  Pass 2 reads the
-// distance row once (16-byte loads after a scalar head to 16-byte alignment), skipping items
-// beyond the last positive, and bins the rest into an LDS histogram through a bucket table
-// of the positives (no per-item binary search: that search was 2/3 of the kernel).  Wave 0
-// scans the histogram into ranks; lane 0 does the AP sum.  Queries with more than EVW_MAXP
-// positives or EVW_MAXJ junk items are left to eval_rows_kernel (valid = 2).
+// eval_rows_wg_kernel: one 256-thread workgroup (4 waves) per query, ~17 KiB of LDS, 8
+// workgroups per CU.  Pass 1 streams the gallery labels (uint16-packed, L2-resident: every
+// query reads the same lines) and compacts the indices of the query's pid (ballot + one LDS
+// atomic per wave and hit); their cameras and distances then come in ONE round trip and
+// split them into positives and junk; the positives are bitonic-sorted in LDS.  Pass 2 reads
+// the distance row once (16-byte loads after a scalar head to 16-byte alignment), skipping
+// items beyond the last positive, and bins the rest into an LDS histogram through a bucket
+// table of the positives (no per-item binary search: that search was 2/3 of the kernel).
+// Wave 0 scans the histogram into ranks and sums the AP lane-parallel.  Queries with more
+// than EVW_MAXP positives or EVW_MAXJ junk items are left to eval_rows_kernel (valid = 2).
+// Per-phase cycle stamps: profiles/r02/eval_rows_phase_stamps.txt (-DEV_STAMPS build).
 constexpr int EVW_MAXP = 512, EVW_MAXJ = 256, EVW_T = 1024;
 
-__global__ __launch_bounds__(256) void eval_rows_wg_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void eval_rows_wg_kernel(
     const float* __restrict__ dist, int64_t G, int64_t ld, const int64_t* __restrict__ qp,
     const int64_t* __restrict__ gp, const int64_t* __restrict__ qc, const int64_t* __restrict__ gc,
     const unsigned long long* __restrict__ mm, const uint16_t* __restrict__ pk, int32_t* __restrict__ valid,
@@ -595,44 +635,39 @@ __global__ __launch_bounds__(256) void eval_rows_wg_kernel(
     __shared__ int hist[EVW_MAXP + 1];
     __shared__ float jv[EVW_MAXJ];
     __shared__ int ji[EVW_MAXJ];
-    __shared__ int s_m, s_nj;
+    __shared__ int s_m, s_nj, s_ns;
     __shared__ double tvals[AP_STACK];
     __shared__ int tops[AP_STACK];
     __shared__ int2 bucket[EVW_T];  // [S[t], S[t+1]): the positives whose bucket is t
     const int tid = threadIdx.x, lane = tid & 63;
+#ifdef EV_STAMPS
+    const uint64_t t0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t t1 = 0, t2 = 0, t3 = 0;
+#endif
     const int64_t q = blockIdx.x;
     const float* row = dist + q * ld;
     const int64_t qpid = qp[q], qcam = qc[q];
     const uint64_t below = (1ull << lane) - 1;
-    if (tid == 0) { s_m = 0; s_nj = 0; }
+    int* sidx = (int*)bucket;  // same-pid gallery indices of pass 1 (the bucket table comes later)
+    constexpr int SCAP = EVW_MAXP + EVW_MAXJ;
+    if (tid == 0) { s_m = 0; s_nj = 0; s_ns = 0; }
     __syncthreads();
-    // ---- pass 1: labels -> positive / junk index lists (ballot compaction + one LDS atomic
-    // per wave and step).  Every workgroup reads the same label lines, so each starts at its
-    // own chunk; the camera is loaded only for items of the query's pid.
+    // ---- pass 1: labels -> indices of the gallery items with the query's pid (ballot
+    // compaction, one LDS atomic per wave and hit).  Every workgroup reads the same label
+    // lines, so each starts at its own chunk.
     auto take = [&](bool same, int64_t j) {
-        const bool samecam = same && gc[j] == qcam;
-        const bool pos = same && !samecam, junk = samecam;
-        const uint64_t mp = __ballot(pos), mj = __ballot(junk);
-        if (mp) {
-            int base = 0;
-            if (lane == 0) base = atomicAdd(&s_m, __popcll(mp));
-            base = __shfl(base, 0, 64);
-            const int sl = base + __popcll(mp & below);
-            if (pos && sl < EVW_MAXP) pi[sl] = (int)j;
-        }
-        if (mj) {
-            int base = 0;
-            if (lane == 0) base = atomicAdd(&s_nj, __popcll(mj));
-            base = __shfl(base, 0, 64);
-            const int sl = base + __popcll(mj & below);
-            if (junk && sl < EVW_MAXJ) ji[sl] = (int)j;
-        }
+        const uint64_t ms = __ballot(same);
+        int base = 0;
+        if (lane == 0) base = atomicAdd(&s_ns, __popcll(ms));
+        base = __shfl(base, 0, 64);
+        const int sl = base + __popcll(ms & below);
+        if (same && sl < SCAP) sidx[sl] = (int)j;
     };
     const int64_t plo = unord64(mm[0]), phi = unord64(mm[1]);
     if ((uint64_t)(phi - plo) < 0xFFFFull) {  // packed uint16 labels, 8 per 16-byte load
         if (qpid >= plo && qpid <= phi) {
             const uint16_t key = (uint16_t)(qpid - plo);
-            constexpr int U1 = 2, CH = 2048 * U1;
+            constexpr int U1 = 4, CH = 2048 * U1;
             const int64_t nch = (G + CH - 1) / CH;
             const int64_t c0 = (q * 37) % nch;
             const int64_t n8 = (G + 7) / 8;
@@ -670,28 +705,51 @@ __global__ __launch_bounds__(256) void eval_rows_wg_kernel(
                 pid[u] = j < G ? gp[j] : qpid + 1;
             }
 #pragma unroll
-            for (int u = 0; u < U1; u++) take(pid[u] == qpid, j0 + u * 256 + tid);
+            for (int u = 0; u < U1; u++) {
+                const bool same = pid[u] == qpid;
+                if (__ballot(same)) take(same, j0 + u * 256 + tid);
+            }
+        }
+    }
+    __syncthreads();
+    const int ns = s_ns;
+    // ---- split them into positives (other camera) and junk (same camera, removed,
+    // evaluate.py:55-56), their cameras and distances loaded in one round trip
+    if (ns <= SCAP) {
+        for (int t = tid; t < ns; t += 256) {
+            const int j = sidx[t];
+            const int64_t cam = gc[j];
+            const float v = row[j];
+            if (cam == qcam) {
+                const int sl = atomicAdd(&s_nj, 1);
+                if (sl < EVW_MAXJ) { ji[sl] = j; jv[sl] = v; }
+            } else {
+                const int sl = atomicAdd(&s_m, 1);
+                if (sl < EVW_MAXP) { pi[sl] = j; pv[sl] = v; }
+            }
         }
     }
     __syncthreads();
     const int m = s_m, nj = s_nj;
+#ifdef EV_STAMPS
+    t1 = __builtin_amdgcn_s_memtime();
+#endif
+    if (ns > SCAP || m > EVW_MAXP || nj > EVW_MAXJ) {  // eval_rows_kernel (large lists) takes it
+        if (tid == 0) valid[q] = 2;
+        return;
+    }
     if (tid == 0) nkept[q] = G - nj;
     if (m == 0) {
         if (tid == 0) { valid[q] = 0; first[q] = -1; ap[q] = 0.0; }
         return;
     }
-    if (m > EVW_MAXP || nj > EVW_MAXJ) {  // eval_rows_kernel (large lists) takes it
-        if (tid == 0) valid[q] = 2;
-        return;
-    }
-    // ---- gather the positives' / junk distances, sort the positives by (value, index)
+    // ---- sort the positives by (value, index)
     int P = 1;
     while (P < m) P <<= 1;
-    for (int t = tid; t < P; t += 256) {
-        if (t < m) pv[t] = row[pi[t]];
-        else { pv[t] = __builtin_inff(); pi[t] = 0x7fffffff; }
+    for (int t = m + tid; t < P; t += 256) {
+        pv[t] = __builtin_inff();
+        pi[t] = 0x7fffffff;
     }
-    for (int t = tid; t < nj; t += 256) jv[t] = row[ji[t]];
     for (int t = tid; t <= m; t += 256) hist[t] = 0;
     __syncthreads();
     bitonic_sort_kv(pv, pi, P);
@@ -704,14 +762,14 @@ __global__ __launch_bounds__(256) void eval_rows_wg_kernel(
     const int li = pi[m - 1];
     const float v0 = pv[0];
     const int T = 8 * P < EVW_T ? (8 * P > 64 ? 8 * P : 64) : EVW_T;  // ~8 buckets per positive
-    // t(x) = floor(med3(x * scale - v_0 * scale, 0, T-1)): one fma, one med3, one floor-convert
+    // t(x) = floor(med3(x * scale - v_0 * scale, 0, T-1)): one fma, one med3, one convert
     // per item; when the positives tie (scale inf / NaN) every item goes to bucket 0 and the
     // exact compares decide
     float scale = (float)T / (lv - v0);
     if (!(scale <= 3.0e38f)) scale = 0.0f;
     const float c0 = -v0 * scale, tmax = (float)(T - 1);
-    auto bucket_of = [&](float x) {
-        return (int)__builtin_floorf(__builtin_amdgcn_fmed3f(__builtin_fmaf(x, scale, c0), 0.0f, tmax));
+    auto bucket_of = [&](float x) {  // med3 clamps to [0, T-1], so truncation is the floor
+        return (int)__builtin_amdgcn_fmed3f(__builtin_fmaf(x, scale, c0), 0.0f, tmax);
     };
     for (int t = tid; t < T; t += 256) {  // S[t] = #{k : t(pv_k) < t}
         int lo = 0, hi = m;
@@ -727,6 +785,9 @@ __global__ __launch_bounds__(256) void eval_rows_wg_kernel(
         bucket[t] = make_int2(lo, lo2);
     }
     __syncthreads();
+#ifdef EV_STAMPS
+    t2 = __builtin_amdgcn_s_memtime();
+#endif
     auto bin = [&](float v, int j) {
         // after the last positive (b = m, not needed); NaN sorts last (np.argsort):
         // key_less(lv, li, v, j) || v != v, with the NaN test folded into !(v <= lv)
@@ -749,20 +810,45 @@ __global__ __launch_bounds__(256) void eval_rows_wg_kernel(
             const int64_t g = g0 + u * 256 + tid;
             v[u] = g < nv ? r4[g] : make_float4(0.f, 0.f, 0.f, 0.f);
         }
+        // 8 items at a time: their bucket indices first, then the 8 bucket-table reads issued
+        // together (one LDS round trip per 8 items, not one per item), then the rare exact
+        // compares and the histogram adds
 #pragma unroll
-        for (int u = 0; u < U2; u++) {
-            const int64_t g = g0 + u * 256 + tid;
-            if (g < nv) {
-                const int j = h + (int)g * 4;
-                bin(v[u].x, j);
-                bin(v[u].y, j + 1);
-                bin(v[u].z, j + 2);
-                bin(v[u].w, j + 3);
+        for (int hu = 0; hu < U2; hu += 2) {
+            float x[8];
+            int jj[8], tb[8];
+            bool ok[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const int u = hu + (k >> 2);
+                const int64_t g = g0 + u * 256 + tid;
+                x[k] = (k & 3) == 0 ? v[u].x : (k & 3) == 1 ? v[u].y : (k & 3) == 2 ? v[u].z : v[u].w;
+                jj[k] = h + (int)g * 4 + (k & 3);
+                // items after the last positive are not needed (b = m); NaN sorts last
+                // (np.argsort) and fails x <= lv.  An item tied with the last positive's value
+                // but after it (x == lv, j > li) is binned: the exact compares give it b = m,
+                // a count in hist[m] that no rank reads
+                ok[k] = g < nv && x[k] <= lv;
+                tb[k] = ok[k] ? bucket_of(x[k]) : 0;
+            }
+            int2 se[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) se[k] = bucket[tb[k]];
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                if (ok[k]) {
+                    int b = se[k].x;
+                    while (b < se[k].y && key_less(pv[b], pi[b], x[k], jj[k])) b++;
+                    atomicAdd(&hist[b], 1);
+                }
             }
         }
     }
     for (int64_t j = h + nv * 4 + tid; j < G; j += 256) bin(row[j], (int)j);
     __syncthreads();
+#ifdef EV_STAMPS
+    t3 = __builtin_amdgcn_s_memtime();
+#endif
     // ---- ranks (wave 0): inclusive scan of hist, minus the item itself and the junk before it
     if (tid < 64) {
         int carry = 0;
@@ -788,14 +874,20 @@ __global__ __launch_bounds__(256) void eval_rows_wg_kernel(
         __builtin_amdgcn_wave_barrier();
         const int* rk = hist;
         const double sum =
-            m <= 64 ? pairwise_tree_regs(lane < m ? rk[lane] : 0,
-                                         [](int t, int r) { return (double)(t + 1) / (double)(r + 1); }, m, G - nj)
+            m <= 64 ? pairwise_tree_par(lane < m ? rk[lane] : 0, rk,
+                                        [](int t, int r) { return (double)(t + 1) / (double)(r + 1); }, m, G - nj)
                     : pairwise_tree_wave(rk, [&](int t) { return (double)(t + 1) / (double)(rk[t] + 1); }, m, G - nj,
                                          (uint32_t*)pv, pi, tvals, tops);  // pv / pi are free now
         if (lane == 0) {
             valid[q] = 1;
             first[q] = rk[0];
             ap[q] = sum / (double)m;
+#ifdef EV_STAMPS
+            const uint64_t t4 = __builtin_amdgcn_s_memtime();
+            first[q] = (int64_t)((t1 - t0) | ((t2 - t1) << 32));
+            nkept[q] = (int64_t)((t3 - t2) | ((t4 - t3) << 32));
+            ap[q] = (double)rt0;
+#endif
         }
     }
 }
@@ -1028,14 +1120,19 @@ REIDMI_API int reidmi_eval_rows(const float* dist, int64_t Q, int64_t G, int64_t
     unsigned long long* mm = (unsigned long long*)ws_;
     uint16_t* pk = (uint16_t*)((char*)ws_ + 256);
     const int64_t G8 = (G + 7) / 8 * 8;
-    hipLaunchKernelGGL(ev_minmax_init_kernel, dim3(1), dim3(1), 0, s, mm);
-    RM_LAUNCHED();
-    hipLaunchKernelGGL(ev_minmax_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(G, 256), 1024)), dim3(256), 0, s,
-                       g_pids, G, mm);
-    RM_LAUNCHED();
-    hipLaunchKernelGGL(ev_pack_kernel, dim3(ceil_div(G8, 256)), dim3(256), 0, s, g_pids, G, G8,
-                       (const unsigned long long*)mm, pk);
-    RM_LAUNCHED();
+    if (G <= EV_PREP1_MAX) {
+        hipLaunchKernelGGL(ev_prep1_kernel, dim3(1), dim3(1024), 0, s, g_pids, G, G8, mm, pk, overflow);
+        RM_LAUNCHED();
+    } else {
+        hipLaunchKernelGGL(ev_minmax_init_kernel, dim3(1), dim3(1), 0, s, mm, overflow);
+        RM_LAUNCHED();
+        hipLaunchKernelGGL(ev_minmax_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(G, 256), 1024)), dim3(256), 0,
+                           s, g_pids, G, mm);
+        RM_LAUNCHED();
+        hipLaunchKernelGGL(ev_pack_kernel, dim3(ceil_div(G8, 256)), dim3(256), 0, s, g_pids, G, G8,
+                           (const unsigned long long*)mm, pk);
+        RM_LAUNCHED();
+    }
     hipLaunchKernelGGL(eval_rows_wg_kernel, dim3((unsigned)Q), dim3(256), 0, s, dist, G, ldd, q_pids, g_pids, q_cams,
                        g_cams, (const unsigned long long*)mm, (const uint16_t*)pk, valid, first, ap, nkept);
     RM_LAUNCHED();

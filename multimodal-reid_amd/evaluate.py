@@ -84,7 +84,7 @@ def eval_rows_device(dist, q_pids, g_pids, q_camids, g_camids):
     first = torch.empty(Q, device=dev, dtype=torch.int64)
     ap = torch.empty(Q, device=dev, dtype=torch.float64)
     nkept = torch.empty(Q, device=dev, dtype=torch.int64)
-    overflow = torch.zeros(1, device=dev, dtype=torch.int32)
+    overflow = torch.empty(1, device=dev, dtype=torch.int32)  # written by the call
     ws = torch.empty(_lib.load().reidmi_eval_rows_workspace_bytes(G), device=dev, dtype=torch.uint8)
     _lib.call("reidmi_eval_rows", _lib.ptr(dist), Q, G, dist.stride(0), _lib.ptr(qp), _lib.ptr(gp), _lib.ptr(qc),
               _lib.ptr(gc), _lib.ptr(valid), _lib.ptr(first), _lib.ptr(ap), _lib.ptr(nkept), _lib.ptr(overflow),
