@@ -63,14 +63,15 @@ int reidmi_topk_rows_f32(const float* x, int64_t rows, int64_t cols, int64_t ldx
 
 /* Per-query part of eval_func — evaluate.py:40-80.  For query q: valid[q] (any match kept),
  * first[q] (0-based kept-rank of the first match), ap[q] (float64 AP exactly as numpy sums
- * it), nkept[q] (gallery items left after same-pid-same-cam removal).  overflow: one int32,
- * written by the call: 1 if some query has > 2048 positives (that query's valid = -1), else 0. */
+ * it), nkept[q] (gallery items left after same-pid-same-cam removal).  No capacity limit
+ * on positives or junk items per query.  overflow: one int32, written 0 by the call (kept for
+ * ABI compatibility with builds that had a positive-list capacity). */
 int reidmi_eval_rows(const float* dist, int64_t Q, int64_t G, int64_t ldd, const int64_t* q_pids,
                      const int64_t* g_pids, const int64_t* q_cams, const int64_t* g_cams, int32_t* valid,
                      int64_t* first, double* ap, int64_t* nkept, int32_t* overflow, void* ws, int64_t ws_bytes,
                      void* stream);
 /* Device workspace bytes (16-byte aligned) for reidmi_eval_rows: the gallery labels packed
- * once per call (O(G)). */
+ * once per call and the scratch of a query with more positives than fit LDS (O(G)). */
 int64_t reidmi_eval_rows_workspace_bytes(int64_t G);
 
 

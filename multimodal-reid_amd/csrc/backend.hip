@@ -546,6 +546,8 @@ __device__ __forceinline__ int64_t unord64(uint64_t v) { return (int64_t)(v ^ 0x
 __global__ void ev_minmax_init_kernel(unsigned long long* mm, int32_t* overflow) {
     mm[0] = ~0ull;
     mm[1] = 0ull;
+    mm[2] = 0ull;  // eval_rows_kernel's arrival counter and huge-query count
+    mm[3] = 0ull;  // "a query was deferred to eval_rows_kernel"
     *overflow = 0;
 }
 
@@ -578,7 +580,7 @@ __global__ __launch_bounds__(1024) void ev_prep1_kernel(const int64_t* __restric
         lo = slo[w] < lo ? slo[w] : lo;
         hi = shi[w] > hi ? shi[w] : hi;
     }
-    if (tid == 0) { mm[0] = lo; mm[1] = hi; *overflow = 0; }
+    if (tid == 0) { mm[0] = lo; mm[1] = hi; mm[2] = 0ull; mm[3] = 0ull; *overflow = 0; }
     const int64_t plo = unord64(lo), phi = unord64(hi);
     if ((uint64_t)(phi - plo) >= 0xFFFFull) return;  // wide pid range: the int64 path
     for (int64_t j = tid; j < G8; j += 1024) pk[j] = j < G ? (uint16_t)(gp[j] - plo) : (uint16_t)0xFFFF;
@@ -629,7 +631,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
     const float* __restrict__ dist, int64_t G, int64_t ld, const int64_t* __restrict__ qp,
     const int64_t* __restrict__ gp, const int64_t* __restrict__ qc, const int64_t* __restrict__ gc,
     const unsigned long long* __restrict__ mm, const uint16_t* __restrict__ pk, int32_t* __restrict__ valid,
-    int64_t* __restrict__ first, double* __restrict__ ap, int64_t* __restrict__ nkept) {
+    int64_t* __restrict__ first, double* __restrict__ ap, int64_t* __restrict__ nkept, int32_t* __restrict__ large) {
     __shared__ float pv[EVW_MAXP];
     __shared__ int pi[EVW_MAXP];
     __shared__ int hist[EVW_MAXP + 1];
@@ -735,7 +737,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
     t1 = __builtin_amdgcn_s_memtime();
 #endif
     if (ns > SCAP || m > EVW_MAXP || nj > EVW_MAXJ) {  // eval_rows_kernel (large lists) takes it
-        if (tid == 0) valid[q] = 2;
+        if (tid == 0) {
+            valid[q] = 2;
+            *large = 1;
+        }
         return;
     }
     if (tid == 0) nkept[q] = G - nj;
@@ -895,10 +900,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
 constexpr int EV_MAXP = 2048;
 
 // Fallback for the queries eval_rows_wg_kernel left (valid == 2: more than EVW_MAXP
-// positives or EVW_MAXJ junk items): one workgroup per query, up to EV_MAXP positives.
-// Positives are collected and sorted; every other kept gallery item is binned by how many
-// positives precede it (binary search).  Queries beyond EV_MAXP set *overflow and
-// valid = -1 (the host refuses to aggregate them).
+// positives or EVW_MAXJ junk items): one workgroup per query, up to EV_MAXP positives in
+// LDS.  Positives are collected and sorted; every other kept gallery item is binned by how
+// many positives precede it (binary search).  A query with more positives than that is
+// marked valid = 3 and evaluated by the kernel's LAST workgroup to finish, with the same
+// code on scratch arrays in the call's workspace sized for the whole gallery (EvScratch):
+// no capacity limit, as in the reference.
 struct EvLargeLds {
     float pv[EV_MAXP];
     int pi[EV_MAXP];
@@ -909,16 +916,26 @@ struct EvLargeLds {
     PwFrame pw[PW_DEPTH];
 };
 
-__device__ void eval_row_large(int64_t q, const float* __restrict__ dist, int64_t G, int64_t ld,
+struct EvScratch {  // arrays of the large-list evaluation (LDS, or global memory)
+    float* pv;
+    int* pi;
+    int* hist;
+    int64_t* rk;
+    double* rv;
+    int64_t cap;  // positives the arrays hold (pv / pi hold pow2_ceil(cap))
+};
+
+// returns false (and sets nothing) when the query has more than S.cap positives
+__device__ bool eval_row_large(int64_t q, const float* __restrict__ dist, int64_t G, int64_t ld,
                                const int64_t* __restrict__ qp, const int64_t* __restrict__ gp,
                                const int64_t* __restrict__ qc, const int64_t* __restrict__ gc,
                                int32_t* __restrict__ valid, int64_t* __restrict__ first, double* __restrict__ ap,
-                               int64_t* __restrict__ nkept, int32_t* __restrict__ overflow, EvLargeLds& L) {
-    float* pv = L.pv;
-    int* pi = L.pi;
-    int* hist = L.hist;
-    int64_t* rk = L.rk;
-    double* rv = L.rv;
+                               int64_t* __restrict__ nkept, const EvScratch& S, EvLargeLds& L) {
+    float* pv = S.pv;
+    int* pi = S.pi;
+    int* hist = S.hist;
+    int64_t* rk = S.rk;
+    double* rv = S.rv;
     int& s_m = L.s_m;
     int& s_junk = L.s_junk;
     PwFrame* pw = L.pw;
@@ -931,16 +948,13 @@ __device__ void eval_row_large(int64_t q, const float* __restrict__ dist, int64_
             if (gc[j] == qcam) atomicAdd(&s_junk, 1);
             else {
                 int p = atomicAdd(&s_m, 1);
-                if (p < EV_MAXP) { pv[p] = row[j]; pi[p] = (int)j; }
+                if (p < S.cap) { pv[p] = row[j]; pi[p] = (int)j; }
             }
         }
     }
     __syncthreads();
     const int m = s_m;
-    if (m > EV_MAXP) {
-        if (threadIdx.x == 0) { atomicExch(overflow, 1); valid[q] = -1; first[q] = -1; ap[q] = 0.0; nkept[q] = G - s_junk; }
-        return;
-    }
+    if (m > S.cap) return false;
     const int P = pow2_ceil(m < 2 ? 2 : m);
     for (int t = m + threadIdx.x; t < P; t += blockDim.x) { pv[t] = __builtin_inff(); pi[t] = 0x7fffffff; }
     for (int t = threadIdx.x; t <= m; t += blockDim.x) hist[t] = 0;
@@ -970,18 +984,57 @@ __device__ void eval_row_large(int64_t q, const float* __restrict__ dist, int64_
         first[q] = rk[0];
         ap[q] = pairwise_sparse([&](int t) { return rk[t]; }, [&](int t) { return rv[t]; }, m, n, pw) / (double)m;
     }
+    __syncthreads();
+    return true;
 }
 
-// Grid-stride over the queries (a few workgroups per CU instead of one launch-slot per query).
+// Grid-stride over the queries (a few workgroups per CU instead of one launch-slot per query);
+// the last workgroup to finish takes the queries marked valid = 3.  A workgroup that marked
+// one counts it (hugecount) and issues a release fence before its arrival; the last arrival
+// issues an acquire fence and, only when the count is non-zero, scans valid[] in parallel —
+// nothing of this runs unless eval_rows_wg_kernel deferred a query (*large).
 __global__ __launch_bounds__(256) void eval_rows_kernel(
     const float* __restrict__ dist, int64_t Q, int64_t G, int64_t ld, const int64_t* __restrict__ qp,
     const int64_t* __restrict__ gp, const int64_t* __restrict__ qc, const int64_t* __restrict__ gc,
     int32_t* __restrict__ valid, int64_t* __restrict__ first, double* __restrict__ ap,
-    int64_t* __restrict__ nkept, int32_t* __restrict__ overflow) {
+    int64_t* __restrict__ nkept, const int32_t* __restrict__ large, unsigned int* __restrict__ arrivals,
+    unsigned int* __restrict__ hugecount, EvScratch huge) {
+    if (*large == 0) return;  // no query left for this kernel (the common case: one load per workgroup)
     __shared__ EvLargeLds L;
+    __shared__ int s_last, s_mark;
+    __shared__ unsigned int s_cnt;
+    const EvScratch lds{L.pv, L.pi, L.hist, L.rk, L.rv, EV_MAXP};
+    if (threadIdx.x == 0) s_mark = 0;
+    __syncthreads();
     for (int64_t q = blockIdx.x; q < Q; q += gridDim.x) {
         if (valid[q] != 2) continue;  // uniform per workgroup
-        eval_row_large(q, dist, G, ld, qp, gp, qc, gc, valid, first, ap, nkept, overflow, L);
+        if (!eval_row_large(q, dist, G, ld, qp, gp, qc, gc, valid, first, ap, nkept, lds, L) && threadIdx.x == 0) {
+            valid[q] = 3;
+            s_mark = 1;
+            atomicAdd(hugecount, 1u);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        if (s_mark) __threadfence();
+        const unsigned int prev = __hip_atomic_fetch_add(arrivals, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = prev == gridDim.x - 1;
+        s_cnt = 0;
+        if (s_last) {
+            __threadfence();
+            s_cnt = __hip_atomic_load(hugecount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    __syncthreads();
+    if (!s_last || s_cnt == 0) return;
+    __shared__ int flag[256];
+    for (int64_t q0 = 0; q0 < Q; q0 += blockDim.x) {
+        const int64_t q = q0 + threadIdx.x;
+        const bool h = q < Q && valid[q] == 3;
+        flag[threadIdx.x] = h;
+        if (!__syncthreads_or(h)) continue;
+        for (int t = 0; t < (int)blockDim.x; t++)
+            if (flag[t]) eval_row_large(q0 + t, dist, G, ld, qp, gp, qc, gc, valid, first, ap, nkept, huge, L);
         __syncthreads();
     }
 }
@@ -1101,7 +1154,20 @@ REIDMI_API int reidmi_topk_rows_f32(const float* x, int64_t rows, int64_t cols, 
     return topk_launch(x, rows, cols, ldx, row_div, k, out_idx, out_val, ldo, (hipStream_t)stream);
 }
 
-static int64_t ev_ws_bytes(int64_t G) { return 256 + ((G + 7) / 8 * 8) * 2; }
+// workspace: [0, 256) min/max + arrival counter | packed labels (G8 uint16) | large-list
+// scratch for one query of up to G positives: pv, pi (pow2_ceil(G) each), hist (G + 1),
+// rk, rv (G each)
+static int64_t ev_pow2(int64_t G) {
+    int64_t p = 2;
+    while (p < G) p <<= 1;
+    return p;
+}
+static int64_t ev_lab_bytes(int64_t G) { return ((G + 7) / 8 * 8) * 2; }
+static int64_t ev_huge_off(int64_t G) { return (256 + ev_lab_bytes(G) + 15) / 16 * 16; }
+static int64_t ev_ws_bytes(int64_t G) {
+    const int64_t P2 = ev_pow2(G);
+    return ev_huge_off(G) + P2 * 8 + ((G + 1) * 4 + 7) / 8 * 8 + G * 16;
+}
 
 REIDMI_API int64_t reidmi_eval_rows_workspace_bytes(int64_t G) { return G > 0 ? ev_ws_bytes(G) : -1; }
 
@@ -1134,10 +1200,23 @@ REIDMI_API int reidmi_eval_rows(const float* dist, int64_t Q, int64_t G, int64_t
         RM_LAUNCHED();
     }
     hipLaunchKernelGGL(eval_rows_wg_kernel, dim3((unsigned)Q), dim3(256), 0, s, dist, G, ldd, q_pids, g_pids, q_cams,
-                       g_cams, (const unsigned long long*)mm, (const uint16_t*)pk, valid, first, ap, nkept);
+                       g_cams, (const unsigned long long*)mm, (const uint16_t*)pk, valid, first, ap, nkept,
+                       (int32_t*)(mm + 3));
     RM_LAUNCHED();
+    EvScratch huge{};
+    {
+        char* h = (char*)ws_ + ev_huge_off(G);
+        const int64_t P2 = ev_pow2(G);
+        huge.pv = (float*)h;
+        huge.pi = (int*)(h + P2 * 4);
+        huge.hist = (int*)(h + P2 * 8);
+        huge.rk = (int64_t*)(h + P2 * 8 + ((G + 1) * 4 + 7) / 8 * 8);
+        huge.rv = (double*)((char*)huge.rk + G * 8);
+        huge.cap = G;
+    }
     hipLaunchKernelGGL(eval_rows_kernel, dim3((unsigned)std::min<int64_t>(Q, 512)), dim3(256), 0, s, dist, Q, G, ldd,
-                       q_pids, g_pids, q_cams, g_cams, valid, first, ap, nkept, overflow);
+                       q_pids, g_pids, q_cams, g_cams, valid, first, ap, nkept, (const int32_t*)(mm + 3),
+                       (unsigned int*)(mm + 2), (unsigned int*)(mm + 2) + 1, huge);
     RM_LAUNCHED();
     return OK;
 }

@@ -74,8 +74,9 @@ def topk_rows_device(x, k, row_div=None, with_values=False):
 
 
 def eval_rows_device(dist, q_pids, g_pids, q_camids, g_camids):
-    """Per-query (valid, first_match_rank, AP, n_kept) for eval_func (evaluate.py:40-80);
-    valid = -1 marks a query beyond the kernel's positive-list capacity (aggregate refuses it)."""
+    """Per-query (valid, first_match_rank, AP, n_kept) for eval_func (evaluate.py:40-80), any
+    number of positives per query.  (valid = -1 / overflow = 1 were a capacity signal of older
+    builds; aggregate_cmc_map still refuses them.)"""
     dist = _as_dev_f32(dist)
     Q, G = dist.shape
     qp, gp, qc, gc = (_as_dev_i64(a) for a in (q_pids, g_pids, q_camids, g_camids))
@@ -98,7 +99,7 @@ def aggregate_cmc_map(valid, first, ap, nkept, num_g, max_rank=50, overflow=None
     valid = np.asarray(valid)
     if (overflow is not None and int(np.asarray(overflow).reshape(-1)[0])) or \
             (valid.dtype != bool and (valid < 0).any()):
-        raise _lib.ReidmiError("eval_rows: a query has more than 2048 positives (kernel capacity)")
+        raise _lib.ReidmiError("eval_rows: a query was not evaluated (overflow flag or valid < 0)")
     valid = valid > 0
     first, ap, nkept = np.asarray(first), np.asarray(ap), np.asarray(nkept)
     if num_g < max_rank:

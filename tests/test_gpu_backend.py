@@ -160,6 +160,32 @@ def test_eval_many_positives_and_junk_vs_oracle(gpu, G, pid_shift, pid_scale):
         assert np.array_equal(a.astype(b.dtype), b)
 
 
+@pytest.mark.parametrize("G,pid_shift", [(6007, 0), (9001, -(1 << 40))])
+def test_eval_beyond_lds_lists_vs_oracle(gpu, G, pid_shift):
+    """Queries with more positives than the large-list kernel's LDS holds (> 2048) are
+    evaluated by its last workgroup on workspace scratch: no capacity limit, as in the
+    reference (evaluate.py:40-80).  Bit-exact against the oracle, overflow stays 0."""
+    r = np.random.default_rng(G)
+    Q = 5
+    gp = r.integers(1, 3, G).astype(np.int64)  # pids 1..2: ~G/2 items each
+    gc = r.integers(0, 2, G).astype(np.int64)
+    gp[::11] = 9
+    qp = (np.array([1, 2, 1, 9, 4], np.int64) + pid_shift)
+    gp = gp + pid_shift
+    qc = np.array([0, 1, 3, 0, 0], np.int64)
+    dist = (np.round(r.random((Q, G)) * 256) / 256).astype(np.float32)
+    ev = _ev()
+    d = torch.from_numpy(dist).cuda()
+    v, f, a, n, o = ev.eval_rows_device(d, qp, gp, qc, gc)
+    assert int(o.cpu()[0]) == 0
+    ref = oracle.eval_rows(dist, qp, gp, qc, gc)
+    for a_, b_ in zip((v, f, a, n), ref):
+        assert np.array_equal(a_.cpu().numpy().astype(b_.dtype), b_)
+    cmc, mAP = ev.eval_func(dist, qp, gp, qc, gc, max_rank=50)
+    ocmc, omap = oracle.eval_func(dist, qp, gp, qc, gc, 50)
+    assert np.array_equal(cmc, ocmc) and mAP == omap
+
+
 def test_eval_edge_cases(gpu):
     ev = _ev()
     r = np.random.default_rng(3)
