@@ -533,14 +533,16 @@ def main():
             line["msmt17"] = ms17
         line["backend"] = backend_rooflines(wl)
         line["preprocess"] = preprocess_leg(dev)
+        # host-side baselines at N = 1 only (the other ranks would idle at the final barrier)
+        cpu = not a.no_cpu_baseline and world == 1
         if not a.no_jpeg:
-            line["jpeg"] = jpeg_leg(dev, cpu=not a.no_cpu_baseline)
+            line["jpeg"] = jpeg_leg(dev, cpu=cpu)
         threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
         if not a.no_rerank:
-            line["rerank"] = rerank_leg(dev, cpu=not a.no_cpu_baseline, threads=threads)
+            line["rerank"] = rerank_leg(dev, cpu=cpu, threads=threads)
         if not a.no_text:
-            line["text"] = text_leg(dev, cpu=not a.no_cpu_baseline, threads=threads)
-        if not a.no_cpu_baseline:
+            line["text"] = text_leg(dev, cpu=cpu, threads=threads)
+        if cpu:
             line["cpu_baseline"] = cpu_baseline(wl, threads)
         print(json.dumps(line))
     if world > 1:
