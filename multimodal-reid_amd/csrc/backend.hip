@@ -101,16 +101,27 @@ __global__ __launch_bounds__(256) void distmat_f32_kernel(
             }
 }
 
-// Pipelined variant (D, ldq, ldg multiples of 4, 16-byte aligned rows): K-step 32, two LDS
-// stages, the next K-step's operands loaded as coalesced float4 (8 lanes per 128-byte row
-// segment) into registers while the current one is multiplied, one barrier per K-step.
+// Pipelined variant (D, ldq, ldg multiples of 4, 16-byte aligned rows): K-step DM2_BK, two
+// LDS stages, the next K-step's operands loaded as coalesced float4 into registers while the
+// current one is multiplied, one barrier per K-step.
 // LDS rows padded by 1 dword so the transposed scalar stores are conflict-free.  The MFMA
 // sequence per output (k pairs ascending on v_mfma_f32_32x32x2_f32) is the one above, so the
 // result is bit-identical to distmat_f32_kernel (and to the oracle's fmaf chain).
-constexpr int DM2_BK = 32, DM2_LD = DM_BM + 1;
+// K-step 16 (33 KB of LDS, 112 VGPRs): four workgroups per CU; K-step 32 ran two (66 KB) and
+// was 5 % slower at MSMT17 / re-rank-chunk sizes (profiles/r02/distmat_kstep_ab.txt).  The
+// macros are A/B hooks for tools/build_variant.py.
+#ifndef DM2_BK_
+#define DM2_BK_ 16
+#endif
+#ifndef DM2_MINWG_
+#define DM2_MINWG_ 4
+#endif
+constexpr int DM2_BK = DM2_BK_, DM2_LD = DM_BM + 1;
+constexpr int DM2_F4 = DM2_BK / 4;            // float4 per operand row and K-step
+constexpr int DM2_U = DM_BM * DM2_F4 / 256;   // float4 staging slots per thread and operand
 
 template <bool COSINE>
-__global__ __launch_bounds__(256, 2) void distmat2_f32_kernel(
+__global__ __launch_bounds__(256, DM2_MINWG_) void distmat2_f32_kernel(
     const float* __restrict__ q, const float* __restrict__ g, const float* __restrict__ qq,
     const float* __restrict__ gg, int64_t Q, int64_t G, int64_t D, int64_t ldq, int64_t ldg,
     float* __restrict__ out, int64_t ldo) {
@@ -126,25 +137,25 @@ __global__ __launch_bounds__(256, 2) void distmat2_f32_kernel(
     const int64_t bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
     const int64_t wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
     const int64_t bm = (wg % tiles_m) * DM_BM, bn = (wg / tiles_m) * DM_BN;
-    // staging slots: float4 f = tid + 256u -> row f >> 3, k group (f & 7) * 4
-    const float* pa[4];
-    const float* pb[4];
-    bool va[4], vb[4];
-    int srow[4], sk[4];
+    // staging slots: float4 f = tid + 256u -> row f / DM2_F4, k group (f % DM2_F4) * 4
+    const float* pa[DM2_U];
+    const float* pb[DM2_U];
+    bool va[DM2_U], vb[DM2_U];
+    int srow[DM2_U], sk[DM2_U];
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
+    for (int u = 0; u < DM2_U; u++) {
         const int f = tid + 256 * u;
-        srow[u] = f >> 3;
-        sk[u] = (f & 7) * 4;
+        srow[u] = f / DM2_F4;
+        sk[u] = (f % DM2_F4) * 4;
         va[u] = bm + srow[u] < Q;
         vb[u] = bn + srow[u] < G;
         pa[u] = q + (va[u] ? bm + srow[u] : 0) * ldq + sk[u];
         pb[u] = g + (vb[u] ? bn + srow[u] : 0) * ldg + sk[u];
     }
-    float4 ra[4], rb[4];
+    float4 ra[DM2_U], rb[DM2_U];
     auto gload = [&](int64_t k0) {
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < DM2_U; u++) {
             const bool kin = k0 + sk[u] < D;  // D % 4 == 0: a float4 is wholly in or out
             ra[u] = va[u] && kin ? *(const float4*)(pa[u] + k0) : make_float4(0.f, 0.f, 0.f, 0.f);
             rb[u] = vb[u] && kin ? *(const float4*)(pb[u] + k0) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -152,7 +163,7 @@ __global__ __launch_bounds__(256, 2) void distmat2_f32_kernel(
     };
     auto lstore = [&](int st) {
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < DM2_U; u++) {
             sA[st][sk[u] + 0][srow[u]] = ra[u].x;
             sA[st][sk[u] + 1][srow[u]] = ra[u].y;
             sA[st][sk[u] + 2][srow[u]] = ra[u].z;
