@@ -129,6 +129,10 @@ int reidmi_rr_jaccard_rows(const float* feat, int64_t N, int64_t D, int64_t ldf,
                            const int32_t* qcol, const uint16_t* qval, const int64_t* coff, const int32_t* irow,
                            const uint16_t* ival, uint16_t one_minus_lambda_h, float lambda_f, float* out, int64_t ldo,
                            float* chunk, int64_t chunk_rows, void* stream);
+/* Rows (of N-Q floats each) at the end of reidmi_rr_jaccard_rows' `chunk` scratch that the call
+ * keeps for the per-column chunk bounds of the inverted lists; chunk_rows must exceed it (the
+ * distance rows per pass are chunk_rows minus this). */
+int64_t reidmi_rr_jaccard_reserved_rows(int64_t N, int64_t G);
 
 /* ------------------------------------------------------------------ encoders */
 

@@ -18,6 +18,9 @@ _f32 = ctypes.c_float
 _u16 = ctypes.c_uint16
 
 # name -> argtypes (all return int status)
+# entry points returning int64 besides the *_bytes sizes
+INT64_RESULT = {"reidmi_rr_jaccard_reserved_rows"}
+
 SIGNATURES = {
     "reidmi_row_sqnorm_f32": [_vp, _i64, _i64, _i64, _vp, _vp],
     "reidmi_l2norm_f32": [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp],
@@ -42,6 +45,7 @@ SIGNATURES = {
     "reidmi_rr_csc": [_i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i64, _vp],
     "reidmi_rr_jaccard_rows": [_vp, _i64, _i64, _i64, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp,
                                _u16, _f32, _vp, _i64, _vp, _i64, _vp],
+    "reidmi_rr_jaccard_reserved_rows": [_i64, _i64],
     "reidmi_attn_lpad": [_i32],
     "reidmi_prof_enable": [_i32],
     "reidmi_gemm_set_tile": [_i32],
@@ -87,7 +91,7 @@ def load():
     for name, args in SIGNATURES.items():
         fn = getattr(L, name)
         fn.argtypes = args
-        fn.restype = _i64 if name.endswith("_bytes") else _i32
+        fn.restype = _i64 if name.endswith("_bytes") or name in INT64_RESULT else _i32
     _LIB = L
     return L
 

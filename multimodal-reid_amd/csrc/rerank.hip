@@ -507,11 +507,33 @@ __global__ __launch_bounds__(256) void csc_sort_kernel(const int64_t* __restrict
 // the chunk's sub-range of each list is found by binary search.  Epilogue: Jaccard in fp16
 // (reranking.py:93), blend with od in fp32 (reranking.py:95), write final[blockIdx.y][r-Q].
 // od of (i, r) = OD[blockIdx.y * ld + (r - odc0)] / rowdiv[i].
+// Chunk boundaries of every column's sorted row list, once per call: cbnd[c * (nch + 1) + b]
+// = first position p in [off[c], off[c+1]) with irow[p] >= Q + b * JCH (b = nch: off[c+1]).
+// jaccard_kernel then reads its slice with two loads instead of two binary searches per
+// (query row, column) — those searches were a serial chain of dependent loads.
+__global__ __launch_bounds__(256) void jaccard_bounds_kernel(const int64_t* __restrict__ off,
+                                                             const int32_t* __restrict__ irow, int64_t N, int64_t Q,
+                                                             int nch, int64_t* __restrict__ cbnd) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= N * (nch + 1)) return;
+    const int64_t c = t / (nch + 1);
+    const int b = (int)(t - c * (nch + 1));
+    int64_t lo = off[c], hi = off[c + 1];
+    if (b < nch) {
+        const int64_t key = Q + (int64_t)b * JCH;
+        while (lo < hi) { const int64_t m = (lo + hi) >> 1; if (irow[m] < key) lo = m + 1; else hi = m; }
+    } else {
+        lo = hi;  // every row index is < N
+    }
+    cbnd[t] = lo;
+}
+
 __global__ __launch_bounds__(256) void jaccard_kernel(const float* __restrict__ OD, int64_t ld, int64_t odc0,
                                                       const float* __restrict__ rowdiv, int64_t q0, int64_t Q,
                                                       int64_t N, Rows Vq, const int64_t* __restrict__ off,
                                                       const int32_t* __restrict__ irow, const uint16_t* __restrict__ ival,
-                                                      uint16_t lam16, float lam_f, float* __restrict__ out, int64_t ldo) {
+                                                      const int64_t* __restrict__ cbnd, uint16_t lam16, float lam_f,
+                                                      float* __restrict__ out, int64_t ldo) {
     __shared__ uint16_t tmin[JCH];
     const int64_t y = blockIdx.y;
     const int64_t i = q0 + y;
@@ -522,18 +544,12 @@ __global__ __launch_bounds__(256) void jaccard_kernel(const float* __restrict__ 
     __syncthreads();
     const int nz = Vq.len(i);
     const int64_t qb = Vq.beg(i);
+    const int nb1 = (int)gridDim.x + 1;
     for (int e = 0; e < nz; e++) {
         const int32_t c = Vq.col[qb + e];
         const float vi = h2f_bits(Vq.val[qb + e]);
-        int64_t p0 = off[c], p1 = off[c + 1];
-        {
-            int64_t lo = p0, hi = p1;
-            while (lo < hi) { const int64_t m = (lo + hi) >> 1; if (irow[m] < base) lo = m + 1; else hi = m; }
-            p0 = lo;
-            hi = p1;
-            while (lo < hi) { const int64_t m = (lo + hi) >> 1; if (irow[m] < end) lo = m + 1; else hi = m; }
-            p1 = lo;
-        }
+        // this chunk's slice of column c's sorted row list (jaccard_bounds_kernel)
+        const int64_t p0 = cbnd[(int64_t)c * nb1 + blockIdx.x], p1 = cbnd[(int64_t)c * nb1 + blockIdx.x + 1];
         for (int64_t p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
             const int k = (int)(irow[p] - base);
             const float vr = h2f_bits(ival[p]);
@@ -860,6 +876,17 @@ REIDMI_API int reidmi_rr_csc(int64_t N, const int64_t* qoff, const int32_t* qcol
     return OK;
 }
 
+// rows of G floats of the jaccard scratch kept for the column chunk bounds (int64 per column
+// and chunk boundary, 16-byte aligned)
+static int64_t jaccard_reserved_rows(int64_t N, int64_t G) {
+    const int64_t nch = (G + JCH - 1) / JCH;
+    return (N * (nch + 1) * 8 + G * 4 - 1) / (G * 4) + 1;
+}
+
+REIDMI_API int64_t reidmi_rr_jaccard_reserved_rows(int64_t N, int64_t G) {
+    return N > 0 && G > 0 ? jaccard_reserved_rows(N, G) : -1;
+}
+
 REIDMI_API int reidmi_rr_jaccard_rows(const float* feat, int64_t N, int64_t D, int64_t ldf, const float* sqn,
                                       const float* rowmax, int64_t Q, int64_t qlo, int64_t qhi, const int64_t* qoff,
                                       const int32_t* qcol, const uint16_t* qval, const int64_t* coff,
@@ -873,6 +900,15 @@ REIDMI_API int reidmi_rr_jaccard_rows(const float* feat, int64_t N, int64_t D, i
     if (qhi == qlo || G == 0) return OK;
     hipStream_t s = (hipStream_t)stream;
     const Rows Vq{qoff, nullptr, 0, qcol, qval};
+    // the column chunk boundaries take the last rows of the distance scratch
+    const int nch = ceil_div(G, JCH);
+    const int64_t steal = jaccard_reserved_rows(N, G);
+    RM_REQUIRE(chunk_rows > steal, "rr_jaccard_rows: chunk_rows must exceed reidmi_rr_jaccard_reserved_rows(N, N-Q)");
+    chunk_rows -= steal;
+    int64_t* cbnd = (int64_t*)(((uintptr_t)(chunk + chunk_rows * G) + 15) & ~(uintptr_t)15);
+    hipLaunchKernelGGL(jaccard_bounds_kernel, dim3(ceil_div(N * (nch + 1), 256)), dim3(256), 0, s, coff, irow, N, Q,
+                       nch, cbnd);
+    RM_LAUNCHED();
     int rc;
     for (int64_t a = qlo; a < qhi; a += chunk_rows) {
         const int64_t nb = qhi - a < chunk_rows ? qhi - a : chunk_rows;
@@ -881,7 +917,7 @@ REIDMI_API int reidmi_rr_jaccard_rows(const float* feat, int64_t N, int64_t D, i
             return rc;
         dim3 grid(ceil_div(G, JCH), (unsigned)nb);
         hipLaunchKernelGGL(jaccard_kernel, grid, dim3(256), 0, s, (const float*)chunk, G, Q, rowmax, a, Q, N, Vq, coff,
-                           irow, ival, one_minus_lambda_h, lambda_f, out + (a - qlo) * ldo, ldo);
+                           irow, ival, (const int64_t*)cbnd, one_minus_lambda_h, lambda_f, out + (a - qlo) * ldo, ldo);
         RM_LAUNCHED();
     }
     return OK;

@@ -166,7 +166,9 @@ class HipStages:
         del ws
         out = torch.empty((qhi - qlo, G), device=self.dev, dtype=torch.float32)
         if qhi > qlo and G > 0:
-            cr = int(max(1, min(65535, qhi - qlo, self.chunk_rows * N // max(G, 1))))
+            # distance rows per pass + the rows the call keeps for its column chunk bounds
+            extra = int(_lib.load().reidmi_rr_jaccard_reserved_rows(N, G))
+            cr = int(max(1, min(65535 - extra, qhi - qlo, self.chunk_rows * N // max(G, 1)))) + extra
             _lib.call("reidmi_rr_jaccard_rows", _lib.ptr(self.feat), N, self.D, self.D, _lib.ptr(self.sqn),
                       _lib.ptr(rmax), Q, qlo, qhi, _lib.ptr(off), _lib.ptr(col), _lib.ptr(val), _lib.ptr(coff),
                       _lib.ptr(irow), _lib.ptr(ival), self.lam_h, self.lam_f, _lib.ptr(out), G,

@@ -26,7 +26,7 @@ def open_lib(path):
     for name, args in L.SIGNATURES.items():
         fn = getattr(lib, name)
         fn.argtypes = args
-        fn.restype = ctypes.c_int64 if name.endswith("_bytes") else ctypes.c_int32
+        fn.restype = ctypes.c_int64 if name.endswith("_bytes") or name in L.INT64_RESULT else ctypes.c_int32
     return lib
 
 
