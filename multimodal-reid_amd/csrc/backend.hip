@@ -120,7 +120,7 @@ constexpr int DM2_BK = DM2_BK_, DM2_LD = DM_BM + 1;
 constexpr int DM2_F4 = DM2_BK / 4;            // float4 per operand row and K-step
 constexpr int DM2_U = DM_BM * DM2_F4 / 256;   // float4 staging slots per thread and operand
 
-template <bool COSINE>
+template <bool COSINE, bool SYM = false>
 __global__ __launch_bounds__(256, DM2_MINWG_) void distmat2_f32_kernel(
     const float* __restrict__ q, const float* __restrict__ g, const float* __restrict__ qq,
     const float* __restrict__ gg, int64_t Q, int64_t G, int64_t D, int64_t ldq, int64_t ldg,
@@ -136,7 +136,21 @@ __global__ __launch_bounds__(256, DM2_MINWG_) void distmat2_f32_kernel(
     const int64_t nwg = (int64_t)gridDim.x;
     const int64_t bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
     const int64_t wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-    const int64_t bm = (wg % tiles_m) * DM_BM, bn = (wg / tiles_m) * DM_BN;
+    int64_t bm, bn;
+    if constexpr (SYM) {
+        // the self-distance of one row set (q == g): tiles (tm, tn) with tm <= tn only, column
+        // panel tn holding tiles 0..tn (tn (tn + 1) / 2 tiles before it); the epilogue also
+        // writes the mirrored tile.  Bit-for-bit symmetric: fma(a, b, c) == fma(b, a, c) in
+        // every step of the chain, and qq[i] + gg[j] == qq[j] + gg[i] (same array).
+        int64_t tn = (int64_t)((__builtin_sqrt(8.0 * (double)wg + 1.0) - 1.0) * 0.5);
+        while ((tn + 1) * (tn + 2) / 2 <= wg) tn++;
+        while (tn * (tn + 1) / 2 > wg) tn--;
+        bm = (wg - tn * (tn + 1) / 2) * DM_BM;
+        bn = tn * DM_BN;
+    } else {
+        bm = (wg % tiles_m) * DM_BM;
+        bn = (wg / tiles_m) * DM_BN;
+    }
     // staging slots: float4 f = tid + 256u -> row f / DM2_F4, k group (f % DM2_F4) * 4
     const float* pa[DM2_U];
     const float* pb[DM2_U];
@@ -214,7 +228,9 @@ __global__ __launch_bounds__(256, DM2_MINWG_) void distmat2_f32_kernel(
                         const float c = acc[mt][nt][r] * (1.0f / (__builtin_sqrtf(qq[i]) * __builtin_sqrtf(gg[j])));
                         out[i * ldo + j] = acosf(fminf(fmaxf(c, -1.0f + 1e-5f), 1.0f - 1e-5f));
                     } else {
-                        out[i * ldo + j] = __builtin_fmaf(-2.0f, acc[mt][nt][r], qq[i] + gg[j]);
+                        const float v = __builtin_fmaf(-2.0f, acc[mt][nt][r], qq[i] + gg[j]);
+                        out[i * ldo + j] = v;
+                        if (SYM && bm != bn) out[j * ldo + i] = v;  // the mirrored tile
                     }
                 }
             }
@@ -222,6 +238,31 @@ __global__ __launch_bounds__(256, DM2_MINWG_) void distmat2_f32_kernel(
 
 int g_dm_variant = 0;
 static int distmat_variant() { return g_dm_variant; }
+
+static bool dm2_ok(const float* q, int64_t ldq, const float* g, int64_t ldg, int64_t D);
+
+// Self-distance of x [N][D] (the one-call re-rank's N x N matrix, reranking.py:36-44): the
+// upper-triangle tiles and their mirror images, half the FLOPs of distmat_launch(x, x), same
+// bits.  ws: N floats.
+int distmat_self_launch(const float* x, int64_t N, int64_t ldx, int64_t D, float* out, int64_t ldo, float* ws,
+                        hipStream_t s) {
+    RM_REQUIRE(N > 0 && D > 0 && ldx >= D && ldo >= N && ws != nullptr, "distmat_self: bad shape");
+    hipLaunchKernelGGL(row_sqnorm_kernel, dim3(ceil_div(N, 256)), dim3(256), 0, s, x, N, D, ldx, ws);
+    RM_LAUNCHED();
+    if (!dm2_ok(x, ldx, x, ldx, D) || distmat_variant() == 1) {
+        dim3 grid(ceil_div(N, DM_BN), ceil_div(N, DM_BM));
+        RM_REQUIRE(grid.y <= 65535, "distmat: too many query rows for one launch");
+        hipLaunchKernelGGL(distmat_f32_kernel<false>, grid, dim3(256), 0, s, x, x, ws, ws, N, N, D, ldx, ldx, out, ldo);
+    } else {
+        const int64_t T = (N + DM_BM - 1) / DM_BM;
+        const int64_t tiles = T * (T + 1) / 2;
+        RM_REQUIRE(tiles < (1ll << 31), "distmat_self: too many tiles");
+        hipLaunchKernelGGL((distmat2_f32_kernel<false, true>), dim3((unsigned)tiles), dim3(256), 0, s, x, x, ws, ws, N, N,
+                           D, ldx, ldx, out, ldo);
+    }
+    RM_LAUNCHED();
+    return OK;
+}
 
 static bool dm2_ok(const float* q, int64_t ldq, const float* g, int64_t ldg, int64_t D) {
     return D % 4 == 0 && ldq % 4 == 0 && ldg % 4 == 0 && ((uintptr_t)q & 15) == 0 && ((uintptr_t)g & 15) == 0;

@@ -22,6 +22,8 @@ namespace reidmi {
 
 int topk_launch(const float* x, int64_t rows, int64_t cols, int64_t ldx, const float* row_div, int k,
                 int32_t* out_idx, float* out_val, int64_t ldo, hipStream_t s);
+int distmat_self_launch(const float* x, int64_t N, int64_t ldx, int64_t D, float* out, int64_t ldo, float* ws,
+                        hipStream_t s);
 int distmat_launch(const float* q, int64_t Q, int64_t ldq, const float* g, int64_t G, int64_t ldg, int64_t D,
                    float* out, int64_t ldo, float* ws, hipStream_t s);
 int distmat_pre_launch(const float* q, int64_t Q, int64_t ldq, const float* g, int64_t G, int64_t ldg, int64_t D,
@@ -731,8 +733,9 @@ REIDMI_API int reidmi_rerank(const float* feat, int64_t Q, int64_t G, int64_t D,
     char* ws = (char*)ws_;
     float* Dm = (float*)(ws + P.dist);
     int rc;
-    // R1: exact-fp32 distance over cat(q, g); symmetric bit-for-bit, so od rows = D rows
-    if ((rc = distmat_launch(feat, N, ldf, feat, N, ldf, D, Dm, N, Dm + N * N, s))) return rc;
+    // R1: exact-fp32 distance over cat(q, g); symmetric bit-for-bit (computed as the upper
+    // triangle + its mirror), so od rows = D rows
+    if ((rc = distmat_self_launch(feat, N, ldf, D, Dm, N, Dm + N * N, s))) return rc;
     return rerank_core(Dm, N, Q, k1, k2, one_minus_lambda_h, lambda_f, final_dist, ldo, ws, P, flags, s);
 }
 
