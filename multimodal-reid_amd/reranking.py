@@ -82,7 +82,7 @@ def re_ranking(probFea, galFea, k1, k2, lambda_value, local_distmat=None, only_l
 class HipStages:
     """The product's stage kernels (libreidmi)."""
 
-    def __init__(self, feat, num_query, k1, k2, lambda_value, chunk_bytes=2 << 30):
+    def __init__(self, feat, num_query, k1, k2, lambda_value, chunk_bytes=8 << 30):
         _lib.require_cuda(feat)
         self.feat = _as_dev_f32(feat).contiguous()
         self.N, self.D = self.feat.shape
@@ -94,7 +94,10 @@ class HipStages:
         self.st = _lib.stream()
         self.sqn = torch.empty(self.N, device=self.dev, dtype=torch.float32)
         _lib.call("reidmi_row_sqnorm_f32", _lib.ptr(self.feat), self.N, self.D, self.D, _lib.ptr(self.sqn), self.st)
-        self.chunk_rows = int(max(1, min(65535, chunk_bytes // (4 * self.N))))
+        # distance rows per pass: whole 128-row tiles of the distance kernel when possible (a
+        # ragged last tile of every pass costs up to a tile's FLOPs per pass at 1M items)
+        rows = int(max(1, min(65535, chunk_bytes // (4 * self.N))))
+        self.chunk_rows = rows // 128 * 128 if rows >= 128 else rows
         self._chunk = None
         self.flags = torch.zeros(1, device=self.dev, dtype=torch.int32)
         vc, qc = ctypes.c_int(), ctypes.c_int()
@@ -207,7 +210,7 @@ def staged_rerank(stages, N, Q):
     return out
 
 
-def re_ranking_sharded(probFea, galFea, k1, k2, lambda_value, chunk_bytes=2 << 30):
+def re_ranking_sharded(probFea, galFea, k1, k2, lambda_value, chunk_bytes=8 << 30):
     """Sharded re_ranking: probFea / galFea are the FULL query and gallery features on this
     rank's GPU (all-gathered after a sharded embed).  Returns this rank's query rows
     shard(Q, rank, W) of the re-ranked (Q, G) distance as a device tensor; with one process
