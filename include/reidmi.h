@@ -106,6 +106,17 @@ int reidmi_rr_rank_rows(const float* feat, int64_t N, int64_t D, int64_t ldf, co
                         int K, int32_t* rank_out, float* rowmax_out, float* chunk, int64_t chunk_rows, void* stream);
 /* R3 (reranking.py:51-71): V rows lo..hi (ELL [hi-lo][vcap]) from the full rank[N][K] and
  * rowmax[N]; distance entries recomputed from feat with the distance kernel's arithmetic. */
+/* fp16 copy of the features for reidmi_rr_rank_rows_f16: [Np][Dp] zero-padded (Np % 256 == 0,
+ * Dp % 64 == 0); *range_ok (device int32, set to 1 by the caller) is cleared when some |x| > 2^15
+ * or is not finite, and the pre-filter must then not be used. */
+int reidmi_rr_feat16(const float* feat, int64_t N, int64_t D, int64_t ldf, void* feat16, int64_t Np, int64_t Dp,
+                     int32_t* range_ok, void* stream);
+/* reidmi_rr_rank_rows with an fp16 MFMA pre-filter (same rank_out / rowmax_out bits): the fp16
+ * product bounds every exact distance (error bound in backend.hip rank_select_kernel); only the
+ * candidates are recomputed with the exact fp32 chain.  nrm = sqrt(sqn); chunk [chunk_rows][Np]. */
+int reidmi_rr_rank_rows_f16(const float* feat, int64_t N, int64_t D, int64_t ldf, const float* sqn, const float* nrm,
+                            const void* feat16, int64_t Np, int64_t Dp, int64_t lo, int64_t hi, int K,
+                            int32_t* rank_out, float* rowmax_out, float* chunk, int64_t chunk_rows, void* stream);
 int reidmi_rr_v_rows(const float* feat, int64_t N, int64_t D, int64_t ldf, const float* sqn, const float* rowmax,
                      const int32_t* rank, int K, int64_t lo, int64_t hi, int k1, int32_t* vcol, uint16_t* vval,
                      int32_t* vnnz, int32_t* flags, void* stream);

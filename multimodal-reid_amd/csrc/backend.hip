@@ -11,6 +11,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <cmath>
 
 namespace reidmi {
 
@@ -305,59 +306,230 @@ __device__ __forceinline__ int pow2_ceil(int n) {
 // divisor implements reranking.py:46 (od[i,:] = D[i,:] / colmax[i] for symmetric D).
 constexpr int TK_CAP = 2048, TK_CHUNK = 1024;
 
-__global__ __launch_bounds__(256) void topk_rows_kernel(const float* __restrict__ x, int64_t cols, int64_t ld,
-                                                        const float* __restrict__ row_div, int K,
-                                                        int32_t* __restrict__ out_idx, float* __restrict__ out_val,
-                                                        int64_t ldo) {
-    __shared__ float sv[TK_CAP];
-    __shared__ int si[TK_CAP];
-    __shared__ int s_cnt, s_nsel;
-    __shared__ float s_tv;
-    __shared__ int s_ti;
-    const int64_t row = blockIdx.x;
-    const float* base = x + row * ld;
-    const bool has_div = row_div != nullptr;
-    const float dv = has_div ? row_div[row] : 1.0f;
-    if (threadIdx.x == 0) { s_cnt = 0; s_nsel = 0; s_tv = __builtin_inff(); s_ti = 0x7fffffff; }
+struct TkLds {
+    float sv[TK_CAP];
+    int si[TK_CAP];
+    int s_cnt, s_nsel;
+    float s_tv;
+    int s_ti;
+};
+
+// The selection of one row by the whole workgroup: afterwards L.sv / L.si [0, min(K, cols))
+// hold the K smallest (val(j), j) in ascending (value, index) order.
+template <typename VAL>
+__device__ void topk_row_dev(VAL val, int64_t cols, int K, TkLds& L) {
+    if (threadIdx.x == 0) { L.s_cnt = 0; L.s_nsel = 0; L.s_tv = __builtin_inff(); L.s_ti = 0x7fffffff; }
     __syncthreads();
     for (int64_t c0 = 0; c0 < cols; c0 += TK_CHUNK) {
-        const float tv = s_tv;
-        const int ti = s_ti, nsel = s_nsel;
+        const float tv = L.s_tv;
+        const int ti = L.s_ti, nsel = L.s_nsel;
 #pragma unroll
         for (int u = 0; u < TK_CHUNK / 256; u++) {
             int64_t j = c0 + u * 256 + threadIdx.x;
             if (j < cols) {
-                float v = base[j];
-                if (has_div) v = v / dv;
+                const float v = val(j);
                 if (key_less(v, (int)j, tv, ti)) {
-                    int p = atomicAdd(&s_cnt, 1);
-                    sv[nsel + p] = v;
-                    si[nsel + p] = (int)j;
+                    int p = atomicAdd(&L.s_cnt, 1);
+                    L.sv[nsel + p] = v;
+                    L.si[nsel + p] = (int)j;
                 }
             }
         }
         __syncthreads();
         const bool last = c0 + TK_CHUNK >= cols;
-        const int n = s_nsel + s_cnt;
+        const int n = L.s_nsel + L.s_cnt;
         __syncthreads();  // every thread has read s_cnt before anyone appends again
         if (last || n > TK_CAP - TK_CHUNK) {
             const int P = pow2_ceil(n < 2 ? 2 : n);
-            for (int t = n + threadIdx.x; t < P; t += blockDim.x) { sv[t] = __builtin_inff(); si[t] = 0x7fffffff; }
+            for (int t = n + threadIdx.x; t < P; t += blockDim.x) { L.sv[t] = __builtin_inff(); L.si[t] = 0x7fffffff; }
             __syncthreads();
-            bitonic_sort_kv(sv, si, P);
+            bitonic_sort_kv(L.sv, L.si, P);
             if (threadIdx.x == 0) {
                 int ns = n < K ? n : K;
-                s_nsel = ns;
-                s_cnt = 0;
-                if (ns == K) { s_tv = sv[K - 1]; s_ti = si[K - 1]; }
+                L.s_nsel = ns;
+                L.s_cnt = 0;
+                if (ns == K) { L.s_tv = L.sv[K - 1]; L.s_ti = L.si[K - 1]; }
             }
             __syncthreads();
         }
     }
+}
+
+__global__ __launch_bounds__(256) void topk_rows_kernel(const float* __restrict__ x, int64_t cols, int64_t ld,
+                                                        const float* __restrict__ row_div, int K,
+                                                        int32_t* __restrict__ out_idx, float* __restrict__ out_val,
+                                                        int64_t ldo) {
+    __shared__ TkLds L;
+    const int64_t row = blockIdx.x;
+    const float* base = x + row * ld;
+    const bool has_div = row_div != nullptr;
+    const float dv = has_div ? row_div[row] : 1.0f;
+    topk_row_dev(
+        [&](int64_t j) {
+            float v = base[j];
+            if (has_div) v = v / dv;
+            return v;
+        },
+        cols, K, L);
     for (int r = threadIdx.x; r < K; r += blockDim.x) {
-        out_idx[row * ldo + r] = si[r];
-        if (out_val) out_val[row * ldo + r] = sv[r];
+        out_idx[row * ldo + r] = L.si[r];
+        if (out_val) out_val[row * ldo + r] = L.sv[r];
     }
+}
+
+// ------------------------------------------------- re-rank R2 with an fp16 pre-filter
+// The staged re-rank's initial_rank rows (reranking.py:45-48: od[i,:] = D[i,:] / max_j D[i,j]
+// for the symmetric D, stable argsort, first K) without the exact N-wide distance row: the
+// fp16 GEMM gives dot~_ij = x~_i . x~_j (x~ = fp16(x), fp32 accumulation) and
+//   |d~_ij - d_ij| <= e_ij = 1.01 (c_rel n_i n_j + 2^-23 (s_i + s_j) + c_abs (n_i + n_j) + D 2^-49)
+// with d~ = fma(-2, dot~, s_i + s_j), d the exact fp32 chain value (dist_exact, the distance
+// kernel's bits), s = squared norms, n = sqrt(s), c_rel = 2 (2^-10 + 2^-22 + 2.02 D 2^-24) +
+// 2.02 2^-23 (fp16 operand rounding 2^-11 relative + 2^-25 absolute per element, both
+// accumulation chains, the final fma), c_abs = 2.01 2^-25 sqrt(D).  Then, with lo = d~ - e,
+// hi = d~ + e:
+//   * the K smallest (od, j) all satisfy d_j <= tau' = tau + |tau| 2^-21, tau = the K-th
+//     smallest hi (K items have d <= hi <= tau; od = fl(d / r) is monotone and one rounding
+//     cannot move a d above tau (1 + 2^-22) to an od at or below fl(tau / r)), and every such
+//     item has lo <= d <= tau': the candidate set {j : lo_j <= tau'} contains them;
+//   * the row max is attained among {j : hi_j >= max_k lo_k}.
+// The candidates' exact distances then give the same rowmax and the same K indices as the
+// full row, bit for bit.  A row whose candidate lists overflow, or with a non-finite bound or
+// max, takes the exact path (all N distances recomputed into the row buffer, then the same
+// selection as rank_rows).
+constexpr int RS_CCAP = 2048, RS_MCAP = 512;
+
+__device__ __forceinline__ float dist_exact(const float* __restrict__ feat, int64_t ldf, int D,
+                                            const float* __restrict__ sqn, int64_t i, int64_t c) {
+    const float* a = feat + i * ldf;
+    const float* b = feat + c * ldf;
+    float acc = 0.0f;
+    int k = 0;
+    if ((ldf & 3) == 0) {
+        for (; k + 4 <= D; k += 4) {
+            const float4 x = *(const float4*)(a + k), y = *(const float4*)(b + k);
+            acc = __builtin_fmaf(x.x, y.x, acc);
+            acc = __builtin_fmaf(x.y, y.y, acc);
+            acc = __builtin_fmaf(x.z, y.z, acc);
+            acc = __builtin_fmaf(x.w, y.w, acc);
+        }
+    }
+    for (; k < D; k++) acc = __builtin_fmaf(a[k], b[k], acc);
+    return __builtin_fmaf(-2.0f, acc, sqn[i] + sqn[c]);
+}
+
+__device__ __forceinline__ float block_max(float v, float* red) {
+    v = wave_max(v);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    float m = red[0];
+    for (int w = 1; w < (int)(blockDim.x >> 6); w++) m = fmaxf(m, red[w]);
+    __syncthreads();
+    return m;
+}
+
+__global__ __launch_bounds__(256) void rank_select_kernel(float* __restrict__ dot, int64_t ldd,
+                                                          const float* __restrict__ feat, int64_t ldf, int D,
+                                                          const float* __restrict__ sqn, const float* __restrict__ nrm,
+                                                          int64_t row0, int64_t N, int K, float c_rel, float c_abs,
+                                                          float c_d, int32_t* __restrict__ rank_out,
+                                                          float* __restrict__ rowmax_out) {
+    __shared__ TkLds L;
+    __shared__ float cv[RS_CCAP];
+    __shared__ int ci[RS_CCAP];
+    __shared__ int mi[RS_MCAP];
+    __shared__ int s_nc, s_nm, s_bad;
+    __shared__ float red[4];
+    const int64_t r = blockIdx.x, i = row0 + r;
+    float* drow = dot + r * ldd;
+    const float s_i = sqn[i], n_i = nrm[i];
+    auto bounds = [&](int64_t j, float& lo, float& hi) {
+        const float s = s_i + sqn[j];
+        const float dt = __builtin_fmaf(-2.0f, drow[j], s);
+        const float nj = nrm[j];
+        const float e = 1.01f * (__builtin_fmaf(c_rel * n_i, nj, 0x1p-23f * s) + c_abs * (n_i + nj) + c_d);
+        lo = dt - e;
+        hi = dt + e;
+    };
+    if (threadIdx.x == 0) { s_nc = 0; s_nm = 0; s_bad = 0; }
+    // pass A: tau = the K-th smallest upper bound; the largest lower bound
+    topk_row_dev(
+        [&](int64_t j) {
+            float lo, hi;
+            bounds(j, lo, hi);
+            return hi;
+        },
+        N, K, L);
+    const float tau = L.sv[K - 1];
+    float ml = -__builtin_inff();
+    bool bad = !(tau <= 3.0e38f && tau >= -3.0e38f);
+    for (int64_t j = threadIdx.x; j < N; j += blockDim.x) {
+        float lo, hi;
+        bounds(j, lo, hi);
+        ml = fmaxf(ml, lo);
+        bad = bad || !(lo == lo && hi == hi && hi < __builtin_inff());
+    }
+    if (bad) s_bad = 1;
+    const float mlo = block_max(ml, red);
+    const float thr = tau + fabsf(tau) * 0x1p-21f + 1e-37f;
+    // pass B: candidate lists
+    if (!s_bad) {
+        for (int64_t j = threadIdx.x; j < N; j += blockDim.x) {
+            float lo, hi;
+            bounds(j, lo, hi);
+            if (lo <= thr) {
+                const int p = atomicAdd(&s_nc, 1);
+                if (p < RS_CCAP) ci[p] = (int)j;
+            }
+            if (hi >= mlo) {
+                const int p = atomicAdd(&s_nm, 1);
+                if (p < RS_MCAP) mi[p] = (int)j;
+            }
+        }
+    }
+    __syncthreads();
+    const int nc = s_nc, nm = s_nm;
+    bool exact = s_bad || nc > RS_CCAP || nm > RS_MCAP;
+    float rmax = 0.0f;
+    if (!exact) {
+        float m = -__builtin_inff();
+        for (int t = threadIdx.x; t < nm; t += blockDim.x) m = fmaxf(m, dist_exact(feat, ldf, D, sqn, i, mi[t]));
+        rmax = block_max(m, red);
+        exact = !(rmax > 0.0f && rmax < __builtin_inff());  // degenerate rows: the exact path
+    }
+    if (!exact) {
+        for (int t = threadIdx.x; t < nc; t += blockDim.x) cv[t] = dist_exact(feat, ldf, D, sqn, i, ci[t]) / rmax;
+        const int P = pow2_ceil(nc < 2 ? 2 : nc);
+        for (int t = nc + threadIdx.x; t < P; t += blockDim.x) { cv[t] = __builtin_inff(); ci[t] = 0x7fffffff; }
+        __syncthreads();
+        bitonic_sort_kv(cv, ci, P);
+        for (int t = threadIdx.x; t < K; t += blockDim.x) rank_out[r * K + t] = ci[t];
+        if (threadIdx.x == 0) rowmax_out[r] = rmax;
+        return;
+    }
+    // exact path: the full row, as reidmi_rr_rank_rows computes it
+    for (int64_t j = threadIdx.x; j < N; j += blockDim.x) drow[j] = dist_exact(feat, ldf, D, sqn, i, j);
+    __syncthreads();
+    float m = -__builtin_inff();
+    for (int64_t j = threadIdx.x; j < N; j += blockDim.x) m = fmaxf(m, drow[j]);
+    rmax = block_max(m, red);
+    topk_row_dev([&](int64_t j) { return drow[j] / rmax; }, N, K, L);
+    for (int t = threadIdx.x; t < K; t += blockDim.x) rank_out[r * K + t] = L.si[t];
+    if (threadIdx.x == 0) rowmax_out[r] = rmax;
+}
+
+// fp16 copy of the features for the pre-filter GEMM: [Np][Dp], zero-padded rows / columns;
+// *range_ok cleared when an element is beyond +-2^15 (fp16 would overflow) or not finite.
+__global__ void feat16_kernel(const float* __restrict__ x, int64_t N, int64_t D, int64_t ldx, _Float16* __restrict__ y,
+                              int64_t Np, int64_t Dp, int32_t* __restrict__ range_ok) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= Np * Dp) return;
+    const int64_t r = t / Dp, c = t - r * Dp;
+    float v = 0.0f;
+    if (r < N && c < D) {
+        v = x[r * ldx + c];
+        if (!(fabsf(v) <= 32768.0f)) { *range_ok = 0; v = 0.0f; }
+    }
+    y[t] = (_Float16)v;
 }
 
 // ------------------------------------------------------------------- eval rows
@@ -1089,6 +1261,32 @@ __global__ __launch_bounds__(256) void eval_rows_kernel(
             if (flag[t]) eval_row_large(q0 + t, dist, G, ld, qp, gp, qc, gc, valid, first, ap, nkept, huge, L);
         __syncthreads();
     }
+}
+
+// rank_select_kernel over rows [row0, row0 + rows) of the fp16 pre-filter product `dot`
+// ([rows][ldd] fp32, ldd >= N): see the kernel for the bound.
+int rank_select_launch(float* dot, int64_t ldd, const float* feat, int64_t ldf, int D, const float* sqn,
+                       const float* nrm, int64_t row0, int64_t rows, int64_t N, int K, int32_t* rank_out,
+                       float* rowmax_out, hipStream_t s) {
+    RM_REQUIRE(K >= 1 && K <= 64 && K <= N && ldd >= N && rows >= 0, "rank_select: bad arguments");
+    if (rows == 0) return OK;
+    const double c_rel = 2.0 * (0x1p-10 + 0x1p-22 + 2.02 * D * 0x1p-24) + 2.02 * 0x1p-23;
+    const double c_abs = 2.01 * 0x1p-25 * std::sqrt((double)D);
+    const double c_d = D * 0x1p-49;
+    hipLaunchKernelGGL(rank_select_kernel, dim3((unsigned)rows), dim3(256), 0, s, dot, ldd, feat, ldf, D, sqn, nrm, row0,
+                       N, K, (float)(c_rel * (1.0 + 0x1p-20)), (float)(c_abs * (1.0 + 0x1p-20)),
+                       (float)(c_d * (1.0 + 0x1p-20)), rank_out, rowmax_out);
+    RM_LAUNCHED();
+    return OK;
+}
+
+int feat16_launch(const float* x, int64_t N, int64_t D, int64_t ldx, void* y, int64_t Np, int64_t Dp,
+                  int32_t* range_ok, hipStream_t s) {
+    RM_REQUIRE(N > 0 && D > 0 && ldx >= D && Np >= N && Dp >= D && range_ok, "feat16: bad arguments");
+    hipLaunchKernelGGL(feat16_kernel, dim3((unsigned)ceil_div(Np * Dp, 256)), dim3(256), 0, s, x, N, D, ldx,
+                       (_Float16*)y, Np, Dp, range_ok);
+    RM_LAUNCHED();
+    return OK;
 }
 
 int topk_launch(const float* x, int64_t rows, int64_t cols, int64_t ldx, const float* row_div, int K,

@@ -16,10 +16,16 @@
 // Arithmetic mirrors numpy exactly: float32 exp = numpy's AVX512F/AVX2 polynomial
 // (pinned against numpy 2.2.6), float32 pairwise sum, fp16 ufuncs = op in fp32 then RNE.
 #include "common.h"
+#include "gemm.h"
 
 
 namespace reidmi {
 
+int rank_select_launch(float* dot, int64_t ldd, const float* feat, int64_t ldf, int D, const float* sqn,
+                       const float* nrm, int64_t row0, int64_t rows, int64_t N, int K, int32_t* rank_out,
+                       float* rowmax_out, hipStream_t s);
+int feat16_launch(const float* x, int64_t N, int64_t D, int64_t ldx, void* y, int64_t Np, int64_t Dp,
+                  int32_t* range_ok, hipStream_t s);
 int topk_launch(const float* x, int64_t rows, int64_t cols, int64_t ldx, const float* row_div, int k,
                 int32_t* out_idx, float* out_val, int64_t ldo, hipStream_t s);
 int distmat_self_launch(const float* x, int64_t N, int64_t ldx, int64_t D, float* out, int64_t ldo, float* ws,
@@ -784,6 +790,43 @@ REIDMI_API int reidmi_rr_rank_rows(const float* feat, int64_t N, int64_t D, int6
         hipLaunchKernelGGL(rowmax_kernel, dim3(ceil_div(nb, 4)), dim3(256), 0, s, chunk, nb, N, N, rowmax_out + (a - lo));
         RM_LAUNCHED();
         if ((rc = topk_launch(chunk, nb, N, N, rowmax_out + (a - lo), K, rank_out + (a - lo) * K, nullptr, K, s)))
+            return rc;
+    }
+    return OK;
+}
+
+// fp16 copy of the features for reidmi_rr_rank_rows_f16: [Np][Dp] (Np a multiple of 256 >= N,
+// Dp a multiple of 64 >= D), zero-padded; *range_ok (device int32, set to 1 by the caller) is
+// cleared when some |x| > 2^15 or is not finite (the pre-filter must not be used then).
+REIDMI_API int reidmi_rr_feat16(const float* feat, int64_t N, int64_t D, int64_t ldf, void* feat16, int64_t Np,
+                                int64_t Dp, int32_t* range_ok, void* stream) {
+    RM_REQUIRE(Np % 256 == 0 && Dp % 64 == 0, "rr_feat16: Np % 256 == 0 and Dp % 64 == 0");
+    return feat16_launch(feat, N, D, ldf, feat16, Np, Dp, range_ok, (hipStream_t)stream);
+}
+
+// reidmi_rr_rank_rows with an fp16 pre-filter: per row pass, the fp16 MFMA product of the
+// rows with all items (chunk [rows][Np] fp32) bounds every exact distance; only the rows'
+// candidates are recomputed with the exact chain.  Same rank_out / rowmax_out bits as
+// reidmi_rr_rank_rows (rank_select_kernel).  nrm = sqrt(sqn) [N].
+REIDMI_API int reidmi_rr_rank_rows_f16(const float* feat, int64_t N, int64_t D, int64_t ldf, const float* sqn,
+                                       const float* nrm, const void* feat16, int64_t Np, int64_t Dp, int64_t lo,
+                                       int64_t hi, int K, int32_t* rank_out, float* rowmax_out, float* chunk,
+                                       int64_t chunk_rows, void* stream) {
+    RM_REQUIRE(N > 0 && D > 0 && ldf >= D && 0 <= lo && lo <= hi && hi <= N && chunk_rows > 0 && K >= 1 && K <= N &&
+                   K <= 64 && Np >= N && Np % 256 == 0 && Dp >= D && Dp % 64 == 0,
+               "rr_rank_rows_f16: bad arguments");
+    RM_REQUIRE(N < 0x7fffffff, "rr_rank_rows_f16: too many items");
+    hipStream_t s = (hipStream_t)stream;
+    const _Float16* x16 = (const _Float16*)feat16;
+    int rc;
+    for (int64_t a = lo; a < hi; a += chunk_rows) {
+        const int64_t nb = hi - a < chunk_rows ? hi - a : chunk_rows;
+        EpiArgs ea{};
+        ea.out = chunk;
+        ea.ldc = Np;
+        if ((rc = gemm_f16(EPI_F32, x16 + a * Dp, Dp, x16, Dp, nb, Np, Dp, ea, s))) return rc;
+        if ((rc = rank_select_launch(chunk, Np, feat, ldf, (int)D, sqn, nrm, a, nb, N, K, rank_out + (a - lo) * K,
+                                     rowmax_out + (a - lo), s)))
             return rc;
     }
     return OK;

@@ -80,3 +80,48 @@ def test_sharded_two_ranks_one_gpu(gpu):
     one = reranking.re_ranking_device(f[:120], f[120:], 50, 15, 0.3).cpu().numpy()
     for r in range(2):
         assert np.array_equal(out[r].view(np.uint32), one.view(np.uint32))
+
+
+def _rank_rows(f, Q, prefilter, chunk_bytes):
+    from multimodal_reid_amd import reranking
+    old = reranking.RANK_PREFILTER
+    reranking.RANK_PREFILTER = prefilter
+    try:
+        st = reranking.HipStages(f, Q, 50, 15, 0.3, chunk_bytes=chunk_bytes)
+        R, rmax = st.rank_rows(0, f.shape[0])
+        return R.cpu().numpy(), rmax.cpu().numpy(), st
+    finally:
+        reranking.RANK_PREFILTER = old
+
+
+@pytest.mark.parametrize("case", ["clustered", "near_dup", "exact_dup", "large_norm", "gaussian_1792", "fp16_range"])
+def test_rank_prefilter_bitexact(gpu, case):
+    """R2 through the fp16 pre-filter (reidmi_rr_rank_rows_f16) equals the exact rows
+    (reidmi_rr_rank_rows) bit for bit: initial_rank and the row maxima, on inputs that stress
+    the error bound — near-duplicates and exact duplicates (dense ties at the K-th distance,
+    candidate overflow -> the exact path), unnormalised features, concentrated high-dimensional
+    distances — and features beyond fp16's range (the pre-filter is then not used)."""
+    r = np.random.default_rng(len(case))
+    if case == "clustered":
+        f = _feats(200, 1800, seed=3)
+    elif case == "near_dup":
+        base = r.standard_normal((40, 256)).astype(np.float32)
+        f = np.repeat(base, 50, axis=0) + 1e-4 * r.standard_normal((2000, 256)).astype(np.float32)
+        f = oracle.l2norm(f)
+    elif case == "exact_dup":
+        base = oracle.l2norm(r.standard_normal((30, 128)).astype(np.float32))
+        f = np.repeat(base, 70, axis=0)
+    elif case == "large_norm":
+        f = (r.standard_normal((1500, 320)) * 40).astype(np.float32)
+    elif case == "gaussian_1792":
+        f = oracle.l2norm(r.standard_normal((1300, 1792)).astype(np.float32))
+    else:
+        f = r.standard_normal((900, 256)).astype(np.float32)
+        f[7, 3] = 40000.0
+    f = torch.from_numpy(np.ascontiguousarray(f)).to(gpu)
+    N = f.shape[0]
+    Rf, mf, st = _rank_rows(f, 100, True, 4 * N * 300)
+    Re, me, _ = _rank_rows(f, 100, False, 4 * N * 300)
+    assert st._f16[4] == (case != "fp16_range")
+    assert np.array_equal(Rf, Re)
+    assert np.array_equal(mf.view(np.uint32), me.view(np.uint32))
