@@ -113,10 +113,13 @@ int reidmi_rr_feat16(const float* feat, int64_t N, int64_t D, int64_t ldf, void*
                      int32_t* range_ok, void* stream);
 /* reidmi_rr_rank_rows with an fp16 MFMA pre-filter (same rank_out / rowmax_out bits): the fp16
  * product bounds every exact distance (error bound in backend.hip rank_select_kernel); only the
- * candidates are recomputed with the exact fp32 chain.  nrm = sqrt(sqn); chunk [chunk_rows][Np]. */
+ * candidates are recomputed with the exact fp32 chain.  Rows whose distances are too
+ * concentrated for the bound (or not finite) get need[r] = 1 and no output: the caller runs the
+ * exact rows for them.  nrm = sqrt(sqn); need [hi - lo] int32; chunk [chunk_rows][Np]. */
 int reidmi_rr_rank_rows_f16(const float* feat, int64_t N, int64_t D, int64_t ldf, const float* sqn, const float* nrm,
                             const void* feat16, int64_t Np, int64_t Dp, int64_t lo, int64_t hi, int K,
-                            int32_t* rank_out, float* rowmax_out, float* chunk, int64_t chunk_rows, void* stream);
+                            int32_t* rank_out, float* rowmax_out, int32_t* need, float* chunk, int64_t chunk_rows,
+                            void* stream);
 int reidmi_rr_v_rows(const float* feat, int64_t N, int64_t D, int64_t ldf, const float* sqn, const float* rowmax,
                      const int32_t* rank, int K, int64_t lo, int64_t hi, int k1, int32_t* vcol, uint16_t* vval,
                      int32_t* vnnz, int32_t* flags, void* stream);

@@ -394,8 +394,8 @@ __global__ __launch_bounds__(256) void topk_rows_kernel(const float* __restrict_
 //   * the row max is attained among {j : hi_j >= max_k lo_k}.
 // The candidates' exact distances then give the same rowmax and the same K indices as the
 // full row, bit for bit.  A row whose candidate lists overflow, or with a non-finite bound or
-// max, takes the exact path (all N distances recomputed into the row buffer, then the same
-// selection as rank_rows).
+// max, is marked in need[] for the exact rows (reranking.HipStages.rank_rows runs them through
+// the exact distance kernel + selection).
 constexpr int RS_CCAP = 2048, RS_MCAP = 512;
 
 __device__ __forceinline__ float dist_exact(const float* __restrict__ feat, int64_t ldf, int D,
@@ -432,7 +432,7 @@ __global__ __launch_bounds__(256) void rank_select_kernel(float* __restrict__ do
                                                           const float* __restrict__ sqn, const float* __restrict__ nrm,
                                                           int64_t row0, int64_t N, int K, float c_rel, float c_abs,
                                                           float c_d, int32_t* __restrict__ rank_out,
-                                                          float* __restrict__ rowmax_out) {
+                                                          float* __restrict__ rowmax_out, int32_t* __restrict__ need) {
     __shared__ TkLds L;
     __shared__ float cv[RS_CCAP];
     __shared__ int ci[RS_CCAP];
@@ -503,18 +503,15 @@ __global__ __launch_bounds__(256) void rank_select_kernel(float* __restrict__ do
         __syncthreads();
         bitonic_sort_kv(cv, ci, P);
         for (int t = threadIdx.x; t < K; t += blockDim.x) rank_out[r * K + t] = ci[t];
-        if (threadIdx.x == 0) rowmax_out[r] = rmax;
+        if (threadIdx.x == 0) {
+            rowmax_out[r] = rmax;
+            need[r] = 0;
+        }
         return;
     }
-    // exact path: the full row, as reidmi_rr_rank_rows computes it
-    for (int64_t j = threadIdx.x; j < N; j += blockDim.x) drow[j] = dist_exact(feat, ldf, D, sqn, i, j);
-    __syncthreads();
-    float m = -__builtin_inff();
-    for (int64_t j = threadIdx.x; j < N; j += blockDim.x) m = fmaxf(m, drow[j]);
-    rmax = block_max(m, red);
-    topk_row_dev([&](int64_t j) { return drow[j] / rmax; }, N, K, L);
-    for (int t = threadIdx.x; t < K; t += blockDim.x) rank_out[r * K + t] = L.si[t];
-    if (threadIdx.x == 0) rowmax_out[r] = rmax;
+    // the row needs the exact path (its distances are too concentrated for the bound, or not
+    // finite): the caller runs reidmi_rr_rank_rows' exact MFMA rows for the rows marked here
+    if (threadIdx.x == 0) need[r] = 1;
 }
 
 // fp16 copy of the features for the pre-filter GEMM: [Np][Dp], zero-padded rows / columns;
@@ -1267,7 +1264,7 @@ __global__ __launch_bounds__(256) void eval_rows_kernel(
 // ([rows][ldd] fp32, ldd >= N): see the kernel for the bound.
 int rank_select_launch(float* dot, int64_t ldd, const float* feat, int64_t ldf, int D, const float* sqn,
                        const float* nrm, int64_t row0, int64_t rows, int64_t N, int K, int32_t* rank_out,
-                       float* rowmax_out, hipStream_t s) {
+                       float* rowmax_out, int32_t* need, hipStream_t s) {
     RM_REQUIRE(K >= 1 && K <= 64 && K <= N && ldd >= N && rows >= 0, "rank_select: bad arguments");
     if (rows == 0) return OK;
     const double c_rel = 2.0 * (0x1p-10 + 0x1p-22 + 2.02 * D * 0x1p-24) + 2.02 * 0x1p-23;
@@ -1275,7 +1272,7 @@ int rank_select_launch(float* dot, int64_t ldd, const float* feat, int64_t ldf, 
     const double c_d = D * 0x1p-49;
     hipLaunchKernelGGL(rank_select_kernel, dim3((unsigned)rows), dim3(256), 0, s, dot, ldd, feat, ldf, D, sqn, nrm, row0,
                        N, K, (float)(c_rel * (1.0 + 0x1p-20)), (float)(c_abs * (1.0 + 0x1p-20)),
-                       (float)(c_d * (1.0 + 0x1p-20)), rank_out, rowmax_out);
+                       (float)(c_d * (1.0 + 0x1p-20)), rank_out, rowmax_out, need);
     RM_LAUNCHED();
     return OK;
 }

@@ -23,7 +23,7 @@ namespace reidmi {
 
 int rank_select_launch(float* dot, int64_t ldd, const float* feat, int64_t ldf, int D, const float* sqn,
                        const float* nrm, int64_t row0, int64_t rows, int64_t N, int K, int32_t* rank_out,
-                       float* rowmax_out, hipStream_t s);
+                       float* rowmax_out, int32_t* need, hipStream_t s);
 int feat16_launch(const float* x, int64_t N, int64_t D, int64_t ldx, void* y, int64_t Np, int64_t Dp,
                   int32_t* range_ok, hipStream_t s);
 int topk_launch(const float* x, int64_t rows, int64_t cols, int64_t ldx, const float* row_div, int k,
@@ -807,11 +807,12 @@ REIDMI_API int reidmi_rr_feat16(const float* feat, int64_t N, int64_t D, int64_t
 // reidmi_rr_rank_rows with an fp16 pre-filter: per row pass, the fp16 MFMA product of the
 // rows with all items (chunk [rows][Np] fp32) bounds every exact distance; only the rows'
 // candidates are recomputed with the exact chain.  Same rank_out / rowmax_out bits as
-// reidmi_rr_rank_rows (rank_select_kernel).  nrm = sqrt(sqn) [N].
+// reidmi_rr_rank_rows (rank_select_kernel) for the rows with need[r] = 0; rows with need[r] = 1
+// (concentrated or non-finite distances) are left for the exact rows.  nrm = sqrt(sqn) [N].
 REIDMI_API int reidmi_rr_rank_rows_f16(const float* feat, int64_t N, int64_t D, int64_t ldf, const float* sqn,
                                        const float* nrm, const void* feat16, int64_t Np, int64_t Dp, int64_t lo,
-                                       int64_t hi, int K, int32_t* rank_out, float* rowmax_out, float* chunk,
-                                       int64_t chunk_rows, void* stream) {
+                                       int64_t hi, int K, int32_t* rank_out, float* rowmax_out, int32_t* need,
+                                       float* chunk, int64_t chunk_rows, void* stream) {
     RM_REQUIRE(N > 0 && D > 0 && ldf >= D && 0 <= lo && lo <= hi && hi <= N && chunk_rows > 0 && K >= 1 && K <= N &&
                    K <= 64 && Np >= N && Np % 256 == 0 && Dp >= D && Dp % 64 == 0,
                "rr_rank_rows_f16: bad arguments");
@@ -826,7 +827,7 @@ REIDMI_API int reidmi_rr_rank_rows_f16(const float* feat, int64_t N, int64_t D, 
         ea.ldc = Np;
         if ((rc = gemm_f16(EPI_F32, x16 + a * Dp, Dp, x16, Dp, nb, Np, Dp, ea, s))) return rc;
         if ((rc = rank_select_launch(chunk, Np, feat, ldf, (int)D, sqn, nrm, a, nb, N, K, rank_out + (a - lo) * K,
-                                     rowmax_out + (a - lo), s)))
+                                     rowmax_out + (a - lo), need + (a - lo), s)))
             return rc;
     }
     return OK;

@@ -128,21 +128,61 @@ class HipStages:
             self._f16 = (x16, Np, Dp, torch.sqrt(self.sqn), bool(ok.item()))
         return self._f16
 
+    def _exact_rows(self, lo, idx, R, rmax):
+        """R2 of rows lo + idx with the exact distance kernel: the same distance bits as
+        reidmi_rr_rank_rows (per-pair fp32 chain, same squared norms), row max, stable top-K of
+        D / rowmax (reidmi_topk_rows_f32, as rr_rank_rows)."""
+        n = int(idx.numel())
+        if n == 0:
+            return
+        step = max(1, self.chunk_rows)
+        for s in range(0, n, step):
+            sub = idx[s:s + step]
+            rows = self.feat[lo + sub].contiguous()
+            d = torch.empty((rows.shape[0], self.N), device=self.dev, dtype=torch.float32)
+            ws = torch.empty(rows.shape[0] + self.N, device=self.dev, dtype=torch.float32)
+            _lib.call("reidmi_distmat_f32", _lib.ptr(rows), rows.shape[0], self.D, _lib.ptr(self.feat), self.N,
+                      self.D, self.D, _lib.ptr(d), self.N, _lib.ptr(ws), self.st)
+            # rowmax_kernel's fmaxf reduction: NaN entries are skipped
+            m = torch.where(torch.isnan(d), float("-inf"), d).max(dim=1).values.contiguous()
+            k = torch.empty((rows.shape[0], self.K), device=self.dev, dtype=torch.int32)
+            _lib.call("reidmi_topk_rows_f32", _lib.ptr(d), rows.shape[0], self.N, self.N, _lib.ptr(m), self.K,
+                      _lib.ptr(k), None, self.K, self.st)
+            R[sub] = k
+            rmax[sub] = m
+
     def rank_rows(self, lo, hi):
         R = torch.empty((hi - lo, self.K), device=self.dev, dtype=torch.int32)
         rmax = torch.empty(hi - lo, device=self.dev, dtype=torch.float32)
         if hi > lo:
             x16, Np, Dp, nrm, fits = self._feat16() if RANK_PREFILTER else (None, 0, 0, None, False)
+            a = lo
             if fits:
-                # the fp16 pre-filter (bit-identical to the exact rows; reidmi_rr_rank_rows_f16)
+                # the fp16 pre-filter (bit-identical to the exact rows; reidmi_rr_rank_rows_f16),
+                # one row pass at a time: rows it cannot decide (distances too concentrated
+                # for its bound) go through the exact rows, and once a pass has more of those
+                # than not (a random network's embeddings) the rest skips the filter
                 cr = min(max(256, self.chunk_rows * self.N // Np // 256 * 256), hi - lo)
-                _lib.call("reidmi_rr_rank_rows_f16", _lib.ptr(self.feat), self.N, self.D, self.D, _lib.ptr(self.sqn),
-                          _lib.ptr(nrm), _lib.ptr(x16), Np, Dp, lo, hi, self.K, _lib.ptr(R), _lib.ptr(rmax),
-                          _lib.ptr(self._chunk_buf(cr, Np)), cr, self.st)
-            else:
-                cr = min(self.chunk_rows, hi - lo)
-                _lib.call("reidmi_rr_rank_rows", _lib.ptr(self.feat), self.N, self.D, self.D, _lib.ptr(self.sqn), lo,
-                          hi, self.K, _lib.ptr(R), _lib.ptr(rmax), _lib.ptr(self._chunk_buf(cr, self.N)), cr, self.st)
+                need = torch.empty(cr, device=self.dev, dtype=torch.int32)
+                first = True
+                while a < hi:
+                    b = min(a + (min(cr, 512) if first else cr), hi)  # a small probe pass first
+                    first = False
+                    _lib.call("reidmi_rr_rank_rows_f16", _lib.ptr(self.feat), self.N, self.D, self.D,
+                              _lib.ptr(self.sqn), _lib.ptr(nrm), _lib.ptr(x16), Np, Dp, a, b, self.K,
+                              _lib.ptr(R[a - lo:]), _lib.ptr(rmax[a - lo:]), _lib.ptr(need),
+                              _lib.ptr(self._chunk_buf(cr, Np)), cr, self.st)
+                    idx = torch.nonzero(need[:b - a]).flatten()
+                    self._exact_rows(a, idx, R[a - lo:b - lo], rmax[a - lo:b - lo])
+                    undecided, rows = int(idx.numel()), b - a
+                    a = b
+                    if 2 * undecided > rows:
+                        break
+            if a < hi:
+                cr = min(self.chunk_rows, hi - a)
+                _lib.call("reidmi_rr_rank_rows", _lib.ptr(self.feat), self.N, self.D, self.D, _lib.ptr(self.sqn), a,
+                          hi, self.K, _lib.ptr(R[a - lo:]), _lib.ptr(rmax[a - lo:]),
+                          _lib.ptr(self._chunk_buf(cr, self.N)), cr, self.st)
         return R, rmax
 
     def offsets(self, nnz):

@@ -94,13 +94,15 @@ def _rank_rows(f, Q, prefilter, chunk_bytes):
         reranking.RANK_PREFILTER = old
 
 
-@pytest.mark.parametrize("case", ["clustered", "near_dup", "exact_dup", "large_norm", "gaussian_1792", "fp16_range"])
+@pytest.mark.parametrize("case", ["clustered", "near_dup", "exact_dup", "large_norm", "gaussian_1792", "fp16_range",
+                                  "concentrated"])
 def test_rank_prefilter_bitexact(gpu, case):
     """R2 through the fp16 pre-filter (reidmi_rr_rank_rows_f16) equals the exact rows
     (reidmi_rr_rank_rows) bit for bit: initial_rank and the row maxima, on inputs that stress
     the error bound — near-duplicates and exact duplicates (dense ties at the K-th distance,
     candidate overflow -> the exact path), unnormalised features, concentrated high-dimensional
-    distances — and features beyond fp16's range (the pre-filter is then not used)."""
+    distances, a random network's concentrated embeddings (every row to the exact rows) — and
+    features beyond fp16's range (the pre-filter is then not used)."""
     r = np.random.default_rng(len(case))
     if case == "clustered":
         f = _feats(200, 1800, seed=3)
@@ -115,9 +117,12 @@ def test_rank_prefilter_bitexact(gpu, case):
         f = (r.standard_normal((1500, 320)) * 40).astype(np.float32)
     elif case == "gaussian_1792":
         f = oracle.l2norm(r.standard_normal((1300, 1792)).astype(np.float32))
-    else:
+    elif case == "fp16_range":
         f = r.standard_normal((900, 256)).astype(np.float32)
         f[7, 3] = 40000.0
+    else:
+        # a random network's embeddings: every distance inside the bound -> the exact rows
+        f = oracle.l2norm(np.ones((1200, 512), np.float32) + 1e-3 * r.standard_normal((1200, 512)).astype(np.float32))
     f = torch.from_numpy(np.ascontiguousarray(f)).to(gpu)
     N = f.shape[0]
     Rf, mf, st = _rank_rows(f, 100, True, 4 * N * 300)
