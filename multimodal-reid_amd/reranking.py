@@ -139,7 +139,8 @@ class HipStages:
         for s in range(0, n, step):
             sub = idx[s:s + step]
             rows = self.feat[lo + sub].contiguous()
-            d = torch.empty((rows.shape[0], self.N), device=self.dev, dtype=torch.float32)
+            # the row-pass scratch (stream-ordered after the pass that marked these rows)
+            d = self._chunk_buf(rows.shape[0], self.N)[:rows.shape[0] * self.N].view(rows.shape[0], self.N)
             ws = torch.empty(rows.shape[0] + self.N, device=self.dev, dtype=torch.float32)
             _lib.call("reidmi_distmat_f32", _lib.ptr(rows), rows.shape[0], self.D, _lib.ptr(self.feat), self.N,
                       self.D, self.D, _lib.ptr(d), self.N, _lib.ptr(ws), self.st)
