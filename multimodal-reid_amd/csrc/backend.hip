@@ -902,14 +902,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
                     const int64_t v = v0 + u * 256 + tid;
                     w[u] = v < n8 ? ((const uint4*)pk)[v] : make_uint4(~0u, ~0u, ~0u, ~0u);
                 }
+                // 8 labels per lane tested at once: a 16-bit half of x = d ^ (key | key << 16)
+                // is zero iff that label is the key (padding 0xFFFF never equals a key); one
+                // ballot per 8 labels, the per-label ballots only where some lane hit
+                const uint32_t kk = (uint32_t)key * 0x10001u;
 #pragma unroll
                 for (int u = 0; u < U1; u++) {
                     const int64_t jb = (v0 + u * 256 + tid) * 8;
-                    const uint32_t d[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
+                    const uint32_t d[4] = {w[u].x ^ kk, w[u].y ^ kk, w[u].z ^ kk, w[u].w ^ kk};
+                    bool any = false;
+#pragma unroll
+                    for (int e = 0; e < 4; e++) any = any || (d[e] & 0xFFFFu) == 0u || (d[e] >> 16) == 0u;
+                    if (!__ballot(any)) continue;
 #pragma unroll
                     for (int e = 0; e < 8; e++) {
-                        const uint16_t lab = (uint16_t)(d[e >> 1] >> (16 * (e & 1)));
-                        const bool same = lab == key;  // padding 0xFFFF never equals a key
+                        const bool same = ((d[e >> 1] >> (16 * (e & 1))) & 0xFFFFu) == 0u;
                         if (__ballot(same)) take(same, jb + e);
                     }
                 }
