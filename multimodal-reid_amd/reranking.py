@@ -87,7 +87,7 @@ RANK_PREFILTER = True
 class HipStages:
     """The product's stage kernels (libreidmi)."""
 
-    def __init__(self, feat, num_query, k1, k2, lambda_value, chunk_bytes=8 << 30):
+    def __init__(self, feat, num_query, k1, k2, lambda_value, chunk_bytes=16 << 30):
         _lib.require_cuda(feat)
         self.feat = _as_dev_f32(feat).contiguous()
         self.N, self.D = self.feat.shape
@@ -277,7 +277,7 @@ def staged_rerank(stages, N, Q):
     return out
 
 
-def re_ranking_sharded(probFea, galFea, k1, k2, lambda_value, chunk_bytes=8 << 30):
+def re_ranking_sharded(probFea, galFea, k1, k2, lambda_value, chunk_bytes=16 << 30):
     """Sharded re_ranking: probFea / galFea are the FULL query and gallery features on this
     rank's GPU (all-gathered after a sharded embed).  Returns this rank's query rows
     shard(Q, rank, W) of the re-ranked (Q, G) distance as a device tensor; with one process
