@@ -427,7 +427,7 @@ __device__ __forceinline__ float block_max(float v, float* red) {
     return m;
 }
 
-__global__ __launch_bounds__(256) void rank_select_kernel(float* __restrict__ dot, int64_t ldd,
+__global__ __launch_bounds__(256) void rank_select_kernel(const float* __restrict__ dot, int64_t ldd,
                                                           const float* __restrict__ feat, int64_t ldf, int D,
                                                           const float* __restrict__ sqn, const float* __restrict__ nrm,
                                                           int64_t row0, int64_t N, int K, float c_rel, float c_abs,
@@ -440,7 +440,7 @@ __global__ __launch_bounds__(256) void rank_select_kernel(float* __restrict__ do
     __shared__ int s_nc, s_nm, s_bad;
     __shared__ float red[4];
     const int64_t r = blockIdx.x, i = row0 + r;
-    float* drow = dot + r * ldd;
+    const float* drow = dot + r * ldd;
     const float s_i = sqn[i], n_i = nrm[i];
     auto bounds = [&](int64_t j, float& lo, float& hi) {
         const float s = s_i + sqn[j];
@@ -511,6 +511,181 @@ __global__ __launch_bounds__(256) void rank_select_kernel(float* __restrict__ do
     }
     // the row needs the exact path (its distances are too concentrated for the bound, or not
     // finite): the caller runs reidmi_rr_rank_rows' exact MFMA rows for the rows marked here
+    if (threadIdx.x == 0) need[r] = 1;
+}
+
+// Keep the entries j of idx[0, n) with keep(j) (order preserved, in place); one full wave.
+template <typename KEEP>
+__device__ int compact_wave(int* idx, int n, KEEP keep) {
+    const int lane = threadIdx.x & 63;
+    int w = 0;
+    for (int b = 0; b < n; b += 64) {
+        const int t = b + lane;
+        const int j = t < n ? idx[t] : 0;
+        const bool k = t < n && keep(j);
+        const uint64_t m = __ballot(k);
+        if (k) idx[w + __popcll(m & ((1ull << lane) - 1))] = j;
+        w += __popcll(m);
+    }
+    return w;
+}
+
+// Single-pass form of rank_select_kernel (same bound, same output bits): one stream over the
+// row feeds the K-smallest-hi selection and both candidate lists at once, against the running
+// thresholds -- the running K-th smallest hi only decreases and the running max lo only
+// increases, so each list holds a superset of the final one; a list near capacity, and both
+// lists at the end, are filtered against the current thresholds (exact set of the 3-pass form).
+constexpr int RS1_MCAP = 1536;
+
+__global__ __launch_bounds__(256) void rank_select1_kernel(const float* __restrict__ dot, int64_t ldd,
+                                                           const float* __restrict__ feat, int64_t ldf, int D,
+                                                           const float* __restrict__ sqn,
+                                                           const float* __restrict__ nrm, int64_t row0, int64_t N,
+                                                           int K, float c_rel, float c_abs, float c_d,
+                                                           int32_t* __restrict__ rank_out,
+                                                           float* __restrict__ rowmax_out, int32_t* __restrict__ need) {
+    __shared__ TkLds L;
+    __shared__ int ci[RS_CCAP];
+    __shared__ int mi[RS1_MCAP];
+    __shared__ int s_nc, s_nm, s_bad;
+    __shared__ float red[4];
+    const int64_t r = blockIdx.x, i = row0 + r;
+    const float* drow = dot + r * ldd;
+    const float s_i = sqn[i], n_i = nrm[i];
+    const int wv = threadIdx.x >> 6;
+    auto bounds = [&](int64_t j, float& lo, float& hi) {
+        const float s = s_i + sqn[j];
+        const float dt = __builtin_fmaf(-2.0f, drow[j], s);
+        const float nj = nrm[j];
+        const float e = 1.01f * (__builtin_fmaf(c_rel * n_i, nj, 0x1p-23f * s) + c_abs * (n_i + nj) + c_d);
+        lo = dt - e;
+        hi = dt + e;
+    };
+    auto thr_of = [](float tau) { return tau + fabsf(tau) * 0x1p-21f + 1e-37f; };
+    // the max-list threshold starts at the first chunk's largest lo
+    float ml = -__builtin_inff();
+    for (int64_t j = threadIdx.x; j < N && j < TK_CHUNK; j += blockDim.x) {
+        float lo, hi;
+        bounds(j, lo, hi);
+        ml = fmaxf(ml, lo);
+    }
+    float mlo = block_max(ml, red);
+    if (threadIdx.x == 0) { L.s_cnt = 0; L.s_nsel = 0; L.s_tv = __builtin_inff(); L.s_ti = 0x7fffffff; s_nc = 0; s_nm = 0; s_bad = 0; }
+    __syncthreads();
+    bool bad = false, c_lost = false, m_lost = false;
+    float thr = __builtin_inff();
+    for (int64_t c0 = 0; c0 < N; c0 += TK_CHUNK) {
+        const float tv = L.s_tv;
+        const int ti = L.s_ti, nsel = L.s_nsel;
+#pragma unroll
+        for (int u = 0; u < TK_CHUNK / 256; u++) {
+            const int64_t j = c0 + u * 256 + threadIdx.x;
+            if (j < N) {
+                float lo, hi;
+                bounds(j, lo, hi);
+                ml = fmaxf(ml, lo);
+                bad = bad || !(lo == lo && hi == hi && hi < __builtin_inff());
+                if (key_less(hi, (int)j, tv, ti)) {
+                    const int p = atomicAdd(&L.s_cnt, 1);
+                    L.sv[nsel + p] = hi;
+                    L.si[nsel + p] = (int)j;
+                }
+                if (!c_lost && lo <= thr) ci[atomicAdd(&s_nc, 1)] = (int)j;
+                if (!m_lost && hi >= mlo) mi[atomicAdd(&s_nm, 1)] = (int)j;
+            }
+        }
+        const float wm = wave_max(ml);
+        if ((threadIdx.x & 63) == 0) red[wv] = wm;
+        __syncthreads();
+        const bool last = c0 + TK_CHUNK >= N;
+        const int n = L.s_nsel + L.s_cnt, nc = s_nc, nm = s_nm;
+        mlo = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+        __syncthreads();  // every thread has read the counters before anyone appends again
+        if (last || n > TK_CAP - TK_CHUNK) {
+            const int P = pow2_ceil(n < 2 ? 2 : n);
+            for (int t = n + threadIdx.x; t < P; t += blockDim.x) { L.sv[t] = __builtin_inff(); L.si[t] = 0x7fffffff; }
+            __syncthreads();
+            bitonic_sort_kv(L.sv, L.si, P);
+            if (threadIdx.x == 0) {
+                const int ns = n < K ? n : K;
+                L.s_nsel = ns;
+                L.s_cnt = 0;
+                if (ns == K) { L.s_tv = L.sv[K - 1]; L.s_ti = L.si[K - 1]; }
+            }
+            __syncthreads();
+        }
+        if (L.s_nsel == K) thr = thr_of(L.s_tv);
+        // filter the lists when the next chunk could overrun them, and at the end; a list
+        // still too long afterwards is dropped and rebuilt by a second pass with the final
+        // thresholds
+        if (last || (!c_lost && nc > RS_CCAP - TK_CHUNK) || (!m_lost && nm > RS1_MCAP - TK_CHUNK)) {
+            if (wv == 0 && !c_lost) {
+                const int k = compact_wave(ci, nc, [&](int j) {
+                    float lo, hi;
+                    bounds(j, lo, hi);
+                    return lo <= thr;
+                });
+                if (threadIdx.x == 0) s_nc = k;
+            } else if (wv == 1 && !m_lost) {
+                const int k = compact_wave(mi, nm, [&](int j) {
+                    float lo, hi;
+                    bounds(j, lo, hi);
+                    return hi >= mlo;
+                });
+                if (threadIdx.x == 64) s_nm = k;
+            }
+            __syncthreads();
+            c_lost = c_lost || (!last && s_nc > RS_CCAP - TK_CHUNK);
+            m_lost = m_lost || (!last && s_nm > RS1_MCAP - TK_CHUNK);
+            __syncthreads();  // every thread has read the counters before anyone appends again
+        }
+    }
+    if (bad) s_bad = 1;
+    __syncthreads();
+    if ((c_lost || m_lost) && !s_bad) {  // uniform
+        if (threadIdx.x == 0) {
+            if (c_lost) s_nc = 0;
+            if (m_lost) s_nm = 0;
+        }
+        __syncthreads();
+        for (int64_t j = threadIdx.x; j < N; j += blockDim.x) {
+            float lo, hi;
+            bounds(j, lo, hi);
+            if (c_lost && lo <= thr) {
+                const int p = atomicAdd(&s_nc, 1);
+                if (p < RS_CCAP) ci[p] = (int)j;
+            }
+            if (m_lost && hi >= mlo) {
+                const int p = atomicAdd(&s_nm, 1);
+                if (p < RS1_MCAP) mi[p] = (int)j;
+            }
+        }
+        __syncthreads();
+    }
+    const float tau = L.sv[K - 1];
+    const int nc = s_nc, nm = s_nm;
+    bool exact = s_bad || !(tau <= 3.0e38f && tau >= -3.0e38f) || nc > RS_CCAP || nm > RS1_MCAP;
+    float rmax = 0.0f;
+    if (!exact) {
+        float m = -__builtin_inff();
+        for (int t = threadIdx.x; t < nm; t += blockDim.x) m = fmaxf(m, dist_exact(feat, ldf, D, sqn, i, mi[t]));
+        rmax = block_max(m, red);
+        exact = !(rmax > 0.0f && rmax < __builtin_inff());  // degenerate rows: the exact path
+    }
+    if (!exact) {
+        float* cv = L.sv;  // the selection buffer is free once tau is read
+        for (int t = threadIdx.x; t < nc; t += blockDim.x) cv[t] = dist_exact(feat, ldf, D, sqn, i, ci[t]) / rmax;
+        const int P = pow2_ceil(nc < 2 ? 2 : nc);
+        for (int t = nc + threadIdx.x; t < P; t += blockDim.x) { cv[t] = __builtin_inff(); ci[t] = 0x7fffffff; }
+        __syncthreads();
+        bitonic_sort_kv(cv, ci, P);
+        for (int t = threadIdx.x; t < K; t += blockDim.x) rank_out[r * K + t] = ci[t];
+        if (threadIdx.x == 0) {
+            rowmax_out[r] = rmax;
+            need[r] = 0;
+        }
+        return;
+    }
     if (threadIdx.x == 0) need[r] = 1;
 }
 
@@ -1277,7 +1452,10 @@ int rank_select_launch(float* dot, int64_t ldd, const float* feat, int64_t ldf, 
     const double c_rel = 2.0 * (0x1p-10 + 0x1p-22 + 2.02 * D * 0x1p-24) + 2.02 * 0x1p-23;
     const double c_abs = 2.01 * 0x1p-25 * std::sqrt((double)D);
     const double c_d = D * 0x1p-49;
-    hipLaunchKernelGGL(rank_select_kernel, dim3((unsigned)rows), dim3(256), 0, s, dot, ldd, feat, ldf, D, sqn, nrm, row0,
+#ifndef RS_SINGLE_PASS
+#define RS_SINGLE_PASS 1
+#endif
+    hipLaunchKernelGGL(RS_SINGLE_PASS ? rank_select1_kernel : rank_select_kernel, dim3((unsigned)rows), dim3(256), 0, s, dot, ldd, feat, ldf, D, sqn, nrm, row0,
                        N, K, (float)(c_rel * (1.0 + 0x1p-20)), (float)(c_abs * (1.0 + 0x1p-20)),
                        (float)(c_d * (1.0 + 0x1p-20)), rank_out, rowmax_out, need);
     RM_LAUNCHED();
