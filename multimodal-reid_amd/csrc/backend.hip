@@ -553,13 +553,25 @@ __global__ __launch_bounds__(256) void rank_select1_kernel(const float* __restri
     const float* drow = dot + r * ldd;
     const float s_i = sqn[i], n_i = nrm[i];
     const int wv = threadIdx.x >> 6;
-    auto bounds = [&](int64_t j, float& lo, float& hi) {
-        const float s = s_i + sqn[j];
-        const float dt = __builtin_fmaf(-2.0f, drow[j], s);
-        const float nj = nrm[j];
+    auto bounds_v = [&](float dj, float sj, float nj, float& lo, float& hi) {
+        const float s = s_i + sj;
+        const float dt = __builtin_fmaf(-2.0f, dj, s);
         const float e = 1.01f * (__builtin_fmaf(c_rel * n_i, nj, 0x1p-23f * s) + c_abs * (n_i + nj) + c_d);
         lo = dt - e;
         hi = dt + e;
+    };
+    auto bounds = [&](int64_t j, float& lo, float& hi) { bounds_v(drow[j], sqn[j], nrm[j], lo, hi); };
+    // chunk loads run one chunk ahead of the selection (its barriers no longer wait on HBM)
+    constexpr int U = TK_CHUNK / 256;
+    auto load = [&](int64_t c0, float* d, float* sj, float* nj) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int64_t j = c0 + u * 256 + threadIdx.x;
+            const bool in = j < N;
+            d[u] = in ? drow[j] : 0.0f;
+            sj[u] = in ? sqn[j] : 0.0f;
+            nj[u] = in ? nrm[j] : 0.0f;
+        }
     };
     auto thr_of = [](float tau) { return tau + fabsf(tau) * 0x1p-21f + 1e-37f; };
     // the max-list threshold starts at the first chunk's largest lo
@@ -574,15 +586,19 @@ __global__ __launch_bounds__(256) void rank_select1_kernel(const float* __restri
     __syncthreads();
     bool bad = false, c_lost = false, m_lost = false;
     float thr = __builtin_inff();
+    float cd[U], cs[U], cn[U];
+    load(0, cd, cs, cn);
     for (int64_t c0 = 0; c0 < N; c0 += TK_CHUNK) {
         const float tv = L.s_tv;
         const int ti = L.s_ti, nsel = L.s_nsel;
+        float nd[U], ns[U], nn[U];
+        load(c0 + TK_CHUNK, nd, ns, nn);
 #pragma unroll
-        for (int u = 0; u < TK_CHUNK / 256; u++) {
+        for (int u = 0; u < U; u++) {
             const int64_t j = c0 + u * 256 + threadIdx.x;
             if (j < N) {
                 float lo, hi;
-                bounds(j, lo, hi);
+                bounds_v(cd[u], cs[u], cn[u], lo, hi);
                 ml = fmaxf(ml, lo);
                 bad = bad || !(lo == lo && hi == hi && hi < __builtin_inff());
                 if (key_less(hi, (int)j, tv, ti)) {
@@ -639,6 +655,8 @@ __global__ __launch_bounds__(256) void rank_select1_kernel(const float* __restri
             m_lost = m_lost || (!last && s_nm > RS1_MCAP - TK_CHUNK);
             __syncthreads();  // every thread has read the counters before anyone appends again
         }
+#pragma unroll
+        for (int u = 0; u < U; u++) { cd[u] = nd[u]; cs[u] = ns[u]; cn[u] = nn[u]; }
     }
     if (bad) s_bad = 1;
     __syncthreads();
