@@ -397,6 +397,9 @@ __global__ __launch_bounds__(256) void topk_rows_kernel(const float* __restrict_
 // max, is marked in need[] for the exact rows (reranking.HipStages.rank_rows runs them through
 // the exact distance kernel + selection).
 constexpr int RS_CCAP = 2048, RS_MCAP = 512;
+#ifndef DE_UNROLL
+#define DE_UNROLL 16
+#endif
 
 __device__ __forceinline__ float dist_exact(const float* __restrict__ feat, int64_t ldf, int D,
                                             const float* __restrict__ sqn, int64_t i, int64_t c) {
@@ -405,6 +408,8 @@ __device__ __forceinline__ float dist_exact(const float* __restrict__ feat, int6
     float acc = 0.0f;
     int k = 0;
     if ((ldf & 3) == 0) {
+        // unrolled so that many row loads are in flight ahead of the (sequential) fma chain
+#pragma unroll DE_UNROLL
         for (; k + 4 <= D; k += 4) {
             const float4 x = *(const float4*)(a + k), y = *(const float4*)(b + k);
             acc = __builtin_fmaf(x.x, y.x, acc);
