@@ -540,6 +540,9 @@ __device__ int compact_wave(int* idx, int n, KEEP keep) {
 // thresholds -- the running K-th smallest hi only decreases and the running max lo only
 // increases, so each list holds a superset of the final one; a list near capacity, and both
 // lists at the end, are filtered against the current thresholds (exact set of the 3-pass form).
+#ifndef RS1_CCAP
+#define RS1_CCAP 2048
+#endif
 constexpr int RS1_MCAP = 1536;
 
 __global__ __launch_bounds__(256) void rank_select1_kernel(const float* __restrict__ dot, int64_t ldd,
@@ -550,7 +553,7 @@ __global__ __launch_bounds__(256) void rank_select1_kernel(const float* __restri
                                                            int32_t* __restrict__ rank_out,
                                                            float* __restrict__ rowmax_out, int32_t* __restrict__ need) {
     __shared__ TkLds L;
-    __shared__ int ci[RS_CCAP];
+    __shared__ int ci[RS1_CCAP];
     __shared__ int mi[RS1_MCAP];
     __shared__ int s_nc, s_nm, s_bad;
     __shared__ float red[4];
@@ -622,7 +625,9 @@ __global__ __launch_bounds__(256) void rank_select1_kernel(const float* __restri
         const int n = L.s_nsel + L.s_cnt, nc = s_nc, nm = s_nm;
         mlo = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
         __syncthreads();  // every thread has read the counters before anyone appends again
-        if (last || n > TK_CAP - TK_CHUNK) {
+        // the selection is also merged before the candidate list is filtered, so that the
+        // filter uses the current K-th bound (the selection buffer alone merges rarely)
+        if (last || n > TK_CAP - TK_CHUNK || (!c_lost && nc > RS1_CCAP - TK_CHUNK)) {
             const int P = pow2_ceil(n < 2 ? 2 : n);
             for (int t = n + threadIdx.x; t < P; t += blockDim.x) { L.sv[t] = __builtin_inff(); L.si[t] = 0x7fffffff; }
             __syncthreads();
@@ -639,7 +644,7 @@ __global__ __launch_bounds__(256) void rank_select1_kernel(const float* __restri
         // filter the lists when the next chunk could overrun them, and at the end; a list
         // still too long afterwards is dropped and rebuilt by a second pass with the final
         // thresholds
-        if (last || (!c_lost && nc > RS_CCAP - TK_CHUNK) || (!m_lost && nm > RS1_MCAP - TK_CHUNK)) {
+        if (last || (!c_lost && nc > RS1_CCAP - TK_CHUNK) || (!m_lost && nm > RS1_MCAP - TK_CHUNK)) {
             if (wv == 0 && !c_lost) {
                 const int k = compact_wave(ci, nc, [&](int j) {
                     float lo, hi;
@@ -656,7 +661,7 @@ __global__ __launch_bounds__(256) void rank_select1_kernel(const float* __restri
                 if (threadIdx.x == 64) s_nm = k;
             }
             __syncthreads();
-            c_lost = c_lost || (!last && s_nc > RS_CCAP - TK_CHUNK);
+            c_lost = c_lost || (!last && s_nc > RS1_CCAP - TK_CHUNK);
             m_lost = m_lost || (!last && s_nm > RS1_MCAP - TK_CHUNK);
             __syncthreads();  // every thread has read the counters before anyone appends again
         }
@@ -676,7 +681,7 @@ __global__ __launch_bounds__(256) void rank_select1_kernel(const float* __restri
             bounds(j, lo, hi);
             if (c_lost && lo <= thr) {
                 const int p = atomicAdd(&s_nc, 1);
-                if (p < RS_CCAP) ci[p] = (int)j;
+                if (p < RS1_CCAP) ci[p] = (int)j;
             }
             if (m_lost && hi >= mlo) {
                 const int p = atomicAdd(&s_nm, 1);
@@ -687,7 +692,11 @@ __global__ __launch_bounds__(256) void rank_select1_kernel(const float* __restri
     }
     const float tau = L.sv[K - 1];
     const int nc = s_nc, nm = s_nm;
-    bool exact = s_bad || !(tau <= 3.0e38f && tau >= -3.0e38f) || nc > RS_CCAP || nm > RS1_MCAP;
+#ifdef RS_STATS
+    if (threadIdx.x == 0 && (blockIdx.x % 1024) == 7)
+        printf("RS row %lld nc %d nm %d clost %d mlost %d bad %d\n", (long long)i, nc, nm, (int)c_lost, (int)m_lost, s_bad);
+#endif
+    bool exact = s_bad || !(tau <= 3.0e38f && tau >= -3.0e38f) || nc > TK_CAP || nm > RS1_MCAP;  // the sort runs in the selection buffer
     float rmax = 0.0f;
     if (!exact) {
         float m = -__builtin_inff();
