@@ -569,7 +569,7 @@ __global__ __launch_bounds__(256) void rank_select1_kernel(const float* __restri
         hi = dt + e;
     };
     auto bounds = [&](int64_t j, float& lo, float& hi) { bounds_v(drow[j], sqn[j], nrm[j], lo, hi); };
-    // chunk loads run one chunk ahead of the selection (its barriers no longer wait on HBM)
+    // chunk loads (see the stream below)
     constexpr int U = TK_CHUNK / 256;
     auto load = [&](int64_t c0, float* d, float* sj, float* nj) {
 #pragma unroll
@@ -594,13 +594,10 @@ __global__ __launch_bounds__(256) void rank_select1_kernel(const float* __restri
     __syncthreads();
     bool bad = false, c_lost = false, m_lost = false;
     float thr = __builtin_inff();
-    float cd[U], cs[U], cn[U];
-    load(0, cd, cs, cn);
-    for (int64_t c0 = 0; c0 < N; c0 += TK_CHUNK) {
+    // the chunk loads run two chunks ahead of the selection (three register sets in turn)
+    auto chunk = [&](int64_t c0, const float* cd, const float* cs, const float* cn) {
         const float tv = L.s_tv;
         const int ti = L.s_ti, nsel = L.s_nsel;
-        float nd[U], ns[U], nn[U];
-        load(c0 + TK_CHUNK, nd, ns, nn);
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const int64_t j = c0 + u * 256 + threadIdx.x;
@@ -665,8 +662,19 @@ __global__ __launch_bounds__(256) void rank_select1_kernel(const float* __restri
             m_lost = m_lost || (!last && s_nm > RS1_MCAP - TK_CHUNK);
             __syncthreads();  // every thread has read the counters before anyone appends again
         }
-#pragma unroll
-        for (int u = 0; u < U; u++) { cd[u] = nd[u]; cs[u] = ns[u]; cn[u] = nn[u]; }
+    };
+    float xd[U], xs[U], xn[U], yd[U], ys[U], yn[U], zd[U], zs[U], zn[U];
+    load(0, xd, xs, xn);
+    load(TK_CHUNK, yd, ys, yn);
+    for (int64_t c0 = 0; c0 < N; c0 += 3 * TK_CHUNK) {
+        load(c0 + 2 * TK_CHUNK, zd, zs, zn);
+        chunk(c0, xd, xs, xn);
+        if (c0 + TK_CHUNK >= N) break;
+        load(c0 + 3 * TK_CHUNK, xd, xs, xn);
+        chunk(c0 + TK_CHUNK, yd, ys, yn);
+        if (c0 + 2 * TK_CHUNK >= N) break;
+        load(c0 + 4 * TK_CHUNK, yd, ys, yn);
+        chunk(c0 + 2 * TK_CHUNK, zd, zs, zn);
     }
     if (bad) s_bad = 1;
     __syncthreads();
