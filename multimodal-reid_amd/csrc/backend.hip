@@ -540,10 +540,18 @@ __device__ int compact_wave(int* idx, int n, KEEP keep) {
 // thresholds -- the running K-th smallest hi only decreases and the running max lo only
 // increases, so each list holds a superset of the final one; a list near capacity, and both
 // lists at the end, are filtered against the current thresholds (exact set of the 3-pass form).
-#ifndef RS1_CCAP
-#define RS1_CCAP 2048
+#ifndef RS1_CHUNK
+#define RS1_CHUNK 1024
 #endif
-constexpr int RS1_MCAP = 1536;
+// chunk of the stream, selection buffer, candidate and max-list capacities
+constexpr int RS1_CH = RS1_CHUNK, RS1_TKCAP = 2 * RS1_CH, RS1_CCAP = 2 * RS1_CH, RS1_MCAP = RS1_CH + RS1_CH / 2;
+struct Rs1Lds {
+    float sv[RS1_TKCAP];
+    int si[RS1_TKCAP];
+    int s_cnt, s_nsel;
+    float s_tv;
+    int s_ti;
+};
 
 __global__ __launch_bounds__(256) void rank_select1_kernel(const float* __restrict__ dot, int64_t ldd,
                                                            const float* __restrict__ feat, int64_t ldf, int D,
@@ -552,7 +560,7 @@ __global__ __launch_bounds__(256) void rank_select1_kernel(const float* __restri
                                                            int K, float c_rel, float c_abs, float c_d,
                                                            int32_t* __restrict__ rank_out,
                                                            float* __restrict__ rowmax_out, int32_t* __restrict__ need) {
-    __shared__ TkLds L;
+    __shared__ Rs1Lds L;
     __shared__ int ci[RS1_CCAP];
     __shared__ int mi[RS1_MCAP];
     __shared__ int s_nc, s_nm, s_bad;
@@ -570,7 +578,7 @@ __global__ __launch_bounds__(256) void rank_select1_kernel(const float* __restri
     };
     auto bounds = [&](int64_t j, float& lo, float& hi) { bounds_v(drow[j], sqn[j], nrm[j], lo, hi); };
     // chunk loads (see the stream below)
-    constexpr int U = TK_CHUNK / 256;
+    constexpr int U = RS1_CH / 256;
     auto load = [&](int64_t c0, float* d, float* sj, float* nj) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
@@ -584,7 +592,7 @@ __global__ __launch_bounds__(256) void rank_select1_kernel(const float* __restri
     auto thr_of = [](float tau) { return tau + fabsf(tau) * 0x1p-21f + 1e-37f; };
     // the max-list threshold starts at the first chunk's largest lo
     float ml = -__builtin_inff();
-    for (int64_t j = threadIdx.x; j < N && j < TK_CHUNK; j += blockDim.x) {
+    for (int64_t j = threadIdx.x; j < N && j < RS1_CH; j += blockDim.x) {
         float lo, hi;
         bounds(j, lo, hi);
         ml = fmaxf(ml, lo);
@@ -618,13 +626,13 @@ __global__ __launch_bounds__(256) void rank_select1_kernel(const float* __restri
         const float wm = wave_max(ml);
         if ((threadIdx.x & 63) == 0) red[wv] = wm;
         __syncthreads();
-        const bool last = c0 + TK_CHUNK >= N;
+        const bool last = c0 + RS1_CH >= N;
         const int n = L.s_nsel + L.s_cnt, nc = s_nc, nm = s_nm;
         mlo = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
         __syncthreads();  // every thread has read the counters before anyone appends again
         // the selection is also merged before the candidate list is filtered, so that the
         // filter uses the current K-th bound (the selection buffer alone merges rarely)
-        if (last || n > TK_CAP - TK_CHUNK || (!c_lost && nc > RS1_CCAP - TK_CHUNK)) {
+        if (last || n > RS1_TKCAP - RS1_CH || (!c_lost && nc > RS1_CCAP - RS1_CH)) {
             const int P = pow2_ceil(n < 2 ? 2 : n);
             for (int t = n + threadIdx.x; t < P; t += blockDim.x) { L.sv[t] = __builtin_inff(); L.si[t] = 0x7fffffff; }
             __syncthreads();
@@ -641,7 +649,7 @@ __global__ __launch_bounds__(256) void rank_select1_kernel(const float* __restri
         // filter the lists when the next chunk could overrun them, and at the end; a list
         // still too long afterwards is dropped and rebuilt by a second pass with the final
         // thresholds
-        if (last || (!c_lost && nc > RS1_CCAP - TK_CHUNK) || (!m_lost && nm > RS1_MCAP - TK_CHUNK)) {
+        if (last || (!c_lost && nc > RS1_CCAP - RS1_CH) || (!m_lost && nm > RS1_MCAP - RS1_CH)) {
             if (wv == 0 && !c_lost) {
                 const int k = compact_wave(ci, nc, [&](int j) {
                     float lo, hi;
@@ -658,23 +666,23 @@ __global__ __launch_bounds__(256) void rank_select1_kernel(const float* __restri
                 if (threadIdx.x == 64) s_nm = k;
             }
             __syncthreads();
-            c_lost = c_lost || (!last && s_nc > RS1_CCAP - TK_CHUNK);
-            m_lost = m_lost || (!last && s_nm > RS1_MCAP - TK_CHUNK);
+            c_lost = c_lost || (!last && s_nc > RS1_CCAP - RS1_CH);
+            m_lost = m_lost || (!last && s_nm > RS1_MCAP - RS1_CH);
             __syncthreads();  // every thread has read the counters before anyone appends again
         }
     };
     float xd[U], xs[U], xn[U], yd[U], ys[U], yn[U], zd[U], zs[U], zn[U];
     load(0, xd, xs, xn);
-    load(TK_CHUNK, yd, ys, yn);
-    for (int64_t c0 = 0; c0 < N; c0 += 3 * TK_CHUNK) {
-        load(c0 + 2 * TK_CHUNK, zd, zs, zn);
+    load(RS1_CH, yd, ys, yn);
+    for (int64_t c0 = 0; c0 < N; c0 += 3 * RS1_CH) {
+        load(c0 + 2 * RS1_CH, zd, zs, zn);
         chunk(c0, xd, xs, xn);
-        if (c0 + TK_CHUNK >= N) break;
-        load(c0 + 3 * TK_CHUNK, xd, xs, xn);
-        chunk(c0 + TK_CHUNK, yd, ys, yn);
-        if (c0 + 2 * TK_CHUNK >= N) break;
-        load(c0 + 4 * TK_CHUNK, yd, ys, yn);
-        chunk(c0 + 2 * TK_CHUNK, zd, zs, zn);
+        if (c0 + RS1_CH >= N) break;
+        load(c0 + 3 * RS1_CH, xd, xs, xn);
+        chunk(c0 + RS1_CH, yd, ys, yn);
+        if (c0 + 2 * RS1_CH >= N) break;
+        load(c0 + 4 * RS1_CH, yd, ys, yn);
+        chunk(c0 + 2 * RS1_CH, zd, zs, zn);
     }
     if (bad) s_bad = 1;
     __syncthreads();
@@ -704,7 +712,7 @@ __global__ __launch_bounds__(256) void rank_select1_kernel(const float* __restri
     if (threadIdx.x == 0 && (blockIdx.x % 1024) == 7)
         printf("RS row %lld nc %d nm %d clost %d mlost %d bad %d\n", (long long)i, nc, nm, (int)c_lost, (int)m_lost, s_bad);
 #endif
-    bool exact = s_bad || !(tau <= 3.0e38f && tau >= -3.0e38f) || nc > TK_CAP || nm > RS1_MCAP;  // the sort runs in the selection buffer
+    bool exact = s_bad || !(tau <= 3.0e38f && tau >= -3.0e38f) || nc > RS1_TKCAP || nm > RS1_MCAP;  // the sort runs in the selection buffer
     float rmax = 0.0f;
     if (!exact) {
         float m = -__builtin_inff();
