@@ -121,6 +121,9 @@ struct Rows {
 // (i, c) = od[(i - row0) * ld + c]) or recomputed from the features with the distance
 // kernel's exact arithmetic — an fmaf chain over k ascending, then fmaf(-2, dot, |i|^2 +
 // |c|^2) (backend.hip distmat_f32_kernel; the fp32 MFMA accumulates in the same order).
+#ifndef DA_UNROLL
+#define DA_UNROLL 16
+#endif
 struct DistSrc {
     const float* od;
     int64_t ld, row0;
@@ -137,6 +140,8 @@ __device__ __forceinline__ float dist_at(const DistSrc& s, int64_t i, int64_t c)
     float acc = 0.0f;
     int k = 0;
     if ((s.ldf & 3) == 0) {
+        // unrolled so that many row loads are in flight ahead of the (sequential) fma chain
+#pragma unroll DA_UNROLL
         for (; k + 4 <= s.D; k += 4) {
             const float4 x = *(const float4*)(a + k), y = *(const float4*)(b + k);
             acc = __builtin_fmaf(x.x, y.x, acc);
