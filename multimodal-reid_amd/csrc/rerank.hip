@@ -38,7 +38,10 @@ int distmat_pre_launch(const float* q, int64_t Q, int64_t ldq, const float* g, i
 constexpr int VCAP = 1408;   // >= (k1+1) + (k1+1)(round(k1/2)+1) unique entries for k1 <= 50
 constexpr int QCAP = 4096;   // V_qe row capacity
 constexpr int LCAP = 6144;   // staged entries of the k2 rows in qe_kernel
-constexpr int JCH = 32768;   // gallery columns per Jaccard workgroup (fp16 accumulators in LDS)
+#ifndef RR_JCH
+#define RR_JCH 8192
+#endif
+constexpr int JCH = RR_JCH;   // gallery columns per Jaccard workgroup (fp16 accumulators in LDS)
 
 enum RrFlag : int { RR_VCAP = 1, RR_QCAP = 2, RR_LCAP = 4 };
 
@@ -558,18 +561,52 @@ __global__ __launch_bounds__(256) void jaccard_kernel(const float* __restrict__ 
     const int nz = Vq.len(i);
     const int64_t qb = Vq.beg(i);
     const int nb1 = (int)gridDim.x + 1;
-    for (int e = 0; e < nz; e++) {
-        const int32_t c = Vq.col[qb + e];
-        const float vi = h2f_bits(Vq.val[qb + e]);
-        // this chunk's slice of column c's sorted row list (jaccard_bounds_kernel)
-        const int64_t p0 = cbnd[(int64_t)c * nb1 + blockIdx.x], p1 = cbnd[(int64_t)c * nb1 + blockIdx.x + 1];
-        for (int64_t p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
-            const int k = (int)(irow[p] - base);
-            const float vr = h2f_bits(ival[p]);
-            const float mn = vr < vi ? vr : vi;
-            tmin[k] = f2h_bits(h2f_bits(tmin[k]) + mn);
+    // V_qe[i]'s columns in batches of 256: each thread fetches one column's value and slice
+    // bounds (jaccard_bounds_kernel) at once, so the column walk below has no dependent
+    // bound loads; a thread's element of the next column's slice is loaded before the
+    // barrier of the current one
+    __shared__ int64_t s_p0[256];
+    __shared__ int s_n[256];
+    __shared__ float s_vi[256];
+    for (int e0 = 0; e0 < nz; e0 += 256) {
+        const int m = nz - e0 < 256 ? nz - e0 : 256;
+        if ((int)threadIdx.x < m) {
+            const int32_t c = Vq.col[qb + e0 + threadIdx.x];
+            const int64_t p0 = cbnd[(int64_t)c * nb1 + blockIdx.x], p1 = cbnd[(int64_t)c * nb1 + blockIdx.x + 1];
+            s_p0[threadIdx.x] = p0;
+            s_n[threadIdx.x] = (int)(p1 - p0);
+            s_vi[threadIdx.x] = h2f_bits(Vq.val[qb + e0 + threadIdx.x]);
         }
         __syncthreads();
+        int nk = -1;
+        float nv = 0.0f;
+        auto fetch = [&](int e) {
+            nk = -1;
+            if ((int)threadIdx.x < s_n[e]) {
+                const int64_t p = s_p0[e] + threadIdx.x;
+                nk = (int)(irow[p] - base);
+                nv = h2f_bits(ival[p]);
+            }
+        };
+        fetch(0);
+        for (int e = 0; e < m; e++) {
+            const int k = nk;
+            const float vr = nv;
+            const float vi = s_vi[e];
+            const int n = s_n[e];
+            if (e + 1 < m) fetch(e + 1);
+            if (k >= 0) {
+                const float mn = vr < vi ? vr : vi;
+                tmin[k] = f2h_bits(h2f_bits(tmin[k]) + mn);
+            }
+            for (int64_t p = s_p0[e] + 256 + threadIdx.x; p < s_p0[e] + n; p += blockDim.x) {  // long slices
+                const int kk = (int)(irow[p] - base);
+                const float vr2 = h2f_bits(ival[p]);
+                const float mn = vr2 < vi ? vr2 : vi;
+                tmin[kk] = f2h_bits(h2f_bits(tmin[kk]) + mn);
+            }
+            __syncthreads();
+        }
     }
     const float lam = h2f_bits(lam16);
     const float dv = rowdiv[i];
