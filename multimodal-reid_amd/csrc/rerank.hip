@@ -315,14 +315,23 @@ __global__ __launch_bounds__(256) void qe_kernel(const int32_t* __restrict__ R, 
     __shared__ int32_t ocol[QCAP];
     __shared__ uint16_t oval[QCAP];
     __shared__ int s_no, s_bad;
+    __shared__ int64_t s_rb[32];
+    __shared__ int s_len[32];
     const int64_t b = blockIdx.x;
     const int64_t i = row0 + b;
     const int tid = threadIdx.x;
+    // the k2 rows' extents in parallel (one thread each), then their offsets
+    if (tid < k2) {
+        const int64_t r = R[i * ldr + tid];
+        s_rb[tid] = V.beg(r);
+        s_len[tid] = V.len(r);
+    }
+    __syncthreads();
     if (tid == 0) {
         int o = 0;
         for (int j = 0; j < k2; j++) {
             soff[j] = o;
-            o += V.len(R[i * ldr + j]);
+            o += s_len[j];
         }
         soff[k2] = o;
         s_no = 0;
@@ -334,8 +343,7 @@ __global__ __launch_bounds__(256) void qe_kernel(const int32_t* __restrict__ R, 
         return;
     }
     for (int j = 0; j < k2; j++) {
-        const int64_t r = R[i * ldr + j];
-        const int64_t rb = V.beg(r);
+        const int64_t rb = s_rb[j];
         const int n = soff[j + 1] - soff[j];
         for (int t = tid; t < n; t += blockDim.x) {
             scol[soff[j] + t] = V.col[rb + t];
