@@ -57,22 +57,45 @@ EPI_GELU = 1  # the c_fc GEMM (+QuickGELU epilogue): the largest single kernel p
 C_FC_TRAFFIC_BYTES = (2 * 736400 + 1296384) * 1024
 
 
+def _max_over_ranks(values, dev):
+    """Max over ranks of host floats (RCCL moves device tensors, gloo host tensors)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [float(v) for v in values]
+    t = torch.tensor(values, dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(v) for v in t.cpu()]
+
+
+def _crops(lo, hi, seed, dev, block=128):
+    """fp16 U(-1,1) crops [hi-lo, 3, 256, 128] of global image indices lo..hi: block b of
+    `block` images comes from a generator seeded (seed, b), so a shard's images do not depend
+    on how the split is sharded."""
+    out = torch.empty((hi - lo, 3, 256, 128), dtype=torch.float16, device=dev)
+    gen = torch.Generator(device=dev)
+    for b in range(lo // block, -(-hi // block)):
+        a, z = max(lo, b * block), min(hi, (b + 1) * block)
+        gen.manual_seed(seed * 1000003 + b)
+        x = torch.rand((block, 3, 256, 128), generator=gen, device=dev)
+        out[a - lo:z - lo] = (x[a - b * block:z - b * block] * 2 - 1).half()
+    return out
+
+
 class Workload:
     def __init__(self, dev, rank, world, batch, dataset="market1501", model=None):
-        sp = syn.DATASET_SPLITS[dataset]
+        # dataset: a name of synthetic.DATASET_SPLITS, or such a dict (tests run reduced splits)
+        sp = syn.DATASET_SPLITS[dataset] if isinstance(dataset, str) else dataset
         self.Q, self.G = sp["num_query"], sp["num_gallery"]
         self.q_pids, self.g_pids, self.q_cams, self.g_cams = syn.labels(
             self.Q, self.G, sp["num_ids"], sp["num_cams"], seed=0, distractor_frac=0.1, junk_frac=0.02)
         self.rank, self.world, self.batch, self.dev = rank, world, batch, dev
         self.sd = syn.vit_state_dict("ViT-B/16", seed=0) if model is None else None
         self.model = VisionTransformer(self.sd, device=dev) if model is None else model
-        # synthetic crops of this rank's shards, resident in HBM as fp16 (U(-1,1))
-        gen = torch.Generator(device=dev)
+        # synthetic crops of this rank's shards, resident in HBM as fp16 (U(-1,1)); image k of a
+        # split is the same for every world size (generated in seeded blocks of global indices)
         self.qlo, self.qhi = shard(self.Q, rank, world)
         self.glo, self.ghi = shard(self.G, rank, world)
-        gen.manual_seed(1000 + rank)
-        self.q_img = (torch.rand((self.qhi - self.qlo, 3, 256, 128), generator=gen, device=dev) * 2 - 1).half()
-        self.g_img = (torch.rand((self.ghi - self.glo, 3, 256, 128), generator=gen, device=dev) * 2 - 1).half()
+        self.q_img = _crops(self.qlo, self.qhi, 1000, dev)
+        self.g_img = _crops(self.glo, self.ghi, 2000, dev)
         self.q_tta = torch.from_numpy(syn.tta_offsets(self.qhi - self.qlo, seed=1, offset=self.qlo)).to(dev)
         self.g_tta = torch.from_numpy(syn.tta_offsets(self.ghi - self.glo, seed=2, offset=self.glo)).to(dev)
         D = self.model.width + self.model.out_dim
@@ -106,14 +129,14 @@ class Workload:
         return cmc, mAP, t1 - t0, t2 - t1
 
 
-def msmt17_leg(model, dev, rank, world, batch):
+def msmt17_leg(model, dev, rank, world, batch, dataset="msmt17"):
     """configs[3] + the north star's target: MSMT17 (11659q x 82161g) end to end — sharded
     embed of every image (2 TTA passes), RCCL all-gather of the normalised feature blocks,
     exact distmat + CMC/mAP, then the sharded k-reciprocal re-rank (k1=50, k2=15, lambda=0.3;
     row-range stages with all-gathers of initial_rank / V / V_qe) + CMC/mAP.  Timed once,
     after the Market steps (kernels warm); wall seconds are max over ranks."""
     from multimodal_reid_amd import reranking
-    wl = Workload(dev, rank, world, batch, dataset="msmt17", model=model)
+    wl = Workload(dev, rank, world, batch, dataset=dataset, model=model)
     Q, G = wl.Q, wl.G
 
     def sync():
@@ -145,17 +168,14 @@ def msmt17_leg(model, dev, rank, world, batch):
     _, mAP_rr = rows_to_map(final)
     sync()
     t3 = time.perf_counter()
-    times = torch.tensor([t1 - t0, t2 - t1, t3 - t2], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(times, op=dist.ReduceOp.MAX)
-    te, tv, tr = (float(v) for v in times.cpu())
+    te, tv, tr = _max_over_ranks([t1 - t0, t2 - t1, t3 - t2], dev)
     del wl, final, qn, gn
     torch.cuda.empty_cache()
     return {"config": f"MSMT17 {Q}q x {G}g, ViT-B/16 2 passes/img, {world} GPU(s): sharded embed + all-gather, "
                       "exact distmat + CMC/mAP, sharded k-reciprocal re-rank (k1=50 k2=15 lambda=0.3) + CMC/mAP",
             "imgs_per_s": round((Q + G) / te, 1), "embed_wall_s": round(te, 4), "eval_wall_s": round(tv, 4),
             "rerank_eval_wall_s": round(tr, 4), "end_to_end_wall_s": round(te + tv + tr, 4),
-            "mAP": round(float(mAP), 6), "mAP_rerank": round(float(mAP_rr), 6)}
+            "mAP": float(mAP), "mAP_rerank": float(mAP_rr)}
 
 
 def rerank_leg(dev, cpu=True, threads=1):
@@ -493,10 +513,7 @@ def main():
     L.reidmi_prof_collect_min(EPI_GELU, ctypes.c_double(full), ctypes.byref(ms), ctypes.byref(cnt),
                               ctypes.byref(fl))
     L.reidmi_prof_enable(0)
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = _max_over_ranks([elapsed], dev)[0]
     ms17 = None if a.no_msmt17 else msmt17_leg(wl.model, dev, rank, world, a.batch)
     if rank == 0:
         imgs = (wl.Q + wl.G) * a.steps

@@ -49,14 +49,17 @@ int reidmi_distmat_f32(const float* q, int64_t Q, int64_t ldq, const float* g, i
 int reidmi_cosine_f32(const float* q, int64_t Q, int64_t ldq, const float* g, int64_t G, int64_t ldg, int64_t D,
                       float* out, int64_t ldo, float* ws, void* stream);
 
-/* Distance kernel selection for tests / A-B timing: 0 = auto (K-step-32 pipelined kernel when
- * D, ldq, ldg are multiples of 4 and the operands 16-byte aligned), 1 = single-stage kernel.
- * Both run the same MFMA sequence per output: bit-identical. */
-int reidmi_distmat_set_variant(int v);
+/* reidmi_distmat_f32 with an explicit kernel choice (tests / A-B timing; no process-global
+ * state): variant 0 = auto (K-step-32 pipelined kernel when D, ldq, ldg are multiples of 4 and
+ * the operands 16-byte aligned), 1 = single-stage kernel.  Both run the same MFMA sequence per
+ * output: bit-identical. */
+int reidmi_distmat_f32_variant(const float* q, int64_t Q, int64_t ldq, const float* g, int64_t G, int64_t ldg,
+                               int64_t D, float* out, int64_t ldo, float* ws, int variant, void* stream);
 
 /* np.argsort(x, axis=1)[:, :k] with ties in index order (kind="stable") — evaluate.py:40,
  * reranking.py:48.  row_div (nullable): rows are divided by row_div[row] first
- * (reranking.py:46 column-max normalisation of a symmetric distance).  k <= 64.
+ * (reranking.py:46 column-max normalisation of a symmetric distance).  Any k <= cols (k > 1024
+ * runs in rounds of 1024, one stream over the row each).
  * out_val (nullable) receives the selected values. */
 int reidmi_topk_rows_f32(const float* x, int64_t rows, int64_t cols, int64_t ldx, const float* row_div, int k,
                          int32_t* out_idx, float* out_val, int64_t ldo, void* stream);
@@ -79,8 +82,11 @@ int64_t reidmi_eval_rows_workspace_bytes(int64_t G);
  * bit-exact with the reference's numpy arithmetic given the same distances (stable ties).
  * feat [Q+G][ldf] fp32 = cat(probFea, galFea).  final_dist [Q][ldo] fp32 = re-ranked q x g
  * distances.  one_minus_lambda_h = np.float16(1 - lambda) bits, lambda_f = np.float32(lambda)
- * (numpy's weak-scalar conversions, reranking.py:95).  1 <= k1 <= 50, 1 <= k2 <= 32.
- * flags: device int32, OR-ed with 1/2/4 when a row exceeds the V / V_qe / staging capacity. */
+ * (numpy's weak-scalar conversions, reranking.py:95).  Any k1 >= 1, k2 >= 1 and any neighbourhood
+ * density (no capacity limit, as the reference): the workspace holds V and V_qe at their
+ * worst-case row widths (kf (kh1 + 1) and k2 times that, capped at N) and the scratch of the
+ * kernels for rows beyond the on-chip ones.  flags: device int32, 0 after a correct run (8 would
+ * mean a row beyond the sized scratch: a bug, reported instead of a fault). */
 int64_t reidmi_rerank_workspace_bytes(int64_t Q, int64_t G, int k1, int k2, int from_dist, int need_transpose);
 int reidmi_rerank(const float* feat, int64_t Q, int64_t G, int64_t D, int64_t ldf, int k1, int k2,
                   uint16_t one_minus_lambda_h, float lambda_f, float* final_dist, int64_t ldo, void* ws,
@@ -97,9 +103,13 @@ int reidmi_rerank_from_dist(const float* dist, const float* add, int64_t Q, int6
  * is never materialised (chunk_rows x N row blocks are), and every stage takes a row range,
  * so ranks can each own [lo, hi) and all-gather R / V / V_qe between stages.
  * feat [N][ldf] fp32 = cat(probFea, galFea); sqn[N] = squared row norms (reidmi_row_sqnorm_f32).
- * K = max(k1 + 1, k2) columns of initial_rank.  ELL outputs have vcap / qcap entries per row;
- * CSR inputs are (off[N+1] int64, col int32, fp16 bits), columns ascending per row. */
-int reidmi_rr_caps(int* vcap, int* qcap);
+ * K = min(max(k1 + 1, k2), N) columns of initial_rank.  CSR inputs are (off[N+1] int64, col
+ * int32, fp16 bits), columns ascending per row.
+ * reidmi_rr_caps: ELL widths vcap (V rows: the bound kf (kh1 + 1), capped at N) and qcap (the
+ * V_qe rows reidmi_rr_qe_rows assembles on chip), and the workspace bytes of reidmi_rr_v_rows
+ * (0 when k1 <= 61: on chip) and of reidmi_rr_qe_deferred. */
+int reidmi_rr_caps(int64_t N, int k1, int k2, int64_t* vcap, int64_t* qcap, int64_t* v_ws_bytes,
+                   int64_t* qe_ws_bytes);
 /* R1+R2 (reranking.py:36-48): rank_out[hi-lo][K] = stable argsort prefix of od rows lo..hi,
  * rowmax_out[hi-lo] = the od divisors (column maxima of the symmetric distance). */
 int reidmi_rr_rank_rows(const float* feat, int64_t N, int64_t D, int64_t ldf, const float* sqn, int64_t lo, int64_t hi,
@@ -120,33 +130,80 @@ int reidmi_rr_rank_rows_f16(const float* feat, int64_t N, int64_t D, int64_t ldf
                             const void* feat16, int64_t Np, int64_t Dp, int64_t lo, int64_t hi, int K,
                             int32_t* rank_out, float* rowmax_out, int32_t* need, float* chunk, int64_t chunk_rows,
                             void* stream);
+/* R3 (reranking.py:51-71): V rows lo..hi (ELL [hi-lo][vcap]) from the full rank[N][K] and
+ * rowmax[N]; distance entries recomputed from feat with the distance kernel's arithmetic.
+ * ws: reidmi_rr_caps' v_ws_bytes (nullable when 0). */
 int reidmi_rr_v_rows(const float* feat, int64_t N, int64_t D, int64_t ldf, const float* sqn, const float* rowmax,
                      const int32_t* rank, int K, int64_t lo, int64_t hi, int k1, int32_t* vcol, uint16_t* vval,
-                     int32_t* vnnz, int32_t* flags, void* stream);
+                     int32_t* vnnz, void* ws, int64_t ws_bytes, int32_t* flags, void* stream);
 /* off[0..rows] = exclusive scan of nnz[0..rows) (off[rows] = total). */
 int reidmi_rr_row_offsets(const int32_t* nnz, int64_t rows, int64_t* off, void* stream);
 /* ELL rows -> CSR storage at off[]. */
 int reidmi_rr_pack(const int32_t* ell_col, const uint16_t* ell_val, const int32_t* nnz, int64_t rows, int64_t cap,
                    const int64_t* off, int32_t* col, uint16_t* val, void* stream);
-/* R4 (reranking.py:73-78): V_qe rows lo..hi (ELL [hi-lo][qcap]) from the full V (CSR). */
+/* R4 (reranking.py:73-78): V_qe rows lo..hi (ELL [hi-lo][qcap]) from the full V (CSR).  Rows
+ * beyond the on-chip assembly (or every row when k2 > 32) get qnnz = 0 and are listed in
+ * dlist[0 .. *dcount) (dlist int32 [hi-lo], dcount device int32, both written by the call);
+ * reidmi_rr_qe_deferred then computes them: mode 0 -> their entry counts into qnnz[b], mode 1 ->
+ * the rows into CSR at qoff[b] (qoff = offsets of rows lo..hi).  ws: reidmi_rr_caps' qe_ws_bytes. */
 int reidmi_rr_qe_rows(const int32_t* rank, int K, int k2, int64_t lo, int64_t hi, const int64_t* voff,
                       const int32_t* vcol, const uint16_t* vval, int32_t* qcol, uint16_t* qval, int32_t* qnnz,
-                      int32_t* flags, void* stream);
+                      int32_t* dlist, int32_t* dcount, void* stream);
+int reidmi_rr_qe_deferred(const int32_t* rank, int K, int k1, int k2, int64_t lo, int64_t N, const int64_t* voff,
+                          const int32_t* vcol, const uint16_t* vval, const int32_t* dlist, int64_t n_def, int mode,
+                          const int64_t* qoff, int32_t* qcol, uint16_t* qval, int32_t* qnnz, void* ws,
+                          int64_t ws_bytes, int32_t* flags, void* stream);
 /* R5 (reranking.py:80-82): inverted index of the full V_qe (CSR, nnz entries) as CSC with
  * rows ascending per column: coff[N+1], irow[nnz], ival[nnz]. */
 int64_t reidmi_rr_csc_workspace_bytes(int64_t N, int64_t nnz);
 int reidmi_rr_csc(int64_t N, const int64_t* qoff, const int32_t* qcol, const uint16_t* qval, int64_t nnz, int64_t* coff,
                   int32_t* irow, uint16_t* ival, void* ws, int64_t ws_bytes, void* stream);
-/* R6+R7 (reranking.py:84-100): final rows for queries qlo..qhi: out[qhi-qlo][ldo] (G columns). */
+/* R6+R7 (reranking.py:84-100): final rows for queries qlo..qhi: out[qhi-qlo][ldo] (G columns).
+ * chunk: distance scratch of chunk_rows x G floats (chunk_rows <= 65535); bounds: device
+ * scratch of reidmi_rr_jaccard_bounds_bytes(N, G) bytes for the per-column chunk bounds of the
+ * inverted lists. */
 int reidmi_rr_jaccard_rows(const float* feat, int64_t N, int64_t D, int64_t ldf, const float* sqn,
                            const float* rowmax, int64_t Q, int64_t qlo, int64_t qhi, const int64_t* qoff,
                            const int32_t* qcol, const uint16_t* qval, const int64_t* coff, const int32_t* irow,
                            const uint16_t* ival, uint16_t one_minus_lambda_h, float lambda_f, float* out, int64_t ldo,
-                           float* chunk, int64_t chunk_rows, void* stream);
-/* Rows (of N-Q floats each) at the end of reidmi_rr_jaccard_rows' `chunk` scratch that the call
- * keeps for the per-column chunk bounds of the inverted lists; chunk_rows must exceed it (the
- * distance rows per pass are chunk_rows minus this). */
-int64_t reidmi_rr_jaccard_reserved_rows(int64_t N, int64_t G);
+                           float* chunk, int64_t chunk_rows, void* bounds, int64_t bounds_bytes, void* stream);
+int64_t reidmi_rr_jaccard_bounds_bytes(int64_t N, int64_t G);
+/* Row utilities of the staged driver's exact-row fallback (reranking.HipStages): row maxima
+ * skipping NaN (the od divisors, reranking.py:46); ordered compaction idx[0..*count) = positions
+ * of the nonzero flags (np.nonzero; count: device int32); out[r] = x[row0 + idx[r]] (fp32 rows). */
+int reidmi_rowmax_f32(const float* x, int64_t rows, int64_t cols, int64_t ldx, float* out, void* stream);
+int reidmi_nonzero_i32(const int32_t* flags, int64_t n, int32_t* idx, int32_t* count, void* stream);
+int reidmi_gather_rows_f32(const float* x, int64_t ldx, int64_t d, int64_t row0, const int32_t* idx, int64_t n,
+                           float* out, int64_t ldo, void* stream);
+
+/* ---------------------------------------------- multi-GPU exchange (RCCL, §8e) */
+
+/* The eval path's one exchange step for callers that are not Python (the Python drop-in uses
+ * torch.distributed's "nccl" group, multimodal_reid_amd/distributed.py, with the same layout):
+ * gallery feature rows are sharded contiguously over the ranks of one node — rank r of W owns
+ * rows [n*r/W, n*(r+1)/W) — embedded locally, all-gathered (reidmi_comm_allgather_rows), each
+ * rank scores its own query rows (reidmi_distmat_f32 + reidmi_eval_rows, or the staged re-rank),
+ * and the per-query results are all-gathered the same way and reduced on the host in query
+ * order (bit-identical CMC/mAP for every W).  RCCL (NCCL API) is opened at first use from
+ * librccl.so.1 (torch's copy when torch is loaded).  No collective is made by any other entry
+ * point. */
+#define REIDMI_COMM_ID_BYTES 128
+typedef struct reidmi_comm* reidmi_comm_t;
+/* ncclGetUniqueId: rank 0 creates the id (HOST buffer of REIDMI_COMM_ID_BYTES) and hands it to
+ * the other ranks out of band (as for ncclCommInitRank). */
+int reidmi_comm_unique_id(void* id);
+/* One communicator per process; device = the HIP device of this rank. */
+int reidmi_comm_init(reidmi_comm_t* comm, int nranks, int rank, const void* id, int device);
+int reidmi_comm_destroy(reidmi_comm_t comm);
+int reidmi_comm_rank(reidmi_comm_t comm, int* rank, int* nranks);
+/* All-gather of contiguous row shards: send = this rank's rows [n*r/W, n*(r+1)/W) of row_bytes
+ * each, recv = all n_total rows in order.  scratch: device, reidmi_comm_allgather_rows_scratch_bytes
+ * (W * ceil(n_total / W) * row_bytes; the padded in-place all-gather). */
+int64_t reidmi_comm_allgather_rows_scratch_bytes(int nranks, int64_t n_total, int64_t row_bytes);
+int reidmi_comm_allgather_rows(reidmi_comm_t comm, const void* send, int64_t n_total, int64_t row_bytes, void* recv,
+                               void* scratch, int64_t scratch_bytes, void* stream);
+/* Sum all-reduce of count elements; dtype 0 = fp32, 1 = fp64, 2 = int32, 3 = int64. */
+int reidmi_comm_allreduce(reidmi_comm_t comm, const void* send, void* recv, int64_t count, int dtype, void* stream);
 
 /* ------------------------------------------------------------------ encoders */
 
@@ -173,14 +230,14 @@ int reidmi_prof_collect(int epi, double* total_ms, int64_t* count, double* flops
  * so that the average matches that kernel's row in a rocprofv3 --stats summary). */
 int reidmi_prof_collect_min(int epi, double min_flops, double* total_ms, int64_t* count, double* flops);
 
-/* GEMM tile selection (tests): 0 = auto (the persistent 256x256x64 LDS-DMA tile for >= 256
- * tiles, else 128x128x64), 1 = force 128x128, 2 = force persistent.  Bit-identical results. */
-int reidmi_gemm_set_tile(int t);
-
-/* Persistent tile walk: the XCDs are split into ngroups (1, 2, 4, 8) groups, each owning
- * 1/ngroups of the N-tiles (smaller weight share per XCD L2); 0 = auto (default).
- * Bit-identical results. */
-int reidmi_gemm_set_walk(int ngroups);
+/* reidmi_gemm_f16 with an explicit tiling (tests / A-B timing; no process-global state):
+ * tile 0 = auto (the persistent 256x256x64 LDS-DMA tile for >= 256 tiles, else 128x128x64),
+ * 1 = force 128x128, 2 = force persistent; ngroups = the persistent walk's XCD groups (1, 2, 4,
+ * 8; each owns 1/ngroups of the N-tiles, a smaller weight share per XCD L2), 0 = auto.
+ * Every choice is bit-identical. */
+int reidmi_gemm_f16_tiled(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N,
+                          int64_t K, const float* bias, const void* rowstat, const float* colsum, void* out,
+                          int64_t ldc, int tile, int ngroups, void* stream);
 
 /* Key padding used for an L-token sequence by the attention kernel (rows of v^T). */
 int reidmi_attn_lpad(int L);

@@ -19,14 +19,14 @@ _u16 = ctypes.c_uint16
 
 # name -> argtypes (all return int status)
 # entry points returning int64 besides the *_bytes sizes
-INT64_RESULT = {"reidmi_rr_jaccard_reserved_rows"}
+INT64_RESULT = set()
 
 SIGNATURES = {
     "reidmi_row_sqnorm_f32": [_vp, _i64, _i64, _i64, _vp, _vp],
     "reidmi_l2norm_f32": [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp],
     "reidmi_distmat_f32": [_vp, _i64, _i64, _vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp],
     "reidmi_cosine_f32": [_vp, _i64, _i64, _vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp],
-    "reidmi_distmat_set_variant": [_i32],
+    "reidmi_distmat_f32_variant": [_vp, _i64, _i64, _vp, _i64, _i64, _i64, _vp, _i64, _vp, _i32, _vp],
     "reidmi_topk_rows_f32": [_vp, _i64, _i64, _i64, _vp, _i32, _vp, _vp, _i64, _vp],
     "reidmi_eval_rows": [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp],
     "reidmi_eval_rows_workspace_bytes": [_i64],
@@ -35,24 +35,29 @@ SIGNATURES = {
     "reidmi_rerank": [_vp, _i64, _i64, _i64, _i64, _i32, _i32, _u16, _f32, _vp, _i64, _vp, _i64, _vp, _vp],
     "reidmi_rerank_from_dist": [_vp, _vp, _i64, _i64, _i32, _i32, _i32, _u16, _f32, _vp, _i64, _vp, _i64, _vp,
                                 _vp],
-    "reidmi_rr_caps": [_vp, _vp],
+    "reidmi_rr_caps": [_i64, _i32, _i32, _vp, _vp, _vp, _vp],
     "reidmi_rr_rank_rows": [_vp, _i64, _i64, _i64, _vp, _i64, _i64, _i32, _vp, _vp, _vp, _i64, _vp],
     "reidmi_rr_feat16": [_vp, _i64, _i64, _i64, _vp, _i64, _i64, _vp, _vp],
     "reidmi_rr_rank_rows_f16": [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i32, _vp, _vp, _vp,
                                 _vp, _i64, _vp],
-    "reidmi_rr_v_rows": [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _i32, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp],
+    "reidmi_rr_v_rows": [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _i32, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _i64, _vp,
+                         _vp],
     "reidmi_rr_row_offsets": [_vp, _i64, _vp, _vp],
     "reidmi_rr_pack": [_vp, _vp, _vp, _i64, _i64, _vp, _vp, _vp, _vp],
-    "reidmi_rr_qe_rows": [_vp, _i32, _i32, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "reidmi_rr_qe_rows": [_vp, _i32, _i32, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "reidmi_rr_qe_deferred": [_vp, _i32, _i32, _i32, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp,
+                              _vp, _i64, _vp, _vp],
     "reidmi_rr_csc_workspace_bytes": [_i64, _i64],
     "reidmi_rr_csc": [_i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i64, _vp],
     "reidmi_rr_jaccard_rows": [_vp, _i64, _i64, _i64, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp,
-                               _u16, _f32, _vp, _i64, _vp, _i64, _vp],
-    "reidmi_rr_jaccard_reserved_rows": [_i64, _i64],
+                               _u16, _f32, _vp, _i64, _vp, _i64, _vp, _i64, _vp],
+    "reidmi_rr_jaccard_bounds_bytes": [_i64, _i64],
+    "reidmi_rowmax_f32": [_vp, _i64, _i64, _i64, _vp, _vp],
+    "reidmi_nonzero_i32": [_vp, _i64, _vp, _vp, _vp],
+    "reidmi_gather_rows_f32": [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp],
     "reidmi_attn_lpad": [_i32],
     "reidmi_prof_enable": [_i32],
-    "reidmi_gemm_set_tile": [_i32],
-    "reidmi_gemm_set_walk": [_i32],
+    "reidmi_gemm_f16_tiled": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _vp],
     "reidmi_prof_collect": [_i32, _vp, _vp, _vp],
     "reidmi_prof_collect_min": [_i32, ctypes.c_double, _vp, _vp, _vp],
     "reidmi_mhsa_f16": [_vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp],
@@ -67,6 +72,13 @@ SIGNATURES = {
     "reidmi_preprocess_lds_size": [_i32, _i32, _i32, _i32, _vp],
     "reidmi_jpeg_plan": [_vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp],
     "reidmi_jpeg_decode": [_vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp],
+    "reidmi_comm_unique_id": [_vp],
+    "reidmi_comm_init": [_vp, _i32, _i32, _vp, _i32],
+    "reidmi_comm_destroy": [_vp],
+    "reidmi_comm_rank": [_vp, _vp, _vp],
+    "reidmi_comm_allgather_rows_scratch_bytes": [_i32, _i64, _i64],
+    "reidmi_comm_allgather_rows": [_vp, _vp, _i64, _i64, _vp, _vp, _i64, _vp],
+    "reidmi_comm_allreduce": [_vp, _vp, _vp, _i64, _i32, _vp],
 }
 # entry points with struct arguments are typed in model.py (reidmi_vit_*, reidmi_text_*)
 STRUCT_ENTRY_POINTS = ("reidmi_vit_workspace_bytes", "reidmi_vit_forward", "reidmi_text_workspace_bytes",
@@ -88,6 +100,10 @@ def load():
     if not os.path.exists(LIB_PATH):
         raise ReidmiError(f"{LIB_PATH} is not built: run `python __graft_entry__.py build` "
                           "(there is no CPU fallback)")
+    from . import build_lib
+    if not build_lib.manifest_matches():
+        raise ReidmiError(f"{LIB_PATH} was not built from the sources next to it (libreidmi.manifest.json "
+                          "differs): run `python __graft_entry__.py build`")
     L = ctypes.CDLL(LIB_PATH)
     L.reidmi_last_error.restype = ctypes.c_char_p
     L.reidmi_abi_version.restype = _i32

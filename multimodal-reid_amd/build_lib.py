@@ -3,8 +3,16 @@
 Plain shared library with a C ABI (include/reidmi.h): no torch headers, no
 pybind.  It links libamdhip64.so.7 by soname, so inside a process that already
 imported torch it binds to the HIP runtime torch loaded (one runtime, shared
-streams)."""
+streams).
+
+Rebuilds are decided by content, not by file times: every object records the sha256 of its
+source, the headers and the compiler flags, and the library is written together with
+libreidmi.manifest.json (the same digests).  _lib.load() refuses a library whose manifest
+does not match the sources next to it, so a stale or foreign libreidmi.so cannot be used
+silently, and the manifest says which sources a given library was built from."""
 import concurrent.futures as cf
+import hashlib
+import json
 import os
 import subprocess
 import sys
@@ -13,50 +21,106 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, "csrc")
 OBJ = os.path.join(PKG, "build")
 LIB = os.path.join(PKG, "libreidmi.so")
+MANIFEST = os.path.join(PKG, "libreidmi.manifest.json")
 INCLUDE = os.path.join(os.path.dirname(PKG), "include")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=off",
          "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-gpu-rdc", "-Wno-unused-result",
          f"-I{CSRC}", f"-I{INCLUDE}"]
+LDFLAGS = [f"--offload-arch={ARCH}", "-shared", "-fPIC", "-ldl"]
+
+
+def _flags_key():
+    """The compiler/linker flags with the include paths made relative (the GPU box runs the
+    tree from another directory)."""
+    rel = [f if not f.startswith("-I") else "-I" + os.path.relpath(f[2:], PKG) for f in FLAGS]
+    return " ".join(rel + LDFLAGS)
 
 
 def _sources():
     return sorted(f for f in os.listdir(CSRC) if f.endswith(".hip"))
 
 
-def _headers_mtime():
-    hs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
-    hs += [os.path.join(INCLUDE, f) for f in os.listdir(INCLUDE) if f.endswith(".h")] if os.path.isdir(INCLUDE) else []
-    return max([os.path.getmtime(h) for h in hs] + [os.path.getmtime(__file__)])
+def _headers():
+    hs = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h"))
+    if os.path.isdir(INCLUDE):
+        hs += sorted(os.path.join(INCLUDE, f) for f in os.listdir(INCLUDE) if f.endswith(".h"))
+    return hs
 
 
-def _compile(src):
+def _sha(path):
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def source_digests():
+    """{relative path: sha256} of every input of the library (sources, headers, flags)."""
+    d = {os.path.relpath(os.path.join(CSRC, s), PKG): _sha(os.path.join(CSRC, s)) for s in _sources()}
+    d.update({os.path.relpath(h, PKG): _sha(h) for h in _headers()})
+    d["flags"] = hashlib.sha256(_flags_key().encode()).hexdigest()
+    return d
+
+
+def _headers_digest():
+    h = hashlib.sha256()
+    for p in _headers():
+        h.update(os.path.basename(p).encode())
+        h.update(_sha(p).encode())
+    h.update(_flags_key().encode())
+    return h.hexdigest()
+
+
+def _compile(src, hdr):
     obj = os.path.join(OBJ, src.replace(".hip", ".o"))
+    stamp = obj + ".sha256"
     srcp = os.path.join(CSRC, src)
-    if os.path.exists(obj) and os.path.getmtime(obj) > max(os.path.getmtime(srcp), _headers_mtime()):
+    key = hashlib.sha256((_sha(srcp) + hdr).encode()).hexdigest()
+    if os.path.exists(obj) and os.path.exists(stamp) and open(stamp).read().strip() == key:
         return obj, False
     cmd = [HIPCC, *FLAGS, "-c", srcp, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-6000:]}")
+    with open(stamp, "w") as f:
+        f.write(key)
     return obj, True
+
+
+def manifest_matches():
+    """True when libreidmi.so exists and its manifest records exactly the current sources."""
+    if not (os.path.exists(LIB) and os.path.exists(MANIFEST)):
+        return False
+    try:
+        with open(MANIFEST) as f:
+            m = json.load(f)
+    except (OSError, ValueError):
+        return False
+    return m.get("inputs") == source_digests() and m.get("lib_sha256") == _sha(LIB)
 
 
 def build(verbose=False, jobs=None):
     os.makedirs(OBJ, exist_ok=True)
     jobs = jobs or min(8, os.cpu_count() or 4, 16)
+    hdr = _headers_digest()
     with cf.ThreadPoolExecutor(jobs) as ex:
-        res = list(ex.map(_compile, _sources()))
+        res = list(ex.map(lambda s: _compile(s, hdr), _sources()))
     objs = [o for o, _ in res]
     changed = any(c for _, c in res)
-    if changed or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs]
+    if changed or not manifest_matches():
+        cmd = [HIPCC, *LDFLAGS, "-o", LIB, *objs]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
+        ver = subprocess.run([HIPCC, "--version"], capture_output=True, text=True).stdout.strip().splitlines()
+        with open(MANIFEST, "w") as f:
+            json.dump({"inputs": source_digests(), "lib_sha256": _sha(LIB), "arch": ARCH,
+                       "compiler": ver[0] if ver else "", "rebuilt": [os.path.basename(o) for o, c in res if c]},
+                      f, indent=1, sort_keys=True)
         if verbose:
-            print("built", LIB)
+            print("built", LIB, "(recompiled:", ", ".join(os.path.basename(o) for o, c in res if c) or "none", ")")
+    elif verbose:
+        print("up to date", LIB)
     return LIB
 
 

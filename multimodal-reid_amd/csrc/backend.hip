@@ -237,9 +237,6 @@ __global__ __launch_bounds__(256, DM2_MINWG_) void distmat2_f32_kernel(
             }
 }
 
-int g_dm_variant = 0;
-static int distmat_variant() { return g_dm_variant; }
-
 static bool dm2_ok(const float* q, int64_t ldq, const float* g, int64_t ldg, int64_t D);
 
 // Self-distance of x [N][D] (the one-call re-rank's N x N matrix, reranking.py:36-44): the
@@ -250,7 +247,7 @@ int distmat_self_launch(const float* x, int64_t N, int64_t ldx, int64_t D, float
     RM_REQUIRE(N > 0 && D > 0 && ldx >= D && ldo >= N && ws != nullptr, "distmat_self: bad shape");
     hipLaunchKernelGGL(row_sqnorm_kernel, dim3(ceil_div(N, 256)), dim3(256), 0, s, x, N, D, ldx, ws);
     RM_LAUNCHED();
-    if (!dm2_ok(x, ldx, x, ldx, D) || distmat_variant() == 1) {
+    if (!dm2_ok(x, ldx, x, ldx, D)) {
         dim3 grid(ceil_div(N, DM_BN), ceil_div(N, DM_BM));
         RM_REQUIRE(grid.y <= 65535, "distmat: too many query rows for one launch");
         hipLaunchKernelGGL(distmat_f32_kernel<false>, grid, dim3(256), 0, s, x, x, ws, ws, N, N, D, ldx, ldx, out, ldo);
@@ -315,9 +312,13 @@ struct TkLds {
 };
 
 // The selection of one row by the whole workgroup: afterwards L.sv / L.si [0, min(K, cols))
-// hold the K smallest (val(j), j) in ascending (value, index) order.
-template <typename VAL>
-__device__ void topk_row_dev(VAL val, int64_t cols, int K, TkLds& L) {
+// hold the K smallest (val(j), j) in ascending (value, index) order among the j with
+// keep(v, j).  K <= TK_CAP - TK_CHUNK.
+struct KeepAll {
+    __device__ bool operator()(float, int) const { return true; }
+};
+template <typename VAL, typename KEEP = KeepAll>
+__device__ void topk_row_dev(VAL val, int64_t cols, int K, TkLds& L, KEEP keep = KEEP{}) {
     if (threadIdx.x == 0) { L.s_cnt = 0; L.s_nsel = 0; L.s_tv = __builtin_inff(); L.s_ti = 0x7fffffff; }
     __syncthreads();
     for (int64_t c0 = 0; c0 < cols; c0 += TK_CHUNK) {
@@ -328,7 +329,7 @@ __device__ void topk_row_dev(VAL val, int64_t cols, int K, TkLds& L) {
             int64_t j = c0 + u * 256 + threadIdx.x;
             if (j < cols) {
                 const float v = val(j);
-                if (key_less(v, (int)j, tv, ti)) {
+                if (key_less(v, (int)j, tv, ti) && keep(v, (int)j)) {
                     int p = atomicAdd(&L.s_cnt, 1);
                     L.sv[nsel + p] = v;
                     L.si[nsel + p] = (int)j;
@@ -355,6 +356,11 @@ __device__ void topk_row_dev(VAL val, int64_t cols, int K, TkLds& L) {
     }
 }
 
+// K > TK_RUN (reranking.py:48's initial_rank for k1 or k2 beyond 1023): rounds of TK_RUN, each
+// a fresh stream over the row keeping only the keys after the last one selected (keys are
+// unique: the index breaks every tie), so the rounds concatenate to the stable argsort prefix.
+constexpr int TK_RUN = TK_CAP - TK_CHUNK;
+
 __global__ __launch_bounds__(256) void topk_rows_kernel(const float* __restrict__ x, int64_t cols, int64_t ld,
                                                         const float* __restrict__ row_div, int K,
                                                         int32_t* __restrict__ out_idx, float* __restrict__ out_val,
@@ -364,16 +370,27 @@ __global__ __launch_bounds__(256) void topk_rows_kernel(const float* __restrict_
     const float* base = x + row * ld;
     const bool has_div = row_div != nullptr;
     const float dv = has_div ? row_div[row] : 1.0f;
-    topk_row_dev(
-        [&](int64_t j) {
-            float v = base[j];
-            if (has_div) v = v / dv;
-            return v;
-        },
-        cols, K, L);
-    for (int r = threadIdx.x; r < K; r += blockDim.x) {
-        out_idx[row * ldo + r] = L.si[r];
-        if (out_val) out_val[row * ldo + r] = L.sv[r];
+    auto val = [&](int64_t j) {
+        float v = base[j];
+        if (has_div) v = v / dv;
+        return v;
+    };
+    float lv = -__builtin_inff();
+    int li = -1;
+    for (int done = 0; done < K;) {
+        const int kk = K - done < TK_RUN ? K - done : TK_RUN;
+        if (done == 0)
+            topk_row_dev(val, cols, kk, L);
+        else
+            topk_row_dev(val, cols, kk, L, [&](float v, int j) { return key_less(lv, li, v, j); });
+        for (int r = threadIdx.x; r < kk; r += blockDim.x) {
+            out_idx[row * ldo + done + r] = L.si[r];
+            if (out_val) out_val[row * ldo + done + r] = L.sv[r];
+        }
+        lv = L.sv[kk - 1];
+        li = L.si[kk - 1];
+        done += kk;
+        __syncthreads();  // every thread has read the selection before the next round refills it
     }
 }
 
@@ -1521,8 +1538,8 @@ int feat16_launch(const float* x, int64_t N, int64_t D, int64_t ldx, void* y, in
 
 int topk_launch(const float* x, int64_t rows, int64_t cols, int64_t ldx, const float* row_div, int K,
                 int32_t* out_idx, float* out_val, int64_t ldo, hipStream_t s) {
-    RM_REQUIRE(rows >= 0 && cols > 0 && ldx >= cols && K > 0 && K <= 64 && K <= cols && ldo >= K,
-               "topk_rows: need 0 < k <= min(64, cols)");
+    RM_REQUIRE(rows >= 0 && cols > 0 && ldx >= cols && K > 0 && K <= cols && ldo >= K,
+               "topk_rows: need 0 < k <= cols, ldo >= k");
     RM_REQUIRE(cols < 0x7fffffff, "topk_rows: cols must fit int32");
     if (rows == 0) return OK;
     hipLaunchKernelGGL(topk_rows_kernel, dim3((unsigned)rows), dim3(256), 0, s, x, cols, ldx, row_div, K, out_idx,
@@ -1532,7 +1549,7 @@ int topk_launch(const float* x, int64_t rows, int64_t cols, int64_t ldx, const f
 }
 
 int distmat_impl(bool cosine, const float* q, int64_t Q, int64_t ldq, const float* g, int64_t G, int64_t ldg,
-                 int64_t D, float* out, int64_t ldo, float* ws, void* stream);
+                 int64_t D, float* out, int64_t ldo, float* ws, void* stream, int variant = 0);
 
 int distmat_launch(const float* q, int64_t Q, int64_t ldq, const float* g, int64_t G, int64_t ldg, int64_t D,
                    float* out, int64_t ldo, float* ws, hipStream_t s) {
@@ -1546,7 +1563,7 @@ int distmat_pre_launch(const float* q, int64_t Q, int64_t ldq, const float* g, i
     if (Q == 0 || G == 0) return OK;
     dim3 grid(ceil_div(G, DM_BN), ceil_div(Q, DM_BM));
     RM_REQUIRE(grid.y <= 65535, "distmat: too many query rows for one launch");
-    if (dm2_ok(q, ldq, g, ldg, D) && distmat_variant() != 1)
+    if (dm2_ok(q, ldq, g, ldg, D))
         hipLaunchKernelGGL(distmat2_f32_kernel<false>, dim3((unsigned)((int64_t)grid.x * grid.y)), dim3(256), 0, s, q, g,
                            qq, gg, Q, G, D, ldq, ldg, out, ldo);
     else
@@ -1556,14 +1573,6 @@ int distmat_pre_launch(const float* q, int64_t Q, int64_t ldq, const float* g, i
 }
 
 }  // namespace reidmi
-
-// Distance-kernel selection (tests / A-B timing): 0 = auto (pipelined when the operands allow),
-// 1 = the single-stage kernel.
-REIDMI_API int reidmi_distmat_set_variant(int v) {
-    RM_REQUIRE(v == 0 || v == 1, "distmat variant: 0 auto, 1 single-stage");
-    reidmi::g_dm_variant = v;
-    return reidmi::OK;
-}
 
 using namespace reidmi;
 
@@ -1588,7 +1597,8 @@ REIDMI_API int reidmi_l2norm_f32(const float* x, int64_t n, int64_t d, int64_t l
 }
 
 int reidmi::distmat_impl(bool cosine, const float* q, int64_t Q, int64_t ldq, const float* g, int64_t G,
-                        int64_t ldg, int64_t D, float* out, int64_t ldo, float* ws, void* stream) {
+                        int64_t ldg, int64_t D, float* out, int64_t ldo, float* ws, void* stream, int variant) {
+    RM_REQUIRE(variant == 0 || variant == 1, "distmat variant: 0 auto, 1 single-stage");
     RM_REQUIRE(Q >= 0 && G >= 0 && D > 0 && ldq >= D && ldg >= D && ldo >= G, "distmat: bad shape");
     RM_REQUIRE(ws != nullptr, "distmat: workspace (Q+G floats) required");
     if (Q == 0 || G == 0) return OK;
@@ -1601,7 +1611,7 @@ int reidmi::distmat_impl(bool cosine, const float* q, int64_t Q, int64_t ldq, co
     RM_LAUNCHED();
     dim3 grid(ceil_div(G, DM_BN), ceil_div(Q, DM_BM));
     RM_REQUIRE(grid.y <= 65535, "distmat: too many query rows for one launch");
-    const bool v2 = dm2_ok(q, ldq, g, ldg, D) && distmat_variant() != 1;
+    const bool v2 = dm2_ok(q, ldq, g, ldg, D) && variant != 1;
     const dim3 grid1((unsigned)((int64_t)grid.x * grid.y));
     if (cosine) {
         if (v2)
@@ -1622,6 +1632,14 @@ int reidmi::distmat_impl(bool cosine, const float* q, int64_t Q, int64_t ldq, co
 REIDMI_API int reidmi_distmat_f32(const float* q, int64_t Q, int64_t ldq, const float* g, int64_t G, int64_t ldg,
                                   int64_t D, float* out, int64_t ldo, float* ws, void* stream) {
     return distmat_impl(false, q, Q, ldq, g, G, ldg, D, out, ldo, ws, stream);
+}
+
+// Per-call kernel selection (tests / A-B timing): 0 = auto (pipelined when the operands
+// allow), 1 = the single-stage kernel; the same MFMA chain per output (bit-identical).
+REIDMI_API int reidmi_distmat_f32_variant(const float* q, int64_t Q, int64_t ldq, const float* g, int64_t G,
+                                          int64_t ldg, int64_t D, float* out, int64_t ldo, float* ws, int variant,
+                                          void* stream) {
+    return distmat_impl(false, q, Q, ldq, g, G, ldg, D, out, ldo, ws, stream, variant);
 }
 
 REIDMI_API int reidmi_cosine_f32(const float* q, int64_t Q, int64_t ldq, const float* g, int64_t G, int64_t ldg,

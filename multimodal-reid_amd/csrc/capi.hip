@@ -11,4 +11,6 @@ int fail(int code, const std::string& m) {
 }  // namespace reidmi
 
 REIDMI_API const char* reidmi_last_error(void) { return reidmi::g_err.c_str(); }
-REIDMI_API int reidmi_abi_version(void) { return 1; }
+// 2: per-call GEMM tiling / distance variant entry points replace the process-global setters;
+//    RCCL exchange (reidmi_comm_*); re-ranking without capacity limits.
+REIDMI_API int reidmi_abi_version(void) { return 2; }

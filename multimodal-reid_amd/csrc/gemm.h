@@ -54,9 +54,18 @@ struct EpiArgs {
     int64_t ldp;
 };
 
+// Per-call tiling choice (tests, A/B tools): tile 0 = auto (the persistent 256x256 LDS-DMA
+// tile when the GEMM has >= 256 of them, else 128x128), 1 = force 128x128, 2 = force
+// persistent; ngroups = XCD N-groups of the persistent walk (0 = auto, 1, 2, 4, 8).  Every
+// choice runs the same MFMA chain per output element: bit-identical results.
+struct GemmOpts {
+    int tile = 0;
+    int ngroups = 0;
+};
+
 // Launch C = A . W^T with epilogue `epi`.  Requires N % 128 == 0, K % 64 == 0, lda/ldw
 // multiples of 8 (16-byte rows); M arbitrary.  ea.rowstat / ea.colsum enable the fold.
 int gemm_f16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N, int64_t K,
-             const EpiArgs& ea, hipStream_t stream);
+             const EpiArgs& ea, hipStream_t stream, const GemmOpts& opts = GemmOpts{});
 
 }  // namespace reidmi

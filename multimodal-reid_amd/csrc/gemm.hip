@@ -35,16 +35,6 @@ static std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
 static size_t used = 0;
 }  // namespace prof
 
-// Tile selection for tests (reidmi_gemm_set_tile): 0 = auto (persistent 256x256 tile when
-// the GEMM has >= 256 of them, else 128x128), 1 = force 128x128, 2 = force persistent.
-static int g_tile = 0;
-// Persistent tile walk (reidmi_gemm_set_walk; see gemm_persistent_kernel): N-groups the
-// XCDs are split into (1 = every XCD walks all N-tiles of its M range); 0 = auto: 2 groups
-// when the N-tiles split evenly and there are >= 8 of them (c_fc: 12 tiles, +2 %, 15 % less
-// L2 fetch; an uneven split idles the XCDs of the smaller group), else 1
-// (profiles/r02/walk_ab.txt).
-static int g_ngroups = 0;
-
 constexpr int GB_M = 128, GB_N = 128, GB_K = 64;
 
 __device__ __forceinline__ int swz(int r, int kc) { return r * GB_K + ((kc ^ ((r >> 1) & 7)) << 3); }
@@ -806,10 +796,10 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
 
 template <int EPI>
 static int launch(const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N, int64_t K,
-                  const EpiArgs& ea, hipStream_t s) {
+                  const EpiArgs& ea, hipStream_t s, const GemmOpts& opt) {
     const int64_t tiles256 = (int64_t)ceil_div(M, G2_M) * (N / G2_N);
     const bool fits = N % G2_N == 0 && K >= 2 * GB_K && lda * G2_M < (1ll << 31) && ldw * G2_N < (1ll << 31);
-    if (fits && (g_tile == 2 || (g_tile == 0 && tiles256 >= 256))) {
+    if (fits && (opt.tile == 2 || (opt.tile == 0 && tiles256 >= 256))) {
         const int tiles_m = ceil_div(M, G2_M), tiles_n = (int)(N / G2_N);
         RM_REQUIRE(tiles256 < (1ll << 31), "gemm: grid too large");
         // two operand stages + bias / colsum / rowstat slots (8 waves x 1 KiB each)
@@ -821,7 +811,10 @@ static int launch(const void* A, int64_t lda, const void* W, int64_t ldw, int64_
             attr = true;
         }
         const int grid = (int)(tiles256 < 256 ? tiles256 : 256);
-        const int ngroups = g_ngroups > 0 ? g_ngroups : (tiles_n % 2 == 0 && tiles_n >= 8 ? 2 : 1);
+        // XCD N-groups: auto = 2 when the N-tiles split evenly and there are >= 8 of them
+        // (c_fc: 12 tiles, +2 %, 15 % less L2 fetch; an uneven split idles the XCDs of the
+        // smaller group), else 1 (profiles/r02/walk_ab.txt)
+        const int ngroups = opt.ngroups > 0 ? opt.ngroups : (tiles_n % 2 == 0 && tiles_n >= 8 ? 2 : 1);
         hipLaunchKernelGGL((gemm_persistent_kernel<EPI>), dim3((unsigned)grid), dim3(512), lds, s, (const _Float16*)A,
                            lda, (const _Float16*)W, ldw, M, (int)N, (int)K, ea, tiles_m, tiles_n, ngroups);
         RM_LAUNCHED();
@@ -837,7 +830,10 @@ static int launch(const void* A, int64_t lda, const void* W, int64_t ldw, int64_
 }
 
 int gemm_f16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N, int64_t K,
-             const EpiArgs& ea, hipStream_t s) {
+             const EpiArgs& ea, hipStream_t s, const GemmOpts& opt) {
+    RM_REQUIRE(opt.tile >= 0 && opt.tile <= 2, "gemm tile: 0 auto, 1 128x128, 2 persistent 256x256");
+    RM_REQUIRE(opt.ngroups == 0 || opt.ngroups == 1 || opt.ngroups == 2 || opt.ngroups == 4 || opt.ngroups == 8,
+               "gemm walk: ngroups in {0 (auto), 1, 2, 4, 8}");
     RM_REQUIRE(M >= 0 && N > 0 && K > 0, "gemm: bad shape");
     RM_REQUIRE((epi != EPI_QKV && epi != EPI_PATCH) || M < (1ll << 31), "gemm: head split / patch rows need M < 2^31");
     RM_REQUIRE(N % GB_N == 0 && K % GB_K == 0, "gemm: needs N % 128 == 0 and K % 64 == 0");
@@ -864,12 +860,12 @@ int gemm_f16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, in
     }
     int rc;
     switch (epi) {
-        case EPI_H16: rc = launch<EPI_H16>(A, lda, W, ldw, M, N, K, ea, s); break;
-        case EPI_GELU_H16: rc = launch<EPI_GELU_H16>(A, lda, W, ldw, M, N, K, ea, s); break;
-        case EPI_QKV: rc = launch<EPI_QKV>(A, lda, W, ldw, M, N, K, ea, s); break;
-        case EPI_PATCH: rc = launch<EPI_PATCH>(A, lda, W, ldw, M, N, K, ea, s); break;
-        case EPI_F32: rc = launch<EPI_F32>(A, lda, W, ldw, M, N, K, ea, s); break;
-        case EPI_RESID_F16: rc = launch<EPI_RESID_F16>(A, lda, W, ldw, M, N, K, ea, s); break;
+        case EPI_H16: rc = launch<EPI_H16>(A, lda, W, ldw, M, N, K, ea, s, opt); break;
+        case EPI_GELU_H16: rc = launch<EPI_GELU_H16>(A, lda, W, ldw, M, N, K, ea, s, opt); break;
+        case EPI_QKV: rc = launch<EPI_QKV>(A, lda, W, ldw, M, N, K, ea, s, opt); break;
+        case EPI_PATCH: rc = launch<EPI_PATCH>(A, lda, W, ldw, M, N, K, ea, s, opt); break;
+        case EPI_F32: rc = launch<EPI_F32>(A, lda, W, ldw, M, N, K, ea, s, opt); break;
+        case EPI_RESID_F16: rc = launch<EPI_RESID_F16>(A, lda, W, ldw, M, N, K, ea, s, opt); break;
         default: return fail(EINVAL_, "gemm: unknown epilogue");
     }
     if (ev_b) RM_CHECK_HIP(hipEventRecord(ev_b, s));
@@ -879,19 +875,6 @@ int gemm_f16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, in
 }  // namespace reidmi
 
 using namespace reidmi;
-
-REIDMI_API int reidmi_gemm_set_tile(int t) {
-    RM_REQUIRE(t >= 0 && t <= 2, "gemm tile: 0 auto, 1 128x128, 2 persistent 256x256");
-    g_tile = t;
-    return OK;
-}
-
-REIDMI_API int reidmi_gemm_set_walk(int ngroups) {
-    RM_REQUIRE(ngroups == 0 || ngroups == 1 || ngroups == 2 || ngroups == 4 || ngroups == 8,
-               "gemm walk: ngroups in {0 (auto), 1, 2, 4, 8}");
-    g_ngroups = ngroups;
-    return OK;
-}
 
 REIDMI_API int reidmi_prof_enable(int on) {
     std::lock_guard<std::mutex> g(prof::mu);
@@ -930,9 +913,9 @@ REIDMI_API int reidmi_prof_collect(int epi, double* total_ms, int64_t* count, do
     return reidmi_prof_collect_min(epi, 0.0, total_ms, count, flops);
 }
 
-REIDMI_API int reidmi_gemm_f16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N,
-                               int64_t K, const float* bias, const void* rowstat, const float* colsum, void* out,
-                               int64_t ldc, void* stream) {
+static int gemm_api(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N, int64_t K,
+                    const float* bias, const void* rowstat, const float* colsum, void* out, int64_t ldc,
+                    const GemmOpts& opt, void* stream) {
     RM_REQUIRE(epi == EPI_H16 || epi == EPI_GELU_H16 || epi == EPI_F32 || epi == EPI_RESID_F16,
                "reidmi_gemm_f16: epi must be 0 (fp16), 1 (QuickGELU fp16), 5 (fp32) or 6 (fp16 residual)");
     EpiArgs ea{};
@@ -941,5 +924,20 @@ REIDMI_API int reidmi_gemm_f16(int epi, const void* A, int64_t lda, const void* 
     ea.bias = bias;
     ea.rowstat = (const float2*)rowstat;
     ea.colsum = colsum;
-    return gemm_f16(epi, A, lda, W, ldw, M, N, K, ea, (hipStream_t)stream);
+    return gemm_f16(epi, A, lda, W, ldw, M, N, K, ea, (hipStream_t)stream, opt);
+}
+
+REIDMI_API int reidmi_gemm_f16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N,
+                               int64_t K, const float* bias, const void* rowstat, const float* colsum, void* out,
+                               int64_t ldc, void* stream) {
+    return gemm_api(epi, A, lda, W, ldw, M, N, K, bias, rowstat, colsum, out, ldc, GemmOpts{}, stream);
+}
+
+REIDMI_API int reidmi_gemm_f16_tiled(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M,
+                                     int64_t N, int64_t K, const float* bias, const void* rowstat, const float* colsum,
+                                     void* out, int64_t ldc, int tile, int ngroups, void* stream) {
+    GemmOpts opt;
+    opt.tile = tile;
+    opt.ngroups = ngroups;
+    return gemm_api(epi, A, lda, W, ldw, M, N, K, bias, rowstat, colsum, out, ldc, opt, stream);
 }

@@ -35,15 +35,96 @@ int distmat_launch(const float* q, int64_t Q, int64_t ldq, const float* g, int64
 int distmat_pre_launch(const float* q, int64_t Q, int64_t ldq, const float* g, int64_t G, int64_t ldg, int64_t D,
                        const float* qq, const float* gg, float* out, int64_t ldo, hipStream_t s);
 
-constexpr int VCAP = 1408;   // >= (k1+1) + (k1+1)(round(k1/2)+1) unique entries for k1 <= 50
-constexpr int QCAP = 4096;   // V_qe row capacity
-constexpr int LCAP = 6144;   // staged entries of the k2 rows in qe_kernel
+// No capacity limits (the reference has none, reranking.py:51-78): every bound below only
+// picks the kernel.  A V row holds at most kf (kh1 + 1) entries (the k-reciprocal set plus one
+// half-depth set per accepted candidate), so its ELL width is that bound (rr_caps); rows whose
+// expansion list fits KR_LST run in LDS (kreciprocal_kernel, k1 <= 61), others on workspace
+// scratch (kreciprocal_generic_kernel).  A V_qe row of k2 <= QE_FAST_K2 rows with at most LCAP
+// staged entries and QCAP outputs is assembled in LDS (qe_kernel); any other row is deferred to
+// qe_generic_kernel, whose scratch is sized for the worst case (k2 rows of the V bound).
+constexpr int KR_LST = 2048;   // expansion list of kreciprocal_kernel (LDS)
+constexpr int QCAP = 4096;     // V_qe entries qe_kernel assembles in LDS
+constexpr int LCAP = 6144;     // staged entries of the k2 rows in qe_kernel
+constexpr int QE_FAST_K2 = 32;
+constexpr int GEN_WG = 256;    // workgroups of the generic kernels (one per CU), each with its slab
 #ifndef RR_JCH
 #define RR_JCH 8192
 #endif
 constexpr int JCH = RR_JCH;   // gallery columns per Jaccard workgroup (fp16 accumulators in LDS)
 
-enum RrFlag : int { RR_VCAP = 1, RR_QCAP = 2, RR_LCAP = 4 };
+// flags: a generic kernel found a row beyond the scratch bound it was sized for (cannot happen
+// for bounds from rr_caps; a caller passing smaller scratch gets this instead of a fault)
+enum RrFlag : int { RR_SCRATCH = 8 };
+
+static int pow2_ceil64(int64_t n) {
+    int64_t p = 2;
+    while (p < n) p <<= 1;
+    return (int)p;
+}
+static int64_t al16(int64_t v) { return (v + 15) & ~(int64_t)15; }
+
+// kf = min(k1 + 1, N), kh1 = min(round(k1 / 2) + 1, N): the two depths of reranking.py:53,60
+static void kr_depths(int k1, int64_t N, int& kf, int& kh1) {
+    kf = (int)(k1 + 1 < N ? k1 + 1 : N);
+    const int kh = (int)__builtin_nearbyint((double)k1 / 2.0);  // int(np.around(k1/2))
+    kh1 = (int)(kh + 1 < N ? kh + 1 : N);
+}
+
+struct RrCaps {
+    int kf, kh1, K, k2e;
+    int64_t vcap;  // entries of a V row (ELL width)
+    int64_t tcap;  // staged entries of a V_qe row: k2e V rows
+    int64_t qcap;  // entries of a V_qe row (one-call ELL width)
+    bool kr_fast;
+};
+static RrCaps rr_caps(int64_t N, int k1, int k2) {
+    RrCaps c{};
+    kr_depths(k1, N, c.kf, c.kh1);
+    int64_t K = k1 + 1 > k2 ? k1 + 1 : k2;
+    c.K = (int)(K < N ? K : N);
+    c.k2e = k2 < c.K ? k2 : c.K;  // initial_rank[i, :k2] has min(k2, N) entries
+    const int64_t vb = (int64_t)c.kf * (c.kh1 + 1);
+    c.vcap = vb < N ? vb : N;
+    c.tcap = (int64_t)c.k2e * c.vcap;
+    c.qcap = c.tcap < N ? c.tcap : N;
+    c.kr_fast = c.kf <= 64 && vb <= KR_LST;
+    return c;
+}
+
+// Per-workgroup scratch of kreciprocal_generic_kernel (byte offsets in one slab)
+struct KrSlab {
+    int64_t kr, krs, ncnt, acc, cs, lst, w, bytes;
+};
+static KrSlab kr_slab(int kf, int kh1) {
+    KrSlab s{};
+    const int64_t nb = (int64_t)kf * (kh1 + 1);
+    int64_t o = 0;
+    s.kr = o; o = al16(o + (int64_t)kf * 4);
+    s.krs = o; o = al16(o + (int64_t)pow2_ceil64(kf) * 4);
+    s.ncnt = o; o = al16(o + (int64_t)kf * 4);
+    s.acc = o; o = al16(o + (int64_t)kf * 4);
+    s.cs = o; o = al16(o + (int64_t)kf * kh1 * 4);
+    s.lst = o; o = al16(o + (int64_t)pow2_ceil64(nb) * 4);
+    s.w = o; o = al16(o + nb * 4);
+    s.bytes = o;
+    return s;
+}
+// ... and of qe_generic_kernel
+struct QeSlab {
+    int64_t soff, scol, sval, okey, oval, bytes;
+};
+static QeSlab qe_slab(int k2e, int64_t tcap) {
+    QeSlab s{};
+    const int64_t P = pow2_ceil64(tcap);
+    int64_t o = 0;
+    s.soff = o; o = al16(o + (int64_t)(k2e + 1) * 4);
+    s.scol = o; o = al16(o + tcap * 4);
+    s.sval = o; o = al16(o + tcap * 2);
+    s.okey = o; o = al16(o + P * 4);
+    s.oval = o; o = al16(o + P * 2);
+    s.bytes = o;
+    return s;
+}
 
 // numpy float32 exp (simd_exp_f32, AVX512F/AVX2): see oracle/reid_oracle.c orc_np_expf.
 __device__ __forceinline__ float np_expf(float x) {
@@ -222,10 +303,10 @@ __global__ __launch_bounds__(256) void kreciprocal_kernel(DistSrc ds, const floa
                                                           const int32_t* __restrict__ R, int64_t ldr, int64_t row0,
                                                           int kf, int kh1, int32_t* __restrict__ vcol,
                                                           uint16_t* __restrict__ vval, int32_t* __restrict__ vnnz,
-                                                          int32_t* __restrict__ flags) {
+                                                          int64_t vcap, int32_t* __restrict__ flags) {
     __shared__ int32_t kr[64];
-    __shared__ int32_t lst[2048];
-    __shared__ float w[2048];
+    __shared__ int32_t lst[KR_LST];
+    __shared__ float w[KR_LST];
     __shared__ int s_nk, s_n, s_nu;
     __shared__ float s_sum;
     const int64_t b = blockIdx.x;
@@ -289,16 +370,131 @@ __global__ __launch_bounds__(256) void kreciprocal_kernel(DistSrc ds, const floa
     __syncthreads();
     if (tid == 0) s_sum = pairwise_f32(w, nu);
     __syncthreads();
-    if (nu > VCAP) {
-        if (tid == 0) { atomicOr(flags, RR_VCAP); vnnz[b] = 0; }
+    if (nu > vcap) {  // cannot happen: nu <= kf (kh1 + 1) = the width rr_caps gives
+        if (tid == 0) { atomicOr(flags, RR_SCRATCH); vnnz[b] = 0; }
         return;
     }
     const float sum = s_sum;
     for (int t = tid; t < nu; t += blockDim.x) {
-        vcol[b * VCAP + t] = lst[t];
-        vval[b * VCAP + t] = f2h_bits(w[t] / sum);
+        vcol[b * vcap + t] = lst[t];
+        vval[b * vcap + t] = f2h_bits(w[t] / sum);
     }
     if (tid == 0) vnnz[b] = nu;
+}
+
+// R3 for any k1: the same steps as kreciprocal_kernel with the lists on a per-workgroup slab
+// of global scratch (KrSlab; a workgroup's slab is only touched by its own threads, ordered by
+// its barriers).  Rows b = blockIdx.x, + gridDim.x, ... < nrows.
+__global__ __launch_bounds__(256) void kreciprocal_generic_kernel(DistSrc ds, const float* __restrict__ rowdiv,
+                                                                  const int32_t* __restrict__ R, int64_t ldr,
+                                                                  int64_t row0, int64_t nrows, int kf, int kh1,
+                                                                  KrSlab sl, char* __restrict__ slab,
+                                                                  int32_t* __restrict__ vcol,
+                                                                  uint16_t* __restrict__ vval,
+                                                                  int32_t* __restrict__ vnnz, int64_t vcap,
+                                                                  int32_t* __restrict__ flags) {
+    __shared__ int wsum[4];
+    __shared__ int s_nk, s_n, s_nu;
+    __shared__ float s_sum;
+    char* base = slab + (int64_t)blockIdx.x * sl.bytes;
+    int32_t* kr = (int32_t*)(base + sl.kr);
+    int32_t* krs = (int32_t*)(base + sl.krs);
+    int32_t* ncnt = (int32_t*)(base + sl.ncnt);
+    int32_t* acc = (int32_t*)(base + sl.acc);
+    int32_t* cs = (int32_t*)(base + sl.cs);
+    int32_t* lst = (int32_t*)(base + sl.lst);
+    float* w = (float*)(base + sl.w);
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    for (int64_t b = blockIdx.x; b < nrows; b += gridDim.x) {
+        const int64_t i = row0 + b;
+        // k-reciprocal set of i at depth kf in forward order (reranking.py:53-56)
+        if (tid == 0) s_nk = 0;
+        __syncthreads();
+        for (int f0 = 0; f0 < kf; f0 += 256) {
+            const int f = f0 + tid;
+            bool keep = false;
+            int32_t c = -1;
+            if (f < kf) {
+                c = R[i * ldr + f];
+                keep = row_has(R, ldr, c, kf, (int32_t)i);
+            }
+            const unsigned long long m = __ballot(keep);
+            if (lane == 0) wsum[wv] = __popcll(m);
+            __syncthreads();
+            int before = s_nk;
+            for (int q = 0; q < wv; q++) before += wsum[q];
+            if (keep) kr[before + __popcll(m & ((1ull << lane) - 1ull))] = c;
+            __syncthreads();
+            if (tid == 0) s_nk += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+            __syncthreads();
+        }
+        const int nk = s_nk;
+        // a sorted copy for the intersection counts (np.intersect1d of unique sets)
+        const int Pk = pow2_ceil_i(nk < 2 ? 2 : nk);
+        for (int t = tid; t < Pk; t += blockDim.x) krs[t] = t < nk ? kr[t] : 0x7fffffff;
+        __syncthreads();
+        bitonic_sort_i32(krs, Pk);
+        // each candidate's half-depth reciprocal set and the 2/3 overlap rule (reranking.py:57-65)
+        for (int t = tid; t < nk; t += blockDim.x) {
+            const int32_t a = kr[t];
+            int32_t* ct = cs + (int64_t)t * kh1;
+            int nc = 0;
+            for (int f = 0; f < kh1; f++) {
+                const int32_t c = R[(int64_t)a * ldr + f];
+                if (row_has(R, ldr, c, kh1, a)) ct[nc++] = c;
+            }
+            int inter = 0;
+            for (int q = 0; q < nc; q++) {
+                int lo = 0, hi = nk;
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (krs[mid] < ct[q]) lo = mid + 1; else hi = mid;
+                }
+                inter += lo < nk && krs[lo] == ct[q];
+            }
+            ncnt[t] = nc;
+            acc[t] = (double)inter > 2.0 / 3.0 * (double)nc;
+        }
+        if (tid == 0) s_n = nk;
+        for (int t = tid; t < nk; t += blockDim.x) lst[t] = kr[t];
+        __syncthreads();
+        for (int t = tid; t < nk; t += blockDim.x)
+            if (acc[t]) {
+                const int nc = ncnt[t];
+                const int bs = atomicAdd(&s_n, nc);
+                for (int q = 0; q < nc; q++) lst[bs + q] = cs[(int64_t)t * kh1 + q];
+            }
+        __syncthreads();
+        const int n = s_n;
+        const int P = pow2_ceil_i(n < 2 ? 2 : n);
+        for (int t = n + tid; t < P; t += blockDim.x) lst[t] = 0x7fffffff;
+        __syncthreads();
+        bitonic_sort_i32(lst, P);
+        if (tid == 0) {  // np.unique
+            int nu = 0;
+            for (int t = 0; t < n; t++)
+                if (nu == 0 || lst[t] != lst[nu - 1]) lst[nu++] = lst[t];
+            s_nu = nu;
+        }
+        __syncthreads();
+        const int nu = s_nu;
+        const float dv = rowdiv[i];
+        for (int t = tid; t < nu; t += blockDim.x) w[t] = np_expf(-(dist_at(ds, i, lst[t]) / dv));
+        __syncthreads();
+        if (tid == 0) s_sum = pairwise_f32(w, nu);
+        __syncthreads();
+        if (nu > vcap) {
+            if (tid == 0) { atomicOr(flags, RR_SCRATCH); vnnz[b] = 0; }
+        } else {
+            const float sum = s_sum;
+            for (int t = tid; t < nu; t += blockDim.x) {
+                vcol[b * vcap + t] = lst[t];
+                vval[b * vcap + t] = f2h_bits(w[t] / sum);
+            }
+            if (tid == 0) vnnz[b] = nu;
+        }
+        __syncthreads();  // the slab and the shared counters are reused by the next row
+    }
 }
 
 // --------------------------------------------------------------------- R4: QE
@@ -306,9 +502,12 @@ __global__ __launch_bounds__(256) void kreciprocal_kernel(DistSrc ds, const floa
 // i = row0 + blockIdx.x (output row blockIdx.x).  Entries of the k2 (column-sorted) rows
 // are staged in LDS; the first occurrence of each column owns it and sums that column over
 // all k2 rows in j order (binary search).
+// A row whose k2 rows stage more than LCAP entries, or that produces more than QCAP, is appended
+// to the deferred list (dlist[atomicAdd(dcount)] = b, qnnz[b] = 0) for qe_generic_kernel.
 __global__ __launch_bounds__(256) void qe_kernel(const int32_t* __restrict__ R, int64_t ldr, int k2, int64_t row0,
                                                  Rows V, int32_t* __restrict__ qcol, uint16_t* __restrict__ qval,
-                                                 int32_t* __restrict__ qnnz, int32_t* __restrict__ flags) {
+                                                 int32_t* __restrict__ qnnz, int64_t qcap,
+                                                 int32_t* __restrict__ dlist, int32_t* __restrict__ dcount) {
     __shared__ int32_t scol[LCAP];
     __shared__ uint16_t sval[LCAP];
     __shared__ int soff[33];
@@ -339,7 +538,7 @@ __global__ __launch_bounds__(256) void qe_kernel(const int32_t* __restrict__ R, 
     }
     __syncthreads();
     if (s_bad) {
-        if (tid == 0) { atomicOr(flags, RR_LCAP); qnnz[b] = 0; }
+        if (tid == 0) { qnnz[b] = 0; dlist[atomicAdd(dcount, 1)] = (int32_t)b; }
         return;
     }
     for (int j = 0; j < k2; j++) {
@@ -379,7 +578,7 @@ __global__ __launch_bounds__(256) void qe_kernel(const int32_t* __restrict__ R, 
     __syncthreads();
     const int no = s_no;
     if (no > QCAP) {
-        if (tid == 0) { atomicOr(flags, RR_QCAP); qnnz[b] = 0; }
+        if (tid == 0) { qnnz[b] = 0; dlist[atomicAdd(dcount, 1)] = (int32_t)b; }
         return;
     }
     // sort (column, bits) pairs by column: reuse the int sort on packed keys
@@ -405,10 +604,137 @@ __global__ __launch_bounds__(256) void qe_kernel(const int32_t* __restrict__ R, 
         }
     for (int t = tid; t < no; t += blockDim.x) {
         const int32_t k = keys[t];
-        qcol[b * QCAP + t] = ocol[k];
-        qval[b * QCAP + t] = oval[k];
+        qcol[b * qcap + t] = ocol[k];
+        qval[b * qcap + t] = oval[k];
     }
     if (tid == 0) qnnz[b] = no;
+}
+
+// Every row(s) of i = row0 + b to all deferred rows b = dlist[d], d < *dcount (or all rows b <
+// nrows when dlist is null): the same arithmetic as qe_kernel (first occurrence of a column owns
+// it and sums it over the k2 rows in j order) with the k2 rows staged on a per-workgroup slab
+// (QeSlab, sized for k2 rows of the V bound) and the output sorted there.  mode 0: qnnz[b] = the
+// row's entry count only; mode 1: the row to CSR at qoff[b] (qnnz untouched); mode 2: the row
+// to ELL row b (width qcap) and qnnz[b].
+__device__ void bitonic_sort_i32_u16(int32_t* k, uint16_t* v, int P) {
+    for (int kk = 2; kk <= P; kk <<= 1)
+        for (int j = kk >> 1; j > 0; j >>= 1) {
+            for (int t = threadIdx.x; t < P; t += blockDim.x) {
+                const int o = t ^ j;
+                if (o > t) {
+                    const bool up = (t & kk) == 0;
+                    const int32_t x = k[t], y = k[o];
+                    if ((x > y) == up) {
+                        k[t] = y;
+                        k[o] = x;
+                        const uint16_t a = v[t];
+                        v[t] = v[o];
+                        v[o] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+}
+
+__global__ __launch_bounds__(256) void qe_generic_kernel(const int32_t* __restrict__ R, int64_t ldr, int k2,
+                                                         int64_t row0, Rows V, const int32_t* __restrict__ dlist,
+                                                         const int32_t* __restrict__ dcount, int64_t nrows, int mode,
+                                                         int32_t* __restrict__ qcol, uint16_t* __restrict__ qval,
+                                                         int32_t* __restrict__ qnnz, int64_t qcap,
+                                                         const int64_t* __restrict__ qoff, QeSlab sl,
+                                                         char* __restrict__ slab, int64_t tcap,
+                                                         int32_t* __restrict__ flags) {
+    __shared__ int s_tot, s_no;
+    char* base = slab + (int64_t)blockIdx.x * sl.bytes;
+    int32_t* soff = (int32_t*)(base + sl.soff);
+    int32_t* scol = (int32_t*)(base + sl.scol);
+    uint16_t* sval = (uint16_t*)(base + sl.sval);
+    int32_t* okey = (int32_t*)(base + sl.okey);
+    uint16_t* oval = (uint16_t*)(base + sl.oval);
+    const int tid = threadIdx.x;
+    const int64_t nd = dcount ? (int64_t)*dcount : nrows;
+    const float fk2 = (float)k2;
+    for (int64_t d = blockIdx.x; d < nd; d += gridDim.x) {
+        const int64_t b = dlist ? dlist[d] : d;
+        const int64_t i = row0 + b;
+        if (tid == 0) {
+            int64_t o = 0;
+            for (int j = 0; j < k2; j++) {
+                soff[j] = (int32_t)o;
+                o += V.len(R[i * ldr + j]);
+            }
+            soff[k2] = (int32_t)(o < tcap ? o : tcap);
+            s_tot = o > tcap ? -1 : (int)o;
+            s_no = 0;
+        }
+        __syncthreads();
+        const int tot = s_tot;
+        if (tot < 0) {  // beyond the slab (not for tcap from rr_caps)
+            if (tid == 0) {
+                atomicOr(flags, RR_SCRATCH);
+                if (mode != 1) qnnz[b] = 0;
+            }
+            __syncthreads();
+            continue;
+        }
+        for (int j = 0; j < k2; j++) {
+            const int64_t rb = V.beg(R[i * ldr + j]);
+            const int n = soff[j + 1] - soff[j];
+            for (int t = tid; t < n; t += blockDim.x) {
+                scol[soff[j] + t] = V.col[rb + t];
+                sval[soff[j] + t] = V.val[rb + t];
+            }
+        }
+        __syncthreads();
+        for (int e = tid; e < tot; e += blockDim.x) {
+            int lo = 0, hi = k2;  // the row of entry e: the largest j with soff[j] <= e
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (soff[mid] <= e) lo = mid; else hi = mid - 1;
+            }
+            const int j = lo;
+            const int32_t c = scol[e];
+            bool first = true;
+            float acc = 0.f;
+            for (int jj = 0; jj < k2; jj++) {
+                int a = soff[jj], z = soff[jj + 1];
+                while (a < z) {
+                    const int mid = (a + z) >> 1;
+                    if (scol[mid] < c) a = mid + 1; else z = mid;
+                }
+                const bool hit = a < soff[jj + 1] && scol[a] == c;
+                if (hit && jj < j) { first = false; break; }
+                if (hit) acc += h2f_bits(sval[a]);
+            }
+            if (!first) continue;
+            const uint16_t h = f2h_bits(acc / fk2);
+            if (h & 0x7fff) {
+                const int p = atomicAdd(&s_no, 1);
+                okey[p] = c;
+                oval[p] = h;
+            }
+        }
+        __syncthreads();
+        const int no = s_no;
+        if (mode == 0) {
+            if (tid == 0) qnnz[b] = no;
+            __syncthreads();
+            continue;
+        }
+        const int P = pow2_ceil_i(no < 2 ? 2 : no);
+        for (int t = no + tid; t < P; t += blockDim.x) { okey[t] = 0x7fffffff; oval[t] = 0; }
+        __syncthreads();
+        bitonic_sort_i32_u16(okey, oval, P);
+        if (mode == 1) {
+            const int64_t o = qoff[b];
+            for (int t = tid; t < no; t += blockDim.x) { qcol[o + t] = okey[t]; qval[o + t] = oval[t]; }
+        } else {
+            for (int t = tid; t < no; t += blockDim.x) { qcol[b * qcap + t] = okey[t]; qval[b * qcap + t] = oval[t]; }
+            if (tid == 0) qnnz[b] = no;
+        }
+        __syncthreads();
+    }
 }
 
 // ---------------------------------------------------- ELL -> CSR, row lengths
@@ -632,41 +958,64 @@ __global__ __launch_bounds__(256) void jaccard_kernel(const float* __restrict__ 
 
 // ---------------------------------------------------------------- workspace
 struct RrPlan {
-    int64_t dist, tdist, rowmax, rank, vcol, vval, vnnz, qcol, qval, qnnz, cnt, off, cur, irow, ival, total;
-    int K;
+    int64_t dist, tdist, rowmax, rank, vcol, vval, vnnz, qcol, qval, qnnz, cnt, off, cur, irow, ival, dlist, dcount,
+        krslab, qeslab, total;
+    RrCaps caps;
+    KrSlab kr;
+    QeSlab qe;
 };
 
 static int64_t al(int64_t v) { return (v + 255) & ~(int64_t)255; }
 
+// One-call driver: V and V_qe as ELL of their worst-case widths (rr_caps), so no row can
+// overflow; the generic kernels' slabs only when a row can need them.
 static RrPlan rr_plan(int64_t N, int k1, int k2, bool need_dist, bool need_t) {
     RrPlan p{};
-    int K = k1 + 1 > k2 ? k1 + 1 : k2;
-    if (K > N) K = (int)N;
-    p.K = K;
+    p.caps = rr_caps(N, k1, k2);
+    const RrCaps& c = p.caps;
+    const int64_t qw = k2 != 1 ? c.qcap : 0;
+    p.kr = kr_slab(c.kf, c.kh1);
+    p.qe = qe_slab(c.k2e, c.tcap);
     int64_t o = 0;
     p.dist = o; o = al(o + (need_dist ? N * N * 4 : 0) + (need_dist ? N * 4 : 0));
     p.tdist = o; o = al(o + (need_t ? N * N * 4 : 0));
     p.rowmax = o; o = al(o + N * 4);
-    p.rank = o; o = al(o + N * (int64_t)K * 4);
-    p.vcol = o; o = al(o + N * (int64_t)VCAP * 4);
-    p.vval = o; o = al(o + N * (int64_t)VCAP * 2);
+    p.rank = o; o = al(o + N * (int64_t)c.K * 4);
+    p.vcol = o; o = al(o + N * c.vcap * 4);
+    p.vval = o; o = al(o + N * c.vcap * 2);
     p.vnnz = o; o = al(o + N * 4);
-    p.qcol = o; o = al(o + N * (int64_t)QCAP * 4);
-    p.qval = o; o = al(o + N * (int64_t)QCAP * 2);
+    p.qcol = o; o = al(o + N * qw * 4);
+    p.qval = o; o = al(o + N * qw * 2);
     p.qnnz = o; o = al(o + N * 4);
     p.cnt = o; o = al(o + N * 4);
     p.off = o; o = al(o + (N + 1) * 8);
     p.cur = o; o = al(o + N * 4);
-    p.irow = o; o = al(o + N * (int64_t)QCAP * 4);
-    p.ival = o; o = al(o + N * (int64_t)QCAP * 2);
+    const int64_t inv = k2 != 1 ? qw : c.vcap;  // inverted-index entries per row (upper bound)
+    p.irow = o; o = al(o + N * inv * 4);
+    p.ival = o; o = al(o + N * inv * 2);
+    p.dlist = o; o = al(o + N * 4);
+    p.dcount = o; o = al(o + 16);
+    p.krslab = o; o = al(o + (c.kr_fast ? 0 : GEN_WG * p.kr.bytes));
+    p.qeslab = o; o = al(o + (k2 != 1 ? GEN_WG * p.qe.bytes : 0));
     p.total = o;
     return p;
 }
 
-static void kr_depths(int k1, int64_t N, int& kf, int& kh1) {
-    kf = (int)(k1 + 1 < N ? k1 + 1 : N);
-    const int kh = (int)__builtin_nearbyint((double)k1 / 2.0);  // int(np.around(k1/2))
-    kh1 = (int)(kh + 1 < N ? kh + 1 : N);
+// R3 over rows [row0, row0 + n) into the ELL (vcol, vval, vnnz) of width caps.vcap.
+static int v_rows_launch(const DistSrc& ds, const float* rowdiv, const int32_t* R, int64_t ldr, int64_t row0,
+                         int64_t n, const RrCaps& c, char* krslab, int32_t* vcol, uint16_t* vval, int32_t* vnnz,
+                         int32_t* flags, hipStream_t s) {
+    if (n == 0) return OK;
+    if (c.kr_fast) {
+        hipLaunchKernelGGL(kreciprocal_kernel, dim3((unsigned)n), dim3(256), 0, s, ds, rowdiv, R, ldr, row0, c.kf, c.kh1,
+                           vcol, vval, vnnz, c.vcap, flags);
+    } else {
+        const KrSlab sl = kr_slab(c.kf, c.kh1);
+        hipLaunchKernelGGL(kreciprocal_generic_kernel, dim3((unsigned)(n < GEN_WG ? n : GEN_WG)), dim3(256), 0, s, ds,
+                           rowdiv, R, ldr, row0, n, c.kf, c.kh1, sl, krslab, vcol, vval, vnnz, c.vcap, flags);
+    }
+    RM_LAUNCHED();
+    return OK;
 }
 
 // Jaccard over unsorted inverted lists: every chunk scans whole lists and filters rows.
@@ -716,32 +1065,39 @@ __global__ __launch_bounds__(256) void jaccard_scan_kernel(const float* __restri
 // od rows: OD (N x N, row i = distances from item i, scaled by 1/rowdiv[i] on the fly).
 static int rerank_core(const float* OD, int64_t N, int64_t Q, int k1, int k2, uint16_t lam16, float lam_f,
                        float* out, int64_t ldo, char* ws, const RrPlan& P, int32_t* flags, hipStream_t s) {
+    const RrCaps& c = P.caps;
     float* rmax = (float*)(ws + P.rowmax);
     int32_t* R = (int32_t*)(ws + P.rank);
     hipLaunchKernelGGL(rowmax_kernel, dim3(ceil_div(N, 4)), dim3(256), 0, s, OD, N, N, N, rmax);
     RM_LAUNCHED();
     int rc;
-    if ((rc = topk_launch(OD, N, N, N, rmax, P.K, R, nullptr, P.K, s))) return rc;
-    int kf, kh1;
-    kr_depths(k1, N, kf, kh1);
-    RM_REQUIRE(k1 >= 1 && k1 <= 50, "rerank: 1 <= k1 <= 50 (expansion list capacity)");
+    if ((rc = topk_launch(OD, N, N, N, rmax, c.K, R, nullptr, c.K, s))) return rc;
     int32_t* vcol = (int32_t*)(ws + P.vcol);
     uint16_t* vval = (uint16_t*)(ws + P.vval);
     int32_t* vnnz = (int32_t*)(ws + P.vnnz);
     const DistSrc ds{OD, N, 0, nullptr, 0, 0, nullptr};
-    hipLaunchKernelGGL(kreciprocal_kernel, dim3((unsigned)N), dim3(256), 0, s, ds, rmax, R, (int64_t)P.K, (int64_t)0,
-                       kf, kh1, vcol, vval, vnnz, flags);
-    RM_LAUNCHED();
-    Rows Vq{nullptr, vnnz, VCAP, vcol, vval};
+    if ((rc = v_rows_launch(ds, rmax, R, c.K, 0, N, c, ws + P.krslab, vcol, vval, vnnz, flags, s))) return rc;
+    Rows Vq{nullptr, vnnz, c.vcap, vcol, vval};
     if (k2 != 1) {
-        RM_REQUIRE(k2 <= 32 && k2 <= P.K, "rerank: k2 must be <= 32");
         int32_t* qcol = (int32_t*)(ws + P.qcol);
         uint16_t* qval = (uint16_t*)(ws + P.qval);
         int32_t* qnnz = (int32_t*)(ws + P.qnnz);
-        hipLaunchKernelGGL(qe_kernel, dim3((unsigned)N), dim3(256), 0, s, R, (int64_t)P.K, k2, (int64_t)0,
-                           Rows{nullptr, vnnz, VCAP, vcol, vval}, qcol, qval, qnnz, flags);
+        int32_t* dlist = (int32_t*)(ws + P.dlist);
+        int32_t* dcount = (int32_t*)(ws + P.dcount);
+        const Rows V{nullptr, vnnz, c.vcap, vcol, vval};
+        if (c.k2e <= QE_FAST_K2) {
+            RM_CHECK_HIP(hipMemsetAsync(dcount, 0, 4, s));
+            hipLaunchKernelGGL(qe_kernel, dim3((unsigned)N), dim3(256), 0, s, R, (int64_t)c.K, c.k2e, (int64_t)0, V, qcol,
+                               qval, qnnz, c.qcap, dlist, dcount);
+            RM_LAUNCHED();
+        }
+        // the rows qe_kernel deferred (or every row): their count is read on the device
+        hipLaunchKernelGGL(qe_generic_kernel, dim3(GEN_WG), dim3(256), 0, s, R, (int64_t)c.K, c.k2e, (int64_t)0, V,
+                           c.k2e <= QE_FAST_K2 ? (const int32_t*)dlist : nullptr,
+                           c.k2e <= QE_FAST_K2 ? (const int32_t*)dcount : nullptr, N, 2, qcol,
+                           qval, qnnz, c.qcap, (const int64_t*)nullptr, P.qe, ws + P.qeslab, c.tcap, flags);
         RM_LAUNCHED();
-        Vq = Rows{nullptr, qnnz, QCAP, qcol, qval};
+        Vq = Rows{nullptr, qnnz, c.qcap, qcol, qval};
     }
     int32_t* cnt = (int32_t*)(ws + P.cnt);
     int64_t* off = (int64_t*)(ws + P.off);
@@ -774,6 +1130,7 @@ using namespace reidmi;
 REIDMI_API int64_t reidmi_rerank_workspace_bytes(int64_t Q, int64_t G, int k1, int k2, int from_dist,
                                                  int need_transpose) {
     const int64_t N = Q + G;
+    if (Q < 0 || G < 0 || N <= 0 || k1 < 1 || k2 < 1) return -1;
     return rr_plan(N, k1, k2, !from_dist, from_dist && need_transpose).total;
 }
 
@@ -781,7 +1138,8 @@ REIDMI_API int reidmi_rerank(const float* feat, int64_t Q, int64_t G, int64_t D,
                              uint16_t one_minus_lambda_h, float lambda_f, float* final_dist, int64_t ldo, void* ws_,
                              int64_t ws_bytes, int32_t* flags, void* stream) {
     const int64_t N = Q + G;
-    RM_REQUIRE(Q >= 0 && G >= 0 && N > 0 && D > 0 && ldf >= D && ldo >= G && flags, "rerank: bad arguments");
+    RM_REQUIRE(Q >= 0 && G >= 0 && N > 0 && D > 0 && ldf >= D && ldo >= G && flags && k1 >= 1 && k2 >= 1,
+               "rerank: bad arguments");
     RM_REQUIRE(N < 0x7fffffff, "rerank: too many items");
     const RrPlan P = rr_plan(N, k1, k2, true, false);
     RM_REQUIRE(ws_bytes >= P.total, "rerank: workspace too small");
@@ -799,7 +1157,8 @@ REIDMI_API int reidmi_rerank_from_dist(const float* dist, const float* add, int6
                                        int k1, int k2, uint16_t one_minus_lambda_h, float lambda_f, float* final_dist,
                                        int64_t ldo, void* ws_, int64_t ws_bytes, int32_t* flags, void* stream) {
     const int64_t N = Q + G;
-    RM_REQUIRE(Q >= 0 && G >= 0 && N > 0 && ldo >= G && flags, "rerank_from_dist: bad arguments");
+    RM_REQUIRE(Q >= 0 && G >= 0 && N > 0 && ldo >= G && flags && k1 >= 1 && k2 >= 1,
+               "rerank_from_dist: bad arguments");
     const bool need_t = !symmetric || add != nullptr;
     const RrPlan P = rr_plan(N, k1, k2, false, need_t);
     RM_REQUIRE(ws_bytes >= P.total, "rerank_from_dist: workspace too small");
@@ -815,14 +1174,65 @@ REIDMI_API int reidmi_rerank_from_dist(const float* dist, const float* add, int6
     return rerank_core(OD, N, Q, k1, k2, one_minus_lambda_h, lambda_f, final_dist, ldo, ws, P, flags, s);
 }
 
+// dlist[t] = t for t < n, *dcount = n (every row deferred)
+__global__ void iota_kernel(int32_t* __restrict__ dlist, int64_t n, int32_t* __restrict__ dcount) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < n) dlist[t] = (int32_t)t;
+    if (t == 0) *dcount = (int32_t)n;
+}
+
+// ------------------------------------------------- small row utilities (staged R2)
+// Ordered compaction: idx[0 .. *count) = the positions p < n with flags[p] != 0, ascending
+// (np.nonzero).  One 1024-thread workgroup: each pass ballots 1024 flags, the waves' counts
+// are scanned in LDS.
+__global__ __launch_bounds__(1024) void nonzero_kernel(const int32_t* __restrict__ flags, int64_t n,
+                                                       int32_t* __restrict__ idx, int32_t* __restrict__ count) {
+    __shared__ int wsum[16];
+    __shared__ int s_base;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (threadIdx.x == 0) s_base = 0;
+    __syncthreads();
+    for (int64_t p0 = 0; p0 < n; p0 += 1024) {
+        const int64_t p = p0 + threadIdx.x;
+        const bool k = p < n && flags[p] != 0;
+        const uint64_t m = __ballot(k);
+        if (lane == 0) wsum[wv] = __popcll(m);
+        __syncthreads();
+        int before = s_base;
+        for (int w = 0; w < wv; w++) before += wsum[w];
+        if (k) idx[before + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)p;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int t = 0;
+            for (int w = 0; w < 16; w++) t += wsum[w];
+            s_base += t;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *count = s_base;
+}
+
+// out[r][:] = x[row0 + idx[r]][:] (fp32 rows of d floats, 16-byte loads when aligned)
+__global__ void gather_rows_kernel(const float* __restrict__ x, int64_t ldx, int64_t d, int64_t row0,
+                                   const int32_t* __restrict__ idx, float* __restrict__ out, int64_t ldo) {
+    const int64_t r = blockIdx.x;
+    const float* src = x + (row0 + idx[r]) * ldx;
+    float* dst = out + r * ldo;
+    for (int64_t c = threadIdx.x; c < d; c += blockDim.x) dst[c] = src[c];
+}
+
 // ------------------------------------------------------------ staged re-ranking
 // The same R1-R7 as row-range stages over caller-allocated, exactly sized buffers, so the
 // N x N distance is never materialised (row chunks of it are) and the rows can be sharded
 // over ranks with all-gathers between stages (multimodal_reid_amd/reranking.py).
-REIDMI_API int reidmi_rr_caps(int* vcap, int* qcap) {
-    RM_REQUIRE(vcap && qcap, "rr_caps: null");
-    *vcap = VCAP;
+REIDMI_API int reidmi_rr_caps(int64_t N, int k1, int k2, int64_t* vcap, int64_t* qcap, int64_t* v_ws_bytes,
+                              int64_t* qe_ws_bytes) {
+    RM_REQUIRE(N > 0 && k1 >= 1 && k2 >= 1 && vcap && qcap, "rr_caps: bad arguments");
+    const RrCaps c = rr_caps(N, k1, k2);
+    *vcap = c.vcap;
     *qcap = QCAP;
+    if (v_ws_bytes) *v_ws_bytes = c.kr_fast ? 0 : GEN_WG * kr_slab(c.kf, c.kh1).bytes;
+    if (qe_ws_bytes) *qe_ws_bytes = GEN_WG * qe_slab(c.k2e, c.tcap).bytes;
     return OK;
 }
 
@@ -885,17 +1295,15 @@ REIDMI_API int reidmi_rr_rank_rows_f16(const float* feat, int64_t N, int64_t D, 
 
 REIDMI_API int reidmi_rr_v_rows(const float* feat, int64_t N, int64_t D, int64_t ldf, const float* sqn,
                                 const float* rowmax, const int32_t* rank, int K, int64_t lo, int64_t hi, int k1,
-                                int32_t* vcol, uint16_t* vval, int32_t* vnnz, int32_t* flags, void* stream) {
+                                int32_t* vcol, uint16_t* vval, int32_t* vnnz, void* ws, int64_t ws_bytes,
+                                int32_t* flags, void* stream) {
     RM_REQUIRE(N > 0 && D > 0 && ldf >= D && 0 <= lo && lo <= hi && hi <= N && flags, "rr_v_rows: bad arguments");
-    RM_REQUIRE(k1 >= 1 && k1 <= 50 && K >= (k1 + 1 < N ? k1 + 1 : N), "rr_v_rows: 1 <= k1 <= 50, K >= k1+1");
-    if (hi == lo) return OK;
-    int kf, kh1;
-    kr_depths(k1, N, kf, kh1);
+    RM_REQUIRE(k1 >= 1 && K >= (k1 + 1 < N ? k1 + 1 : N), "rr_v_rows: k1 >= 1, K >= min(k1 + 1, N)");
+    const RrCaps c = rr_caps(N, k1, 1);
+    RM_REQUIRE(c.kr_fast || (ws && ws_bytes >= GEN_WG * kr_slab(c.kf, c.kh1).bytes),
+               "rr_v_rows: workspace of reidmi_rr_caps' v_ws_bytes required");
     const DistSrc ds{nullptr, 0, 0, feat, ldf, (int)D, sqn};
-    hipLaunchKernelGGL(kreciprocal_kernel, dim3((unsigned)(hi - lo)), dim3(256), 0, (hipStream_t)stream, ds, rowmax,
-                       rank, (int64_t)K, lo, kf, kh1, vcol, vval, vnnz, flags);
-    RM_LAUNCHED();
-    return OK;
+    return v_rows_launch(ds, rowmax, rank, K, lo, hi - lo, c, (char*)ws, vcol, vval, vnnz, flags, (hipStream_t)stream);
 }
 
 REIDMI_API int reidmi_rr_row_offsets(const int32_t* nnz, int64_t rows, int64_t* off, void* stream) {
@@ -915,14 +1323,52 @@ REIDMI_API int reidmi_rr_pack(const int32_t* ell_col, const uint16_t* ell_val, c
     return OK;
 }
 
+// R4 main pass: rows lo..hi of V_qe into the ELL (qcol, qval, qnnz) of width
+// reidmi_rr_caps' qcap; rows it cannot assemble in LDS get qnnz = 0 and are listed in
+// dlist[0 .. *dcount) (dcount: device int32, cleared by the call) for reidmi_rr_qe_deferred.
 REIDMI_API int reidmi_rr_qe_rows(const int32_t* rank, int K, int k2, int64_t lo, int64_t hi, const int64_t* voff,
                                  const int32_t* vcol, const uint16_t* vval, int32_t* qcol, uint16_t* qval,
-                                 int32_t* qnnz, int32_t* flags, void* stream) {
-    RM_REQUIRE(0 <= lo && lo <= hi && flags && voff, "rr_qe_rows: bad arguments");
-    RM_REQUIRE(k2 >= 2 && k2 <= 32 && k2 <= K, "rr_qe_rows: 2 <= k2 <= min(32, K) (k2 = 1 means V_qe = V)");
-    if (hi == lo) return OK;
-    hipLaunchKernelGGL(qe_kernel, dim3((unsigned)(hi - lo)), dim3(256), 0, (hipStream_t)stream, rank, (int64_t)K, k2,
-                       lo, Rows{voff, nullptr, 0, vcol, vval}, qcol, qval, qnnz, flags);
+                                 int32_t* qnnz, int32_t* dlist, int32_t* dcount, void* stream) {
+    RM_REQUIRE(0 <= lo && lo <= hi && voff && dlist && dcount, "rr_qe_rows: bad arguments");
+    RM_REQUIRE(k2 >= 2 && k2 <= K, "rr_qe_rows: 2 <= k2 <= K (k2 = 1 means V_qe = V)");
+    hipStream_t s = (hipStream_t)stream;
+    const int64_t n = hi - lo;
+    if (k2 <= QE_FAST_K2) {
+        RM_CHECK_HIP(hipMemsetAsync(dcount, 0, 4, s));
+        if (n == 0) return OK;
+        hipLaunchKernelGGL(qe_kernel, dim3((unsigned)n), dim3(256), 0, s, rank, (int64_t)K, k2, lo,
+                           Rows{voff, nullptr, 0, vcol, vval}, qcol, qval, qnnz, (int64_t)QCAP, dlist, dcount);
+        RM_LAUNCHED();
+        return OK;
+    }
+    // k2 beyond the LDS kernel: every row is deferred
+    RM_CHECK_HIP(hipMemsetAsync(qnnz, 0, n * 4, s));
+    hipLaunchKernelGGL(iota_kernel, dim3(ceil_div(n > 0 ? n : 1, 256)), dim3(256), 0, s, dlist, n, dcount);
+    RM_LAUNCHED();
+    return OK;
+}
+
+// R4 for the rows deferred by reidmi_rr_qe_rows (dlist[0 .. n_def), relative to lo), on the
+// workspace slabs (reidmi_rr_caps' qe_ws_bytes for the same N, k1, k2): mode 0 writes their
+// entry counts to qnnz[b]; mode 1 writes the rows to CSR at qoff[b] (qoff: offsets of rows lo..hi).
+REIDMI_API int reidmi_rr_qe_deferred(const int32_t* rank, int K, int k1, int k2, int64_t lo, int64_t N,
+                                     const int64_t* voff, const int32_t* vcol, const uint16_t* vval,
+                                     const int32_t* dlist, int64_t n_def, int mode, const int64_t* qoff, int32_t* qcol,
+                                     uint16_t* qval, int32_t* qnnz, void* ws, int64_t ws_bytes, int32_t* flags,
+                                     void* stream) {
+    RM_REQUIRE(lo >= 0 && N > 0 && k1 >= 1 && voff && n_def >= 0 && (mode == 0 || mode == 1) && flags,
+               "rr_qe_deferred: bad arguments");
+    RM_REQUIRE(k2 >= 2 && k2 <= K, "rr_qe_deferred: 2 <= k2 <= K");
+    RM_REQUIRE(mode == 0 ? qnnz != nullptr : (qoff && qcol && qval), "rr_qe_deferred: outputs");
+    if (n_def == 0) return OK;
+    RM_REQUIRE(dlist && n_def < (1ll << 31), "rr_qe_deferred: dlist");
+    const RrCaps c = rr_caps(N, k1, k2);
+    const QeSlab sl = qe_slab(k2, c.tcap);
+    RM_REQUIRE(ws && ws_bytes >= GEN_WG * sl.bytes, "rr_qe_deferred: workspace of reidmi_rr_caps' qe_ws_bytes required");
+    hipLaunchKernelGGL(qe_generic_kernel, dim3((unsigned)(n_def < GEN_WG ? n_def : GEN_WG)), dim3(256), 0,
+                       (hipStream_t)stream, rank, (int64_t)K, k2, lo, Rows{voff, nullptr, 0, vcol, vval}, dlist,
+                       (const int32_t*)nullptr, n_def, mode, qcol, qval, qnnz, (int64_t)0, qoff, sl, (char*)ws, c.tcap,
+                       flags);
     RM_LAUNCHED();
     return OK;
 }
@@ -973,15 +1419,15 @@ REIDMI_API int reidmi_rr_csc(int64_t N, const int64_t* qoff, const int32_t* qcol
     return OK;
 }
 
-// rows of G floats of the jaccard scratch kept for the column chunk bounds (int64 per column
-// and chunk boundary, 16-byte aligned)
-static int64_t jaccard_reserved_rows(int64_t N, int64_t G) {
+// bytes of the per-column chunk bounds of reidmi_rr_jaccard_rows (int64 per column and chunk
+// boundary)
+static int64_t jaccard_bounds_bytes(int64_t N, int64_t G) {
     const int64_t nch = (G + JCH - 1) / JCH;
-    return (N * (nch + 1) * 8 + G * 4 - 1) / (G * 4) + 1;
+    return N * (nch + 1) * 8;
 }
 
-REIDMI_API int64_t reidmi_rr_jaccard_reserved_rows(int64_t N, int64_t G) {
-    return N > 0 && G > 0 ? jaccard_reserved_rows(N, G) : -1;
+REIDMI_API int64_t reidmi_rr_jaccard_bounds_bytes(int64_t N, int64_t G) {
+    return N > 0 && G > 0 ? jaccard_bounds_bytes(N, G) : -1;
 }
 
 REIDMI_API int reidmi_rr_jaccard_rows(const float* feat, int64_t N, int64_t D, int64_t ldf, const float* sqn,
@@ -989,7 +1435,7 @@ REIDMI_API int reidmi_rr_jaccard_rows(const float* feat, int64_t N, int64_t D, i
                                       const int32_t* qcol, const uint16_t* qval, const int64_t* coff,
                                       const int32_t* irow, const uint16_t* ival, uint16_t one_minus_lambda_h,
                                       float lambda_f, float* out, int64_t ldo, float* chunk, int64_t chunk_rows,
-                                      void* stream) {
+                                      void* bounds, int64_t bounds_bytes, void* stream) {
     const int64_t G = N - Q;
     RM_REQUIRE(N > 0 && D > 0 && ldf >= D && 0 <= qlo && qlo <= qhi && qhi <= Q && Q <= N && ldo >= G &&
                    chunk_rows > 0 && chunk_rows <= 65535,
@@ -997,12 +1443,10 @@ REIDMI_API int reidmi_rr_jaccard_rows(const float* feat, int64_t N, int64_t D, i
     if (qhi == qlo || G == 0) return OK;
     hipStream_t s = (hipStream_t)stream;
     const Rows Vq{qoff, nullptr, 0, qcol, qval};
-    // the column chunk boundaries take the last rows of the distance scratch
     const int nch = ceil_div(G, JCH);
-    const int64_t steal = jaccard_reserved_rows(N, G);
-    RM_REQUIRE(chunk_rows > steal, "rr_jaccard_rows: chunk_rows must exceed reidmi_rr_jaccard_reserved_rows(N, N-Q)");
-    chunk_rows -= steal;
-    int64_t* cbnd = (int64_t*)(((uintptr_t)(chunk + chunk_rows * G) + 15) & ~(uintptr_t)15);
+    RM_REQUIRE(bounds && ((uintptr_t)bounds & 7) == 0 && bounds_bytes >= jaccard_bounds_bytes(N, G),
+               "rr_jaccard_rows: bounds of reidmi_rr_jaccard_bounds_bytes(N, N-Q) bytes (8-byte aligned) required");
+    int64_t* cbnd = (int64_t*)bounds;
     hipLaunchKernelGGL(jaccard_bounds_kernel, dim3(ceil_div(N * (nch + 1), 256)), dim3(256), 0, s, coff, irow, N, Q,
                        nch, cbnd);
     RM_LAUNCHED();
@@ -1017,5 +1461,34 @@ REIDMI_API int reidmi_rr_jaccard_rows(const float* feat, int64_t N, int64_t D, i
                            irow, ival, (const int64_t*)cbnd, one_minus_lambda_h, lambda_f, out + (a - qlo) * ldo, ldo);
         RM_LAUNCHED();
     }
+    return OK;
+}
+
+// Row maxima skipping NaN (fmaxf), the od divisors of reranking.py:46 for a block of
+// distance rows (rowmax_kernel).
+REIDMI_API int reidmi_rowmax_f32(const float* x, int64_t rows, int64_t cols, int64_t ldx, float* out, void* stream) {
+    RM_REQUIRE(rows >= 0 && cols > 0 && ldx >= cols && out, "rowmax: bad arguments");
+    if (rows == 0) return OK;
+    hipLaunchKernelGGL(rowmax_kernel, dim3(ceil_div(rows, 4)), dim3(256), 0, (hipStream_t)stream, x, rows, cols, ldx,
+                       out);
+    RM_LAUNCHED();
+    return OK;
+}
+
+REIDMI_API int reidmi_nonzero_i32(const int32_t* flags, int64_t n, int32_t* idx, int32_t* count, void* stream) {
+    RM_REQUIRE(n >= 0 && n < 0x7fffffff && count && (n == 0 || (flags && idx)), "nonzero: bad arguments");
+    hipLaunchKernelGGL(nonzero_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, flags, n, idx, count);
+    RM_LAUNCHED();
+    return OK;
+}
+
+REIDMI_API int reidmi_gather_rows_f32(const float* x, int64_t ldx, int64_t d, int64_t row0, const int32_t* idx,
+                                      int64_t n, float* out, int64_t ldo, void* stream) {
+    RM_REQUIRE(n >= 0 && d > 0 && ldx >= d && ldo >= d && (n == 0 || (x && idx && out)), "gather_rows: bad arguments");
+    if (n == 0) return OK;
+    RM_REQUIRE(n < (1ll << 31), "gather_rows: too many rows");
+    hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)n), dim3(256), 0, (hipStream_t)stream, x, ldx, d, row0, idx,
+                       out, ldo);
+    RM_LAUNCHED();
     return OK;
 }

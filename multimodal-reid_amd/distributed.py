@@ -84,6 +84,33 @@ def gather_var(x):
     return torch.cat([bufs[r][:ns[r]] for r in range(W)]).to(x.device).view(dtype)
 
 
+def gather_rows_var(x):
+    """All-gather row blocks of different lengths ([n_r, ...] on rank r); returns (their
+    concatenation in rank order on x's device, [n_0, ..., n_{W-1}]).  The drop-in surface
+    (evaluate.R1_mAP_eval, zero_shot_learning.get_cmc_map) uses it for whatever shards the
+    caller's loaders produced."""
+    rank, W = world()
+    if not _initialized():
+        return x, [x.shape[0]]
+    dev = _collective_device(x)
+    n = torch.tensor([x.shape[0]], dtype=torch.int64, device=dev)
+    ns = [torch.empty_like(n) for _ in range(W)]
+    dist.all_gather(ns, n)
+    ns = [int(v.item()) for v in ns]
+    mx = max(max(ns), 1)
+    pad = torch.zeros((mx,) + tuple(x.shape[1:]), dtype=x.dtype, device=dev)
+    pad[:x.shape[0]] = x.to(dev)
+    if dist.get_backend() == "nccl":
+        out = torch.empty((W * mx,) + tuple(x.shape[1:]), device=dev, dtype=x.dtype)
+        dist.all_gather_into_tensor(out, pad)
+        parts = [out[r * mx:r * mx + ns[r]] for r in range(W)]
+    else:
+        bufs = [torch.empty_like(pad) for _ in range(W)]
+        dist.all_gather(bufs, pad)
+        parts = [bufs[r][:ns[r]] for r in range(W)]
+    return torch.cat(parts).to(x.device), ns
+
+
 def pack_rows(valid, first, ap, nkept):
     """Per-query results as one float64 [Q_local, 4] block (indices < 2^53 are exact)."""
     return torch.stack([torch.as_tensor(valid).double(), torch.as_tensor(first).double(),

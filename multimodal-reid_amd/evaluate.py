@@ -63,7 +63,7 @@ def euclidean_distance_device(qf, gf, out=None):
 
 
 def topk_rows_device(x, k, row_div=None, with_values=False):
-    """np.argsort(x, axis=1, kind='stable')[:, :k] on the GPU (k <= 64)."""
+    """np.argsort(x, axis=1, kind='stable')[:, :k] on the GPU (any k <= columns)."""
     x = _as_dev_f32(x)
     rows, cols = x.shape
     idx = torch.empty((rows, k), device=x.device, dtype=torch.int32)
@@ -147,7 +147,17 @@ def eval_func(distmat, q_pids, g_pids, q_camids, g_camids, max_rank=50):
 class R1_mAP_eval():
     """evaluate.py:91-135.  Features stay on the GPU (the reference copies them to the CPU).
     As in the reference, ``max_rank`` is stored but compute() scores with eval_func's
-    default 50 (evaluate.py:132): the CMC is 50 long whatever max_rank was given."""
+    default 50 (evaluate.py:132): the CMC is 50 long whatever max_rank was given.
+
+    Under a torch.distributed process group (one process per GPU) every rank
+    holds ITS shard: its updates are its query rows followed by its gallery rows, and
+    ``num_query`` is its own query count.  compute() then all-gathers the feature blocks and
+    labels (gallery-sharded embed + RCCL all-gather, the north star's exchange step), scores
+    the query rows shard(Q, rank, W) against the whole gallery (exact distance, or the
+    row-sharded k-reciprocal re-rank), all-gathers the per-query results and reduces them in
+    global query order: every rank returns the CMC/mAP of the single-process run over the
+    rank-ordered concatenation of the shards, bit for bit (contiguous shards in rank order =
+    the single-process order)."""
 
     def __init__(self, num_query, max_rank=50, feat_norm=True, reranking=False):
         super(R1_mAP_eval, self).__init__()
@@ -168,10 +178,13 @@ class R1_mAP_eval():
         self.camids.extend(np.asarray(camid.cpu() if isinstance(camid, torch.Tensor) else camid))
 
     def compute(self):  # called after each epoch
+        from . import distributed as rd
         feats = torch.cat(self.feats, dim=0)
         if self.feat_norm:
             print("The test feature is normalized")
             feats = l2_normalize_device(feats)
+        if rd._initialized():
+            return self._compute_sharded(feats)
         qf = feats[:self.num_query]
         q_pids = np.asarray(self.pids[:self.num_query])
         q_camids = np.asarray(self.camids[:self.num_query])
@@ -186,6 +199,37 @@ class R1_mAP_eval():
             print('=> Computing DistMat with euclidean_distance')
             distmat = euclidean_distance_device(qf, gf)
         cmc, mAP = eval_func_device(distmat, q_pids, g_pids, q_camids, g_camids)
+        self._print(cmc, mAP)
+        return cmc, mAP
+
+    @staticmethod
+    def _print(cmc, mAP):
         print("Rank@{:d}:{:.1%}, Rank@{:d}:{:.1%}, Rank@{:d}:{:.1%}, mAP:{:.1%}".format(
             1, cmc[0], 5, cmc[4], 10, cmc[9], mAP))
+
+    def _compute_sharded(self, feats):
+        from . import distributed as rd
+        rank, W = rd.world()
+        nq = self.num_query
+        lab = torch.from_numpy(np.stack([np.asarray(self.pids, np.int64), np.asarray(self.camids, np.int64)], 1))
+        qf, _ = rd.gather_rows_var(feats[:nq].contiguous())
+        gf, _ = rd.gather_rows_var(feats[nq:].contiguous())
+        ql, _ = rd.gather_rows_var(lab[:nq].contiguous())
+        gl, _ = rd.gather_rows_var(lab[nq:].contiguous())
+        Q, G = qf.shape[0], gf.shape[0]
+        qlo, qhi = rd.shard(Q, rank, W)
+        if self.reranking:
+            print('=> Enter reranking')
+            from .reranking import re_ranking_sharded
+            d = re_ranking_sharded(qf, gf, 50, 15, 0.3)  # this rank's rows shard(Q, rank, W)
+        else:
+            print('=> Computing DistMat with euclidean_distance')
+            d = euclidean_distance_device(qf[qlo:qhi], gf)
+        ql, gl = ql.numpy(), gl.numpy()
+        valid, first, ap, nkept, ovf = eval_rows_device(d, ql[qlo:qhi, 0], gl[:, 0], ql[qlo:qhi, 1], gl[:, 1])
+        if int(ovf.item()):
+            raise _lib.ReidmiError("eval_rows: a query was not evaluated (overflow flag)")
+        rows = rd.gather_rows(rd.pack_rows(valid, first, ap, nkept), Q)
+        cmc, mAP = aggregate_cmc_map(*rd.unpack_rows(rows), G, 50)
+        self._print(cmc, mAP)
         return cmc, mAP

@@ -18,7 +18,9 @@ from . import _lib
 from .evaluate import _as_dev_f32, euclidean_distance_device
 
 STAGED_MIN_N = 32768  # from features, N >= this: staged path (no N x N fp32 buffer)
-_CAP_MSG = {1: "V row capacity", 2: "V_qe row capacity (4096)", 4: "query-expansion staging capacity (6144)"}
+# There is no capacity limit (any k1, k2, neighbourhood density): the flag can only report a
+# row beyond a scratch bound computed from the same caps (a bug), never a data-dependent overflow.
+_CAP_MSG = {8: "a row beyond its sized scratch (internal error)"}
 
 
 def _lam(lambda_value):
@@ -35,12 +37,14 @@ def re_ranking_device(probFea, galFea, k1, k2, lambda_value, local_distmat=None,
     """Device version: returns the (Q, G) fp32 torch tensor on the GPU."""
     Q = probFea.size(0) if isinstance(probFea, torch.Tensor) else len(probFea)
     G = galFea.size(0) if isinstance(galFea, torch.Tensor) else len(galFea)
-    if not (only_local or local_distmat is not None) and Q + G >= STAGED_MIN_N:
-        # N x N buffers would dominate: row-chunked stages, same bits
-        from . import distributed as rd
-        if rd.world()[1] > 1:
-            raise _lib.ReidmiError("re_ranking_device is single-process; use re_ranking_sharded under torch.distributed")
-        return re_ranking_sharded(probFea, galFea, k1, k2, lambda_value)
+    from . import distributed as rd
+    if not (only_local or local_distmat is not None) and (Q + G >= STAGED_MIN_N or rd.world()[1] > 1):
+        # N x N buffers would dominate: row-chunked stages, same bits.  Under a process group of
+        # several ranks (each holding the full features, as the reference's callers do) the
+        # stages are row-sharded over the ranks and the final rows all-gathered, so every rank
+        # returns the whole (Q, G) matrix.
+        out = re_ranking_sharded(probFea, galFea, k1, k2, lambda_value)
+        return rd.gather_rows(out, Q) if rd.world()[1] > 1 else out
     dev = torch.device("cuda", torch.cuda.current_device())
     lam_h, lam_f = _lam(lambda_value)
     out = torch.empty((Q, G), device=dev, dtype=torch.float32)
@@ -84,10 +88,17 @@ def re_ranking(probFea, galFea, k1, k2, lambda_value, local_distmat=None, only_l
 RANK_PREFILTER = True
 
 
+def default_chunk_bytes(dev):
+    """Distance scratch per row pass: 16 GiB (whole 128-row tiles at 1M items, and enough rows
+    for the selection kernels to fill the GPU), but at most a quarter of the free device memory."""
+    free, _ = torch.cuda.mem_get_info(dev)
+    return int(max(64 << 20, min(16 << 30, free // 4)))
+
+
 class HipStages:
     """The product's stage kernels (libreidmi)."""
 
-    def __init__(self, feat, num_query, k1, k2, lambda_value, chunk_bytes=16 << 30):
+    def __init__(self, feat, num_query, k1, k2, lambda_value, chunk_bytes=None):
         _lib.require_cuda(feat)
         self.feat = _as_dev_f32(feat).contiguous()
         self.N, self.D = self.feat.shape
@@ -97,6 +108,8 @@ class HipStages:
         self.lam_h, self.lam_f = _lam(lambda_value)
         self.dev = self.feat.device
         self.st = _lib.stream()
+        if chunk_bytes is None:
+            chunk_bytes = default_chunk_bytes(self.dev)
         self.sqn = torch.empty(self.N, device=self.dev, dtype=torch.float32)
         _lib.call("reidmi_row_sqnorm_f32", _lib.ptr(self.feat), self.N, self.D, self.D, _lib.ptr(self.sqn), self.st)
         # distance rows per pass: whole 128-row tiles of the distance kernel when possible (a
@@ -106,9 +119,16 @@ class HipStages:
         self._chunk = None
         self._f16 = None
         self.flags = torch.zeros(1, device=self.dev, dtype=torch.int32)
-        vc, qc = ctypes.c_int(), ctypes.c_int()
-        _lib.call("reidmi_rr_caps", ctypes.byref(vc), ctypes.byref(qc))
-        self.vcap, self.qcap = vc.value, qc.value
+        vc, qc, vw, qw = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        _lib.call("reidmi_rr_caps", self.N, k1, k2, ctypes.byref(vc), ctypes.byref(qc), ctypes.byref(vw),
+                  ctypes.byref(qw))
+        self.vcap, self.qcap = vc.value, qc.value          # ELL widths of V and of on-chip V_qe rows
+        self.v_ws_bytes, self.qe_ws_bytes = vw.value, qw.value  # scratch of the generic R3 / R4 kernels
+        self.k2e = min(k2, self.K)  # initial_rank[i, :k2] has min(k2, N) entries
+        # ELL batches of R3 / R4 rows: at most this many bytes of ELL at once (the CSR parts of
+        # the batches are concatenated)
+        self.ell_bytes = max(256 << 20, chunk_bytes // 2)
+        self._ws = {}
 
     def _chunk_buf(self, rows, cols):
         n = rows * cols
@@ -128,35 +148,41 @@ class HipStages:
             self._f16 = (x16, Np, Dp, torch.sqrt(self.sqn), bool(ok.item()))
         return self._f16
 
-    def _exact_rows(self, lo, idx, R, rmax):
-        """R2 of rows lo + idx with the exact distance kernel: the same distance bits as
-        reidmi_rr_rank_rows (per-pair fp32 chain, same squared norms), row max, stable top-K of
-        D / rowmax (reidmi_topk_rows_f32, as rr_rank_rows)."""
-        n = int(idx.numel())
+    def _exact_rows(self, lo, idx, n, R, rmax):
+        """R2 of rows lo + idx[:n] (idx: device int32, from reidmi_nonzero_i32) with the exact
+        distance kernel: the same distance bits as reidmi_rr_rank_rows (per-pair fp32 chain,
+        same squared norms), row max (reidmi_rowmax_f32: fmaxf, NaN skipped, as rowmax_kernel),
+        stable top-K of D / rowmax (reidmi_topk_rows_f32, as rr_rank_rows)."""
         if n == 0:
             return
         step = max(1, self.chunk_rows)
         for s in range(0, n, step):
-            sub = idx[s:s + step]
-            rows = self.feat[lo + sub].contiguous()
+            m = min(step, n - s)
+            sub = idx[s:s + m]
+            rows = torch.empty((m, self.D), device=self.dev, dtype=torch.float32)
+            _lib.call("reidmi_gather_rows_f32", _lib.ptr(self.feat), self.D, self.D, lo, _lib.ptr(sub), m,
+                      _lib.ptr(rows), self.D, self.st)
             # the row-pass scratch (stream-ordered after the pass that marked these rows)
-            d = self._chunk_buf(rows.shape[0], self.N)[:rows.shape[0] * self.N].view(rows.shape[0], self.N)
-            ws = torch.empty(rows.shape[0] + self.N, device=self.dev, dtype=torch.float32)
-            _lib.call("reidmi_distmat_f32", _lib.ptr(rows), rows.shape[0], self.D, _lib.ptr(self.feat), self.N,
+            d = self._chunk_buf(m, self.N)[:m * self.N].view(m, self.N)
+            ws = torch.empty(m + self.N, device=self.dev, dtype=torch.float32)
+            _lib.call("reidmi_distmat_f32", _lib.ptr(rows), m, self.D, _lib.ptr(self.feat), self.N,
                       self.D, self.D, _lib.ptr(d), self.N, _lib.ptr(ws), self.st)
-            # rowmax_kernel's fmaxf reduction: NaN entries are skipped
-            m = torch.where(torch.isnan(d), float("-inf"), d).max(dim=1).values.contiguous()
-            k = torch.empty((rows.shape[0], self.K), device=self.dev, dtype=torch.int32)
-            _lib.call("reidmi_topk_rows_f32", _lib.ptr(d), rows.shape[0], self.N, self.N, _lib.ptr(m), self.K,
+            mx = torch.empty(m, device=self.dev, dtype=torch.float32)
+            _lib.call("reidmi_rowmax_f32", _lib.ptr(d), m, self.N, self.N, _lib.ptr(mx), self.st)
+            k = torch.empty((m, self.K), device=self.dev, dtype=torch.int32)
+            _lib.call("reidmi_topk_rows_f32", _lib.ptr(d), m, self.N, self.N, _lib.ptr(mx), self.K,
                       _lib.ptr(k), None, self.K, self.st)
-            R[sub] = k
-            rmax[sub] = m
+            pos = sub.long()
+            R.index_copy_(0, pos, k)
+            rmax.index_copy_(0, pos, mx)
 
     def rank_rows(self, lo, hi):
         R = torch.empty((hi - lo, self.K), device=self.dev, dtype=torch.int32)
         rmax = torch.empty(hi - lo, device=self.dev, dtype=torch.float32)
         if hi > lo:
-            x16, Np, Dp, nrm, fits = self._feat16() if RANK_PREFILTER else (None, 0, 0, None, False)
+            # the pre-filter's selection keeps K <= 64 on chip; larger K take the exact rows
+            use = RANK_PREFILTER and self.K <= 64
+            x16, Np, Dp, nrm, fits = self._feat16() if use else (None, 0, 0, None, False)
             a = lo
             if fits:
                 # the fp16 pre-filter (bit-identical to the exact rows; reidmi_rr_rank_rows_f16),
@@ -165,6 +191,8 @@ class HipStages:
                 # than not (a random network's embeddings) the rest skips the filter
                 cr = min(max(256, self.chunk_rows * self.N // Np // 256 * 256), hi - lo)
                 need = torch.empty(cr, device=self.dev, dtype=torch.int32)
+                idx = torch.empty(cr, device=self.dev, dtype=torch.int32)
+                cnt = torch.empty(1, device=self.dev, dtype=torch.int32)
                 first = True
                 while a < hi:
                     b = min(a + (min(cr, 512) if first else cr), hi)  # a small probe pass first
@@ -173,9 +201,9 @@ class HipStages:
                               _lib.ptr(self.sqn), _lib.ptr(nrm), _lib.ptr(x16), Np, Dp, a, b, self.K,
                               _lib.ptr(R[a - lo:]), _lib.ptr(rmax[a - lo:]), _lib.ptr(need),
                               _lib.ptr(self._chunk_buf(cr, Np)), cr, self.st)
-                    idx = torch.nonzero(need[:b - a]).flatten()
-                    self._exact_rows(a, idx, R[a - lo:b - lo], rmax[a - lo:b - lo])
-                    undecided, rows = int(idx.numel()), b - a
+                    _lib.call("reidmi_nonzero_i32", _lib.ptr(need), b - a, _lib.ptr(idx), _lib.ptr(cnt), self.st)
+                    undecided, rows = int(cnt.item()), b - a
+                    self._exact_rows(a, idx, undecided, R[a - lo:b - lo], rmax[a - lo:b - lo])
                     a = b
                     if 2 * undecided > rows:
                         break
@@ -191,34 +219,86 @@ class HipStages:
         _lib.call("reidmi_rr_row_offsets", _lib.ptr(nnz), nnz.numel(), _lib.ptr(off), self.st)
         return off
 
-    def _pack(self, ecol, eval_, nnz, cap):
-        off = self.offsets(nnz)
+    def _pack(self, ecol, eval_, nnz, cap, full=None):
+        """ELL rows -> CSR (nnz, col, val); `full` = the rows' true entry counts when some rows
+        (the deferred V_qe rows, ELL length 0) are written into the CSR afterwards."""
+        full = nnz if full is None else full
+        off = self.offsets(full)
         total = int(off[-1].item())
         col = torch.empty(max(total, 1), device=self.dev, dtype=torch.int32)
         val = torch.empty(max(total, 1), device=self.dev, dtype=torch.int16)
         _lib.call("reidmi_rr_pack", _lib.ptr(ecol), _lib.ptr(eval_), _lib.ptr(nnz), nnz.numel(), cap, _lib.ptr(off),
                   _lib.ptr(col), _lib.ptr(val), self.st)
-        return nnz, col[:total], val[:total]
+        return full, col[:total], val[:total], off
+
+    def _scratch(self, name, nbytes):
+        if nbytes <= 0:
+            return None
+        t = self._ws.get(name)
+        if t is None or t.numel() < nbytes:
+            t = self._ws[name] = torch.empty(nbytes, device=self.dev, dtype=torch.uint8)
+        return t
+
+    def _batches(self, lo, hi, row_bytes):
+        step = max(1, int(self.ell_bytes // max(row_bytes, 1)))
+        return [(a, min(a + step, hi)) for a in range(lo, hi, step)]
+
+    def _cat(self, parts):
+        if not parts:
+            z = torch.zeros(0, device=self.dev, dtype=torch.int32)
+            return z, z, torch.zeros(0, device=self.dev, dtype=torch.int16)
+        if len(parts) == 1:
+            return parts[0]
+        return tuple(torch.cat([p[k] for p in parts]) for k in range(3))
 
     def v_rows(self, R, rmax, lo, hi):
-        n = hi - lo
-        ecol = torch.empty((max(n, 1), self.vcap), device=self.dev, dtype=torch.int32)
-        evl = torch.empty((max(n, 1), self.vcap), device=self.dev, dtype=torch.int16)
-        nnz = torch.zeros(n, device=self.dev, dtype=torch.int32)
-        _lib.call("reidmi_rr_v_rows", _lib.ptr(self.feat), self.N, self.D, self.D, _lib.ptr(self.sqn), _lib.ptr(rmax),
-                  _lib.ptr(R), self.K, lo, hi, self.k1, _lib.ptr(ecol), _lib.ptr(evl), _lib.ptr(nnz),
-                  _lib.ptr(self.flags), self.st)
-        return self._pack(ecol, evl, nnz, self.vcap)
+        """R3 over rows lo..hi: ELL batches of width vcap (the k-reciprocal bound), packed to CSR."""
+        ws = self._scratch("v", self.v_ws_bytes)
+        parts = []
+        for a, b in self._batches(lo, hi, self.vcap * 6):
+            n = b - a
+            ecol = torch.empty((n, self.vcap), device=self.dev, dtype=torch.int32)
+            evl = torch.empty((n, self.vcap), device=self.dev, dtype=torch.int16)
+            nnz = torch.zeros(n, device=self.dev, dtype=torch.int32)
+            _lib.call("reidmi_rr_v_rows", _lib.ptr(self.feat), self.N, self.D, self.D, _lib.ptr(self.sqn),
+                      _lib.ptr(rmax), _lib.ptr(R), self.K, a, b, self.k1, _lib.ptr(ecol), _lib.ptr(evl), _lib.ptr(nnz),
+                      _lib.ptr(ws), self.v_ws_bytes, _lib.ptr(self.flags), self.st)
+            parts.append(self._pack(ecol, evl, nnz, self.vcap)[:3])
+        return self._cat(parts)
 
     def qe_rows(self, R, V, lo, hi):
+        """R4 over rows lo..hi: rows assembled on chip go through an ELL of width qcap; rows
+        beyond it (dense neighbourhoods, k2 > 32) are counted, then written straight into the
+        CSR by reidmi_rr_qe_deferred."""
         off, col, val = V
-        n = hi - lo
-        ecol = torch.empty((max(n, 1), self.qcap), device=self.dev, dtype=torch.int32)
-        evl = torch.empty((max(n, 1), self.qcap), device=self.dev, dtype=torch.int16)
-        nnz = torch.zeros(n, device=self.dev, dtype=torch.int32)
-        _lib.call("reidmi_rr_qe_rows", _lib.ptr(R), self.K, self.k2, lo, hi, _lib.ptr(off), _lib.ptr(col),
-                  _lib.ptr(val), _lib.ptr(ecol), _lib.ptr(evl), _lib.ptr(nnz), _lib.ptr(self.flags), self.st)
-        return self._pack(ecol, evl, nnz, self.qcap)
+        fast = self.k2e <= 32
+        parts = []
+        for a, b in self._batches(lo, hi, self.qcap * 6 if fast else 4):
+            n = b - a
+            w = n if fast else 1
+            ecol = torch.empty((w, self.qcap), device=self.dev, dtype=torch.int32)
+            evl = torch.empty((w, self.qcap), device=self.dev, dtype=torch.int16)
+            nnz = torch.zeros(n, device=self.dev, dtype=torch.int32)
+            dlist = torch.empty(n, device=self.dev, dtype=torch.int32)
+            dcount = torch.zeros(1, device=self.dev, dtype=torch.int32)
+            _lib.call("reidmi_rr_qe_rows", _lib.ptr(R), self.K, self.k2e, a, b, _lib.ptr(off), _lib.ptr(col),
+                      _lib.ptr(val), _lib.ptr(ecol), _lib.ptr(evl), _lib.ptr(nnz), _lib.ptr(dlist), _lib.ptr(dcount),
+                      self.st)
+            nd = int(dcount.item())
+            full = nnz
+            if nd:
+                ws = self._scratch("qe", self.qe_ws_bytes)
+                full = nnz.clone()
+                _lib.call("reidmi_rr_qe_deferred", _lib.ptr(R), self.K, self.k1, self.k2e, a, self.N, _lib.ptr(off),
+                          _lib.ptr(col), _lib.ptr(val), _lib.ptr(dlist), nd, 0, None, None, None, _lib.ptr(full),
+                          _lib.ptr(ws), self.qe_ws_bytes, _lib.ptr(self.flags), self.st)
+            cnt, qcol, qval, qoff = self._pack(ecol, evl, nnz, self.qcap, full)
+            if nd:
+                _lib.call("reidmi_rr_qe_deferred", _lib.ptr(R), self.K, self.k1, self.k2e, a, self.N, _lib.ptr(off),
+                          _lib.ptr(col), _lib.ptr(val), _lib.ptr(dlist), nd, 1, _lib.ptr(qoff), _lib.ptr(qcol),
+                          _lib.ptr(qval), None, _lib.ptr(ws), self.qe_ws_bytes, _lib.ptr(self.flags), self.st)
+            parts.append((cnt, qcol, qval))
+        return self._cat(parts)
 
     def jaccard_rows(self, rmax, Vq, qlo, qhi):
         off, col, val = Vq
@@ -236,13 +316,14 @@ class HipStages:
         del ws
         out = torch.empty((qhi - qlo, G), device=self.dev, dtype=torch.float32)
         if qhi > qlo and G > 0:
-            # distance rows per pass + the rows the call keeps for its column chunk bounds
-            extra = int(_lib.load().reidmi_rr_jaccard_reserved_rows(N, G))
-            cr = int(max(1, min(65535 - extra, qhi - qlo, self.chunk_rows * N // max(G, 1)))) + extra
+            L = _lib.load()
+            bb = int(L.reidmi_rr_jaccard_bounds_bytes(N, G))
+            bounds = torch.empty((bb + 7) // 8, device=self.dev, dtype=torch.int64)
+            cr = int(max(1, min(65535, qhi - qlo, self.chunk_rows * N // max(G, 1))))
             _lib.call("reidmi_rr_jaccard_rows", _lib.ptr(self.feat), N, self.D, self.D, _lib.ptr(self.sqn),
                       _lib.ptr(rmax), Q, qlo, qhi, _lib.ptr(off), _lib.ptr(col), _lib.ptr(val), _lib.ptr(coff),
                       _lib.ptr(irow), _lib.ptr(ival), self.lam_h, self.lam_f, _lib.ptr(out), G,
-                      _lib.ptr(self._chunk_buf(cr, G)), cr, self.st)
+                      _lib.ptr(self._chunk_buf(cr, G)), cr, _lib.ptr(bounds), bb, self.st)
         return out
 
     def check(self):
@@ -267,7 +348,7 @@ def staged_rerank(stages, N, Q):
     R = rd.gather_rows(R_loc, N)
     rmax = rd.gather_rows(rmax_loc, N)
     V = _gather_csr(stages, *stages.v_rows(R, rmax, lo, hi), N)  # R3 (reranking.py:51-71)
-    if stages.k2 != 1:
+    if stages.k2 != 1 and stages.k2e >= 2:  # (k2 capped at N = 1 row: the mean is V itself)
         Vq = _gather_csr(stages, *stages.qe_rows(R, V, lo, hi), N)  # R4 (reranking.py:73-78)
     else:
         Vq = V
@@ -277,12 +358,13 @@ def staged_rerank(stages, N, Q):
     return out
 
 
-def re_ranking_sharded(probFea, galFea, k1, k2, lambda_value, chunk_bytes=16 << 30):
+def re_ranking_sharded(probFea, galFea, k1, k2, lambda_value, chunk_bytes=None):
     """Sharded re_ranking: probFea / galFea are the FULL query and gallery features on this
     rank's GPU (all-gathered after a sharded embed).  Returns this rank's query rows
     shard(Q, rank, W) of the re-ranked (Q, G) distance as a device tensor; with one process
     it equals re_ranking_device bit for bit, without the N x N buffers."""
-    Q = probFea.size(0)
-    feat = torch.cat([_as_dev_f32(probFea), _as_dev_f32(galFea)]).contiguous()
+    q = _as_dev_f32(probFea)
+    Q = q.shape[0]
+    feat = torch.cat([q, _as_dev_f32(galFea)]).contiguous()
     stages = HipStages(feat, Q, k1, k2, lambda_value, chunk_bytes)
     return staged_rerank(stages, feat.shape[0], Q)

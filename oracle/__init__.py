@@ -196,6 +196,7 @@ class RerankStages:
         self.Q = num_query
         self.k1, self.k2 = k1, k2
         self.K = min(max(k1 + 1, k2), self.N)
+        self.k2e = min(k2, self.K)
         self.lam_h = np.float16(1 - lambda_value).view(np.uint16)
         self.lam_f = np.float32(lambda_value)
 

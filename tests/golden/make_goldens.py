@@ -206,6 +206,24 @@ def _load_vit(sd, model="ViT-B/16", height=256, width=128, stride=12):
     return m.eval()
 
 
+def _half_like_convert_weights(m):
+    """utils.convert_weights (utils.py:145-166): Conv/Linear weights and biases, the MHA
+    in_proj and the projection matrices in fp16; LayerNorm params stay fp32 (custom_clip_model.py
+    LayerNorm upcasts)."""
+    for mod in m.modules():
+        if isinstance(mod, (torch.nn.Conv2d, torch.nn.Linear)):
+            mod.weight.data = mod.weight.data.half()
+            if mod.bias is not None:
+                mod.bias.data = mod.bias.data.half()
+        if isinstance(mod, torch.nn.MultiheadAttention):
+            mod.in_proj_weight.data = mod.in_proj_weight.data.half()
+            mod.in_proj_bias.data = mod.in_proj_bias.data.half()
+    for name in ("proj", "text_projection"):
+        if isinstance(getattr(m, name, None), torch.nn.Parameter):
+            getattr(m, name).data = getattr(m, name).data.half()
+    return m
+
+
 def vit_fixtures(out):
     torch.manual_seed(0)
     sd = syn.vit_state_dict("ViT-B/16", seed=0)
@@ -217,17 +235,7 @@ def vit_fixtures(out):
         x11, x12, xp = m(torch.from_numpy(imgs))
         a11, a12, ap = m(torch.from_numpy(aug))
         # the reference's GPU dtype: conv/linear/MHA/proj in fp16, LN upcast (utils.py:145-166)
-        mh = _load_vit(sd)
-        for mod in mh.modules():
-            if isinstance(mod, (torch.nn.Conv2d, torch.nn.Linear)):
-                mod.weight.data = mod.weight.data.half()
-                if mod.bias is not None:
-                    mod.bias.data = mod.bias.data.half()
-            if isinstance(mod, torch.nn.MultiheadAttention):
-                mod.in_proj_weight.data = mod.in_proj_weight.data.half()
-                mod.in_proj_bias.data = mod.in_proj_bias.data.half()
-        mh.proj.data = mh.proj.data.half()
-        mh.class_embedding.data = mh.class_embedding.data
+        mh = _half_like_convert_weights(_load_vit(sd))
         try:
             h11, h12, hp = mh(torch.from_numpy(imgs).half())
             half = dict(x12cls_fp16=h12[:, 0].float().numpy(), projcls_fp16=hp[:, 0].float().numpy())
@@ -255,8 +263,11 @@ def vitl_fixtures(out):
     imgs = syn.images(2, seed=4)
     with torch.no_grad():
         x11, x12, xp = m(torch.from_numpy(imgs))
+        _half_like_convert_weights(m)  # the reference's GPU dtype (utils.py:145-166)
+        h11, h12, hp = m(torch.from_numpy(imgs).half())
     np.savez_compressed(os.path.join(out, "vit_l14.npz"), x11cls=x11[:, 0].numpy(), x12cls=x12[:, 0].numpy(),
-                        projcls=xp[:, 0].numpy(), x12_tok=x12[1, 200:204].numpy())
+                        projcls=xp[:, 0].numpy(), x12_tok=x12[1, 200:204].numpy(),
+                        x12cls_fp16=h12[:, 0].float().numpy(), projcls_fp16=hp[:, 0].float().numpy())
     print("vit-l fixtures ok")
 
 
@@ -285,7 +296,14 @@ def text_fixtures(out):
     emb = torch.from_numpy(sd["token_embedding.weight"])[torch.from_numpy(tokens)]
     with torch.no_grad():
         feats = enc(emb, torch.from_numpy(tokens))
-    np.savez_compressed(os.path.join(out, "text.npz"), tokens=tokens, text_feat=feats.numpy())
+        # the reference's GPU dtype (convert_weights: fp16 Linear / MHA / text_projection and
+        # token embedding, fp32 LayerNorm)
+        _half_like_convert_weights(c.transformer)
+        c.text_projection.data = c.text_projection.data.half()
+        c.dtype = torch.float16
+        h = ref_te.TextEncoder(c)(emb.half(), torch.from_numpy(tokens))
+    np.savez_compressed(os.path.join(out, "text.npz"), tokens=tokens, text_feat=feats.numpy(),
+                        text_feat_fp16=h.float().numpy())
     print("text fixtures ok")
 
 
@@ -298,17 +316,24 @@ def ivlp_fixtures(out):
     _, maple, _, _ = _stubbed()
     torch.manual_seed(0)
     sd = syn.openai_state_dict("ViT-B/16", seed=6, vpt_ctx=2, text_ctx=2)
-    model = maple.build_model(_torch_sd(sd), 256, 128, IVLP_DESIGN).float().eval()
     imgs = syn.images(2, seed=6)
     tokens = syn.token_ids(5, seed=6)
     with torch.no_grad():
+        # the reference's GPU dtype first (build_model's convert_weights: fp16), then fp32
+        mh = maple.build_model(_torch_sd(sd), 256, 128, IVLP_DESIGN).eval()
+        _, h12, hp = mh.encode_image(torch.from_numpy(imgs))
+        htxt = mh.encode_text(torch.from_numpy(tokens))
+        assert h12.dtype == torch.float16
+        model = maple.build_model(_torch_sd(sd), 256, 128, IVLP_DESIGN).float().eval()
         x11, x12, xp = model.encode_image(torch.from_numpy(imgs))
         txt = model.encode_text(torch.from_numpy(tokens))
     assert x12.shape == (2, 213, 768)
     pos = model.visual.positional_embedding.detach()
     np.savez_compressed(os.path.join(out, "ivlp.npz"), tokens=tokens, x12cls=x12[:, 0].numpy(),
                         x11cls=x11[:, 0].numpy(), projcls=xp[:, 0].numpy(), x12_prompt=x12[1, -2:].numpy(),
-                        proj_tok=xp[0, 100:103].numpy(), text_feat=txt.numpy(), pos_resized=pos.numpy())
+                        proj_tok=xp[0, 100:103].numpy(), text_feat=txt.numpy(), pos_resized=pos.numpy(),
+                        x12cls_fp16=h12[:, 0].float().numpy(), projcls_fp16=hp[:, 0].float().numpy(),
+                        text_feat_fp16=htxt.float().numpy())
     print("ivlp fixtures ok")
 
 

@@ -37,12 +37,17 @@ def test_distmat_bitexact(gpu, Q, G, D):
     g = r.standard_normal((G, D)).astype(np.float32)
     ref = oracle.distmat(q, g).view(np.uint32)
     from multimodal_reid_amd import _lib
-    for v in (0, 1):  # pipelined K-step-32 kernel (D % 4 == 0) and the single-stage one
-        _lib.call("reidmi_distmat_set_variant", v)
-        d = _ev().euclidean_distance(torch.from_numpy(q), torch.from_numpy(g))
-        assert isinstance(d, np.ndarray) and d.dtype == np.float32
-        assert np.array_equal(d.view(np.uint32), ref), v
-    _lib.call("reidmi_distmat_set_variant", 0)
+    d = _ev().euclidean_distance(torch.from_numpy(q), torch.from_numpy(g))
+    assert isinstance(d, np.ndarray) and d.dtype == np.float32
+    assert np.array_equal(d.view(np.uint32), ref)
+    # per-call kernel choice: the pipelined K-step-32 kernel (D % 4 == 0) and the single-stage one
+    qd, gd = torch.from_numpy(q).cuda(), torch.from_numpy(g).cuda()
+    for v in (0, 1):
+        out = torch.empty(Q, G, device="cuda")
+        ws = torch.empty(Q + G, device="cuda")
+        _lib.call("reidmi_distmat_f32_variant", _lib.ptr(qd), Q, D, _lib.ptr(gd), G, D, D, _lib.ptr(out), G,
+                  _lib.ptr(ws), v, _lib.stream())
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), ref), v
 
 
 def test_distmat_matches_reference_fixture(gpu):

@@ -88,3 +88,34 @@ def test_rccl_world1_matches_single_process(gpu):
     assert gathered_ok and var_ok
     assert np.array_equal(cmc, cmc_ref) and mAP == map_ref
     assert np.array_equal(rr.view(np.uint32), rr_ref.view(np.uint32))
+
+
+def test_comm_capi_world1(gpu):
+    """The C ABI's RCCL exchange (reidmi_comm_*, for callers that are not Python) at world 1:
+    the padded in-place all-gather + in-order compaction returns the rows, and the all-reduce
+    the input.  (Several ranks need several GPUs: RCCL refuses two ranks on one device.)"""
+    import ctypes
+    from multimodal_reid_amd import _lib
+    L = _lib.load()
+    uid = ctypes.create_string_buffer(128)
+    _lib.call("reidmi_comm_unique_id", uid)
+    comm = ctypes.c_void_p()
+    _lib.call("reidmi_comm_init", ctypes.byref(comm), 1, 0, uid, 0)
+    try:
+        r, w = ctypes.c_int(), ctypes.c_int()
+        _lib.call("reidmi_comm_rank", comm, ctypes.byref(r), ctypes.byref(w))
+        assert (r.value, w.value) == (0, 1)
+        rows = torch.randint(0, 255, (37, 12), dtype=torch.uint8, device=gpu)
+        out = torch.zeros_like(rows)
+        nb = L.reidmi_comm_allgather_rows_scratch_bytes(1, 37, 12)
+        assert nb == 37 * 12
+        scratch = torch.empty(nb, dtype=torch.uint8, device=gpu)
+        _lib.call("reidmi_comm_allgather_rows", comm, _lib.ptr(rows), 37, 12, _lib.ptr(out), _lib.ptr(scratch), nb,
+                  _lib.stream())
+        x = torch.randn(1000, dtype=torch.float64, device=gpu)
+        y = torch.empty_like(x)
+        _lib.call("reidmi_comm_allreduce", comm, _lib.ptr(x), _lib.ptr(y), 1000, 1, _lib.stream())
+        torch.cuda.synchronize()
+        assert torch.equal(out, rows) and torch.equal(x, y)
+    finally:
+        _lib.call("reidmi_comm_destroy", comm)

@@ -5,7 +5,8 @@ reference-generated fixtures.
 Tolerances (fp16 MFMA operands, fp32 accumulation — the reference's own GPU dtype):
   * kernels vs a torch fp32 reference on the same fp16 operands: rel 2e-3 (fp16 outputs)
   * towers vs oracle with fp16 rounding at the same points: cosine >= 0.99999
-  * towers vs the reference's fp32 outputs: cosine >= 0.9999, max |err| <= 0.05
+  * towers vs the reference's fp32 outputs: max |err| <= 1.5 x the reference's own fp16-vs-fp32
+    deviation on the same inputs (conftest.close_to_reference), cosine >= 0.99995
     (the reference's own fp16 GPU dtype deviates 0.007 on the same inputs)
 """
 import numpy as np
@@ -14,7 +15,7 @@ import torch
 
 from multimodal_reid_amd import synthetic as syn
 from oracle import vit_ref
-from conftest import golden
+from conftest import close_to_reference, golden
 
 pytestmark = pytest.mark.gpu
 
@@ -30,11 +31,15 @@ def _cos(a, b):
     return (a * b).sum(1) / np.linalg.norm(a, axis=1) / np.linalg.norm(b, axis=1)
 
 
-def _gemm(L, epi, A, W, bias, out, rowstat=None, colsum=None):
+def _gemm(L, epi, A, W, bias, out, rowstat=None, colsum=None, tile=None, walk=0):
     M, K = A.shape
     N = W.shape[0]
-    L.call("reidmi_gemm_f16", epi, L.ptr(A), K, L.ptr(W), K, M, N, K, L.ptr(bias), L.ptr(rowstat), L.ptr(colsum),
-           L.ptr(out), out.shape[1], L.stream())
+    if tile is None:
+        L.call("reidmi_gemm_f16", epi, L.ptr(A), K, L.ptr(W), K, M, N, K, L.ptr(bias), L.ptr(rowstat), L.ptr(colsum),
+               L.ptr(out), out.shape[1], L.stream())
+    else:  # per-call tiling (every choice bit-identical)
+        L.call("reidmi_gemm_f16_tiled", epi, L.ptr(A), K, L.ptr(W), K, M, N, K, L.ptr(bias), L.ptr(rowstat),
+               L.ptr(colsum), L.ptr(out), out.shape[1], tile, walk, L.stream())
 
 
 @pytest.mark.parametrize("epi", [0, 1, 5, 6])
@@ -77,16 +82,12 @@ def test_gemm_tiles_and_walks_bitexact(gpu, epi, M, N, K):
     bias = torch.randn(N, generator=g).cuda()
     outs = []
     for tile, walk in ((1, 1), (2, 1), (2, 2), (2, 4), (2, 8)):
-        L.call("reidmi_gemm_set_tile", tile)
-        L.call("reidmi_gemm_set_walk", walk)
         if epi == 6:
             out = torch.ones(M, N, dtype=torch.float16, device="cuda")
         else:
             out = torch.zeros(M, N, dtype=torch.float32 if epi == 5 else torch.float16, device="cuda")
-        _gemm(L, epi, A, W, bias, out)
+        _gemm(L, epi, A, W, bias, out, tile=tile, walk=walk)
         outs.append(out)
-    L.call("reidmi_gemm_set_tile", 0)
-    L.call("reidmi_gemm_set_walk", 0)
     for o in outs[1:]:
         assert torch.equal(outs[0], o)
     rows = torch.arange(0, M, max(1, M // 97), device="cuda")
@@ -123,13 +124,9 @@ def test_gemm_f16_layernorm_fold(gpu, epi, M, N, K):
     dx, dw, dcs, dbf, drs = (t.cuda() for t in (x, wf, cs, bf, rs))
     outs = []
     for tile, walk in ((1, 1), (2, 1), (2, 4)):
-        L.call("reidmi_gemm_set_tile", tile)
-        L.call("reidmi_gemm_set_walk", walk)
         out = torch.zeros(M, N, dtype=torch.float16, device="cuda")
-        _gemm(L, epi, dx, dw, dbf, out, drs, dcs)
+        _gemm(L, epi, dx, dw, dbf, out, drs, dcs, tile=tile, walk=walk)
         outs.append(out)
-    L.call("reidmi_gemm_set_tile", 0)
-    L.call("reidmi_gemm_set_walk", 0)
     for o in outs[1:]:
         assert torch.equal(outs[0], o)
     got = outs[0].double().cpu()
@@ -227,10 +224,13 @@ def test_vit_b16_encode_image_vs_reference(vit_b16):
     imgs = syn.images(3, seed=0)
     x11, x12, xp = (t.cpu().numpy() for t in m.encode_image(torch.from_numpy(imgs)))
     assert x12.shape == (3, 211, 768) and xp.shape == (3, 211, 512) and x11.shape == (3, 211, 768)
-    for got, ref in ((x12[:, 0], g["x12cls"]), (xp[:, 0], g["projcls"]), (x11[:, 0], g["x11cls"]),
-                     (x12[0, :8], g["x12_tok"]), (xp[0, 100:104], g["proj_tok"])):
-        assert _cos(got, ref).min() >= 0.9999
-        assert np.abs(got - ref).max() <= 0.05
+    # bounded by the reference's own fp16 deviation on these inputs (x12cls 0.0071, projcls 0.0047;
+    # the token rows and x11 against the x12cls deviation)
+    close_to_reference(x12[:, 0], g, "x12cls")
+    close_to_reference(xp[:, 0], g, "projcls")
+    close_to_reference(x11[:, 0], g, "x11cls", via="x12cls")
+    close_to_reference(x12[0, :8], g, "x12_tok", via="x12cls")
+    close_to_reference(xp[0, 100:104], g, "proj_tok", via="projcls")
     with torch.no_grad():
         b11, b12, bp = vit_ref.vit_forward(sd, imgs, f16=True)
     assert _cos(x12[:, 0], b12[:, 0].numpy()).min() >= 0.99999
@@ -247,13 +247,14 @@ def test_vit_l14_encode_image_vs_reference(gpu):
     assert m.seq_len == 211 and m.width == 1024 and m.heads == 16
     imgs = syn.images(2, seed=4)
     x11, x12, xp = (t.cpu().numpy() for t in m.encode_image(torch.from_numpy(imgs)))
-    for got, ref in ((x12[:, 0], g["x12cls"]), (xp[:, 0], g["projcls"]), (x11[:, 0], g["x11cls"]),
-                     (x12[1, 200:204], g["x12_tok"])):
-        assert _cos(got, ref).min() >= 0.9999
-        assert np.abs(got - ref).max() <= 0.05
+    # the reference's own fp16 deviation: x12cls 0.0105, projcls 0.0039
+    close_to_reference(x12[:, 0], g, "x12cls")
+    close_to_reference(xp[:, 0], g, "projcls")
+    close_to_reference(x11[:, 0], g, "x11cls", via="x12cls")
+    close_to_reference(x12[1, 200:204], g, "x12_tok", via="x12cls")
     c12, cp = m.encode_cls(torch.from_numpy(imgs))
-    assert _cos(c12.cpu().numpy(), g["x12cls"]).min() >= 0.9999
-    assert _cos(cp.cpu().numpy(), g["projcls"]).min() >= 0.9999
+    close_to_reference(c12.cpu().numpy(), g, "x12cls")
+    close_to_reference(cp.cpu().numpy(), g, "projcls")
     with torch.no_grad():
         _, b12, bp = vit_ref.vit_forward(sd, imgs, f16=True)
     assert _cos(x12[:, 0], b12[:, 0].numpy()).min() >= 0.99999
@@ -272,11 +273,11 @@ def test_vit_cls_path_and_tta(vit_b16):
     assert _cos(c12.cpu().numpy(), x12[:, 0].cpu().numpy()).min() >= 0.999999
     assert _cos(cp.cpu().numpy(), xp[:, 0].cpu().numpy()).min() >= 0.999999
     assert (c12 - x12[:, 0]).abs().max() < 5e-3 and (cp - xp[:, 0]).abs().max() < 5e-3
-    g12 = g["x12cls"]
-    assert _cos(c12.cpu().numpy(), g12).min() >= 0.9999
+    close_to_reference(c12.cpu().numpy(), g, "x12cls")
+    close_to_reference(cp.cpu().numpy(), g, "projcls")
     t12, tp = m.encode_cls(imgs, tta=g["tta_offsets"])  # augmented view built inside im2col
-    assert _cos(t12.cpu().numpy(), g["tta_x12cls"]).min() >= 0.9999
-    assert _cos(tp.cpu().numpy(), g["tta_projcls"]).min() >= 0.9999
+    close_to_reference(t12.cpu().numpy(), g, "tta_x12cls", via="x12cls")
+    close_to_reference(tp.cpu().numpy(), g, "tta_projcls", via="projcls")
     aug = syn.tta_images_np(imgs.numpy(), g["tta_offsets"])
     a12, ap = m.encode_cls(torch.from_numpy(aug))
     assert torch.equal(a12, t12) and torch.equal(ap, tp)
@@ -312,7 +313,7 @@ def test_text_encoder_vs_reference(gpu):
     g = golden("text.npz")
     tm = TextTransformer(sd)
     out = tm.encode_text(torch.from_numpy(g["tokens"])).cpu().numpy()
-    assert _cos(out, g["text_feat"]).min() >= 0.9999
+    close_to_reference(out, g, "text_feat")  # the reference's fp16 deviation: 0.0056
     with torch.no_grad():
         ref = vit_ref.text_forward(sd, g["tokens"], f16=True).numpy()
     assert _cos(out, ref).min() >= 0.99995  # 12 causal blocks: bf16 rounding flips compound

@@ -11,15 +11,16 @@ functions (tests/golden/make_goldens.py with the refstubs/ import stand-ins):
     R1_mAP_eval(reranking=True) on identity-structured crops (north star: mAP within 1e-3,
     rank lists)
 
-Feature tolerances are those of tests/test_gpu_encoder.py (cosine >= 0.9999 against the
-reference's fp32 outputs; the reference's own fp16 GPU dtype sits at the same distance).
+Feature tolerances are those of tests/test_gpu_encoder.py: max |err| against the reference's
+fp32 outputs <= 1.5 x the reference's own fp16-vs-fp32 deviation on the same inputs (the
+fixtures hold both runs; conftest.close_to_reference), cosine >= 0.99995.
 """
 import numpy as np
 import pytest
 import torch
 
 from multimodal_reid_amd import synthetic as syn
-from conftest import golden
+from conftest import close_to_reference, golden
 
 pytestmark = pytest.mark.gpu
 
@@ -48,16 +49,18 @@ def test_ivlp_build_model_vs_reference(gpu):
     assert clip.visual.seq_len == 213 and clip.visual.n_ctx == 2 and clip.text.n_ctx == 2
     imgs = torch.from_numpy(syn.images(2, seed=6))
     x11, x12, xp = (t.cpu().numpy() for t in clip.visual.encode_image(imgs))
-    _close(x12[:, 0], g["x12cls"])
-    _close(x11[:, 0], g["x11cls"])
-    _close(xp[:, 0], g["projcls"])
-    _close(x12[1, -2:], g["x12_prompt"])
-    _close(xp[0, 100:103], g["proj_tok"])
+    # the reference's own fp16 deviation (build_model's convert_weights): x12cls 0.0064,
+    # projcls 0.0047, text 0.0053
+    close_to_reference(x12[:, 0], g, "x12cls")
+    close_to_reference(x11[:, 0], g, "x11cls", via="x12cls")
+    close_to_reference(xp[:, 0], g, "projcls")
+    close_to_reference(x12[1, -2:], g, "x12_prompt", via="x12cls")
+    close_to_reference(xp[0, 100:103], g, "proj_tok", via="projcls")
     c12, cp = clip.visual.encode_cls(imgs)
-    _close(c12.cpu().numpy(), g["x12cls"])
-    _close(cp.cpu().numpy(), g["projcls"])
+    close_to_reference(c12.cpu().numpy(), g, "x12cls")
+    close_to_reference(cp.cpu().numpy(), g, "projcls")
     txt = clip.encode_text(torch.from_numpy(g["tokens"])).cpu().numpy()
-    _close(txt, g["text_feat"])
+    close_to_reference(txt, g, "text_feat")
 
 
 class _FakeVisual:
@@ -155,10 +158,9 @@ def test_model_adaptor_checkpoint_vs_reference(gpu, tmp_path):
     model, bn, bnp = utils.model_adaptor(None, 256, 128, str(path))
     imgs = torch.from_numpy(syn.images(3, seed=10))
     c12, cp = (t.cpu().numpy() for t in model.visual.encode_cls(imgs))
-    _close(c12, g["x12cls"])
-    _close(cp, g["projcls"])
-    _close(c12, g["x12cls_fp16"])
-    _close(cp, g["projcls_fp16"])
+    # the reference's own fp16 deviation: x12cls 0.0061, projcls 0.0042
+    close_to_reference(c12, g, "x12cls")
+    close_to_reference(cp, g, "projcls")
     assert np.array_equal(np.asarray(bn.params["running_mean"]), g["bn_running_mean"])
     assert np.array_equal(np.asarray(bnp.params["weight"]), g["bnp_weight"])
 
@@ -192,7 +194,7 @@ def test_end_to_end_accuracy_vs_reference(gpu):
     model, _, _ = utils.model_adaptor(None, 256, 128, syn.clipreid_checkpoint("ViT-B/16", seed=20))
     feats = _embed_all(model, imgs, offs)
     fsel = torch.cat([feats[:16], feats[Q:Q + 16]]).cpu().numpy()
-    assert _cos(fsel, g["feat32_fp32"]).min() >= 0.9999
+    close_to_reference(fsel, {"f": g["feat32_fp32"], "f_fp16": g["feat32_fp16"]}, "f")  # TTA-averaged features
     cmc, mAP = zsl.get_cmc_map(feats[Q:], feats[:Q], torch.from_numpy(gp), torch.from_numpy(qp),
                                torch.from_numpy(gc), torch.from_numpy(qc))
     d_ref = abs(float(g["map_fp16"]) - float(g["map_fp32"]))

@@ -80,3 +80,59 @@ def test_rerank_duke_scale_properties(gpu):
     fn = evaluate.l2_normalize_device(torch.from_numpy(feats))
     final = _rr().re_ranking_device(fn[:sp["num_query"]], fn[sp["num_query"]:], 50, 15, 0.3)
     assert torch.isfinite(final).all() and float(final.min()) >= 0.0 and float(final.max()) <= 1.001  # fp16(0.7) = 0.7002
+
+
+def _groups(sizes, dim, noise, seed):
+    r = np.random.default_rng(seed)
+    c = r.standard_normal((len(sizes), dim)).astype(np.float32)
+    f = np.concatenate([c[k] + noise * r.standard_normal((n, dim)).astype(np.float32) for k, n in enumerate(sizes)])
+    return oracle.l2norm(f[r.permutation(len(f))])
+
+
+@pytest.mark.parametrize("case", ["k80_k40", "k150_k30_dense", "k20_k1030"])
+def test_rerank_without_capacity_limits_vs_oracle(gpu, case):
+    """The reference's re_ranking has no capacity limit (reranking.py:51-78: dense N x N V and
+    V_qe); neither has this one.  Each case leaves the on-chip kernels:
+      k80_k40        k1 = 80 (k-reciprocal depth 81 > 64: kreciprocal_generic_kernel), k2 = 40
+                     (> 32: every V_qe row through qe_generic_kernel);
+      k150_k30_dense groups of 300 near-duplicates beside groups of 40: most rows' 30 V rows
+                     stage more than the 6144 entries qe_kernel holds -> those rows deferred to
+                     qe_generic_kernel, the rest on chip;
+      k20_k1030      k2 = 1030: initial_rank prefix K = 1030 > 1024 (top-k in two rounds) and each
+                     V_qe row the mean of 1030 V rows (qe_generic_kernel's slab, ~30k entries).
+    One-call (reidmi_rerank) and staged (reidmi_rr_*, deferred rows counted then written into
+    the CSR) must both equal the oracle bit for bit."""
+    rr = _rr()
+    if case == "k80_k40":
+        k1, k2, Q = 80, 40, 80
+        f = _groups([60] * 12, 64, 0.35, 1)
+    elif case == "k150_k30_dense":
+        k1, k2, Q = 150, 30, 100
+        f = _groups([300] * 6 + [40] * 10, 64, 0.2, 2)
+    else:
+        k1, k2, Q = 20, 1030, 60
+        f = _groups([400] * 2 + [100] * 4, 32, 0.5, 3)
+    ref = oracle.re_ranking(f[:Q], f[Q:], k1, k2, 0.3)
+    ft = torch.from_numpy(f).to(gpu)
+    one = rr.re_ranking(ft[:Q], ft[Q:], k1, k2, 0.3)
+    assert np.array_equal(one.view(np.uint32), ref.view(np.uint32))
+    staged = rr.re_ranking_sharded(ft[:Q], ft[Q:], k1, k2, 0.3, chunk_bytes=4 * len(f) * 211).cpu().numpy()
+    assert np.array_equal(staged.view(np.uint32), ref.view(np.uint32))
+    if case == "k150_k30_dense":  # the deferral path was taken by some rows, not all
+        st = rr.HipStages(ft, Q, k1, k2, 0.3)
+        R, rmax = st.rank_rows(0, st.N)
+        V = rr._gather_csr(st, *st.v_rows(R, rmax, 0, st.N), st.N)
+        vlen = torch.diff(V[0]).cpu().numpy()
+        tot = vlen[R[:, :k2].long().cpu().numpy()].sum(1)
+        assert 0 < (tot > 6144).sum() < len(tot)
+
+
+def test_topk_rows_rounds(gpu):
+    """reidmi_topk_rows_f32 beyond 1024: rounds of 1024 over the row, each keeping only the
+    keys after the last selected one -> np.argsort(kind='stable')[:, :k], ties included."""
+    from multimodal_reid_amd import evaluate
+    r = np.random.default_rng(5)
+    x = r.integers(0, 400, (37, 5000)).astype(np.float32)  # dense exact ties
+    for k in (1024, 1025, 2500, 5000):
+        got = evaluate.topk_rows_device(torch.from_numpy(x), k).cpu().numpy()
+        assert np.array_equal(got, np.argsort(x, axis=1, kind="stable")[:, :k].astype(np.int32)), k

@@ -130,3 +130,57 @@ def test_rank_prefilter_bitexact(gpu, case):
     assert st._f16[4] == (case != "fp16_range")
     assert np.array_equal(Rf, Re)
     assert np.array_equal(mf.view(np.uint32), me.view(np.uint32))
+
+
+def _one_call(feat, Q, k1, k2, lam):
+    """reidmi_rerank itself (N x N fp32 distance materialised), whatever N."""
+    from multimodal_reid_amd import _lib, reranking
+    N, D = feat.shape
+    G = N - Q
+    L = _lib.load()
+    nbytes = L.reidmi_rerank_workspace_bytes(Q, G, k1, k2, 0, 0)
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=feat.device)
+    out = torch.empty((Q, G), device=feat.device)
+    flags = torch.zeros(1, dtype=torch.int32, device=feat.device)
+    lh, lf = reranking._lam(lam)
+    _lib.call("reidmi_rerank", _lib.ptr(feat), Q, G, D, D, k1, k2, lh, lf, _lib.ptr(out), G, _lib.ptr(ws), nbytes,
+              _lib.ptr(flags), _lib.stream())
+    reranking._check(flags)
+    del ws
+    return out
+
+
+@pytest.mark.parametrize("case", ["clustered", "tracklets"])
+def test_staged_prefilter_above_min_n_bitexact(gpu, case):
+    """Where the staged path is actually used: N = 33 000 >= STAGED_MIN_N, D = 1280, so
+    re_ranking_device takes the row-chunked stages with the fp16 R2 pre-filter (and
+    R1_mAP_eval(reranking=True) too).  Both must equal the one-call reidmi_rerank (its N x N
+    fp32 distance, 4.4 GB, still fits) bit for bit, and the CMC/mAP must be identical.
+    'tracklets': the gallery is groups of 24 near-identical crops (MSMT17-style tracklets),
+    dense exact-distance ties and duplicate-heavy neighbourhoods."""
+    from multimodal_reid_amd import evaluate, reranking
+    Q, G, D = 1500, 31500, 1280
+    assert Q + G >= reranking.STAGED_MIN_N
+    qp, gp, qc, gc = syn.labels(Q, G, num_ids=1300, num_cams=15, seed=41, distractor_frac=0.1, junk_frac=0.02)
+    if case == "clustered":
+        qf, gf = syn.features(qp, gp, dim=D, seed=41)
+    else:
+        r = np.random.default_rng(41)
+        qf, gf = syn.features(qp, gp, dim=D, seed=41, noise=2.0)
+        base = gf[::24].repeat(24, axis=0)[:G]
+        gf = (base + 1e-3 * r.standard_normal(base.shape)).astype(np.float32)
+        gp = gp[::24].repeat(24)[:G]
+    qn = evaluate.l2_normalize_device(torch.from_numpy(qf).to(gpu))
+    gn = evaluate.l2_normalize_device(torch.from_numpy(gf).to(gpu))
+    auto = reranking.re_ranking_device(qn, gn, 50, 15, 0.3)
+    one = _one_call(torch.cat([qn, gn]).contiguous(), Q, 50, 15, 0.3)
+    assert torch.equal(auto.view(torch.int32), one.view(torch.int32))
+    cmc1, map1 = evaluate.eval_func_device(one, qp, gp, qc, gc)
+    del auto, one
+    torch.cuda.empty_cache()
+    ev = evaluate.R1_mAP_eval(Q, max_rank=50, feat_norm=True, reranking=True)
+    ev.reset()
+    ev.update((torch.cat([torch.from_numpy(qf), torch.from_numpy(gf)]), np.concatenate([qp, gp]),
+               np.concatenate([qc, gc])))
+    cmc2, map2 = ev.compute()
+    assert np.array_equal(cmc1, cmc2) and map1 == map2

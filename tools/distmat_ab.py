@@ -7,13 +7,14 @@ for (Q, G, D) in [(3368, 15913, 1280), (531, 1010000, 1792), (11659, 82161, 1280
     q = torch.randn(Q, D, device=dev); g = torch.randn(G, D, device=dev)
     out = torch.empty(Q, G, device=dev)
     res = {}
+    ws = torch.empty(Q + G, device=dev)
     for v in (1, 0, 1, 0):
-        L.call("reidmi_distmat_set_variant", v)
-        evaluate.euclidean_distance_device(q, g, out=out); torch.cuda.synchronize()
+        run = lambda: L.call("reidmi_distmat_f32_variant", L.ptr(q), Q, D, L.ptr(g), G, D, D, L.ptr(out), G,
+                             L.ptr(ws), v, L.stream())
+        run(); torch.cuda.synchronize()
         t = time.perf_counter()
-        for _ in range(3): evaluate.euclidean_distance_device(q, g, out=out)
+        for _ in range(3): run()
         torch.cuda.synchronize(); ms = (time.perf_counter() - t) / 3 * 1e3
         res.setdefault(v, []).append(2.0 * Q * G * D / ms / 1e9)
     print(Q, G, D, {v: round(max(x), 1) for v, x in res.items()}, "TF/s", flush=True)
     del q, g, out; torch.cuda.empty_cache()
-L.call("reidmi_distmat_set_variant", 0)

@@ -47,19 +47,18 @@ def main():
         for name, args in bufs.items():
             N, K = args[6], args[7]
             for t in tiles:
-                L.call("reidmi_gemm_set_tile", t)
+                targs = args[:13] + (t, 0, args[13])
                 for _ in range(3):
-                    L.call("reidmi_gemm_f16", *args[:14])
+                    L.call("reidmi_gemm_f16_tiled", *targs)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(a.reps):
-                    L.call("reidmi_gemm_f16", *args[:14])
+                    L.call("reidmi_gemm_f16_tiled", *targs)
                 e1.record()
                 torch.cuda.synchronize()
                 ms = e0.elapsed_time(e1) / a.reps
                 print(f"r{r} {name:5s} M={M} N={N} K={K} tile={t}: {ms * 1e3:8.1f} us "
                       f"{2.0 * M * N * K / ms / 1e9:7.1f} TF/s", flush=True)
-    L.call("reidmi_gemm_set_tile", 0)
 
 
 if __name__ == "__main__":

@@ -41,17 +41,16 @@ def main():
     if a.fold == "fold":
         rs = torch.stack([torch.rand(M + 256, device=dev) + 0.5, torch.rand(M + 256, device=dev) - 0.5], 1)
         cs = torch.rand(N, device=dev)
-    args = (epi, L.ptr(A), K, L.ptr(W), K, M, N, K, L.ptr(b), L.ptr(rs), L.ptr(cs), L.ptr(out), N, L.stream())
-    L.call("reidmi_gemm_set_tile", a.tile)
+    base = (epi, L.ptr(A), K, L.ptr(W), K, M, N, K, L.ptr(b), L.ptr(rs), L.ptr(cs), L.ptr(out), N)
     for _ in range(a.warm):  # clocks up before the first timed walk
-        L.call("reidmi_gemm_f16", *args)
+        L.call("reidmi_gemm_f16_tiled", *base, a.tile, 0, L.stream())
     for walk in (int(w) for w in a.walk.split(",")):
-        L.call("reidmi_gemm_set_walk", walk)
-        L.call("reidmi_gemm_f16", *args)
+        args = base + (a.tile, walk, L.stream())
+        L.call("reidmi_gemm_f16_tiled", *args)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(a.reps):
-            L.call("reidmi_gemm_f16", *args)
+            L.call("reidmi_gemm_f16_tiled", *args)
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / a.reps
