@@ -248,6 +248,16 @@ int reidmi_attn_lpad(int L);
 int reidmi_mhsa_f16(const void* q, const void* k, const void* vt, void* o, int64_t nseq, int L, int H, int causal,
                      void* stream);
 
+/* ln_1 -> in_proj -> SDPA of one encoder block (custom_clip_model.py:22-27) with ln_1 folded
+ * (reidmi_gemm_f16's rowstat / colsum / folded bias; wq [3W][ldw] = the folded in_proj weight):
+ * o [nseq*L][W] fp16 = attention output, token-major (the out_proj operand).  fused = 1: one
+ * kernel, q / k / v stay on chip (192 < L <= 224, non-causal: the vision towers; q, k, vt may
+ * be NULL); fused = 0: the QKV GEMM into q, k [nseq*H][L][64] and vt [nseq*H][64][reidmi_attn_lpad(L)]
+ * then reidmi_mhsa_f16.  Bit-identical results; reidmi_vit_forward uses the fused kernel. */
+int reidmi_qkv_attention_f16(const void* x, int64_t ldx, const void* wq, int64_t ldw, const float* bias,
+                             const float* colsum, const void* rowstat, int64_t nseq, int L, int H, int W, void* q,
+                             void* k, void* vt, void* o, int fused, void* stream);
+
 /* LayerNorm over rows of width W in {512,768,1024} (fp32 math, eps) — custom_clip_model.py:43-49.
  * Row r of the output reads input row row_idx ? row_idx[r] : r.  y32 / y16 (fp16) nullable. */
 int reidmi_layernorm(const float* x, int64_t rows, int64_t ldx, const int32_t* row_idx, int64_t W,

@@ -61,6 +61,8 @@ SIGNATURES = {
     "reidmi_prof_collect": [_i32, _vp, _vp, _vp],
     "reidmi_prof_collect_min": [_i32, ctypes.c_double, _vp, _vp, _vp],
     "reidmi_mhsa_f16": [_vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp],
+    "reidmi_qkv_attention_f16": [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i32,
+                                 _vp],
     "reidmi_layernorm": [_vp, _i64, _i64, _vp, _i64, _vp, _vp, _f32, _vp, _i64, _vp, _i64, _vp],
     "reidmi_row_stats_f16": [_vp, _i64, _i64, _i64, _vp, _vp, _vp],
     "reidmi_gemm_f16_resid_partials": [_vp, _i64, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _i64, _vp, _vp],

@@ -20,6 +20,12 @@ __device__ __forceinline__ int kswz(int r, int kc) { return r * 64 + ((kc ^ ((r 
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef float f32x2v __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
+
+// one v_cvt_pk_f16_f32 (RNE) per pair, as gemm.hip's epilogues convert
+__device__ __forceinline__ uint32_t cvt_pk_h(float a, float b) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2v{a, b}, f16x2v));
+}
 
 // One wave's block of 32 queries (row qi = block * 32 + (lane & 31)) against the head's K
 // [LP][64] and V^T [64][vstride] in LDS:
@@ -218,6 +224,292 @@ __global__ __launch_bounds__(512) void mhsa_kernel(const _Float16* __restrict__ 
     }
 }
 
+// ======================================================== fused QKV GEMM + attention
+// ln_1 -> in_proj -> SDPA of a vision block (custom_clip_model.py:12,22-27) in one persistent
+// kernel: the QKV GEMM's 1 GB of q / k / v^T per batch of 1024 crops (and the attention's read
+// of it) never reaches HBM.  Unit = (image b, head h): the 192 columns [q_h | k_h | v_h] of the
+// LayerNorm-folded QKV GEMM over the image's NKB*32 (padded) token rows, K = width in steps of
+// 32, then attention of the head from LDS.  One wave per 32 token rows (= its 32 queries).
+//  * GEMM: exactly the MFMA chain of gemm.hip (v_mfma_f32_16x16x32_f16, W fragment as A, the
+//    same 8-halves-per-lane k assignment, K ascending) and the same fold / bias epilogue and
+//    RNE conversions, so q / k / v are bit-identical to gemm_f16(EPI_QKV) and the attention
+//    (attn_block, the same code as mhsa_kernel) sees the same operands: the fused block equals
+//    the unfused one bit for bit (tests/test_gpu_encoder.py test_qkv_attention_fused_bitexact).
+//  * operands HBM/L2 -> LDS by global_load_lds (1 KiB pieces: 16 rows x 64 B), a 3-stage ring
+//    of K-steps that runs on across units (the next unit's first two K-steps land during this
+//    unit's attention); rows >= L read row L-1 (finite, masked keys / unstored queries).
+//  * LDS row = 64 B (4 chunks of 16 B), chunk XOR (row >> 1) & 3: conflict-free ds_read_b128
+//    fragment reads of any 16-row block.
+//  * units are dealt XCD by XCD in image-major order, so the 12 heads of an image run at about
+//    the same time on one XCD and its token rows are read from HBM once (L2 shared).
+constexpr int QA_KS = 32;     // K-step (halves): 64-byte LDS rows
+constexpr int QA_NC = 192;    // q | k | v columns of one head
+constexpr int QA_STAGES = 3;
+
+__device__ __forceinline__ int qa_swz(int r, int c) { return r * QA_KS + ((c ^ ((r >> 1) & 3)) << 3); }
+
+// LDS reads of an LDS-DMA'd slot by inline asm: hipcc would put a vmcnt(0) in front of a plain
+// read of such a slot, draining the operand DMA in flight (the slot's own DMA is retired by the
+// K-loop's counted wait + barrier).  Completed by the caller's lgkmcnt wait.
+__device__ __forceinline__ float4 lds_read_f4(const float* p) {
+    float4 v;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)p)
+                 : "memory");
+    return v;
+}
+// 0, but not known to the compiler (an inline-asm VGPR operand; inside a __device__ function,
+// since the host pass instantiates __global__ template bodies and rejects the "v" constraint)
+__device__ __forceinline__ int opaque_zero() {
+    int z = 0;
+    asm volatile("" : "+v"(z));
+    return z;
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+__device__ __forceinline__ void lds_write_u2(void* p, uint2 v) {
+    asm volatile("ds_write_b64 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory");
+}
+__device__ __forceinline__ void lds_write_h(void* p, _Float16 v) {
+    asm volatile("ds_write_b16 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory");
+}
+__device__ __forceinline__ f16x8 lds_read_h8(const void* p) {
+    f16x8 v;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(lds_addr(p)) : "memory");
+    return v;
+}
+__device__ __forceinline__ float2 lds_read_f2(const float* p) {
+    float2 v;
+    asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)p)
+                 : "memory");
+    return v;
+}
+
+template <int NKB>
+__global__ __launch_bounds__(NKB * 64, 1) void qkv_attn_kernel(const _Float16* __restrict__ x, int64_t ldx,
+                                                               const _Float16* __restrict__ wq, int64_t ldw,
+                                                               const float* __restrict__ bias,
+                                                               const float* __restrict__ colsum,
+                                                               const float2* __restrict__ rowstat, int L, int H, int Wd,
+                                                               int64_t units, _Float16* __restrict__ o,
+                                                               float scale_log2) {
+    constexpr int R = NKB * 32;                       // padded token rows of an image
+    constexpr int NW = NKB;                           // waves
+    constexpr int SA = R * QA_KS;                     // A part of a stage (halves)
+    constexpr int SS = (R + QA_NC) * QA_KS;           // one stage
+    constexpr int APC = R / 16, PCS = APC + QA_NC / 16;  // 1 KiB DMA pieces per stage
+    constexpr int PPW = (PCS + NW - 1) / NW;          // pieces per wave (uniform: extra ones repeat a W piece)
+    constexpr int VS = R + 4;                         // v^T row stride (vt_stride)
+    extern __shared__ __attribute__((aligned(16))) _Float16 lds[];
+    _Float16* sK = lds + QA_STAGES * SS;
+    _Float16* sV = sK + R * 64;
+    // the unit's epilogue operands, DMA'd at its first K-step (a global load in the epilogue
+    // would wait for the next unit's operand DMA issued before it: vmcnt retires in order):
+    // bias [192] at +0, colsum [192] at +1 KiB, rowstat of the image's R rows at +2 KiB
+    float* sE = (float*)(sV + 64 * VS);
+    const int G = gridDim.x, bid = blockIdx.x;
+    const int ng = G < 8 ? G : 8;
+    const int xg = bid % ng;
+    const int gx = G / ng + ((G % ng) > xg ? 1 : 0);
+    const int64_t ulo = units * xg / ng, uhi = units * (xg + 1) / ng;
+    const int64_t ufirst = ulo + bid / ng;
+    if (ufirst >= uhi) return;
+    const int nk = Wd / QA_KS;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+    // DMA pieces of this wave (the same piece numbers every K-step): pc = wid + NW j; pieces
+    // >= PCS repeat a W piece.  Per-lane source offsets (halves) from the unit's base are fixed.
+    const int rp = lane >> 2;               // row inside the piece
+    const int lch = (lane & 3) ^ ((rp >> 1) & 3);  // logical 16-byte chunk of the lane's physical one
+    uint32_t boff[PPW];  // per-lane byte offset from the piece's wave-uniform source base
+#pragma unroll
+    for (int j = 0; j < PPW; j++) {
+        int pc = wid + NW * j;
+        if (pc >= PCS) pc = pc - PCS + APC;
+        if (pc < APC) {
+            const int r = pc * 16 + rp;
+            boff[j] = (uint32_t)(((r < L ? r : L - 1) * (int)ldx + lch * 8) * 2);
+        } else {
+            const int jj = (pc - APC) * 16 + rp;
+            boff[j] = (uint32_t)((((jj >> 6) * Wd + (jj & 63)) * (int)ldw + lch * 8) * 2);
+        }
+    }
+    struct Pos {
+        int64_t unit;
+        int kt;
+        const _Float16* xb;  // x rows of the unit's image
+        const _Float16* wb;  // the unit's head rows of wq
+    };
+    auto set_unit = [&](Pos& p, int64_t u) {
+        p.unit = u;
+        p.kt = 0;
+        const int64_t b = u / H;
+        p.xb = x + b * L * ldx;
+        p.wb = wq + (u - b * H) * 64 * ldw;
+    };
+    auto adv = [&](Pos& p) {
+        if (++p.kt == nk) set_unit(p, p.unit + gx);
+    };
+    auto issue = [&](const Pos& p, int stage) {
+        _Float16* st = lds + stage * SS;
+#pragma unroll
+        for (int j = 0; j < PPW; j++) {
+            int pc = wid + NW * j;  // wave-uniform
+            if (pc >= PCS) pc = pc - PCS + APC;
+            const bool a = pc < APC;
+            const char* base = (const char*)((a ? p.xb : p.wb) + p.kt * QA_KS);
+            // (a void* source: with a char* the host pass drops the kernel's instantiation)
+            __builtin_amdgcn_global_load_lds((const void*)(base + boff[j]),
+                                             (lds_ptr_t)(st + (a ? pc * 512 : SA + (pc - APC) * 512)), 16, 0, 0);
+        }
+    };
+    // one epilogue-operand DMA per wave per unit: wave 1 colsum, waves 2 / 3 the rowstat rows,
+    // the others the bias (lanes 0-15 q, 16-31 k, 32-47 v columns of the head; waves past 3
+    // repeat wave 0's piece: same bytes, same place)
+    const uint32_t eoff = wid == 2 || wid == 3
+                              ? (uint32_t)(((wid - 2) * 256 + lane * 4) * 4)
+                              : (uint32_t)(((lane >> 4 < 3 ? lane >> 4 : 2) * Wd + (lane & 15) * 4) * 4);
+    auto issue_epi = [&](int64_t u, int z) {
+        const uint32_t eo = eoff + (uint32_t)z;
+        const int64_t b = u / H;
+        const int h = (int)(u - b * H);
+        if (wid == 2 || wid == 3) {
+            __builtin_amdgcn_global_load_lds((const void*)((const char*)(rowstat + b * L) + eo),
+                                             (lds_ptr_t)(sE + 512 + (wid - 2) * 256), 16, 0, 0);
+        } else {
+            const float* v = wid == 1 ? colsum : bias;
+            __builtin_amdgcn_global_load_lds((const void*)((const char*)(v + h * 64) + eo),
+                                             (lds_ptr_t)(sE + (wid == 1 ? 256 : 0)), 16, 0, 0);
+        }
+    };
+
+    f32x4 acc[2][12];
+    Pos pd;  // next DMA position
+    set_unit(pd, ufirst);
+    int stage_d = 0;
+    issue(pd, 0);
+    adv(pd);
+    if (pd.unit < uhi) issue(pd, 1);
+    adv(pd);
+    stage_d = 2;
+    int stage_c = 0;
+    for (int64_t u = ufirst; u < uhi; u += gx) {
+        const int64_t b = u / H;
+        const int h = (int)(u - b * H);  // (one division per unit)
+        // an opaque zero offset: keeps the epilogue's and the attention's LDS / DMA address
+        // arithmetic inside the unit loop (hoisted, it held ~30 VGPRs through the K-loop and
+        // forced spills, whose reloads wait for every DMA in flight)
+        const int z = opaque_zero();
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+#pragma unroll
+            for (int j = 0; j < 12; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int kt = 0; kt < nk; kt++) {
+            // this step's DMA landed (the next step's stays in flight; at step 1 also the
+            // epilogue-operand DMA issued between them), then every wave's
+            if (kt == 1)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW + 1) : "memory");
+            else if (kt + 1 < nk || u + gx < uhi)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            // ... and every wave is past the step that read the stage refilled here (and, at
+            // step 0, past the previous unit's epilogue, which read the epilogue slot)
+            if (kt == 0) issue_epi(u, z);
+            if (pd.unit < uhi) {
+                issue(pd, stage_d);
+                adv(pd);
+                stage_d = stage_d == QA_STAGES - 1 ? 0 : stage_d + 1;
+            }
+            const _Float16* sA = lds + stage_c * SS;
+            const _Float16* sW = sA + SA;
+            // all 14 fragments in flight before the MFMAs (the compiler would otherwise wait
+            // for each W fragment right before its pair of MFMAs)
+            f16x8 af[2], wf[12];
+#pragma unroll
+            for (int i = 0; i < 2; i++) af[i] = *(const f16x8*)(sA + qa_swz(wid * 32 + i * 16 + (lane & 15), lane >> 4));
+#pragma unroll
+            for (int j = 0; j < 12; j++) wf[j] = *(const f16x8*)(sW + qa_swz(j * 16 + (lane & 15), lane >> 4));
+#pragma unroll
+            for (int j = 0; j < 12; j++)
+#pragma unroll
+                for (int i = 0; i < 2; i++)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[j], af[i], acc[i][j], 0, 0, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);  // 8 fragment reads
+#pragma unroll
+            for (int g = 0; g < 6; g++) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // 2 MFMAs
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 read
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
+            stage_c = stage_c == QA_STAGES - 1 ? 0 : stage_c + 1;
+        }
+        // ---- epilogue: ln_1 fold + bias (gemm.hip), fp16 q / k / v (RNE)
+        const int q4 = lane >> 4;
+        float2 rs[2];
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            const int t = wid * 32 + i * 16 + (lane & 15);
+            rs[i] = lds_read_f2(sE + z + 512 + 2 * (t < L ? t : L - 1));
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        auto fold = [&](int j) {
+            const int c = j * 16 + 4 * q4;  // column of the unit's 192
+            const float4 bn = lds_read_f4(sE + z + c), sn = lds_read_f4(sE + z + 256 + c);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+                acc[i][j][0] = __builtin_fmaf(rs[i].x, acc[i][j][0], __builtin_fmaf(rs[i].y, sn.x, bn.x));
+                acc[i][j][1] = __builtin_fmaf(rs[i].x, acc[i][j][1], __builtin_fmaf(rs[i].y, sn.y, bn.y));
+                acc[i][j][2] = __builtin_fmaf(rs[i].x, acc[i][j][2], __builtin_fmaf(rs[i].y, sn.z, bn.z));
+                acc[i][j][3] = __builtin_fmaf(rs[i].x, acc[i][j][3], __builtin_fmaf(rs[i].y, sn.w, bn.w));
+            }
+        };
+        _Float16* qs = sV + z + wid * (32 * 64);  // this wave's q rows, staged in the v^T region
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            fold(j);
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+                const int tl = i * 16 + (lane & 15);
+                const uint2 pk = make_uint2(cvt_pk_h(acc[i][j][0], acc[i][j][1]), cvt_pk_h(acc[i][j][2], acc[i][j][3]));
+                if (j < 4) {
+                    lds_write_u2(qs + tl * 64 + j * 16 + 4 * q4, pk);
+                } else {
+                    const int t = wid * 32 + tl, d0 = (j - 4) * 16 + 4 * q4;
+                    lds_write_u2(sK + z + kswz(t, d0 >> 3) + (d0 & 7), pk);
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 8; j < 12; j++) fold(j);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        f16x8 qf[4];
+        {
+            const int tl = lane & 31, hh = lane >> 5;
+#pragma unroll
+            for (int ks = 0; ks < 4; ks++) qf[ks] = lds_read_h8(qs + tl * 64 + ks * 16 + hh * 8);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();  // every wave has its q: the v^T region is free
+#pragma unroll
+        for (int j = 8; j < 12; j++)
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+                const int t = wid * 32 + i * 16 + (lane & 15), d0 = (j - 8) * 16 + 4 * q4;
+#pragma unroll
+                for (int e = 0; e < 4; e++)
+                    lds_write_h(sV + z + (d0 + e) * VS + t, t < L ? (_Float16)acc[i][j][e] : (_Float16)0.0f);
+            }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        attn_block<NKB, false>(sK + z, sV + z, VS, qf, wid * 32 + (lane & 31), L, u, H, o, scale_log2);
+    }
+}
+
 // V^T row stride (elements): LP + 4, i.e. LP/2 + 2 dwords, which is 2 mod 4 dwords (LP is a
 // multiple of 32): the 32 rows of one half-wave ds_read_b64 then start on 32 distinct even
 // banks (row r at bank 2 * (r * odd mod 32)), so they cover all 64 banks exactly once.  (The
@@ -345,6 +637,35 @@ int mhsa_cls(const void* q, const void* k, const void* vt, void* o, int64_t nseq
     const int64_t nbh = nseq * H;
     hipLaunchKernelGGL(mhsa_cls_kernel, dim3(ceil_div(nbh, 4)), dim3(256), 0, s, (const _Float16*)q, (const _Float16*)k,
                        (const _Float16*)vt, (_Float16*)o, nbh, L, H, lp, 0.125f * 1.4426950408889634f);
+    RM_LAUNCHED();
+    return OK;
+}
+
+// Fused QKV + attention for non-causal blocks of L in (192, 224] tokens (the vision towers:
+// 211, IVLP 213); returns EINVAL for other shapes (the caller then runs the two kernels).
+// x [nseq*L][ldx] fp16 (the residual stream), wq [3W][ldw] fp16 (ln_1-folded in_proj), bias /
+// colsum [3W] fp32, rowstat [nseq*L (+pad)] (rstd, -mean*rstd), o [nseq*L][W] fp16.
+bool qkv_attn_fits(int L, int W, bool causal) { return !causal && L > 192 && L <= 224 && W % QA_KS == 0 && W >= 64; }
+
+int qkv_attn(const void* x, int64_t ldx, const void* wq, int64_t ldw, const float* bias, const float* colsum,
+             const void* rowstat, int64_t nseq, int L, int H, int W, void* o, hipStream_t s) {
+    RM_REQUIRE(qkv_attn_fits(L, W, false) && W == H * 64 && nseq >= 0, "qkv_attn: shape");
+    RM_REQUIRE(bias && colsum && rowstat && ldx >= W && ldw >= W && ldx % 8 == 0 && ldw % 8 == 0, "qkv_attn: args");
+    const int64_t units = nseq * H;
+    if (units == 0) return OK;
+    RM_REQUIRE(units < (1ll << 31), "qkv_attn: too many units");
+    constexpr int NKB = 7, R = NKB * 32;
+    const size_t lds = ((size_t)QA_STAGES * (R + QA_NC) * QA_KS + (size_t)R * 64 + (size_t)64 * (R + 4)) * 2 + 4096;
+    static bool attr = false;
+    if (!attr) {
+        RM_CHECK_HIP(hipFuncSetAttribute((const void*)qkv_attn_kernel<NKB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)lds));
+        attr = true;
+    }
+    const int64_t grid = units < num_cu() ? units : num_cu();
+    hipLaunchKernelGGL((qkv_attn_kernel<NKB>), dim3((unsigned)grid), dim3(NKB * 64), lds, s, (const _Float16*)x, ldx,
+                       (const _Float16*)wq, ldw, bias, colsum, (const float2*)rowstat, L, H, W, units, (_Float16*)o,
+                       0.125f * 1.4426950408889634f);
     RM_LAUNCHED();
     return OK;
 }

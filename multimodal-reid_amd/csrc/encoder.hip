@@ -21,6 +21,9 @@ namespace reidmi {
 int mhsa(const void* q, const void* k, const void* vt, void* o, int64_t nseq, int L, int H, bool causal,
          hipStream_t s);
 int attn_lpad(int L);
+bool qkv_attn_fits(int L, int W, bool causal);
+int qkv_attn(const void* x, int64_t ldx, const void* wq, int64_t ldw, const float* bias, const float* colsum,
+             const void* rowstat, int64_t nseq, int L, int H, int W, void* o, hipStream_t s);
 int mhsa_cls(const void* q, const void* k, const void* vt, void* o, int64_t nseq, int L, int H, hipStream_t s);
 
 // ------------------------------------------------------------------- LayerNorm
@@ -351,18 +354,23 @@ static int run_block(const reidmi_block_weights& bw, char* ws, const Plan& P, in
     int rc;
     // ln_1 (custom_clip_model.py:27)
     if ((rc = x_pst ? row_stats_from_partials(pst, M, W, st, s) : row_stats(x, M, W, W, st, s))) return rc;
-    EpiArgs ea{};
-    ea.bias = bw.qkv_b;
-    ea.rowstat = st;
-    ea.colsum = bw.qkv_s;
-    ea.q = ws + P.q;
-    ea.k = ws + P.k;
-    ea.vt = ws + P.vt;
-    ea.seq = L;
-    ea.heads = H;
-    ea.lpad = attn_lpad(L);
-    if ((rc = gemm_f16(EPI_QKV, x, W, bw.qkv_w, W, M, 3 * W, W, ea, s))) return rc;
-    if ((rc = mhsa(ws + P.q, ws + P.k, ws + P.vt, o, nseq, L, H, causal, s))) return rc;
+    if (qkv_attn_fits(L, W, causal)) {
+        // vision blocks: QKV GEMM + attention fused, q / k / v never leave the CU (attention.hip)
+        if ((rc = qkv_attn(x, W, bw.qkv_w, W, bw.qkv_b, bw.qkv_s, st, nseq, L, H, W, o, s))) return rc;
+    } else {
+        EpiArgs ea{};
+        ea.bias = bw.qkv_b;
+        ea.rowstat = st;
+        ea.colsum = bw.qkv_s;
+        ea.q = ws + P.q;
+        ea.k = ws + P.k;
+        ea.vt = ws + P.vt;
+        ea.seq = L;
+        ea.heads = H;
+        ea.lpad = attn_lpad(L);
+        if ((rc = gemm_f16(EPI_QKV, x, W, bw.qkv_w, W, M, 3 * W, W, ea, s))) return rc;
+        if ((rc = mhsa(ws + P.q, ws + P.k, ws + P.vt, o, nseq, L, H, causal, s))) return rc;
+    }
     EpiArgs er{};
     er.out = x;
     er.ldc = W;
@@ -646,4 +654,33 @@ REIDMI_API int reidmi_gemm_f16_resid_partials(const void* A, int64_t lda, const 
     e.ldp = M;
     return gemm_f16(EPI_RESID_F16, (const _Float16*)A, lda, (const _Float16*)Wt, ldw, M, (int)N, (int)K, e,
                     (hipStream_t)stream);
+}
+
+// ln_1-folded QKV projection + attention of one block (custom_clip_model.py:22-27) on its own,
+// for tests / A-B timing: fused = 1 the single fused kernel, 0 the QKV GEMM (head-split
+// epilogue into q, k [nseq*H][L][64], vt [nseq*H][64][reidmi_attn_lpad(L)]) then the attention
+// kernel.  The two are bit-identical (same MFMA chains, same roundings).
+REIDMI_API int reidmi_qkv_attention_f16(const void* x, int64_t ldx, const void* wq, int64_t ldw, const float* bias,
+                                        const float* colsum, const void* rowstat, int64_t nseq, int L, int H, int W,
+                                        void* q, void* k, void* vt, void* o, int fused, void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    RM_REQUIRE(W == H * 64 && L > 0 && nseq >= 0 && rowstat && colsum && bias, "qkv_attention: bad arguments");
+    if (fused) {
+        RM_REQUIRE(qkv_attn_fits(L, W, false), "qkv_attention: the fused kernel takes 192 < L <= 224 tokens");
+        return qkv_attn(x, ldx, wq, ldw, bias, colsum, rowstat, nseq, L, H, W, o, s);
+    }
+    RM_REQUIRE(q && k && vt, "qkv_attention: q / k / vt scratch required for the unfused path");
+    EpiArgs ea{};
+    ea.bias = bias;
+    ea.rowstat = (const float2*)rowstat;
+    ea.colsum = colsum;
+    ea.q = q;
+    ea.k = k;
+    ea.vt = vt;
+    ea.seq = L;
+    ea.heads = H;
+    ea.lpad = attn_lpad(L);
+    int rc;
+    if ((rc = gemm_f16(EPI_QKV, x, ldx, wq, ldw, nseq * L, 3 * W, W, ea, s))) return rc;
+    return mhsa(q, k, vt, o, nseq, L, H, false, s);
 }

@@ -135,3 +135,48 @@ def text_forward(sd, tokens, prompts=None, f16=False):
         x = block(x, sd, p, heads, True, f16)
     x = _ln(x[torch.arange(N), tokens.argmax(-1)], sd["ln_final.weight"], sd["ln_final.bias"])
     return _r(x, f16) @ _r(_t(sd["text_projection"]), f16)
+
+
+class FastVit:
+    """The same fp32 math as vit_forward(f16=False) laid out the way the reference's modules run
+    it on the CPU (custom_clip_model.py:57-100: Conv2d, nn.MultiheadAttention -> in_proj linear,
+    scaled_dot_product_attention, out_proj; LayerNorm; QuickGELU), with the weights converted
+    once to contiguous fp32 tensors.  bench.py's cpu_baseline times this: the CPU reference
+    path's speed, not the emulation's (vit_forward re-reads the numpy state dict per op and
+    runs the attention as explicit matmul/softmax)."""
+
+    def __init__(self, sd, stride=12):
+        self.w = {k: torch.from_numpy(np.ascontiguousarray(np.asarray(v, np.float32))) for k, v in sd.items()}
+        self.stride = stride
+        self.width = self.w["conv1.weight"].shape[0]
+        self.heads = self.width // 64
+        self.layers = len([k for k in sd if k.startswith("transformer.") and k.endswith(".attn.in_proj_weight")])
+
+    @torch.inference_mode()
+    def __call__(self, img, tta=None):
+        w = self.w
+        img = _t(img)
+        if tta is not None:
+            img = tta_view(img, tta)
+        B = img.shape[0]
+        x = F.conv2d(img, w["conv1.weight"], stride=self.stride)
+        x = x.reshape(B, self.width, -1).permute(0, 2, 1)
+        x = torch.cat([w["class_embedding"].expand(B, 1, -1), x], 1) + w["positional_embedding"]
+        x = F.layer_norm(x, (self.width,), w["ln_pre.weight"], w["ln_pre.bias"], 1e-5)
+        L, H = x.shape[1], self.heads
+        x11 = None
+        for i in range(12):
+            p = f"transformer.resblocks.{i}."
+            h = F.layer_norm(x, (self.width,), w[p + "ln_1.weight"], w[p + "ln_1.bias"], 1e-5)
+            qkv = F.linear(h, w[p + "attn.in_proj_weight"], w[p + "attn.in_proj_bias"])
+            q, k, v = qkv.reshape(B, L, 3, H, 64).permute(2, 0, 3, 1, 4)
+            o = F.scaled_dot_product_attention(q, k, v).permute(0, 2, 1, 3).reshape(B, L, self.width)
+            x = x + F.linear(o, w[p + "attn.out_proj.weight"], w[p + "attn.out_proj.bias"])
+            h = F.layer_norm(x, (self.width,), w[p + "ln_2.weight"], w[p + "ln_2.bias"], 1e-5)
+            u = F.linear(h, w[p + "mlp.c_fc.weight"], w[p + "mlp.c_fc.bias"])
+            u = u * torch.sigmoid(1.702 * u)
+            x = x + F.linear(u, w[p + "mlp.c_proj.weight"], w[p + "mlp.c_proj.bias"])
+            if i == 10:
+                x11 = x
+        x12 = F.layer_norm(x, (self.width,), w["ln_post.weight"], w["ln_post.bias"], 1e-5)
+        return x11, x12, x12 @ w["proj"]

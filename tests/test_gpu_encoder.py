@@ -367,3 +367,43 @@ def test_inference_glue(vit_b16):
     ref_mm = torch.cat([(a12 + b12).cpu() / 2, logits], 1)
     assert emb_mm.shape == (5, 768 + 37)
     assert torch.allclose(emb_mm, ref_mm, atol=1e-5)
+
+
+def _qkv_attention(L, nseq, W, fused, x, wq, bias, cs, rs):
+    from multimodal_reid_amd import _lib as lib
+    H = W // 64
+    lp = lib.load().reidmi_attn_lpad(L)
+    q = k = vt = None
+    if not fused:
+        q = torch.empty(nseq * H * L * 64, dtype=torch.float16, device="cuda")
+        k = torch.empty_like(q)
+        vt = torch.zeros(nseq * H * 64 * lp, dtype=torch.float16, device="cuda")
+    o = torch.full((nseq * L, W), float("nan"), dtype=torch.float16, device="cuda")
+    lib.call("reidmi_qkv_attention_f16", lib.ptr(x), W, lib.ptr(wq), W, lib.ptr(bias), lib.ptr(cs), lib.ptr(rs), nseq,
+             L, H, W, lib.ptr(q), lib.ptr(k), lib.ptr(vt), lib.ptr(o), int(fused), lib.stream())
+    return o
+
+
+@pytest.mark.parametrize("L,nseq,W", [(211, 37, 768), (213, 300, 768), (211, 23, 1024), (224, 5, 768), (193, 9, 768)])
+def test_qkv_attention_fused_bitexact(gpu, L, nseq, W):
+    """The fused QKV GEMM + attention kernel (q / k / v never leave the CU) equals the QKV
+    GEMM (head-split epilogue) followed by the attention kernel bit for bit: the same MFMA
+    chain per q / k / v element, the same fold / bias / RNE epilogue, the same attention code
+    on the same operands.  Vision lengths (211, IVLP 213, ViT-L width 1024) and the ends of the
+    fused kernel's range (193 and 224 tokens); unit counts that do not divide over the XCDs."""
+    from multimodal_reid_amd.model import fold_layernorm
+    g = torch.Generator().manual_seed(L * 7 + nseq + W)
+    M = nseq * L
+    x = (torch.randn(M, W, generator=g) * (0.5 + torch.rand(M, 1, generator=g)) + torch.randn(M, 1, generator=g)).half()
+    gam, bet = 1 + 0.3 * torch.randn(W, generator=g), 0.2 * torch.randn(W, generator=g)
+    Wi, bi = torch.randn(3 * W, W, generator=g) / W ** 0.5, 0.1 * torch.randn(3 * W, generator=g)
+    wf, cs, bf = fold_layernorm(Wi, bi, gam, bet)
+    xd = x.double()
+    mean = xd.mean(1, keepdim=True)
+    rstd = 1 / torch.sqrt(((xd - mean) ** 2).mean(1, keepdim=True) + 1e-5)
+    rs = torch.cat([torch.cat([rstd, -mean * rstd], 1).float(), torch.zeros(256, 2)]).contiguous()
+    args = [t.cuda() for t in (x, wf, bf, cs, rs)]
+    fused = _qkv_attention(L, nseq, W, True, *args)
+    ref = _qkv_attention(L, nseq, W, False, *args)
+    assert torch.isfinite(ref).all()
+    assert torch.equal(fused.view(torch.int16), ref.view(torch.int16))

@@ -125,6 +125,21 @@ def test_vit_b16_oracle_vs_reference():
         assert np.abs(got.numpy() - ref).max() < 2e-5
 
 
+def test_fast_vit_port_equals_reference_module_outputs():
+    """vit_ref.FastVit (the CPU baseline bench.py times) runs the reference modules' op sequence
+    (custom_clip_model.py:77-100) and reproduces their fp32 outputs on the fixture, TTA view too."""
+    from oracle import vit_ref
+    g = golden("vit_b16.npz")
+    fv = vit_ref.FastVit(syn.vit_state_dict("ViT-B/16", seed=0))
+    imgs = syn.images(3, seed=0)
+    x11, x12, xp = fv(imgs)
+    _, t12, tp = fv(imgs, tta=g["tta_offsets"])
+    for got, ref in ((x12[:, 0], g["x12cls"]), (xp[:, 0], g["projcls"]), (x11[:, 0], g["x11cls"]),
+                     (x12[0, :8], g["x12_tok"]), (xp[0, 100:104], g["proj_tok"]),
+                     (t12[:, 0], g["tta_x12cls"]), (tp[:, 0], g["tta_projcls"])):
+        assert np.abs(got.numpy() - ref).max() < 2e-5
+
+
 def test_vit_l14_oracle_vs_reference():
     """ViT-L/14 (configs[4]) as the reference executes it (resblocks[:11] + [11])."""
     from oracle import vit_ref
