@@ -22,6 +22,14 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef float f32x2v __attribute__((ext_vector_type(2)));
 typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
 
+// fp32 -> fp16 (RNE) of a value that must be rounded to fp32 first: the opaque copy keeps the
+// backend from merging the fma that produced x and this conversion into one v_fma_mixlo_f16
+// (a single rounding to fp16, which differs from gemm.hip's in about 1 value in 1500)
+__device__ __forceinline__ _Float16 f32_to_h(float x) {
+    asm("" : "+v"(x));
+    return (_Float16)x;
+}
+
 // one v_cvt_pk_f16_f32 (RNE) per pair, as gemm.hip's epilogues convert
 __device__ __forceinline__ uint32_t cvt_pk_h(float a, float b) {
     return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2v{a, b}, f16x2v));
@@ -251,8 +259,8 @@ __device__ __forceinline__ int qa_swz(int r, int c) { return r * QA_KS + ((c ^ (
 // LDS reads of an LDS-DMA'd slot by inline asm: hipcc would put a vmcnt(0) in front of a plain
 // read of such a slot, draining the operand DMA in flight (the slot's own DMA is retired by the
 // K-loop's counted wait + barrier).  Completed by the caller's lgkmcnt wait.
-__device__ __forceinline__ float4 lds_read_f4(const float* p) {
-    float4 v;
+__device__ __forceinline__ f32x4 lds_read_f4(const float* p) {
+    f32x4 v;
     asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)p)
                  : "memory");
     return v;
@@ -279,12 +287,29 @@ __device__ __forceinline__ f16x8 lds_read_h8(const void* p) {
     asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(lds_addr(p)) : "memory");
     return v;
 }
-__device__ __forceinline__ float2 lds_read_f2(const float* p) {
-    float2 v;
+// The wait that completes inline-asm LDS reads, with the read registers as operands: the
+// compiler then cannot schedule a use of them above it (the hardware does not track VGPRs
+// written by an outstanding LDS read).
+template <typename A, typename B>
+__device__ __forceinline__ void lgkm_wait(A& a, B& b) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b)::"memory");
+}
+template <typename A, typename B, typename C, typename D>
+__device__ __forceinline__ void lgkm_wait(A& a, B& b, C& c, D& d) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d)::"memory");
+}
+
+__device__ __forceinline__ f32x2v lds_read_f2(const float* p) {
+    f32x2v v;
     asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)p)
                  : "memory");
     return v;
 }
+
+#ifdef QA_DEBUG
+__device__ _Float16 *g_dbg_q, *g_dbg_k, *g_dbg_vt;
+__device__ int g_dbg_lp;
+#endif
 
 template <int NKB>
 __global__ __launch_bounds__(NKB * 64, 1) void qkv_attn_kernel(const _Float16* __restrict__ x, int64_t ldx,
@@ -449,17 +474,17 @@ __global__ __launch_bounds__(NKB * 64, 1) void qkv_attn_kernel(const _Float16* _
         }
         // ---- epilogue: ln_1 fold + bias (gemm.hip), fp16 q / k / v (RNE)
         const int q4 = lane >> 4;
-        float2 rs[2];
+        f32x2v rs[2];
 #pragma unroll
         for (int i = 0; i < 2; i++) {
             const int t = wid * 32 + i * 16 + (lane & 15);
             rs[i] = lds_read_f2(sE + z + 512 + 2 * (t < L ? t : L - 1));
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        lgkm_wait(rs[0], rs[1]);
         auto fold = [&](int j) {
             const int c = j * 16 + 4 * q4;  // column of the unit's 192
-            const float4 bn = lds_read_f4(sE + z + c), sn = lds_read_f4(sE + z + 256 + c);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            f32x4 bn = lds_read_f4(sE + z + c), sn = lds_read_f4(sE + z + 256 + c);
+            lgkm_wait(bn, sn);
 #pragma unroll
             for (int i = 0; i < 2; i++) {
                 acc[i][j][0] = __builtin_fmaf(rs[i].x, acc[i][j][0], __builtin_fmaf(rs[i].y, sn.x, bn.x));
@@ -487,12 +512,29 @@ __global__ __launch_bounds__(NKB * 64, 1) void qkv_attn_kernel(const _Float16* _
 #pragma unroll
         for (int j = 8; j < 12; j++) fold(j);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#ifdef QA_DEBUG
+        // debug tap: the folded q / k / v^T in the unfused layouts
+        if (g_dbg_q) {
+            for (int i = 0; i < 2; i++)
+                for (int j = 0; j < 12; j++) {
+                    const int t = wid * 32 + i * 16 + (lane & 15);
+                    if (t >= L) continue;
+                    for (int e = 0; e < 4; e++) {
+                        const int c = j * 16 + 4 * q4 + e;
+                        const _Float16 v = (_Float16)acc[i][j][e];
+                        if (c < 64) g_dbg_q[(u * L + t) * 64 + c] = v;
+                        else if (c < 128) g_dbg_k[(u * L + t) * 64 + c - 64] = v;
+                        else g_dbg_vt[(u * 64 + c - 128) * (int64_t)g_dbg_lp + t] = v;
+                    }
+                }
+        }
+#endif
         f16x8 qf[4];
         {
             const int tl = lane & 31, hh = lane >> 5;
 #pragma unroll
             for (int ks = 0; ks < 4; ks++) qf[ks] = lds_read_h8(qs + tl * 64 + ks * 16 + hh * 8);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            lgkm_wait(qf[0], qf[1], qf[2], qf[3]);
         }
         __builtin_amdgcn_s_barrier();  // every wave has its q: the v^T region is free
 #pragma unroll
@@ -502,7 +544,7 @@ __global__ __launch_bounds__(NKB * 64, 1) void qkv_attn_kernel(const _Float16* _
                 const int t = wid * 32 + i * 16 + (lane & 15), d0 = (j - 8) * 16 + 4 * q4;
 #pragma unroll
                 for (int e = 0; e < 4; e++)
-                    lds_write_h(sV + z + (d0 + e) * VS + t, t < L ? (_Float16)acc[i][j][e] : (_Float16)0.0f);
+                    lds_write_h(sV + z + (d0 + e) * VS + t, t < L ? f32_to_h(acc[i][j][e]) : (_Float16)0.0f);
             }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
@@ -522,8 +564,8 @@ static int g_num_cu = 0;
 static int num_cu() {
     if (!g_num_cu) {
         int dev = 0;
-        hipGetDevice(&dev);
-        hipDeviceGetAttribute(&g_num_cu, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&g_num_cu, hipDeviceAttributeMultiprocessorCount, dev);
         if (g_num_cu <= 0) g_num_cu = 256;
     }
     return g_num_cu;
@@ -705,6 +747,16 @@ int mhsa(const void* q, const void* k, const void* vt, void* o, int64_t nseq, in
 using namespace reidmi;
 
 REIDMI_API int reidmi_attn_lpad(int L) { return attn_lpad(L); }
+
+#ifdef QA_DEBUG
+REIDMI_API int reidmi_qa_dbg_set(void* q, void* k, void* vt, int lp) {
+    RM_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_dbg_q), &q, sizeof(q)));
+    RM_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_dbg_k), &k, sizeof(k)));
+    RM_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_dbg_vt), &vt, sizeof(vt)));
+    RM_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_dbg_lp), &lp, sizeof(lp)));
+    return OK;
+}
+#endif
 
 REIDMI_API int reidmi_mhsa_f16(const void* q, const void* k, const void* vt, void* o, int64_t nseq, int L, int H,
                                 int causal, void* stream) {

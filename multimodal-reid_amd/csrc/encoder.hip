@@ -22,6 +22,10 @@ int mhsa(const void* q, const void* k, const void* vt, void* o, int64_t nseq, in
          hipStream_t s);
 int attn_lpad(int L);
 bool qkv_attn_fits(int L, int W, bool causal);
+// The fused QKV + attention kernel is bit-identical to the two-kernel block but measured slower
+// at the bench batch (B = 1024, L = 211: 1.20 ms vs 1.09-1.12 ms for QKV GEMM + mhsa,
+// tools/qkv_attn_ab.py, profiles/r03), so vision blocks run the two kernels.
+constexpr bool kFuseQkvAttention = false;
 int qkv_attn(const void* x, int64_t ldx, const void* wq, int64_t ldw, const float* bias, const float* colsum,
              const void* rowstat, int64_t nseq, int L, int H, int W, void* o, hipStream_t s);
 int mhsa_cls(const void* q, const void* k, const void* vt, void* o, int64_t nseq, int L, int H, hipStream_t s);
@@ -354,7 +358,7 @@ static int run_block(const reidmi_block_weights& bw, char* ws, const Plan& P, in
     int rc;
     // ln_1 (custom_clip_model.py:27)
     if ((rc = x_pst ? row_stats_from_partials(pst, M, W, st, s) : row_stats(x, M, W, W, st, s))) return rc;
-    if (qkv_attn_fits(L, W, causal)) {
+    if (kFuseQkvAttention && qkv_attn_fits(L, W, causal)) {
         // vision blocks: QKV GEMM + attention fused, q / k / v never leave the CU (attention.hip)
         if ((rc = qkv_attn(x, W, bw.qkv_w, W, bw.qkv_b, bw.qkv_s, st, nseq, L, H, W, o, s))) return rc;
     } else {

@@ -737,7 +737,7 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
             }
         }
         if (has_bias) {
-            float4 b[4];
+            f32x4 b[4];
             // inline ds_read: no compiler-inserted vmcnt(0) for the LDS-DMA'd slot (retired by
             // the tile's first K-step wait)
             const float* bp = bias_slot + wc * 64 + (lane >> 4) * 4;
@@ -746,12 +746,14 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
             asm volatile("ds_read_b128 %0, %1 offset:64" : "=v"(b[1]) : "v"(ba) : "memory");
             asm volatile("ds_read_b128 %0, %1 offset:128" : "=v"(b[2]) : "v"(ba) : "memory");
             asm volatile("ds_read_b128 %0, %1 offset:192" : "=v"(b[3]) : "v"(ba) : "memory");
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            // the wait names the read registers: no use of them can be scheduled above it (the
+            // hardware does not track VGPRs written by an outstanding LDS read)
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3])::"memory");
             // acc <- rstd * acc + (-mean rstd * s_n + b'_n); without a fold (rstd, s) = (1, 0):
             // fma(1, acc, fma(0, 0, b)) == acc + b exactly.  One branch-free update (a branch on
             // acc would duplicate the 128 accumulators).
-            float4 sn[4];
-            float2 rs[8];
+            f32x4 sn[4];
+            f32x2v rs[8];
             if (fold) {
                 const uint32_t ca = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)(
                     cs_slot + wc * 64 + (lane >> 4) * 4);
@@ -769,12 +771,14 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
                 asm volatile("ds_read_b64 %0, %1 offset:640" : "=v"(rs[5]) : "v"(ra) : "memory");
                 asm volatile("ds_read_b64 %0, %1 offset:768" : "=v"(rs[6]) : "v"(ra) : "memory");
                 asm volatile("ds_read_b64 %0, %1 offset:896" : "=v"(rs[7]) : "v"(ra) : "memory");
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                asm volatile("s_waitcnt lgkmcnt(0)"
+                             : "+v"(sn[0]), "+v"(sn[1]), "+v"(sn[2]), "+v"(sn[3]), "+v"(rs[0]), "+v"(rs[1]), "+v"(rs[2]),
+                               "+v"(rs[3]), "+v"(rs[4]), "+v"(rs[5]), "+v"(rs[6]), "+v"(rs[7])::"memory");
             } else {
 #pragma unroll
-                for (int j = 0; j < 4; j++) sn[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+                for (int j = 0; j < 4; j++) sn[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int i = 0; i < 8; i++) rs[i] = make_float2(1.f, 0.f);
+                for (int i = 0; i < 8; i++) rs[i] = f32x2v{1.f, 0.f};
             }
 #pragma unroll
             for (int i = 0; i < 8; i++)

@@ -406,4 +406,12 @@ def test_qkv_attention_fused_bitexact(gpu, L, nseq, W):
     fused = _qkv_attention(L, nseq, W, True, *args)
     ref = _qkv_attention(L, nseq, W, False, *args)
     assert torch.isfinite(ref).all()
-    assert torch.equal(fused.view(torch.int16), ref.view(torch.int16))
+    bad = (fused.view(torch.int16) != ref.view(torch.int16)).cpu()
+    if bad.any():
+        r, c = bad.nonzero(as_tuple=True)
+        t = r % L
+        diff = (fused.float() - ref.float()).abs().cpu()
+        msg = (f"{int(bad.sum())}/{bad.numel()} differ, max |d| {float(diff.max()):.3g}; "
+               f"tokens {sorted(set(t.tolist()))[:12]}, seqs {sorted(set((r // L).tolist()))[:8]}, "
+               f"heads {sorted(set((c // 64).tolist()))[:12]}, dims {sorted(set((c % 64).tolist()))[:16]}")
+        pytest.fail(msg)
