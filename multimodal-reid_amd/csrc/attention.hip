@@ -462,7 +462,11 @@ __global__ __launch_bounds__(NKB * 64, 1) void qkv_attn_kernel(const _Float16* _
             for (int j = 0; j < 12; j++)
 #pragma unroll
                 for (int i = 0; i < 2; i++)
+#ifndef QA_NO_MFMA  // timing variants (tools/qkv_attn_ab.py)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[j], af[i], acc[i][j], 0, 0, 0);
+#else
+                    acc[i][j] += f32x4{(float)wf[j][0], (float)af[i][0], 0.f, 0.f};
+#endif
             __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);  // 8 fragment reads
 #pragma unroll
             for (int g = 0; g < 6; g++) {
@@ -548,7 +552,11 @@ __global__ __launch_bounds__(NKB * 64, 1) void qkv_attn_kernel(const _Float16* _
             }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
+#ifndef QA_NO_ATTN
         attn_block<NKB, false>(sK + z, sV + z, VS, qf, wid * 32 + (lane & 31), L, u, H, o, scale_log2);
+#else
+        if (lane == 0 && wid == 0) o[u] = qf[0][0] + sK[z + lane] + sV[z + 5];
+#endif
     }
 }
 

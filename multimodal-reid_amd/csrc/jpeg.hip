@@ -52,6 +52,21 @@ static void build_huff(const uint8_t* counts, const uint8_t* syms, int nsym, Jpe
     for (int i = 0; i < nsym && i < 256; ++i) t.val[i] = syms[i];
 }
 
+// jdhuff.c jpeg_make_d_derived_tbl's checks on a table the scan uses: no length may hold more
+// codes than it has room for (JERR_BAD_HUFF_TABLE), and a DC table's symbols are sizes <= 15
+static bool huff_ok(const uint8_t* counts, const uint8_t* syms, int nsym, bool dc) {
+    uint32_t code = 0;   // one past the last code of length l: the all-ones code is not allowed
+    for (int l = 1; l <= 16; ++l) {
+        code += counts[l - 1];
+        if (code >= (1u << l)) return false;
+        code <<= 1;
+    }
+    if (dc)
+        for (int i = 0; i < nsym; ++i)
+            if (syms[i] > 15) return false;
+    return true;
+}
+
 struct Pools {
     std::vector<JpegHuff> huff;
     std::vector<std::string> huff_raw;   // 16 counts + symbols of each pooled table
@@ -115,7 +130,8 @@ static int32_t parse_one(const uint8_t* f, int64_t n, int64_t base, JpegImage& i
                 cid[c] = s[6 + 3 * c];
                 im.hs[c] = s[7 + 3 * c] >> 4;
                 im.vs[c] = s[7 + 3 * c] & 15;
-                tq[c] = s[8 + 3 * c] & 3;
+                tq[c] = s[8 + 3 * c];
+                if (tq[c] > 3) return J_BAD_TABLE;   // jdinput.c latch_quant_tables: JERR_NO_QUANT_TABLE
             }
             sof = true;
         } else if ((m >= 0xC2 && m <= 0xCF) && m != 0xC4 && m != 0xC8 && m != 0xCC) {
@@ -136,8 +152,12 @@ static int32_t parse_one(const uint8_t* f, int64_t n, int64_t base, JpegImage& i
             while (i < sl) {
                 const int pq = s[i] >> 4, t = s[i] & 15;
                 if (pq > 1 || t > 3 || i + 1 + 64 * (pq + 1) > sl) return J_BAD_TABLE;
-                for (int k = 0; k < 64; ++k)   // kept in zig-zag order; libjpeg's quantval is
-                    qt[t][k] = (int16_t)(pq ? u16be(s + i + 1 + 2 * k) : s[i + 1 + k]);   // read as-is
+                for (int k = 0; k < 64; ++k) {   // kept in zig-zag order; libjpeg's quantval is
+                    const int q = pq ? u16be(s + i + 1 + 2 * k) : s[i + 1 + k];   // read as-is
+                    // 16-bit entries above int16 (libjpeg keeps UINT16): not decoded here
+                    if (q > 32767) return J_UNSUPPORTED;
+                    qt[t][k] = (int16_t)q;
+                }
                 qdef[t] = true;
                 i += 1 + 64 * (pq + 1);
             }
@@ -159,6 +179,9 @@ static int32_t parse_one(const uint8_t* f, int64_t n, int64_t base, JpegImage& i
                 if (s[1 + 2 * j] != cid[j]) return J_UNSUPPORTED;   // scan order = frame order
                 const int td = s[2 + 2 * j] >> 4, ta = s[2 + 2 * j] & 15;
                 if (td > 3 || ta > 3 || !hdc[td] || !hac[ta]) return J_BAD_TABLE;
+                if (!huff_ok(hdc[td], hdc[td] + 16, hdc_len[td] - 16, true) ||
+                    !huff_ok(hac[ta], hac[ta] + 16, hac_len[ta] - 16, false))
+                    return J_BAD_TABLE;
                 im.dc[j] = pools.add_huff(hdc[td], hdc_len[td]);
                 im.ac[j] = pools.add_huff(hac[ta], hac_len[ta]);
             }
@@ -264,7 +287,9 @@ __global__ __launch_bounds__(64) void jpeg_entropy_kernel(const uint8_t* __restr
         LdsSink sink{blocks[threadIdx.x], nullptr};
         if constexpr (kLds) st = entropy_decode(src, im, lds, coef, sink);
         else st = entropy_decode(src, im, gh, coef, sink);
-        if (st != J_OK) {   // undecodable data: the image's coefficients are defined as zero
+        // undecodable data: the image's coefficients are defined as zero (a truncated file keeps
+        // what libjpeg would decode, the missing data as zeros: check=False callers get that image)
+        if (st != J_OK && st != J_TRUNCATED) {
             int64_t n = 0;
             for (int c = 0; c < im.ncomp; ++c) n += (int64_t)im.bw[c] * im.bh[c] * 64;
             uint4* d = (uint4*)(coef + im.coef_off);

@@ -25,6 +25,7 @@ enum : int32_t {
     J_LAYOUT = 3,          // component count / sampling factors outside 1, 3 x {4:4:4, 4:2:2, 4:2:0}
     J_BAD_TABLE = 4,       // missing or malformed DQT / DHT
     J_BAD_DATA = 5,        // entropy-coded data does not decode (set by the device pass)
+    J_TRUNCATED = 6,       // the file ends before EOI (Pillow: "image file is truncated")
 };
 
 enum : int32_t { CS_GRAY = 0, CS_YCC = 1, CS_RGB = 2 };
@@ -210,8 +211,10 @@ struct DirectSink {
     __host__ __device__ inline void end() {}
 };
 
-// Decodes one image's scan into zig-zag-order int16 coefficient blocks.  Returns J_OK or
-// J_BAD_DATA (then the blocks not yet ended are left as they were).
+// Decodes one image's scan into zig-zag-order int16 coefficient blocks.  Returns J_OK,
+// J_BAD_DATA (then the blocks not yet ended are left as they were) or J_TRUNCATED (no EOI
+// follows the scan: every block is decoded, missing data as zeros, as libjpeg does, but the
+// reference's loader raises for such a file).
 template <class Sink>
 __host__ __device__ inline int32_t entropy_decode(const uint8_t* src, const JpegImage& im, const JpegHuff* huff,
                                                   int16_t* coef, Sink& sink) {
@@ -293,7 +296,12 @@ __host__ __device__ inline int32_t entropy_decode(const uint8_t* src, const Jpeg
             tbl = comp == 0 ? dct0 : (comp == 1 ? dct1 : dct2);
         }
     }
-    return J_OK;
+    // libjpeg then reads the markers up to EOI (jpeg_finish_decompress); a file that ends first
+    // makes the reference's loader raise "image file is truncated" (the reader never moves past
+    // a marker, so the search starts at or before it)
+    for (const uint8_t* q = br.p; q + 1 < br.end; ++q)
+        if (q[0] == 0xFF && q[1] == 0xD9) return J_OK;
+    return J_TRUNCATED;
 }
 
 // ---------------------------------------------------------------- islow IDCT (jidctint.c)

@@ -128,7 +128,8 @@ def _to_device(a, device):
 
 JPEG_STATUS = {1: "not a JPEG or truncated", 2: "progressive / lossless / arithmetic-coded / 12-bit / multi-scan",
                3: "component layout other than grayscale or 3 x {4:4:4, 4:2:2, 4:2:0}",
-               4: "missing or malformed quantisation / Huffman tables", 5: "entropy-coded data does not decode"}
+               4: "missing or malformed quantisation / Huffman tables", 5: "entropy-coded data does not decode",
+               6: "image file is truncated (the file ends inside the entropy-coded data)"}
 
 
 class JpegBatch:

@@ -76,6 +76,70 @@ def test_plan_status_and_meta():
         jb.raise_for_status()
 
 
+def _segments(b):
+    """(marker, offset, length) of the header segments up to SOS."""
+    p, out = 2, []
+    while p < len(b):
+        m, n = b[p + 1], (b[p + 2] << 8) | b[p + 3]
+        out.append((m, p, n))
+        if m == 0xDA:
+            break
+        p += 2 + n
+    return out
+
+
+def _pil_raises(b):
+    try:
+        pil_rgb(b)
+    except OSError:
+        return True
+    return False
+
+
+def corrupt_header_cases():
+    """Header damage libjpeg rejects (Pillow raises) and one table form the device does not
+    take: (name, bytes, expected plan status)."""
+    good = syn.jpeg_files(1, 128, 64, seed=21)[0]
+    seg = _segments(good)
+    out = []
+    b = bytearray(good)   # a component names quantisation table 5 (jdinput.c: JERR_NO_QUANT_TABLE)
+    p = next(p for m, p, _ in seg if m == 0xC0)
+    b[p + 4 + 8] = 5
+    out.append(("tq5", bytes(b), 4))
+    b = bytearray(good)   # DC table with two 1-bit codes (jdhuff.c: JERR_BAD_HUFF_TABLE)
+    p = next(p for m, p, _ in seg if m == 0xC4) + 4
+    assert b[p] >> 4 == 0 and b[p + 3] >= 2
+    b[p + 1] += 2
+    b[p + 3] -= 2
+    out.append(("huff-overfull", bytes(b), 4))
+    b = bytearray(good)   # DC table symbol 16 (a DC category above 15)
+    p = next(p for m, p, _ in seg if m == 0xC4) + 4
+    b[p + 17] = 16
+    out.append(("huff-dc-symbol", bytes(b), 4))
+    # a 16-bit quantisation table with an entry above 32767 (libjpeg keeps UINT16): unsupported
+    p, n = next((p, n) for m, p, n in seg if m == 0xDB)
+    q = good[p + 5:p + 5 + 64]
+    t16 = bytes([0x10]) + b"".join(int(v).to_bytes(2, "big") for v in q)
+    t16 = t16[:3] + (40000).to_bytes(2, "big") + t16[5:]
+    seg16 = b"\xff\xdb" + (2 + len(t16)).to_bytes(2, "big") + t16
+    out.append(("dqt16-big", good[:p] + seg16 + good[p + 2 + n:], 2))
+    return out
+
+
+def test_plan_rejects_corrupt_headers_like_libjpeg():
+    cases = corrupt_header_cases()
+    jb = data_prepare.JpegBatch([b for _, b, _ in cases])
+    assert jb.status.tolist() == [st for _, _, st in cases]
+    for name, b, st in cases:
+        if st == 4:   # the reference's loader fails on these too
+            assert _pil_raises(b), name
+
+
+def truncated_cases():
+    good = syn.jpeg_files(2, 128, 64, seed=22)
+    return [("mid-scan", good[0][:int(len(good[0]) * 0.6)]), ("no-eoi", good[1][:-2])]
+
+
 def test_plan_pools_tables_and_reads_paths(tmp_path):
     files = syn.jpeg_files(20, 128, 64, seed=2)   # one encoder setting: one set of tables
     for i, b in enumerate(files[:3]):
@@ -113,6 +177,16 @@ def test_core_arithmetic_on_host_vs_pillow(tmp_path):
     host.jpeg_host_decode(jb.buf.ctypes.data_as(vp), jb.plan.ctypes.data_as(vp), jb.info.ctypes.data_as(vp),
                           out.ctypes.data_as(vp), err.ctypes.data_as(vp))
     assert not err.any()
+    # files that end before EOI: status 6, where Pillow raises "image file is truncated"
+    tc = truncated_cases()
+    jt = data_prepare.JpegBatch([b for _, b in tc])
+    assert not jt.status.any()   # the headers are whole
+    tout = np.zeros(max(jt.out_bytes, 1), np.uint8)
+    terr = np.zeros(jt.B, np.int32)
+    host.jpeg_host_decode(jt.buf.ctypes.data_as(vp), jt.plan.ctypes.data_as(vp), jt.info.ctypes.data_as(vp),
+                          tout.ctypes.data_as(vp), terr.ctypes.data_as(vp))
+    assert terr.tolist() == [6] * len(tc)
+    assert all(_pil_raises(b) for _, b in tc)
     bad = [name for i, (name, b) in enumerate(cases)
            if not np.array_equal(out[jb.meta[i, 0]:jb.meta[i, 0] + jb.meta[i, 1] * jb.meta[i, 2] * 3]
                                  .reshape(jb.meta[i, 1], jb.meta[i, 2], 3), pil_rgb(b))]
@@ -178,3 +252,16 @@ def test_decode_rejects_unsupported_and_reports_bad_data(gpu):
     torch.cuda.synchronize()
     got = pix.cpu().numpy()[:64 * 32 * 3].reshape(64, 32, 3)
     assert np.array_equal(got, pil_rgb(good[0]))
+
+
+@pytest.mark.gpu
+def test_decode_reports_truncated_files(gpu):
+    """A file that ends inside the scan, or lacks only its EOI, is reported (status 6) where
+    the reference's Image.open(...).convert("RGB") raises; the other files of the batch decode."""
+    tc = truncated_cases()
+    good = syn.jpeg_files(1, 40, 24, seed=23)[0]
+    with pytest.raises(ValueError, match="truncated"):
+        data_prepare.decode_jpeg([good] + [b for _, b in tc])
+    pix, _, jb = data_prepare.decode_jpeg([good] + [b for _, b in tc], check=False)
+    torch.cuda.synchronize()
+    assert np.array_equal(pix.cpu().numpy()[:40 * 24 * 3].reshape(40, 24, 3), pil_rgb(good))

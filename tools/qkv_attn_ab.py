@@ -1,7 +1,10 @@
 """A/B of the fused QKV GEMM + attention kernel against the two-kernel path (QKV GEMM with the
 head-split epilogue, then the attention kernel) at the bench's shape: one vision block at
 batch B (M = B * 211 token rows, ViT-B/16 width 768).  Random operands, HIP events.
-usage: python tools/qkv_attn_ab.py [B] [L] [W] [reps]"""
+usage: python tools/qkv_attn_ab.py [B] [L] [W] [reps] [variant.so ...]
+Each variant library (a build of the same sources with timing macros, e.g. QA_NO_ATTN) is
+timed on the fused path too."""
+import ctypes
 import os
 import sys
 
@@ -34,9 +37,17 @@ def main():
     o = torch.empty(M, W, dtype=torch.float16, device=dev)
     flop = 2.0 * M * 3 * W * W + 4.0 * B * H * L * L * 64
     hbm_unfused = 2.0 * (M * W + 3 * M * W + 3 * M * W + M * W)  # x, q/k/v written + read, o
+    variants = [(os.path.basename(p), ctypes.CDLL(os.path.abspath(p))) for p in sys.argv[5:]]
+    for _, V in variants:
+        V.reidmi_qkv_attention_f16.argtypes = lib.SIGNATURES["reidmi_qkv_attention_f16"]
     for rnd in range(3):
-        for fused in (0, 1):
+        for fused, name, V in [(0, "", None), (1, "", None)] + [(1, n, V) for n, V in variants]:
             def run():
+                if V is not None:
+                    assert V.reidmi_qkv_attention_f16(lib.ptr(x), W, lib.ptr(wq), W, lib.ptr(bias), lib.ptr(cs),
+                                                      lib.ptr(rs), B, L, H, W, None, None, None, lib.ptr(o), 1,
+                                                      lib.stream()) == 0
+                    return
                 lib.call("reidmi_qkv_attention_f16", lib.ptr(x), W, lib.ptr(wq), W, lib.ptr(bias), lib.ptr(cs), lib.ptr(rs),
                          B, L, H, W, lib.ptr(q), lib.ptr(k), lib.ptr(vt), lib.ptr(o), fused, lib.stream())
             for _ in range(3):
@@ -48,7 +59,7 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / reps
-            print(f"r{rnd} B={B} L={L} W={W} fused={fused}: {ms * 1e3:8.1f} us  {flop / ms / 1e9:7.1f} TF/s"
+            print(f"r{rnd} B={B} L={L} W={W} fused={fused}{' ' + name if name else ''}: {ms * 1e3:8.1f} us  {flop / ms / 1e9:7.1f} TF/s"
                   + (f"  (two-kernel HBM bytes {hbm_unfused / 1e9:.2f} GB)" if not fused else ""), flush=True)
 
 
