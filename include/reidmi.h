@@ -121,15 +121,19 @@ int reidmi_rr_rank_rows(const float* feat, int64_t N, int64_t D, int64_t ldf, co
  * or is not finite, and the pre-filter must then not be used. */
 int reidmi_rr_feat16(const float* feat, int64_t N, int64_t D, int64_t ldf, void* feat16, int64_t Np, int64_t Dp,
                      int32_t* range_ok, void* stream);
+/* Largest norm and squared norm over the N items (out2[0], out2[1]: device floats), the input
+ * nmax2 of reidmi_rr_rank_rows_f16. */
+int reidmi_rr_norm_max(const float* sqn, const float* nrm, int64_t N, float* out2, void* stream);
 /* reidmi_rr_rank_rows with an fp16 MFMA pre-filter (same rank_out / rowmax_out bits): the fp16
- * product bounds every exact distance (error bound in backend.hip rank_select_kernel); only the
- * candidates are recomputed with the exact fp32 chain.  Rows whose distances are too
- * concentrated for the bound (or not finite) get need[r] = 1 and no output: the caller runs the
- * exact rows for them.  nrm = sqrt(sqn); need [hi - lo] int32; chunk [chunk_rows][Np]. */
+ * product bounds every exact distance (error bound in backend.hip rank_select_kernel; the GEMM
+ * epilogue writes only the upper bounds, chunk [chunk_rows][Np] fp32); only the candidates are
+ * recomputed with the exact fp32 chain.  Rows whose distances are too concentrated for the
+ * bound (or not finite) get need[r] = 1 and no output: the caller runs the exact rows for them.
+ * nrm = sqrt(sqn); nmax2 = reidmi_rr_norm_max(sqn, nrm); need [hi - lo] int32. */
 int reidmi_rr_rank_rows_f16(const float* feat, int64_t N, int64_t D, int64_t ldf, const float* sqn, const float* nrm,
-                            const void* feat16, int64_t Np, int64_t Dp, int64_t lo, int64_t hi, int K,
-                            int32_t* rank_out, float* rowmax_out, int32_t* need, float* chunk, int64_t chunk_rows,
-                            void* stream);
+                            const float* nmax2, const void* feat16, int64_t Np, int64_t Dp, int64_t lo, int64_t hi,
+                            int K, int32_t* rank_out, float* rowmax_out, int32_t* need, float* chunk,
+                            int64_t chunk_rows, void* stream);
 /* R3 (reranking.py:51-71): V rows lo..hi (ELL [hi-lo][vcap]) from the full rank[N][K] and
  * rowmax[N]; distance entries recomputed from feat with the distance kernel's arithmetic.
  * ws: reidmi_rr_caps' v_ws_bytes (nullable when 0). */

@@ -38,7 +38,8 @@ SIGNATURES = {
     "reidmi_rr_caps": [_i64, _i32, _i32, _vp, _vp, _vp, _vp],
     "reidmi_rr_rank_rows": [_vp, _i64, _i64, _i64, _vp, _i64, _i64, _i32, _vp, _vp, _vp, _i64, _vp],
     "reidmi_rr_feat16": [_vp, _i64, _i64, _i64, _vp, _i64, _i64, _vp, _vp],
-    "reidmi_rr_rank_rows_f16": [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i32, _vp, _vp, _vp,
+    "reidmi_rr_norm_max": [_vp, _vp, _i64, _vp, _vp],
+    "reidmi_rr_rank_rows_f16": [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i32, _vp, _vp, _vp,
                                 _vp, _i64, _vp],
     "reidmi_rr_v_rows": [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _i32, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _i64, _vp,
                          _vp],

@@ -410,7 +410,10 @@ __global__ __launch_bounds__(256) void topk_rows_kernel(const float* __restrict_
 //     item has lo <= d <= tau': the candidate set {j : lo_j <= tau'} contains them;
 //   * the row max is attained among {j : hi_j >= max_k lo_k}.
 // The candidates' exact distances then give the same rowmax and the same K indices as the
-// full row, bit for bit.  A row whose candidate lists overflow, or with a non-finite bound or
+// full row, bit for bit.  Only hi reaches HBM (the GEMM's EPI_RRHI epilogue computes it from
+// the product and the items' norms); the selection takes lo = hi - w_i with the row's width w_i
+// >= hi_ij - lo_ij for every j (rr_width), which only widens both candidate sets.  A row whose
+// candidate lists overflow, or with a non-finite bound or
 // max, is marked in need[] for the exact rows (reranking.HipStages.rank_rows runs them through
 // the exact distance kernel + selection).
 constexpr int RS_CCAP = 2048, RS_MCAP = 512;
@@ -449,11 +452,27 @@ __device__ __forceinline__ float block_max(float v, float* red) {
     return m;
 }
 
+// Width of the pair bound of row i: hi(i, j) - (exact distance lower bound) <= w_i for every j,
+// from the largest norm and squared norm over the items (e is increasing in both; the margin
+// covers the roundings of hi, of fl(dt - e) and of this subtraction, each <= 2^-24 of
+// magnitudes <= 2.2 (s_i + s_max)).  For L2-normalised features (every n_j = 1) it is 2 e + a
+// few ulps, the width of the per-pair bound.
+__device__ __forceinline__ float rr_width(float s_i, float n_i, float n_max, float s_max, float c_rel, float c_abs,
+                                          float c_d) {
+    const float e = 1.01f * (__builtin_fmaf(c_rel * n_i, n_max, 0x1p-23f * (s_i + s_max)) + c_abs * (n_i + n_max) + c_d);
+    return 2.0f * e * (1.0f + 0x1p-10f) + 0x1p-20f * (s_i + s_max + e);
+}
+
+// Rows of the k-reciprocal R2 from the pre-filter bounds hi ([rows][ldd] fp32, the EPI_RRHI
+// GEMM epilogue: gemm.h rr_hi), lo = hi - w_i (rr_width): the K-th smallest hi bounds the K-th
+// smallest exact distance, every item with lo <= that bound is a candidate of the top K, every
+// item with hi >= the largest lo a candidate of the row max; both are recomputed exactly.
 __global__ __launch_bounds__(256) void rank_select_kernel(const float* __restrict__ dot, int64_t ldd,
                                                           const float* __restrict__ feat, int64_t ldf, int D,
                                                           const float* __restrict__ sqn, const float* __restrict__ nrm,
                                                           int64_t row0, int64_t N, int K, float c_rel, float c_abs,
-                                                          float c_d, int32_t* __restrict__ rank_out,
+                                                          float c_d, const float* __restrict__ nmax2,
+                                                          int32_t* __restrict__ rank_out,
                                                           float* __restrict__ rowmax_out, int32_t* __restrict__ need) {
     __shared__ TkLds L;
     __shared__ float cv[RS_CCAP];
@@ -463,14 +482,10 @@ __global__ __launch_bounds__(256) void rank_select_kernel(const float* __restric
     __shared__ float red[4];
     const int64_t r = blockIdx.x, i = row0 + r;
     const float* drow = dot + r * ldd;
-    const float s_i = sqn[i], n_i = nrm[i];
+    const float w = rr_width(sqn[i], nrm[i], nmax2[0], nmax2[1], c_rel, c_abs, c_d);
     auto bounds = [&](int64_t j, float& lo, float& hi) {
-        const float s = s_i + sqn[j];
-        const float dt = __builtin_fmaf(-2.0f, drow[j], s);
-        const float nj = nrm[j];
-        const float e = 1.01f * (__builtin_fmaf(c_rel * n_i, nj, 0x1p-23f * s) + c_abs * (n_i + nj) + c_d);
-        lo = dt - e;
-        hi = dt + e;
+        hi = drow[j];
+        lo = hi - w;
     };
     if (threadIdx.x == 0) { s_nc = 0; s_nm = 0; s_bad = 0; }
     // pass A: tau = the K-th smallest upper bound; the largest lower bound
@@ -575,6 +590,7 @@ __global__ __launch_bounds__(256) void rank_select1_kernel(const float* __restri
                                                            const float* __restrict__ sqn,
                                                            const float* __restrict__ nrm, int64_t row0, int64_t N,
                                                            int K, float c_rel, float c_abs, float c_d,
+                                                           const float* __restrict__ nmax2,
                                                            int32_t* __restrict__ rank_out,
                                                            float* __restrict__ rowmax_out, int32_t* __restrict__ need) {
     __shared__ Rs1Lds L;
@@ -583,27 +599,22 @@ __global__ __launch_bounds__(256) void rank_select1_kernel(const float* __restri
     __shared__ int s_nc, s_nm, s_bad;
     __shared__ float red[4];
     const int64_t r = blockIdx.x, i = row0 + r;
-    const float* drow = dot + r * ldd;
-    const float s_i = sqn[i], n_i = nrm[i];
+    const float* drow = dot + r * ldd;   // the bounds hi of the row (EPI_RRHI)
+    const float w = rr_width(sqn[i], nrm[i], nmax2[0], nmax2[1], c_rel, c_abs, c_d);
     const int wv = threadIdx.x >> 6;
-    auto bounds_v = [&](float dj, float sj, float nj, float& lo, float& hi) {
-        const float s = s_i + sj;
-        const float dt = __builtin_fmaf(-2.0f, dj, s);
-        const float e = 1.01f * (__builtin_fmaf(c_rel * n_i, nj, 0x1p-23f * s) + c_abs * (n_i + nj) + c_d);
-        lo = dt - e;
-        hi = dt + e;
+    auto bounds_v = [&](float hj, float& lo, float& hi) {
+        hi = hj;
+        lo = hj - w;
     };
-    auto bounds = [&](int64_t j, float& lo, float& hi) { bounds_v(drow[j], sqn[j], nrm[j], lo, hi); };
-    // chunk loads (see the stream below)
-    constexpr int U = RS1_CH / 256;
-    auto load = [&](int64_t c0, float* d, float* sj, float* nj) {
+    auto bounds = [&](int64_t j, float& lo, float& hi) { bounds_v(drow[j], lo, hi); };
+    // chunk loads (see the stream below): thread t takes items c0 + 4 (t + 256 u) .. + 3, one
+    // 16-byte load each (ldd % 4 == 0; a vector that starts below N ends below ldd)
+    constexpr int U = RS1_CH / 1024;
+    auto load = [&](int64_t c0, float4* d) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const int64_t j = c0 + u * 256 + threadIdx.x;
-            const bool in = j < N;
-            d[u] = in ? drow[j] : 0.0f;
-            sj[u] = in ? sqn[j] : 0.0f;
-            nj[u] = in ? nrm[j] : 0.0f;
+            const int64_t j = c0 + 4 * (u * 256 + threadIdx.x);
+            d[u] = j < N ? *(const float4*)(drow + j) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
     };
     auto thr_of = [](float tau) { return tau + fabsf(tau) * 0x1p-21f + 1e-37f; };
@@ -619,16 +630,17 @@ __global__ __launch_bounds__(256) void rank_select1_kernel(const float* __restri
     __syncthreads();
     bool bad = false, c_lost = false, m_lost = false;
     float thr = __builtin_inff();
-    // the chunk loads run two chunks ahead of the selection (three register sets in turn)
-    auto chunk = [&](int64_t c0, const float* cd, const float* cs, const float* cn) {
+    // the chunk loads run three chunks ahead of the selection (four register sets in turn)
+    auto chunk = [&](int64_t c0, const float4* cd) {
         const float tv = L.s_tv;
         const int ti = L.s_ti, nsel = L.s_nsel;
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int64_t j = c0 + u * 256 + threadIdx.x;
+        for (int v = 0; v < 4 * U; v++) {
+            const int64_t j = c0 + 4 * ((v >> 2) * 256 + threadIdx.x) + (v & 3);
             if (j < N) {
                 float lo, hi;
-                bounds_v(cd[u], cs[u], cn[u], lo, hi);
+                const float4 q = cd[v >> 2];
+                bounds_v((v & 3) == 0 ? q.x : (v & 3) == 1 ? q.y : (v & 3) == 2 ? q.z : q.w, lo, hi);
                 ml = fmaxf(ml, lo);
                 bad = bad || !(lo == lo && hi == hi && hi < __builtin_inff());
                 if (key_less(hi, (int)j, tv, ti)) {
@@ -688,18 +700,22 @@ __global__ __launch_bounds__(256) void rank_select1_kernel(const float* __restri
             __syncthreads();  // every thread has read the counters before anyone appends again
         }
     };
-    float xd[U], xs[U], xn[U], yd[U], ys[U], yn[U], zd[U], zs[U], zn[U];
-    load(0, xd, xs, xn);
-    load(RS1_CH, yd, ys, yn);
-    for (int64_t c0 = 0; c0 < N; c0 += 3 * RS1_CH) {
-        load(c0 + 2 * RS1_CH, zd, zs, zn);
-        chunk(c0, xd, xs, xn);
+    float4 xd[U], yd[U], zd[U], wd[U];
+    load(0, xd);
+    load(RS1_CH, yd);
+    load(2 * RS1_CH, zd);
+    for (int64_t c0 = 0; c0 < N; c0 += 4 * RS1_CH) {
+        load(c0 + 3 * RS1_CH, wd);
+        chunk(c0, xd);
         if (c0 + RS1_CH >= N) break;
-        load(c0 + 3 * RS1_CH, xd, xs, xn);
-        chunk(c0 + RS1_CH, yd, ys, yn);
+        load(c0 + 4 * RS1_CH, xd);
+        chunk(c0 + RS1_CH, yd);
         if (c0 + 2 * RS1_CH >= N) break;
-        load(c0 + 4 * RS1_CH, yd, ys, yn);
-        chunk(c0 + 2 * RS1_CH, zd, zs, zn);
+        load(c0 + 5 * RS1_CH, yd);
+        chunk(c0 + 2 * RS1_CH, zd);
+        if (c0 + 3 * RS1_CH >= N) break;
+        load(c0 + 6 * RS1_CH, zd);
+        chunk(c0 + 3 * RS1_CH, wd);
     }
     if (bad) s_bad = 1;
     __syncthreads();
@@ -1507,22 +1523,68 @@ __global__ __launch_bounds__(256) void eval_rows_kernel(
     }
 }
 
-// rank_select_kernel over rows [row0, row0 + rows) of the fp16 pre-filter product `dot`
-// ([rows][ldd] fp32, ldd >= N): see the kernel for the bound.
-int rank_select_launch(float* dot, int64_t ldd, const float* feat, int64_t ldf, int D, const float* sqn,
-                       const float* nrm, int64_t row0, int64_t rows, int64_t N, int K, int32_t* rank_out,
-                       float* rowmax_out, int32_t* need, hipStream_t s) {
-    RM_REQUIRE(K >= 1 && K <= 64 && K <= N && ldd >= N && rows >= 0, "rank_select: bad arguments");
-    if (rows == 0) return OK;
+// The pair bound's constants for D-dimensional features (fp16-rounded operands, fp32 MFMA
+// accumulation; the derivation is in rank_select_kernel's description of the bound).
+void rank_select_consts(int D, float c[3]) {
     const double c_rel = 2.0 * (0x1p-10 + 0x1p-22 + 2.02 * D * 0x1p-24) + 2.02 * 0x1p-23;
     const double c_abs = 2.01 * 0x1p-25 * std::sqrt((double)D);
     const double c_d = D * 0x1p-49;
+    c[0] = (float)(c_rel * (1.0 + 0x1p-20));
+    c[1] = (float)(c_abs * (1.0 + 0x1p-20));
+    c[2] = (float)(c_d * (1.0 + 0x1p-20));
+}
+
+// max over the items of the norms (out2[0]) and squared norms (out2[1]); fmaxf skips NaN (a NaN
+// norm makes its bounds NaN, which sends the rows to the exact path)
+__global__ __launch_bounds__(1024) void norm_max_kernel(const float* __restrict__ sqn, const float* __restrict__ nrm,
+                                                        int64_t N, float* __restrict__ out2) {
+    __shared__ float red[2][16];
+    float a = 0.0f, b = 0.0f;
+    for (int64_t j = threadIdx.x; j < N; j += blockDim.x) {
+        a = fmaxf(a, nrm[j]);
+        b = fmaxf(b, sqn[j]);
+    }
+    a = wave_max(a);
+    b = wave_max(b);
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = a;
+        red[1][threadIdx.x >> 6] = b;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 16; w++) {
+            a = fmaxf(a, red[0][w]);
+            b = fmaxf(b, red[1][w]);
+        }
+        out2[0] = a;
+        out2[1] = b;
+    }
+}
+
+int norm_max_launch(const float* sqn, const float* nrm, int64_t N, float* out2, hipStream_t s) {
+    RM_REQUIRE(N > 0 && sqn && nrm && out2, "norm_max: bad arguments");
+    hipLaunchKernelGGL(norm_max_kernel, dim3(1), dim3(1024), 0, s, sqn, nrm, N, out2);
+    RM_LAUNCHED();
+    return OK;
+}
+
+// rank_select_kernel over rows [row0, row0 + rows) of the pre-filter bounds `dot` ([rows][ldd]
+// fp32 hi, ldd >= N, the EPI_RRHI GEMM), nmax2 = norm_max_kernel's maxima.
+int rank_select_launch(float* dot, int64_t ldd, const float* feat, int64_t ldf, int D, const float* sqn,
+                       const float* nrm, const float* nmax2, int64_t row0, int64_t rows, int64_t N, int K,
+                       int32_t* rank_out, float* rowmax_out, int32_t* need, hipStream_t s) {
+    RM_REQUIRE(K >= 1 && K <= 64 && K <= N && ldd >= N && ldd % 4 == 0 && rows >= 0 && nmax2 &&
+                   ((uintptr_t)dot & 15) == 0,
+               "rank_select: bad arguments");
+    if (rows == 0) return OK;
+    float c[3];
+    rank_select_consts(D, c);
 #ifndef RS_SINGLE_PASS
 #define RS_SINGLE_PASS 1
 #endif
-    hipLaunchKernelGGL(RS_SINGLE_PASS ? rank_select1_kernel : rank_select_kernel, dim3((unsigned)rows), dim3(256), 0, s, dot, ldd, feat, ldf, D, sqn, nrm, row0,
-                       N, K, (float)(c_rel * (1.0 + 0x1p-20)), (float)(c_abs * (1.0 + 0x1p-20)),
-                       (float)(c_d * (1.0 + 0x1p-20)), rank_out, rowmax_out, need);
+    hipLaunchKernelGGL(RS_SINGLE_PASS ? rank_select1_kernel : rank_select_kernel, dim3((unsigned)rows), dim3(256), 0,
+                       s, dot, ldd, feat, ldf, D, sqn, nrm, row0, N, K, c[0], c[1], c[2], nmax2, rank_out, rowmax_out,
+                       need);
     RM_LAUNCHED();
     return OK;
 }

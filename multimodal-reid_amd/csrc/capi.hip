@@ -13,4 +13,4 @@ int fail(int code, const std::string& m) {
 REIDMI_API const char* reidmi_last_error(void) { return reidmi::g_err.c_str(); }
 // 2: per-call GEMM tiling / distance variant entry points replace the process-global setters;
 //    RCCL exchange (reidmi_comm_*); re-ranking without capacity limits.
-REIDMI_API int reidmi_abi_version(void) { return 2; }
+REIDMI_API int reidmi_abi_version(void) { return 3; }

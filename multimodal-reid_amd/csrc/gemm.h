@@ -11,6 +11,9 @@
 //   EPI_PATCH     x[b*L+1+p] = acc + pos[1+p]  fp16           (conv1 + pos-embed, :78-86)
 //   EPI_F32       out fp32 = acc + bias                       (proj / text_projection)
 //   EPI_RESID_F16 x fp16 += acc + bias (fp32 sum, one rounding) (out_proj / c_proj + residual, :27-28)
+//   EPI_RRHI      out fp32 = hi(i, j), the upper bound of the exact distance of items i, j from their
+//                 fp16 product (the k-reciprocal re-rank's pre-filter, rerank.hip): only the bound
+//                 reaches HBM, and the selection reads 4 bytes per pair instead of 12
 #pragma once
 #include "common.h"
 
@@ -22,7 +25,8 @@ enum Epi : int {
     EPI_QKV = 3,
     EPI_PATCH = 4,
     EPI_F32 = 5,
-    EPI_RESID_F16 = 6
+    EPI_RESID_F16 = 6,
+    EPI_RRHI = 7
 };
 
 struct EpiArgs {
@@ -52,7 +56,26 @@ struct EpiArgs {
     // coalesced reads in the encoder's rowstat_combine_kernel)
     float2* pstat;
     int64_t ldp;
+    // EPI_RRHI: row m is item rr_row0 + m, column n item n (n >= rr_n: +inf); squared norms and
+    // norms of the items; the bound's constants (c_rel, c_abs, c_d: backend.hip rank_select)
+    const float* rr_sqn;
+    const float* rr_nrm;
+    int64_t rr_row0;
+    int64_t rr_n;
+    float rr_c[3];
 };
+
+// hi(i, j) = fl(dt + e), dt = fl(fma(-2, dot, s_i + s_j)),
+// e = 1.01 (fma(c_rel n_i, n_j, 2^-23 (s_i + s_j)) + c_abs (n_i + n_j) + c_d): the exact fp32
+// distance of i and j is <= hi and >= fl(dt - e) (backend.hip rank_select).  One definition for
+// the GEMM epilogue and the selection's re-evaluation of single pairs.
+__device__ __forceinline__ float rr_hi(float dot, float si, float sj, float crn_i, float ni, float nj,
+                                       const float (&c)[3]) {
+    const float s = si + sj;
+    const float dt = __builtin_fmaf(-2.0f, dot, s);
+    const float e = 1.01f * (__builtin_fmaf(crn_i, nj, 0x1p-23f * s) + c[1] * (ni + nj) + c[2]);
+    return dt + e;
+}
 
 // Per-call tiling choice (tests, A/B tools): tile 0 = auto (the persistent 256x256 LDS-DMA
 // tile when the GEMM has >= 256 of them, else 128x128), 1 = force 128x128, 2 = force

@@ -251,6 +251,52 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
         store_batch(NI - NB);
         return;
     }
+    if constexpr (EPI == EPI_RRHI) {
+        // the items' norms: columns (4 consecutive per lane and fragment) and rows
+        const int64_t n = ea.rr_n;
+        float sj[4][4], nj[4][4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int64_t c0 = ncol + j * 16 + cq;
+            if (c0 + 3 < n) {
+                const float4 a = *(const float4*)(ea.rr_sqn + c0), b = *(const float4*)(ea.rr_nrm + c0);
+                sj[j][0] = a.x, sj[j][1] = a.y, sj[j][2] = a.z, sj[j][3] = a.w;
+                nj[j][0] = b.x, nj[j][1] = b.y, nj[j][2] = b.z, nj[j][3] = b.w;
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    const int64_t c = c0 + e < n ? c0 + e : n - 1;
+                    sj[j][e] = ea.rr_sqn[c];
+                    nj[j][e] = ea.rr_nrm[c];
+                }
+            }
+        }
+        float si[NI], ni[NI];
+#pragma unroll
+        for (int i = 0; i < NI; i++) {
+            const int64_t m = mrow + i * 16 + (lane & 15);
+            const int64_t g = ea.rr_row0 + (m < M ? m : M - 1);
+            si[i] = ea.rr_sqn[g];
+            ni[i] = ea.rr_nrm[g];
+        }
+#pragma unroll
+        for (int i = 0; i < NI; i++) {
+            const int64_t m = mrow + i * 16 + (lane & 15);
+            if (m >= M) continue;
+            const float crn = ea.rr_c[0] * ni[i];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int64_t c0 = ncol + j * 16 + cq;
+                float h[4];
+#pragma unroll
+                for (int e = 0; e < 4; e++)
+                    h[e] = c0 + e < n ? rr_hi(acc[i][j][e], si[i], sj[j][e], crn, ni[i], nj[j][e], ea.rr_c)
+                                      : __builtin_inff();
+                *(float4*)((float*)ea.out + m * ea.ldc + c0) = make_float4(h[0], h[1], h[2], h[3]);
+            }
+        }
+        return;
+    }
     if constexpr (EPI == EPI_F32) {
 #pragma unroll
         for (int i = 0; i < NI; i++) {
@@ -494,8 +540,9 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 // output element -> bit-identical results.
 template <int EPI>
 struct EpiVm {  // vector-memory instructions of one full-tile epilogue_tile<EPI, 8> per wave
+                // (EPI_RRHI: its 32 stores; its norm loads complete before the first store)
     static constexpr int count = EPI == EPI_H16 || EPI == EPI_GELU_H16 || EPI == EPI_QKV ? 16
-                                 : EPI == EPI_RESID_F16 || EPI == EPI_F32                 ? 32
+                                 : EPI == EPI_RESID_F16 || EPI == EPI_F32 || EPI == EPI_RRHI ? 32
                                                                                           : -1;
 };
 
@@ -870,6 +917,7 @@ int gemm_f16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, in
         case EPI_PATCH: rc = launch<EPI_PATCH>(A, lda, W, ldw, M, N, K, ea, s, opt); break;
         case EPI_F32: rc = launch<EPI_F32>(A, lda, W, ldw, M, N, K, ea, s, opt); break;
         case EPI_RESID_F16: rc = launch<EPI_RESID_F16>(A, lda, W, ldw, M, N, K, ea, s, opt); break;
+        case EPI_RRHI: rc = launch<EPI_RRHI>(A, lda, W, ldw, M, N, K, ea, s, opt); break;
         default: return fail(EINVAL_, "gemm: unknown epilogue");
     }
     if (ev_b) RM_CHECK_HIP(hipEventRecord(ev_b, s));

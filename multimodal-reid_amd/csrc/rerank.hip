@@ -22,8 +22,10 @@
 namespace reidmi {
 
 int rank_select_launch(float* dot, int64_t ldd, const float* feat, int64_t ldf, int D, const float* sqn,
-                       const float* nrm, int64_t row0, int64_t rows, int64_t N, int K, int32_t* rank_out,
-                       float* rowmax_out, int32_t* need, hipStream_t s);
+                       const float* nrm, const float* nmax2, int64_t row0, int64_t rows, int64_t N, int K,
+                       int32_t* rank_out, float* rowmax_out, int32_t* need, hipStream_t s);
+void rank_select_consts(int D, float c[3]);
+int norm_max_launch(const float* sqn, const float* nrm, int64_t N, float* out2, hipStream_t s);
 int feat16_launch(const float* x, int64_t N, int64_t D, int64_t ldx, void* y, int64_t Np, int64_t Dp,
                   int32_t* range_ok, hipStream_t s);
 int topk_launch(const float* x, int64_t rows, int64_t cols, int64_t ldx, const float* row_div, int k,
@@ -1264,17 +1266,25 @@ REIDMI_API int reidmi_rr_feat16(const float* feat, int64_t N, int64_t D, int64_t
     return feat16_launch(feat, N, D, ldf, feat16, Np, Dp, range_ok, (hipStream_t)stream);
 }
 
+// Largest norm and squared norm over the items (out2[0], out2[1], device) for
+// reidmi_rr_rank_rows_f16; once per feature set.
+REIDMI_API int reidmi_rr_norm_max(const float* sqn, const float* nrm, int64_t N, float* out2, void* stream) {
+    return norm_max_launch(sqn, nrm, N, out2, (hipStream_t)stream);
+}
+
 // reidmi_rr_rank_rows with an fp16 pre-filter: per row pass, the fp16 MFMA product of the
-// rows with all items (chunk [rows][Np] fp32) bounds every exact distance; only the rows'
-// candidates are recomputed with the exact chain.  Same rank_out / rowmax_out bits as
-// reidmi_rr_rank_rows (rank_select_kernel) for the rows with need[r] = 0; rows with need[r] = 1
-// (concentrated or non-finite distances) are left for the exact rows.  nrm = sqrt(sqn) [N].
+// rows with all items bounds every exact distance; the GEMM's epilogue writes only the upper
+// bounds (chunk [rows][Np] fp32, EPI_RRHI) and the selection recomputes the rows' candidates
+// with the exact chain.  Same rank_out / rowmax_out bits as reidmi_rr_rank_rows for the rows
+// with need[r] = 0; rows with need[r] = 1 (concentrated or non-finite distances) are left for
+// the exact rows.  nrm = sqrt(sqn) [N]; nmax2 = reidmi_rr_norm_max of sqn, nrm.
 REIDMI_API int reidmi_rr_rank_rows_f16(const float* feat, int64_t N, int64_t D, int64_t ldf, const float* sqn,
-                                       const float* nrm, const void* feat16, int64_t Np, int64_t Dp, int64_t lo,
-                                       int64_t hi, int K, int32_t* rank_out, float* rowmax_out, int32_t* need,
-                                       float* chunk, int64_t chunk_rows, void* stream) {
+                                       const float* nrm, const float* nmax2, const void* feat16, int64_t Np,
+                                       int64_t Dp, int64_t lo, int64_t hi, int K, int32_t* rank_out,
+                                       float* rowmax_out, int32_t* need, float* chunk, int64_t chunk_rows,
+                                       void* stream) {
     RM_REQUIRE(N > 0 && D > 0 && ldf >= D && 0 <= lo && lo <= hi && hi <= N && chunk_rows > 0 && K >= 1 && K <= N &&
-                   K <= 64 && Np >= N && Np % 256 == 0 && Dp >= D && Dp % 64 == 0,
+                   K <= 64 && Np >= N && Np % 256 == 0 && Dp >= D && Dp % 64 == 0 && sqn && nrm && nmax2,
                "rr_rank_rows_f16: bad arguments");
     RM_REQUIRE(N < 0x7fffffff, "rr_rank_rows_f16: too many items");
     hipStream_t s = (hipStream_t)stream;
@@ -1285,9 +1295,14 @@ REIDMI_API int reidmi_rr_rank_rows_f16(const float* feat, int64_t N, int64_t D, 
         EpiArgs ea{};
         ea.out = chunk;
         ea.ldc = Np;
-        if ((rc = gemm_f16(EPI_F32, x16 + a * Dp, Dp, x16, Dp, nb, Np, Dp, ea, s))) return rc;
-        if ((rc = rank_select_launch(chunk, Np, feat, ldf, (int)D, sqn, nrm, a, nb, N, K, rank_out + (a - lo) * K,
-                                     rowmax_out + (a - lo), need + (a - lo), s)))
+        ea.rr_sqn = sqn;
+        ea.rr_nrm = nrm;
+        ea.rr_row0 = a;
+        ea.rr_n = N;
+        rank_select_consts((int)D, ea.rr_c);
+        if ((rc = gemm_f16(EPI_RRHI, x16 + a * Dp, Dp, x16, Dp, nb, Np, Dp, ea, s))) return rc;
+        if ((rc = rank_select_launch(chunk, Np, feat, ldf, (int)D, sqn, nrm, nmax2, a, nb, N, K,
+                                     rank_out + (a - lo) * K, rowmax_out + (a - lo), need + (a - lo), s)))
             return rc;
     }
     return OK;

@@ -145,7 +145,10 @@ class HipStages:
             ok = torch.ones(1, device=self.dev, dtype=torch.int32)
             _lib.call("reidmi_rr_feat16", _lib.ptr(self.feat), self.N, self.D, self.D, _lib.ptr(x16), Np, Dp,
                       _lib.ptr(ok), self.st)
-            self._f16 = (x16, Np, Dp, torch.sqrt(self.sqn), bool(ok.item()))
+            nrm = torch.sqrt(self.sqn)
+            nmax2 = torch.empty(2, device=self.dev, dtype=torch.float32)
+            _lib.call("reidmi_rr_norm_max", _lib.ptr(self.sqn), _lib.ptr(nrm), self.N, _lib.ptr(nmax2), self.st)
+            self._f16 = (x16, Np, Dp, nrm, bool(ok.item()), nmax2)
         return self._f16
 
     def _exact_rows(self, lo, idx, n, R, rmax):
@@ -182,7 +185,7 @@ class HipStages:
         if hi > lo:
             # the pre-filter's selection keeps K <= 64 on chip; larger K take the exact rows
             use = RANK_PREFILTER and self.K <= 64
-            x16, Np, Dp, nrm, fits = self._feat16() if use else (None, 0, 0, None, False)
+            x16, Np, Dp, nrm, fits, nmax2 = self._feat16() if use else (None, 0, 0, None, False, None)
             a = lo
             if fits:
                 # the fp16 pre-filter (bit-identical to the exact rows; reidmi_rr_rank_rows_f16),
@@ -198,7 +201,8 @@ class HipStages:
                     b = min(a + (min(cr, 512) if first else cr), hi)  # a small probe pass first
                     first = False
                     _lib.call("reidmi_rr_rank_rows_f16", _lib.ptr(self.feat), self.N, self.D, self.D,
-                              _lib.ptr(self.sqn), _lib.ptr(nrm), _lib.ptr(x16), Np, Dp, a, b, self.K,
+                              _lib.ptr(self.sqn), _lib.ptr(nrm), _lib.ptr(nmax2), _lib.ptr(x16), Np, Dp, a, b,
+                              self.K,
                               _lib.ptr(R[a - lo:]), _lib.ptr(rmax[a - lo:]), _lib.ptr(need),
                               _lib.ptr(self._chunk_buf(cr, Np)), cr, self.st)
                     _lib.call("reidmi_nonzero_i32", _lib.ptr(need), b - a, _lib.ptr(idx), _lib.ptr(cnt), self.st)

@@ -46,6 +46,8 @@ def close_to_reference(got, g, key, via=None, rel=1.5, cos=0.99995):
     err = float(np.abs(got - ref).max())
     a, b = got.reshape(len(got), -1), ref.reshape(len(ref), -1)
     c = float(((a * b).sum(1) / np.linalg.norm(a, axis=1) / np.linalg.norm(b, axis=1)).min())
+    print(f"[parity] {key}: ours max|err| {err:.4g}, reference fp16 {ref_err:.4g} ({err / ref_err:.3f}x), "
+          f"min cos {c:.7f}")
     assert err <= rel * ref_err and c >= cos, \
         f"{key}: ours max|err| {err:.4g} vs the reference's fp16 {ref_err:.4g} (bound x{rel}), cos {c:.7f}"
     return err, ref_err
