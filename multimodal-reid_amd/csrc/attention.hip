@@ -12,9 +12,15 @@
 // Output o [B*L][H*64] fp16 (token-major: the A operand of out_proj).
 #include "common.h"
 
+#include <type_traits>
+
 namespace reidmi {
 
 int attn_lpad(int L);
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
 
 __device__ __forceinline__ int kswz(int r, int kc) { return r * 64 + ((kc ^ ((r >> 1) & 7)) << 3); }
 
@@ -33,6 +39,17 @@ __device__ __forceinline__ _Float16 f32_to_h(float x) {
 // one v_cvt_pk_f16_f32 (RNE) per pair, as gemm.hip's epilogues convert
 __device__ __forceinline__ uint32_t cvt_pk_h(float a, float b) {
     return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2v{a, b}, f16x2v));
+}
+
+// fp16 pair (a * inv, b * inv), each product rounded to fp16 ONCE (v_fma_mixlo / mixhi: the
+// exact product, one rounding).  Left to itself the backend lowers (_Float16)(a * inv) as a
+// mix instruction for some elements and as v_mul + v_cvt_pk (two roundings) for others, so
+// the two attention blocks would differ in ~1 value in 36 000.
+__device__ __forceinline__ uint32_t mul_pk_h(float a, float b, float inv) {
+    uint32_t r;
+    asm("v_fma_mixlo_f16 %0, %1, %2, 0" : "=v"(r) : "v"(a), "v"(inv));
+    asm("v_fma_mixhi_f16 %0, %1, %2, 0" : "+v"(r) : "v"(b), "v"(inv));
+    return r;
 }
 
 // One wave's block of 32 queries (row qi = block * 32 + (lane & 31)) against the head's K
@@ -115,10 +132,250 @@ __device__ __forceinline__ void attn_block(const _Float16* sK, const _Float16* s
         for (int db = 0; db < 2; db++)
 #pragma unroll
             for (int g = 0; g < 4; g++) {
-                f16x4 w = {(_Float16)(oacc[db][4 * g] * inv), (_Float16)(oacc[db][4 * g + 1] * inv),
-                            (_Float16)(oacc[db][4 * g + 2] * inv), (_Float16)(oacc[db][4 * g + 3] * inv)};
-                *(f16x4*)(orow + db * 32 + 8 * g + 4 * hh) = w;
+                const uint2 w = make_uint2(mul_pk_h(oacc[db][4 * g], oacc[db][4 * g + 1], inv),
+                                           mul_pk_h(oacc[db][4 * g + 2], oacc[db][4 * g + 3], inv));
+                *(uint2*)(orow + db * 32 + 8 * g + 4 * hh) = w;
             }
+    }
+}
+
+// ----------------------------------------------------------- software-pipelined block
+// The same arithmetic as attn_block (bit-identical outputs: same MFMA chains, same max, same
+// exp2 arguments, same order of the running sums, same RNE conversions), scheduled so that a
+// wave never waits a whole LDS round trip in front of its MFMAs and its softmax VALU runs in
+// the shadow of its own MFMAs:
+//  * S phase: the K fragments of key block kb+1 are read (inline ds_read_b128, immediate
+//    offsets) while the 4 MFMAs of block kb run; a counted lgkmcnt(4) retires only block kb's;
+//    the max of block kb-1 is folded in beside block kb's MFMAs.
+//  * P.V phase: V^T of block kb+1 is read (ds_read2_b64: v0 | v1 land as one f16x8 operand)
+//    and the exp2 / sum / fp16 pack of block kb+1 are computed while block kb's MFMAs run.
+//  * the cross-half exchanges (max, sum) use v_permlane32_swap: no LDS op of the compiler's
+//    own in the block, so the counted waits are exact.
+//  * O^T is widened to 16-byte stores by one v_permlane32_swap per dword (4 stores per lane
+//    instead of 8 half-width ones): kAttnPipeStores vector-memory ops per wave.
+constexpr int kAttnPipeStores = 4;
+#ifndef ATTN_PIPE
+#define ATTN_PIPE 1
+#endif
+
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + 1, N>(f);
+    }
+}
+
+template <int OFF>
+__device__ __forceinline__ void ds_rd128(f16x8& d, uint32_t a) {
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(a), "n"(OFF) : "memory");
+}
+// two 8-byte reads 16 bytes apart (offsets in units of 8 bytes) -> one f16x8
+template <int OFF8>
+__device__ __forceinline__ void ds_rd2x64(f16x8& d, uint32_t a) {
+    asm volatile("ds_read2_b64 %0, %1 offset0:%2 offset1:%3" : "=v"(d) : "v"(a), "n"(OFF8), "n"(OFF8 + 2) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void lgkm_wait4(f16x8& a, f16x8& b, f16x8& c, f16x8& d) {
+    asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "n"(N) : "memory");
+}
+// {x[l], x[l ^ 32]} in some order per lane.  The results are copied out as uint32_t before any
+// bit_cast: hipcc 7.2 lowers __builtin_bit_cast(float, r[1]) applied to the builtin's vector
+// result as element 0 (both results then read the first register).
+__device__ __forceinline__ void xhalf_pair(float x, float& a, float& b) {
+    const uint32_t u = __builtin_bit_cast(uint32_t, x);
+    const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+    const uint32_t r0 = r[0], r1 = r[1];
+    a = __builtin_bit_cast(float, r0);
+    b = __builtin_bit_cast(float, r1);
+}
+__device__ __forceinline__ float xhalf_max(float x) {  // max(x[l], x[l ^ 32])
+    float a, b;
+    xhalf_pair(x, a, b);
+    return fmaxf(a, b);
+}
+__device__ __forceinline__ float xhalf_sum(float x) {  // x[l] + x[l ^ 32] (commutative: = x + shfl_xor(x, 32))
+    float a, b;
+    xhalf_pair(x, a, b);
+    return a + b;
+}
+
+#ifdef ATTN_STAMPS
+// diagnostic build only (tools/attn_stamps.py): s_memtime per phase of heads 8..15 of every
+// workgroup, 8 stamps per (workgroup, wave, head)
+__device__ uint64_t g_attn_stamps[256 * 8 * 8 * 8];
+#define ATTN_STAMP(i) (stamp[i] = __builtin_amdgcn_s_memtime())
+#else
+#define ATTN_STAMP(i) ((void)0)
+#endif
+
+// mid(): called once in the P.V phase (after block NKB/2's MFMAs), after(): right after the
+// last P.V MFMA, before the O stores — the caller's prefetch for the next head goes there.
+template <int NKB, typename Mid, typename After>
+__device__ __forceinline__ void attn_block_pipe(const _Float16* sK, const _Float16* sV, const f16x8 (&qf)[4], int qi,
+                                                int L, int64_t bh, int H, _Float16* __restrict__ o, float scale_log2,
+                                                Mid&& mid, After&& after
+#ifdef ATTN_STAMPS
+                                                ,
+                                                uint64_t* stamp
+#endif
+) {
+    constexpr int VS = NKB * 32 + 4;  // vt_stride(LP)
+    const int lane = threadIdx.x & 63;
+    const int hh = lane >> 5, ql = lane & 31;
+    // K fragment bases (one per 16-wide k-step; the key block is an immediate: the swizzle
+    // term depends on the row only through (row >> 1) & 7 = (ql >> 1) & 7)
+    uint32_t ka[4];
+#pragma unroll
+    for (int ks = 0; ks < 4; ks++) ka[ks] = lds_addr(sK + ql * 64 + (((2 * ks + hh) ^ ((ql >> 1) & 7)) << 3));
+    // V^T bases of the two 32-row d blocks; key block / half-step offsets are immediates
+    const uint32_t va0 = lds_addr(sV + ql * VS + 4 * hh), va1 = va0 + 32 * VS * 2;
+
+    f32x16 s[NKB];
+    f16x8 kf[2][4];
+    float mx = -__builtin_inff();
+    auto rd_k = [&](auto kbc) {
+        constexpr int kb = decltype(kbc)::value;
+        ds_rd128<kb * 32 * 64 * 2>(kf[kb & 1][0], ka[0]);
+        ds_rd128<kb * 32 * 64 * 2>(kf[kb & 1][1], ka[1]);
+        ds_rd128<kb * 32 * 64 * 2>(kf[kb & 1][2], ka[2]);
+        ds_rd128<kb * 32 * 64 * 2>(kf[kb & 1][3], ka[3]);
+    };
+    auto fold_max = [&](auto kbc) {
+        constexpr int kb = decltype(kbc)::value;
+        if constexpr (kb == NKB - 1) {
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int key = kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+                s[kb][r] = key < L ? s[kb][r] : -__builtin_inff();
+            }
+        }
+        // two independent chains (max is exact: any order gives the same value), pinned into
+        // this block's slot (a volatile asm keeps its place among the reads / waits)
+        float m0 = s[kb][0], m1 = s[kb][1];
+#pragma unroll
+        for (int r = 2; r < 16; r += 4) {
+            m0 = fmaxf(m0, fmaxf(s[kb][r], s[kb][r + 1]));
+            m1 = fmaxf(m1, fmaxf(s[kb][r + 2], s[kb][r + 3]));
+        }
+        mx = fmaxf(mx, fmaxf(m0, m1));
+        asm volatile("" : "+v"(mx));
+    };
+    rd_k(std::integral_constant<int, 0>{});
+    static_for<0, NKB>([&](auto kbc) {
+        constexpr int kb = decltype(kbc)::value;
+        if constexpr (kb + 1 < NKB) {
+            rd_k(std::integral_constant<int, kb + 1>{});
+            lgkm_wait4<4>(kf[kb & 1][0], kf[kb & 1][1], kf[kb & 1][2], kf[kb & 1][3]);
+        } else {
+            lgkm_wait4<0>(kf[kb & 1][0], kf[kb & 1][1], kf[kb & 1][2], kf[kb & 1][3]);
+        }
+        f32x16 a = f32x16{};
+#pragma unroll
+        for (int ks = 0; ks < 4; ks++) a = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[kb & 1][ks], qf[ks], a, 0, 0, 0);
+        s[kb] = a;
+        if constexpr (kb > 0) fold_max(std::integral_constant<int, kb - 1>{});
+    });
+    fold_max(std::integral_constant<int, NKB - 1>{});
+    mx = xhalf_max(mx);
+    ATTN_STAMP(2);
+
+    const float mb = -mx * scale_log2;
+    const f32x2v sc2 = {scale_log2, scale_log2}, mb2 = {mb, mb};
+    f32x2v sum2 = {0.f, 0.f};
+    f16x8 vf[2][2][2];  // [kb parity][sp][db]
+    f16x8 pf[2][2];     // [kb parity][sp]
+    auto rd_v = [&](auto kbc) {
+        constexpr int kb = decltype(kbc)::value;
+        ds_rd2x64<(kb * 64 + 0) / 8>(vf[kb & 1][0][0], va0);
+        ds_rd2x64<(kb * 64 + 0) / 8>(vf[kb & 1][0][1], va1);
+        ds_rd2x64<(kb * 64 + 32) / 8>(vf[kb & 1][1][0], va0);
+        ds_rd2x64<(kb * 64 + 32) / 8>(vf[kb & 1][1][1], va1);
+    };
+    auto softmax_blk = [&](auto kbc) {  // exp2 + running sums + fp16 pack of key block kb
+        constexpr int kb = decltype(kbc)::value;
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+            const f32x2v t = __builtin_elementwise_fma(f32x2v{s[kb][r], s[kb][r + 1]}, sc2, mb2);
+            const f32x2v p = {__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
+            s[kb][r] = p.x;
+            s[kb][r + 1] = p.y;
+            sum2 += p;
+        }
+        // the running sums stay in this block's slot (left alone, the compiler sinks all 56
+        // dependent adds to the end of the phase: a serial chain behind the last MFMA)
+        asm volatile("" : "+v"(sum2));
+#pragma unroll
+        for (int sp = 0; sp < 2; sp++)
+#pragma unroll
+            for (int j = 0; j < 8; j++) pf[kb & 1][sp][j] = (_Float16)s[kb][8 * sp + j];
+    };
+    f32x16 oacc[2] = {f32x16{}, f32x16{}};
+    rd_v(std::integral_constant<int, 0>{});
+    softmax_blk(std::integral_constant<int, 0>{});
+    static_for<0, NKB>([&](auto kbc) {
+        constexpr int kb = decltype(kbc)::value;
+        if constexpr (kb + 1 < NKB) {
+            rd_v(std::integral_constant<int, kb + 1>{});
+            lgkm_wait4<4>(vf[kb & 1][0][0], vf[kb & 1][0][1], vf[kb & 1][1][0], vf[kb & 1][1][1]);
+        } else {
+            lgkm_wait4<0>(vf[kb & 1][0][0], vf[kb & 1][0][1], vf[kb & 1][1][0], vf[kb & 1][1][1]);
+            // V^T key columns >= L hold whatever the DMA brought (the HBM row padding): zero
+            // them in registers (P is exactly 0 there; 0 * NaN would not be), so no pass over
+            // the LDS pad is needed.  Half e of a fragment is key kb*32 + 16 sp + 4 hh + (e & 3)
+            // + 8 (e >> 2); dword j holds halves 2j, 2j + 1.
+#pragma unroll
+            for (int sp = 0; sp < 2; sp++) {
+                uint32_t m[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int key = kb * 32 + 16 * sp + 4 * hh + (2 * j & 3) + 8 * (j >> 1);
+                    m[j] = key >= L ? 0u : key + 1 >= L ? 0x0000ffffu : 0xffffffffu;
+                }
+#pragma unroll
+                for (int db = 0; db < 2; db++) {
+                    uint4 u = __builtin_bit_cast(uint4, vf[kb & 1][sp][db]);
+                    u.x &= m[0];
+                    u.y &= m[1];
+                    u.z &= m[2];
+                    u.w &= m[3];
+                    vf[kb & 1][sp][db] = __builtin_bit_cast(f16x8, u);
+                }
+            }
+        }
+#pragma unroll
+        for (int sp = 0; sp < 2; sp++)
+#pragma unroll
+            for (int db = 0; db < 2; db++)
+                oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf[kb & 1][sp][db], pf[kb & 1][sp], oacc[db], 0, 0, 0);
+        if constexpr (kb + 1 < NKB) softmax_blk(std::integral_constant<int, kb + 1>{});
+        if constexpr (kb == NKB / 2) mid();
+    });
+    after();
+    const float sum = xhalf_sum(sum2.x + sum2.y);
+    const float inv = 1.0f / sum;
+    ATTN_STAMP(3);
+    // lane (ql, hh) holds d = db*32 + 8g + 4hh + 0..3; pair g = 2j, 2j+1 across the halves so
+    // that half 0 stores d 16j..16j+7 and half 1 d 16j+8..16j+15 (16 bytes each)
+    uint4 w[2][2];
+#pragma unroll
+    for (int db = 0; db < 2; db++)
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const int g0 = 2 * j, g1 = 2 * j + 1;
+            auto pk = [&](int e) { return mul_pk_h(oacc[db][e], oacc[db][e + 1], inv); };
+            const uint32_t x0 = pk(4 * g0), x1 = pk(4 * g0 + 2), y0 = pk(4 * g1), y1 = pk(4 * g1 + 2);
+            const auto r0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
+            const auto r1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
+            w[db][j] = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+        }
+    if (qi < L) {
+        const int64_t b = bh / H, hd = bh % H;
+        _Float16* orow = o + (b * L + qi) * (int64_t)(H * 64) + hd * 64 + 8 * hh;
+#pragma unroll
+        for (int db = 0; db < 2; db++)
+#pragma unroll
+            for (int j = 0; j < 2; j++) *(uint4*)(orow + db * 32 + 16 * j) = w[db][j];
     }
 }
 
@@ -232,6 +489,124 @@ __global__ __launch_bounds__(512) void mhsa_kernel(const _Float16* __restrict__ 
     }
 }
 
+// Non-causal blocks (the vision towers): the software-pipelined attn_block_pipe, with the
+// next head's prefetch split by wave age.  Waves w and w + 4 share a SIMD; the younger one
+// (w >= 4) loses every MFMA / VALU arbitration to the older, so it runs the critical path
+// (phase stamps, tools/attn_stamps.py: before this split the younger waves' S phase took 2.2x
+// the older ones', and the older waves then idled ~3k cycles per head at the barrier):
+//  * waves 0-3 issue the next head's K (LDS-DMA) and their own next Q rows at the head start,
+//    and the next head's V^T blob right after their last P.V MFMA (V is needed only by the
+//    next head's P.V phase: most of a head of lead time; those waves idled ~3-4k cycles per
+//    head at the barrier);
+//  * waves 4.. only load their own next Q rows, in the middle of their P.V phase;
+//  * the V^T key padding is zeroed in registers (attn_block_pipe), so a head needs one
+//    barrier: each wave waits for its own prefetch (its O stores stay in flight), barrier.
+template <int NKB>
+__global__ __launch_bounds__(NKB * 64) void mhsa_pipe_kernel(const _Float16* __restrict__ q,
+                                                            const _Float16* __restrict__ k,
+                                                            const _Float16* __restrict__ vt, _Float16* __restrict__ o,
+                                                            int L, int H, int64_t nbh, float scale_log2) {
+    constexpr int LP = NKB * 32, VS = LP + 4, NW = NKB;
+    constexpr int NOLD = NW > 4 ? 4 : NW;              // waves issuing K (and V when NW <= 4)
+    constexpr int STAGE = LP * 64 + 64 * VS;           // K [LP][64] then V^T [64][VS]
+    constexpr int KPIECES = LP / 8;                    // 1-KiB pieces of K
+    constexpr int VBYTES = 64 * VS * 2;                // V^T blob (a multiple of 512 B)
+    constexpr int VPIECES = (VBYTES + 1023) / 1024;    // last may be half
+    constexpr int VLAST = (VBYTES - (VPIECES - 1) * 1024) / 16;
+    extern __shared__ __attribute__((aligned(16))) _Float16 lds[];
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int hh = lane >> 5, ql = lane & 31;
+    const int qi = wid * 32 + ql;
+
+    auto issue_k = [&](int64_t bh, int stage, int w0, int nws) {
+        _Float16* sK = lds + stage * STAGE;
+        const _Float16* kh = k + bh * L * 64;
+        for (int pc = wid - w0; pc < KPIECES; pc += nws) {
+            int r = 8 * pc + (lane >> 3);
+            const int kc = (lane & 7) ^ ((r >> 1) & 7);
+            r = r < L ? r : L - 1;  // rows >= L: any finite key (masked to -inf)
+            __builtin_amdgcn_global_load_lds(kh + (int64_t)r * 64 + kc * 8, (lds_ptr_t)(sK + pc * 512), 16, 0, 0);
+        }
+    };
+    auto issue_v = [&](int64_t bh, int stage, int w0, int nws) {
+        _Float16* sV = lds + stage * STAGE + LP * 64;
+        const _Float16* vh = vt + bh * 64 * (int64_t)VS;
+        for (int pc = wid - w0; pc < VPIECES; pc += nws)
+            if (pc + 1 < VPIECES || lane < VLAST)  // never read or write past the blob
+                __builtin_amdgcn_global_load_lds(vh + pc * 512 + lane * 8, (lds_ptr_t)(sV + pc * 512), 16, 0, 0);
+    };
+    // Q rows of this wave's queries (rows >= L read row L-1: finite, never stored); inline-asm
+    // loads, retired by the kernel's counted waits, every use ordered after them by pin()
+    auto load_q = [&](int64_t bh, f16x8* qf) {
+        const _Float16* qh = q + (bh * L + (qi < L ? qi : L - 1)) * 64 + hh * 8;
+        asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(qf[0]) : "v"(qh) : "memory");
+        asm volatile("global_load_dwordx4 %0, %1, off offset:32" : "=v"(qf[1]) : "v"(qh) : "memory");
+        asm volatile("global_load_dwordx4 %0, %1, off offset:64" : "=v"(qf[2]) : "v"(qh) : "memory");
+        asm volatile("global_load_dwordx4 %0, %1, off offset:96" : "=v"(qf[3]) : "v"(qh) : "memory");
+    };
+    auto pin = [&](f16x8* qf) { asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3])); };
+
+    int64_t bh = blockIdx.x;
+    if (bh >= nbh) return;
+    int stage = 0;
+    issue_k(bh, 0, 0, NW);
+    issue_v(bh, 0, 0, NW);
+    f16x8 qf[4];
+    load_q(bh, qf);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    pin(qf);
+    __builtin_amdgcn_s_barrier();
+#ifdef ATTN_STAMPS
+    uint64_t stamp[8] = {};
+    int it = 0;
+#endif
+    for (; bh < nbh; bh += gridDim.x) {
+        ATTN_STAMP(0);
+        const int64_t nxt = bh + gridDim.x;
+        const bool more = nxt < nbh;
+        f16x8 qn[4];
+        if (more && wid < NOLD) {
+            load_q(nxt, qn);
+            issue_k(nxt, stage ^ 1, 0, NOLD);
+        }
+        ATTN_STAMP(1);
+        const _Float16* sK = lds + stage * STAGE;
+        attn_block_pipe<NKB>(
+            sK, sK + LP * 64, qf, qi, L, bh, H, o, scale_log2,
+            [&] {
+                if (more && wid >= NOLD) load_q(nxt, qn);
+            },
+            [&] {
+                if (more && wid < NOLD) issue_v(nxt, stage ^ 1, 0, NOLD);
+            }
+#ifdef ATTN_STAMPS
+            ,
+            stamp
+#endif
+        );
+        // this wave's prefetch has landed; its kAttnPipeStores O stores (the youngest
+        // vector-memory ops) stay in flight.  A raw barrier (__syncthreads would drain them).
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kAttnPipeStores) : "memory");
+        ATTN_STAMP(4);
+        __builtin_amdgcn_s_barrier();
+        ATTN_STAMP(5);
+        if (more) {
+            pin(qn);
+#pragma unroll
+            for (int ks = 0; ks < 4; ks++) qf[ks] = qn[ks];
+        }
+        stage ^= 1;
+#ifdef ATTN_STAMPS
+        if (it >= 8 && it < 16 && lane == 0 && blockIdx.x < 256) {
+            uint64_t* d = g_attn_stamps + ((blockIdx.x * 8 + wid) * 8 + (it - 8)) * 8;
+            for (int i = 0; i < 6; i++) d[i] = stamp[i];
+        }
+        it++;
+#endif
+    }
+}
+
 // ======================================================== fused QKV GEMM + attention
 // ln_1 -> in_proj -> SDPA of a vision block (custom_clip_model.py:12,22-27) in one persistent
 // kernel: the QKV GEMM's 1 GB of q / k / v^T per batch of 1024 crops (and the attention's read
@@ -273,9 +648,6 @@ __device__ __forceinline__ int opaque_zero() {
     return z;
 }
 
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-}
 __device__ __forceinline__ void lds_write_u2(void* p, uint2 v) {
     asm volatile("ds_write_b64 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory");
 }
@@ -579,9 +951,40 @@ static int num_cu() {
     return g_num_cu;
 }
 
+template <int NKB>
+static int launch_mhsa_pipe(const void* q, const void* k, const void* vt, void* o, int64_t nseq, int L, int H,
+                            hipStream_t s) {
+    constexpr int LP = NKB * 32, VS = LP + 4;
+    const size_t lds = 2 * ((size_t)LP * 64 * 2 + (size_t)64 * VS * 2);
+    static bool attr = false;
+    if (!attr) {
+        RM_CHECK_HIP(hipFuncSetAttribute((const void*)mhsa_pipe_kernel<NKB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)lds));
+        attr = true;
+    }
+    const int64_t nbh = nseq * H;
+    static int occ = 0;
+    if (!occ) {
+        int n = 0;
+        RM_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)mhsa_pipe_kernel<NKB>, NKB * 64, lds));
+        occ = n > 0 ? n : 1;
+    }
+    const int64_t slots = (int64_t)num_cu() * occ;
+    const int64_t grid = nbh < slots ? nbh : slots;
+    hipLaunchKernelGGL((mhsa_pipe_kernel<NKB>), dim3((unsigned)grid), dim3(NKB * 64), lds, s, (const _Float16*)q,
+                       (const _Float16*)k, (const _Float16*)vt, (_Float16*)o, L, H, nbh,
+                       0.125f * 1.4426950408889634f);
+    RM_LAUNCHED();
+    return OK;
+}
+
 template <int NKB, bool CAUSAL>
 static int launch_mhsa(const void* q, const void* k, const void* vt, void* o, int64_t nseq, int L, int H,
                        int lpad_g, hipStream_t s) {
+    if constexpr (!CAUSAL && ATTN_PIPE) {
+        RM_REQUIRE(lpad_g == vt_stride(NKB * 32), "mhsa: v^T row stride must be reidmi_attn_lpad(L)");
+        return launch_mhsa_pipe<NKB>(q, k, vt, o, nseq, L, H, s);
+    }
     constexpr int LP = NKB * 32;
     const int vs = vt_stride(LP);
     RM_REQUIRE(lpad_g == vs, "mhsa: v^T row stride must be reidmi_attn_lpad(L)");
@@ -755,6 +1158,13 @@ int mhsa(const void* q, const void* k, const void* vt, void* o, int64_t nseq, in
 using namespace reidmi;
 
 REIDMI_API int reidmi_attn_lpad(int L) { return attn_lpad(L); }
+
+#ifdef ATTN_STAMPS
+REIDMI_API int reidmi_attn_stamps(uint64_t* host) {
+    RM_CHECK_HIP(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_attn_stamps), sizeof(g_attn_stamps)));
+    return OK;
+}
+#endif
 
 #ifdef QA_DEBUG
 REIDMI_API int reidmi_qa_dbg_set(void* q, void* k, void* vt, int lp) {
