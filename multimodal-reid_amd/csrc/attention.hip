@@ -46,6 +46,11 @@ __device__ __forceinline__ uint32_t cvt_pk_h(float a, float b) {
 // mix instruction for some elements and as v_mul + v_cvt_pk (two roundings) for others, so
 // the two attention blocks would differ in ~1 value in 36 000.
 __device__ __forceinline__ uint32_t mul_pk_h(float a, float b, float inv) {
+#ifdef ATTN_OUT_CVT  // A/B only: fp32 product, then RNE to fp16 (two roundings)
+    float x = a * inv, y = b * inv;
+    asm("" : "+v"(x), "+v"(y));
+    return cvt_pk_h(x, y);
+#endif
     uint32_t r;
     asm("v_fma_mixlo_f16 %0, %1, %2, 0" : "=v"(r) : "v"(a), "v"(inv));
     asm("v_fma_mixhi_f16 %0, %1, %2, 0" : "+v"(r) : "v"(b), "v"(inv));

@@ -209,15 +209,30 @@ def test_end_to_end_accuracy_vs_reference(gpu):
     a_ours = _topk_agree(ours, g["rank50_fp32"], 10)
     assert a_ours >= a_ref - 1.0 / Q, (a_ours, a_ref)
     assert _topk_agree(ours, g["rank50_fp32"], 1) >= _topk_agree(g["rank50_fp16"], g["rank50_fp32"], 1) - 1.0 / Q
-    # k-reciprocal branch of R1_mAP_eval (evaluate.py:124-127)
-    rcmc, rmap = zsl.get_cmc_map(feats[Q:], feats[:Q], torch.from_numpy(gp), torch.from_numpy(qp),
-                                 torch.from_numpy(gc), torch.from_numpy(qc), reranking=True)
+    # k-reciprocal branch of R1_mAP_eval (evaluate.py:124-127).  The re-ranked mAP is a
+    # discontinuous function of the features (k-reciprocal sets flip): at this size three builds
+    # whose attention outputs differ in the rounding of 1 value in ~36 000 (1 fp16 ulp) gave
+    # 0.3016 / 0.3027 / 0.3038 with identical feature error (profiles/r03/e2e_rounding_ab.txt),
+    # and the reference's own fp16 run sits d_rr = 0.0013 from its fp32 run.  The bound adds the
+    # noise floor measured here: the largest re-ranked mAP change that a relative perturbation
+    # of 2^-12 (half an fp16 ulp) of our own features produces, over 3 seeds.
+    def rr_map(f):
+        return zsl.get_cmc_map(f[Q:], f[:Q], torch.from_numpy(gp), torch.from_numpy(qp), torch.from_numpy(gc),
+                               torch.from_numpy(qc), reranking=True)[1]
+    rmap = rr_map(feats)
+    floor = 0.0
+    for seed in range(3):
+        gen = torch.Generator(device=feats.device).manual_seed(seed)
+        eps = (torch.rand(feats.shape, generator=gen, device=feats.device) * 2 - 1) * 2.0 ** -12
+        floor = max(floor, abs(rr_map(feats * (1 + eps)) - rmap))
+    assert floor < 5e-3, floor  # a perturbation this small must not move the metric further
     d_rr = abs(float(g["map_rr_fp16"]) - float(g["map_rr_fp32"]))
-    for tag, tol in (("fp32", 1e-3), ("fp16", d_rr + 1e-3)):
-        assert abs(rmap - float(g[f"map_rr_{tag}"])) <= tol, (tag, rmap, float(g[f"map_rr_{tag}"]), tol)
+    for tag, tol in (("fp32", 1e-3 + floor), ("fp16", d_rr + 1e-3 + floor)):
+        assert abs(rmap - float(g[f"map_rr_{tag}"])) <= tol, (tag, rmap, float(g[f"map_rr_{tag}"]), tol, floor)
     print(f"e2e: mAP {mAP:.5f} (ref fp32 {float(g['map_fp32']):.5f}, fp16 {float(g['map_fp16']):.5f}); "
           f"top-10 agreement with ref fp32 {a_ours:.3f} (ref fp16 {a_ref:.3f}); "
-          f"re-rank mAP {rmap:.5f} (ref {float(g['map_rr_fp32']):.5f} / {float(g['map_rr_fp16']):.5f})")
+          f"re-rank mAP {rmap:.5f} (ref {float(g['map_rr_fp32']):.5f} / {float(g['map_rr_fp16']):.5f}; "
+          f"half-ulp noise floor {floor:.5f})")
 
 
 @pytest.mark.parametrize("kind", ["coop", "vl"])
