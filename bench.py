@@ -20,7 +20,7 @@ zero-shot classifier's text side at Market size (750 x 56 token rows, TF/s); "ba
 "preprocess" = retrieval-kernel and transform rooflines; "jpeg" = the loaders' JPEG decode of
 a Market split of files on the device (and + transform), Pillow timed beside it; "cpu_baseline".
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B (default 1024)] [--no-cpu-baseline] [--no-rerank]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B (default 4096)] [--no-cpu-baseline] [--no-rerank]
                     [--no-msmt17] [--no-text] [--no-jpeg]
 """
 import argparse
@@ -47,14 +47,17 @@ PEAK_F16_TFLOPS = 2500.0  # MI355X dense fp16/bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_F32_MATRIX_TFLOPS = 157.3  # MI355X fp32 matrix (v_mfma_f32_32x32x2_f32)
 PEAK_HBM_GBPS = 8000.0
 EPI_GELU = 1  # the c_fc GEMM (+QuickGELU epilogue): the largest single kernel per block
-# HBM-side bytes per c_fc launch (ln_2-folded fp16 GEMM, M = 1024*211 (the default batch),
-# N = 3072, K = 768, auto tile walk = 2 N-groups) from rocprofv3 PMC passes (tools/prof_round.sh
-# -> profiles/r02/pmc_c_fc_fp16_walk2_{FETCH,WRITE}_SIZE.csv, 6 launches): FETCH_SIZE
-# 736 400 KiB doubled (gfx950 reports half of 16-B/lane streaming reads, MI355X_MICROARCH.md
-# "HBM") + WRITE_SIZE 1 296 384 KiB.  FETCH_SIZE also counts Infinity-Cache hits: A panels
-# are re-read by the 2 XCD groups and W panels by the rounds of an XCD (4 MB L2).
-# Algorithmic: A 332 MB + W 4.7 MB + out 1 327 MB = 1.66 GB.
-C_FC_TRAFFIC_BYTES = (2 * 736400 + 1296384) * 1024
+# HBM-side bytes per full-batch c_fc launch (ln_2-folded fp16 GEMM, M = batch * 211, N = 3072,
+# K = 768, auto tile walk = 2 N-groups), from rocprofv3 PMC passes of that launch
+# (tools/prof_round.sh): FETCH_SIZE doubled (gfx950 reports half of 16-B/lane streaming reads,
+# MI355X_MICROARCH.md "HBM") + WRITE_SIZE, KiB, mean of 6 launches.  FETCH_SIZE also counts
+# Infinity-Cache hits: A panels are re-read by the 2 XCD groups and W panels by the rounds of
+# an XCD (4 MB L2).  Other batches: not measured (null).
+#   batch 1024 (profiles/r02/pmc_c_fc_fp16_walk2_*): 736 400 / 1 296 384 KiB; algorithmic
+#     A 332 MB + W 4.7 MB + out 1 327 MB = 1.66 GB
+#   batch 4096 (profiles/r03/pmc_c_fc_b4096_*): 3 142 462 / 5 185 615 KiB; algorithmic
+#     A 1 327 MB + W 4.7 MB + out 5 310 MB = 6.64 GB
+C_FC_TRAFFIC_BYTES = {1024: (2 * 736400 + 1296384) * 1024, 4096: (2 * 3142462 + 5185615) * 1024}
 
 
 def _max_over_ranks(values, dev):
@@ -476,7 +479,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=1024)
+    # 4096 crops per encoder call (M = 864 256 token rows per GEMM): fewer launches and a
+    # smaller partial last round of tiles per launch than 1024 (+1.5-2 %, profiles/r03/bench_batch_ab.txt)
+    ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-rerank", action="store_true")
     ap.add_argument("--no-msmt17", action="store_true")
@@ -547,7 +552,7 @@ def main():
             "roofline": {"bound": "mfma", "kernel": "gemm_persistent_kernel<1> (ln_2-folded fp16 mlp.c_fc + QuickGELU)",
                          "achieved": round(achieved, 1) if achieved else None, "peak": PEAK_F16_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_F16_TFLOPS, 4) if achieved else None,
-                         "traffic": C_FC_TRAFFIC_BYTES, "traffic_unit": "bytes/launch (PMC)", "avg_launch_ms": round(avg_ms, 4), "launches": cnt.value,
+                         "traffic": C_FC_TRAFFIC_BYTES.get(a.batch), "traffic_unit": "bytes/launch (PMC)", "avg_launch_ms": round(avg_ms, 4), "launches": cnt.value,
                          "flops_per_launch": fl.value / max(cnt.value, 1)},
         }
         if ms17 is not None:
