@@ -125,15 +125,30 @@ int reidmi_rr_feat16(const float* feat, int64_t N, int64_t D, int64_t ldf, void*
  * nmax2 of reidmi_rr_rank_rows_f16. */
 int reidmi_rr_norm_max(const float* sqn, const float* nrm, int64_t N, float* out2, void* stream);
 /* reidmi_rr_rank_rows with an fp16 MFMA pre-filter (same rank_out / rowmax_out bits): the fp16
- * product bounds every exact distance (error bound in backend.hip rank_select_kernel; the GEMM
- * epilogue writes only the upper bounds, chunk [chunk_rows][Np] fp32); only the candidates are
- * recomputed with the exact fp32 chain.  Rows whose distances are too concentrated for the
- * bound (or not finite) get need[r] = 1 and no output: the caller runs the exact rows for them.
- * nrm = sqrt(sqn); nmax2 = reidmi_rr_norm_max(sqn, nrm); need [hi - lo] int32. */
+ * product bounds every exact distance (error bound in backend.hip rank_select_kernel); only the
+ * candidates are recomputed with the exact fp32 chain.  The GEMM's epilogue writes the upper
+ * bounds (chunk [chunk_rows][Np] fp32) for a streaming selection.  Rows whose distances are too
+ * concentrated for the bound (or not finite) get need[r] = 1 and no output: the caller runs the
+ * exact rows for them.  nrm = sqrt(sqn); nmax2 = reidmi_rr_norm_max(sqn, nrm); need [hi - lo]
+ * int32; chunk: chunk_rows x Np fp32. */
 int reidmi_rr_rank_rows_f16(const float* feat, int64_t N, int64_t D, int64_t ldf, const float* sqn, const float* nrm,
                             const float* nmax2, const void* feat16, int64_t Np, int64_t Dp, int64_t lo, int64_t hi,
                             int K, int32_t* rank_out, float* rowmax_out, int32_t* need, float* chunk,
                             int64_t chunk_rows, void* stream);
+/* The same with the sample stride chosen: 0 or 1 = the dense form above at any N; S >= 2 = the
+ * selection inside the GEMM's epilogue against per-row thresholds from every S-th item (no
+ * N-wide row in HBM; backend.hip "R2 pre-filter with the selection in the GEMM"), when
+ * floor(N / S) spans at least one 256-column tile and 4 K items (else the dense form).  Same
+ * output bits; slower than the dense form at every N measured (rerank.hip RR_SAMPLE_STRIDE). */
+int reidmi_rr_rank_rows_f16_ex(const float* feat, int64_t N, int64_t D, int64_t ldf, const float* sqn,
+                               const float* nrm, const float* nmax2, const void* feat16, int64_t Np, int64_t Dp,
+                               int64_t lo, int64_t hi, int K, int32_t* rank_out, float* rowmax_out, int32_t* need,
+                               float* chunk, int64_t chunk_rows, int sample_stride, void* stream);
+/* Rows that one internal pass of reidmi_rr_rank_rows_f16(_ex) processes with a chunk of
+ * chunk_rows x Np floats (the in-epilogue form needs ~0.3 MB per row at N = 1M instead of 4 N
+ * bytes): size the calls' row ranges by it.  sample_stride < 0: the default form's.  -1 on bad
+ * arguments. */
+int64_t reidmi_rr_rank_rows_f16_pass_rows(int64_t N, int64_t Np, int64_t chunk_rows, int K, int sample_stride);
 /* R3 (reranking.py:51-71): V rows lo..hi (ELL [hi-lo][vcap]) from the full rank[N][K] and
  * rowmax[N]; distance entries recomputed from feat with the distance kernel's arithmetic.
  * ws: reidmi_rr_caps' v_ws_bytes (nullable when 0). */

@@ -19,7 +19,7 @@ _u16 = ctypes.c_uint16
 
 # name -> argtypes (all return int status)
 # entry points returning int64 besides the *_bytes sizes
-INT64_RESULT = set()
+INT64_RESULT = {"reidmi_rr_rank_rows_f16_pass_rows"}
 
 SIGNATURES = {
     "reidmi_row_sqnorm_f32": [_vp, _i64, _i64, _i64, _vp, _vp],
@@ -41,6 +41,9 @@ SIGNATURES = {
     "reidmi_rr_norm_max": [_vp, _vp, _i64, _vp, _vp],
     "reidmi_rr_rank_rows_f16": [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i32, _vp, _vp, _vp,
                                 _vp, _i64, _vp],
+    "reidmi_rr_rank_rows_f16_ex": [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i32, _vp, _vp,
+                                   _vp, _vp, _i64, _i32, _vp],
+    "reidmi_rr_rank_rows_f16_pass_rows": [_i64, _i64, _i64, _i32, _i32],
     "reidmi_rr_v_rows": [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _i32, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _i64, _vp,
                          _vp],
     "reidmi_rr_row_offsets": [_vp, _i64, _vp, _vp],

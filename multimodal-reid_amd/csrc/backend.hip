@@ -770,6 +770,167 @@ __global__ __launch_bounds__(256) void rank_select1_kernel(const float* __restri
     if (threadIdx.x == 0) need[r] = 1;
 }
 
+// ------------------------------------------ R2 pre-filter with the selection in the GEMM
+// The dense form above writes hi for every (row, item) pair and streams it back (N^2 fp32: 4 TB
+// each way at N = 1M).  The sampled form keeps the selection's state out of HBM:
+//  1. hi of each row against a sample of the items (every S-th item; EPI_RRHI, [rows][ns]);
+//     rr_sample_kernel: U_r = the K-th smallest hi in the sample bounds tau_r (the K-th
+//     smallest hi over all items) from above, and lb_r = max over the sample of lo = hi - w_r
+//     bounds the row's largest lo from below;
+//  2. the full GEMM with the EPI_RRSV epilogue appends to row r's list only the pairs with
+//     hi <= hmax_r (every pair with lo <= thr(U_r)) or hi >= lb_r (gemm.h) -- a superset of both of rank_select1's final
+//     candidate lists ({lo <= thr(tau)} and {hi >= max lo}), and it holds the K smallest hi
+//     (hi <= tau <= U) and the largest hi (>= max lo >= lb): the list's K-th smallest hi is
+//     tau itself and its largest hi the row's largest;
+//  3. rank_select_sv_kernel: sorts the row's list by (hi, index), takes tau and max lo from it,
+//     and runs rank_select1's exact tail (exact chain for both candidate lists, rowmax, stable
+//     order by od = d / rowmax): the same rank_out / rowmax bits.
+// A row whose list overflows RR_SV_CAP, holds a non-finite bound, or whose candidate lists
+// exceed rank_select1's capacities is marked in need[] for the exact rows, as before.
+constexpr int RR_SV_CAP = 4096;
+
+__global__ __launch_bounds__(256) void rr_sample_kernel(const float* __restrict__ hs, int64_t lds, int64_t ns,
+                                                        const float* __restrict__ sqn, const float* __restrict__ nrm,
+                                                        const float* __restrict__ nmax2, int64_t row0, int K,
+                                                        float c_rel, float c_abs, float c_d,
+                                                        float4* __restrict__ thr, int32_t* __restrict__ cnt,
+                                                        int cap) {
+    __shared__ TkLds L;
+    __shared__ float red[4];
+    const int64_t r = blockIdx.x, i = row0 + r;
+    const float* row = hs + r * lds;
+    const float w = rr_width(sqn[i], nrm[i], nmax2[0], nmax2[1], c_rel, c_abs, c_d);
+    float mx = -__builtin_inff();
+    int bad = 0;
+    for (int64_t j = threadIdx.x; j < ns; j += blockDim.x) {
+        const float v = row[j];
+        bad |= !(v < __builtin_inff());  // NaN or +inf
+        mx = fmaxf(mx, v);
+    }
+    mx = block_max(mx, red);
+    bad = __syncthreads_or(bad);
+    topk_row_dev([&](int64_t j) { return row[j]; }, ns, K, L);
+    if (threadIdx.x == 0) {
+        const float U = L.sv[K - 1];
+        const bool ok = !bad && ns >= K && U < 3.0e38f && U > -3.0e38f && mx < 3.0e38f;
+        // the epilogue keeps a pair unless lb > hi > hmax: hmax bounds from above every hi whose
+        // lo = fl(hi - w) is <= thr(U) (the widening covers the roundings of hi - w and of T + w)
+        const float T = U + fabsf(U) * 0x1p-21f + 1e-37f;
+        const float hmax = (T + w) + (fabsf(T) + w) * 0x1p-20f + 1e-37f;
+        thr[r] = make_float4(hmax, mx - w, w, 0.0f);
+        cnt[r] = ok ? 0 : cap + 1;
+    }
+}
+
+__global__ __launch_bounds__(256) void rank_select_sv_kernel(const int32_t* __restrict__ cnt,
+                                                             const int2* __restrict__ list, int cap,
+                                                             const float4* __restrict__ thr,
+                                                             const float* __restrict__ feat, int64_t ldf, int D,
+                                                             const float* __restrict__ sqn, int64_t row0, int K,
+                                                             int32_t* __restrict__ rank_out,
+                                                             float* __restrict__ rowmax_out,
+                                                             int32_t* __restrict__ need) {
+    __shared__ float sv[RR_SV_CAP];
+    __shared__ int si[RR_SV_CAP];
+    __shared__ float red[4];
+    __shared__ int s_nc, s_fm;
+    const int64_t r = blockIdx.x, i = row0 + r;
+    const int n = cnt[r];
+    if (n > cap || n < K) {  // overflow, a non-finite bound, or (never for N >= K) too few
+        if (threadIdx.x == 0) need[r] = 1;
+        return;
+    }
+    const int2* lr = list + r * cap;
+    const int P = pow2_ceil(n < 2 ? 2 : n);
+    for (int t = threadIdx.x; t < P; t += blockDim.x) {
+        if (t < n) {
+            const int2 e = lr[t];
+            sv[t] = __builtin_bit_cast(float, e.y);
+            si[t] = e.x;
+        } else {
+            sv[t] = __builtin_inff();
+            si[t] = 0x7fffffff;
+        }
+    }
+    int bad = 0;
+    for (int t = threadIdx.x; t < n; t += blockDim.x) bad |= !(sv[t] < __builtin_inff());  // NaN or +inf
+    if (threadIdx.x == 0) { s_nc = 0; s_fm = n; }
+    if (__syncthreads_or(bad)) {  // a non-finite bound: the exact path, as rank_select1
+        if (threadIdx.x == 0) need[r] = 1;
+        return;
+    }
+    bitonic_sort_kv(sv, si, P);  // ascending (hi, index)
+    const float w = thr[r].z;
+    const float tau = sv[K - 1];
+    const float th = tau + fabsf(tau) * 0x1p-21f + 1e-37f;  // rank_select1's thr_of
+    const float mlo = sv[n - 1] - w;                         // the row's largest lo
+    // candidate list = the prefix with lo = hi - w <= th; max list = the suffix with hi >= mlo
+    int pc = 0, fm = n;
+    for (int t = threadIdx.x; t < n; t += blockDim.x) {
+        if (sv[t] - w <= th) pc = t + 1 > pc ? t + 1 : pc;
+        if (sv[t] >= mlo) fm = t < fm ? t : fm;
+    }
+    atomicMax(&s_nc, pc);
+    atomicMin(&s_fm, fm);
+    __syncthreads();
+    const int nc = s_nc, f0 = s_fm, nm = n - f0;
+    bool exact = !(tau <= 3.0e38f && tau >= -3.0e38f) || nc > RS1_TKCAP || nm > RS1_MCAP;
+    float rmax = 0.0f;
+    if (!exact) {
+        float m = -__builtin_inff();
+        for (int t = f0 + threadIdx.x; t < n; t += blockDim.x) m = fmaxf(m, dist_exact(feat, ldf, D, sqn, i, si[t]));
+        rmax = block_max(m, red);
+        exact = !(rmax > 0.0f && rmax < __builtin_inff());  // degenerate rows: the exact path
+    }
+    if (!exact) {
+        // the candidates are sv / si [0, nc): their exact od replaces the bound in place
+        const int P2 = pow2_ceil(nc < 2 ? 2 : nc);
+        __syncthreads();  // every thread is done reading sv / si [f0, n) above
+        for (int t = threadIdx.x; t < P2; t += blockDim.x) {
+            if (t < nc) {
+                sv[t] = dist_exact(feat, ldf, D, sqn, i, si[t]) / rmax;
+            } else {
+                sv[t] = __builtin_inff();
+                si[t] = 0x7fffffff;
+            }
+        }
+        __syncthreads();
+        bitonic_sort_kv(sv, si, P2);
+        for (int t = threadIdx.x; t < K; t += blockDim.x) rank_out[r * K + t] = si[t];
+        if (threadIdx.x == 0) {
+            rowmax_out[r] = rmax;
+            need[r] = 0;
+        }
+        return;
+    }
+    if (threadIdx.x == 0) need[r] = 1;
+}
+
+void rank_select_consts(int D, float c[3]);
+
+int rr_sample_launch(const float* hs, int64_t lds, int64_t ns, const float* sqn, const float* nrm, const float* nmax2,
+                     int64_t row0, int64_t rows, int K, int D, float4* thr, int32_t* cnt, int cap, hipStream_t s) {
+    RM_REQUIRE(K >= 1 && K <= 64 && ns >= K && rows >= 0 && nmax2, "rr_sample: bad arguments");
+    if (rows == 0) return OK;
+    float c[3];
+    rank_select_consts(D, c);
+    hipLaunchKernelGGL(rr_sample_kernel, dim3((unsigned)rows), dim3(256), 0, s, hs, lds, ns, sqn, nrm, nmax2, row0, K,
+                       c[0], c[1], c[2], thr, cnt, cap);
+    RM_LAUNCHED();
+    return OK;
+}
+
+int rank_select_sv_launch(const int32_t* cnt, const int2* list, int cap, const float4* thr, const float* feat,
+                          int64_t ldf, int D, const float* sqn, int64_t row0, int64_t rows, int K, int32_t* rank_out,
+                          float* rowmax_out, int32_t* need, hipStream_t s) {
+    RM_REQUIRE(K >= 1 && K <= 64 && cap >= 1 && cap <= RR_SV_CAP && rows >= 0, "rank_select_sv: bad arguments");
+    if (rows == 0) return OK;
+    hipLaunchKernelGGL(rank_select_sv_kernel, dim3((unsigned)rows), dim3(256), 0, s, cnt, list, cap, thr, feat, ldf, D,
+                       sqn, row0, K, rank_out, rowmax_out, need);
+    RM_LAUNCHED();
+    return OK;
+}
+
 // fp16 copy of the features for the pre-filter GEMM: [Np][Dp], zero-padded rows / columns;
 // *range_ok cleared when an element is beyond +-2^15 (fp16 would overflow) or not finite.
 __global__ void feat16_kernel(const float* __restrict__ x, int64_t N, int64_t D, int64_t ldx, _Float16* __restrict__ y,

@@ -14,6 +14,9 @@
 //   EPI_RRHI      out fp32 = hi(i, j), the upper bound of the exact distance of items i, j from their
 //                 fp16 product (the k-reciprocal re-rank's pre-filter, rerank.hip): only the bound
 //                 reaches HBM, and the selection reads 4 bytes per pair instead of 12
+//   EPI_RRSV      no dense output: the pairs of row i that can still matter to its R2 selection
+//                 (hi - w_i <= thr_i or hi >= lb_i, per-row thresholds from a sampled pass) are
+//                 appended to the row's survivor list, a few hundred of the N columns
 #pragma once
 #include "common.h"
 
@@ -26,7 +29,8 @@ enum Epi : int {
     EPI_PATCH = 4,
     EPI_F32 = 5,
     EPI_RESID_F16 = 6,
-    EPI_RRHI = 7
+    EPI_RRHI = 7,
+    EPI_RRSV = 8
 };
 
 struct EpiArgs {
@@ -63,6 +67,17 @@ struct EpiArgs {
     int64_t rr_row0;
     int64_t rr_n;
     float rr_c[3];
+    const float* rr_csqn;  // the columns' squared norms / norms when they are not items 0..rr_n-1
+    const float* rr_cnrm;  // (a sampled item set); null: rr_sqn / rr_nrm
+    // EPI_RRSV: per row m (rr_thr[m].x = hi_max: a pair with hi <= hi_max can be a candidate
+    // of the K smallest, .y = lb: a pair with hi >= lb can hold the row's largest distance), the
+    // survivor counters and lists [m * sv_cap + p] = (column, hi bits) of the pairs with
+    // !(hi_max < hi < lb) (a NaN survives); counts past sv_cap are kept (the row then takes the
+    // exact path).  (rr_thr[m].z = the row's bound width w, .w unused: rank_select_sv.)
+    const float4* rr_thr;
+    int* sv_cnt;
+    int2* sv_list;
+    int sv_cap;
 };
 
 // hi(i, j) = fl(dt + e), dt = fl(fma(-2, dot, s_i + s_j)),

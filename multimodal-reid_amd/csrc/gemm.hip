@@ -254,20 +254,22 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
     if constexpr (EPI == EPI_RRHI) {
         // the items' norms: columns (4 consecutive per lane and fragment) and rows
         const int64_t n = ea.rr_n;
+        const float* csq = ea.rr_csqn ? ea.rr_csqn : ea.rr_sqn;
+        const float* cnr = ea.rr_cnrm ? ea.rr_cnrm : ea.rr_nrm;
         float sj[4][4], nj[4][4];
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const int64_t c0 = ncol + j * 16 + cq;
             if (c0 + 3 < n) {
-                const float4 a = *(const float4*)(ea.rr_sqn + c0), b = *(const float4*)(ea.rr_nrm + c0);
+                const float4 a = *(const float4*)(csq + c0), b = *(const float4*)(cnr + c0);
                 sj[j][0] = a.x, sj[j][1] = a.y, sj[j][2] = a.z, sj[j][3] = a.w;
                 nj[j][0] = b.x, nj[j][1] = b.y, nj[j][2] = b.z, nj[j][3] = b.w;
             } else {
 #pragma unroll
                 for (int e = 0; e < 4; e++) {
                     const int64_t c = c0 + e < n ? c0 + e : n - 1;
-                    sj[j][e] = ea.rr_sqn[c];
-                    nj[j][e] = ea.rr_nrm[c];
+                    sj[j][e] = csq[c];
+                    nj[j][e] = cnr[c];
                 }
             }
         }
@@ -294,6 +296,115 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
                                       : __builtin_inff();
                 *(float4*)((float*)ea.out + m * ea.ldc + c0) = make_float4(h[0], h[1], h[2], h[3]);
             }
+        }
+        return;
+    }
+    if constexpr (EPI == EPI_RRSV) {
+        // survivors of the R2 pre-filter (gemm.h): per row group i, a lane's 16 candidate bits
+        // (hi overwrites the accumulator in place, so the pass that writes the pairs needs only
+        // acc), the row's count over its 4 lanes (lane groups q = lane >> 4 share a row), one
+        // atomic add per row for the wave's 64 columns (all row groups' atomics in flight
+        // together: one round trip per tile), then each lane writes its pairs at base + the
+        // exclusive prefix over the row's lanes
+        const int64_t n = ea.rr_n;
+        const int q = lane >> 4;
+        const float* csq = ea.rr_csqn ? ea.rr_csqn : ea.rr_sqn;
+        const float* cnr = ea.rr_cnrm ? ea.rr_cnrm : ea.rr_nrm;
+        // phase 1: the survivor bits (acc is left as it is: phase 2 recomputes hi).  A pair
+        // survives unless lb' < hi < hi_max' (rr_thr: x = hi_max', y = lb, gemm.h), so a NaN or
+        // infinite bound survives too and sends the row to the exact path (rank_select_sv).
+        float sj[4][4], nj[4][4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int64_t c0 = ncol + j * 16 + cq;
+            if (c0 + 3 < n) {
+                const float4 x = *(const float4*)(csq + c0), y = *(const float4*)(cnr + c0);
+                sj[j][0] = x.x, sj[j][1] = x.y, sj[j][2] = x.z, sj[j][3] = x.w;
+                nj[j][0] = y.x, nj[j][1] = y.y, nj[j][2] = y.z, nj[j][3] = y.w;
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    const int64_t c = c0 + e < n ? c0 + e : n - 1;
+                    sj[j][e] = csq[c];
+                    nj[j][e] = cnr[c];
+                }
+            }
+        }
+        uint32_t msk[NI];
+#pragma unroll
+        for (int i = 0; i < NI; i++) {
+            const int64_t m = mrow + i * 16 + (lane & 15);
+            const int64_t mm = m < M ? m : M - 1;
+            const float si = ea.rr_sqn[ea.rr_row0 + mm], ni = ea.rr_nrm[ea.rr_row0 + mm];
+            const float2 th = *(const float2*)(ea.rr_thr + mm);
+            uint32_t b = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    const float h = rr_hi(acc[i][j][e], si, sj[j][e], ea.rr_c[0] * ni, ni, nj[j][e], ea.rr_c);
+                    b |= (uint32_t)(m < M && ncol + j * 16 + cq + e < n && !(h > th.x && h < th.y)) << (j * 4 + e);
+                }
+            msk[i] = b;
+        }
+        bool any = false;
+#pragma unroll
+        for (int i = 0; i < NI; i++) any = any || msk[i] != 0;
+        if (!__builtin_amdgcn_ballot_w64(any)) return;  // (nearly every tile)
+        // phase 2 (rare: a tile with survivors): per row group, the row's count over its 4 lanes
+        // (inclusive prefix over lane groups q), one atomic add per row — all row groups'
+        // atomics issued before the first result is used (one round trip) — then each lane
+        // writes its pairs (column, hi bits) at base + its exclusive prefix
+        auto row_prefix = [&](int i, int& pre, int& tot) {
+            const int c = __builtin_popcount(msk[i]);
+            int s = c;
+            const int u1 = __shfl_up(s, 16, 64);
+            s += q >= 1 ? u1 : 0;
+            const int u2 = __shfl_up(s, 32, 64);
+            s += q >= 2 ? u2 : 0;
+            pre = s - c;
+            tot = __shfl(s, (lane & 15) + 48, 64);
+        };
+        // phase 1's column norms are not kept for this (rare) phase: opaque copies of the
+        // pointers keep the compiler from reusing them, which spilled the K-loop's registers
+        const float* csq2 = csq;
+        const float* cnr2 = cnr;
+        const float* rsq2 = ea.rr_sqn;
+        const float* rnr2 = ea.rr_nrm;
+        asm volatile("" : "+s"(csq2), "+s"(cnr2), "+s"(rsq2), "+s"(rnr2));
+        int base[NI];
+#pragma unroll
+        for (int i = 0; i < NI; i++) {
+            int pre, tot;
+            row_prefix(i, pre, tot);
+            const int add = tot;
+            const int64_t m = mrow + i * 16 + (lane & 15);
+            base[i] = 0;
+            if (q == 0 && add != 0) base[i] = atomicAdd(ea.sv_cnt + m, add);
+        }
+#pragma unroll
+        for (int i = 0; i < NI; i++) {
+            // one row group at a time: without the fence the scheduler hoists every group's
+            // addresses and loads, which spilled the K-loop's registers
+            __builtin_amdgcn_sched_barrier(0);
+            const int64_t m = mrow + i * 16 + (lane & 15);
+            int pre, tot;
+            row_prefix(i, pre, tot);
+            int p = __shfl(base[i], lane & 15, 64) + pre;
+            if (msk[i] == 0) continue;
+            const int64_t mm = m < M ? m : M - 1;
+            const float si = rsq2[ea.rr_row0 + mm], ni = rnr2[ea.rr_row0 + mm];
+            // static (j, e) walk: a run-time register index would go through scratch
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+#pragma unroll
+                for (int e = 0; e < 4; e++)
+                    if ((msk[i] >> (j * 4 + e)) & 1u) {
+                        const int c = ncol + j * 16 + cq + e;
+                        const float h = rr_hi(acc[i][j][e], si, csq2[c], ea.rr_c[0] * ni, ni, cnr2[c], ea.rr_c);
+                        if (p < ea.sv_cap) ea.sv_list[m * ea.sv_cap + p] = make_int2(c, __builtin_bit_cast(int, h));
+                        p++;
+                    }
         }
         return;
     }
@@ -918,6 +1029,7 @@ int gemm_f16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, in
         case EPI_F32: rc = launch<EPI_F32>(A, lda, W, ldw, M, N, K, ea, s, opt); break;
         case EPI_RESID_F16: rc = launch<EPI_RESID_F16>(A, lda, W, ldw, M, N, K, ea, s, opt); break;
         case EPI_RRHI: rc = launch<EPI_RRHI>(A, lda, W, ldw, M, N, K, ea, s, opt); break;
+        case EPI_RRSV: rc = launch<EPI_RRSV>(A, lda, W, ldw, M, N, K, ea, s, opt); break;
         default: return fail(EINVAL_, "gemm: unknown epilogue");
     }
     if (ev_b) RM_CHECK_HIP(hipEventRecord(ev_b, s));

@@ -26,6 +26,11 @@ int rank_select_launch(float* dot, int64_t ldd, const float* feat, int64_t ldf, 
                        int32_t* rank_out, float* rowmax_out, int32_t* need, hipStream_t s);
 void rank_select_consts(int D, float c[3]);
 int norm_max_launch(const float* sqn, const float* nrm, int64_t N, float* out2, hipStream_t s);
+int rr_sample_launch(const float* hs, int64_t lds, int64_t ns, const float* sqn, const float* nrm, const float* nmax2,
+                     int64_t row0, int64_t rows, int K, int D, float4* thr, int32_t* cnt, int cap, hipStream_t s);
+int rank_select_sv_launch(const int32_t* cnt, const int2* list, int cap, const float4* thr, const float* feat,
+                          int64_t ldf, int D, const float* sqn, int64_t row0, int64_t rows, int K, int32_t* rank_out,
+                          float* rowmax_out, int32_t* need, hipStream_t s);
 int feat16_launch(const float* x, int64_t N, int64_t D, int64_t ldx, void* y, int64_t Np, int64_t Dp,
                   int32_t* range_ok, hipStream_t s);
 int topk_launch(const float* x, int64_t rows, int64_t cols, int64_t ldx, const float* row_div, int k,
@@ -1272,24 +1277,95 @@ REIDMI_API int reidmi_rr_norm_max(const float* sqn, const float* nrm, int64_t N,
     return norm_max_launch(sqn, nrm, N, out2, (hipStream_t)stream);
 }
 
-// reidmi_rr_rank_rows with an fp16 pre-filter: per row pass, the fp16 MFMA product of the
-// rows with all items bounds every exact distance; the GEMM's epilogue writes only the upper
-// bounds (chunk [rows][Np] fp32, EPI_RRHI) and the selection recomputes the rows' candidates
-// with the exact chain.  Same rank_out / rowmax_out bits as reidmi_rr_rank_rows for the rows
-// with need[r] = 0; rows with need[r] = 1 (concentrated or non-finite distances) are left for
-// the exact rows.  nrm = sqrt(sqn) [N]; nmax2 = reidmi_rr_norm_max of sqn, nrm.
-REIDMI_API int reidmi_rr_rank_rows_f16(const float* feat, int64_t N, int64_t D, int64_t ldf, const float* sqn,
-                                       const float* nrm, const float* nmax2, const void* feat16, int64_t Np,
-                                       int64_t Dp, int64_t lo, int64_t hi, int K, int32_t* rank_out,
-                                       float* rowmax_out, int32_t* need, float* chunk, int64_t chunk_rows,
-                                       void* stream) {
+// Sampled survivor form of the pre-filter (backend.hip rr_sample_kernel / rank_select_sv_kernel):
+// the sample is every S-th item, ns = floor(N / S) rounded down to whole 256-column tiles; per
+// row: the sample's bounds, then the survivor list (RR_SV_CAP pairs) instead of an N-wide row.
+// Measured at N = 1.01 M (profiles/r03/rerank_1m_in_epilogue.txt): bit-identical, but the
+// EPI_RRSV GEMM took 13.0 s against 3.8 s for the dense form's GEMM + 1.7 s of streaming
+// selection -- every 256 x 256 tile holds survivors (~1 000 per row spread over 3 946 column
+// tiles), so the append phase (an atomic round trip per row group, and its registers next to
+// the accumulators spill the K-loop) runs in every tile.  The dense form stays the default
+// (RR_SAMPLE_STRIDE 0); reidmi_rr_rank_rows_f16_ex selects the sampled one.
+constexpr int RR_SAMPLE_STRIDE = 0, RR_SV_CAP_ = 4096;
+
+__global__ void rr_gather_norms_kernel(const float* __restrict__ sqn, const float* __restrict__ nrm, int64_t ns,
+                                       int S, float* __restrict__ sqn_s, float* __restrict__ nrm_s) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < ns) {
+        sqn_s[t] = sqn[t * S];
+        nrm_s[t] = nrm[t * S];
+    }
+}
+
+// bytes of chunk the sampled form needs: the sample's norms once, then per row the sample
+// bounds, the survivor list, its counter and thresholds
+static int64_t rr_sv_ns(int64_t N, int S) { return S >= 2 ? N / S / 256 * 256 : 0; }
+static int64_t rr_sv_row_bytes(int64_t ns) { return 4 * ns + 8 * (int64_t)RR_SV_CAP_ + 4 + 16; }
+// rows per pass of the sampled form in a chunk of chunk_rows x Np floats (0: not applicable)
+static int64_t rr_sv_pass_rows(int64_t N, int64_t Np, int64_t chunk_rows, int K, int S) {
+    const int64_t ns = rr_sv_ns(N, S);
+    if (ns < 256 || ns < 4 * K) return 0;
+    const int64_t avail = chunk_rows * Np * 4 - 8 * ns - 64;
+    const int64_t r = avail / rr_sv_row_bytes(ns);
+    return r >= 64 ? (r < 65536 ? r : 65536) : 0;
+}
+
+static int rank_rows_f16(const float* feat, int64_t N, int64_t D, int64_t ldf, const float* sqn, const float* nrm,
+                         const float* nmax2, const void* feat16, int64_t Np, int64_t Dp, int64_t lo, int64_t hi,
+                         int K, int32_t* rank_out, float* rowmax_out, int32_t* need, float* chunk,
+                         int64_t chunk_rows, int S, hipStream_t s) {
     RM_REQUIRE(N > 0 && D > 0 && ldf >= D && 0 <= lo && lo <= hi && hi <= N && chunk_rows > 0 && K >= 1 && K <= N &&
                    K <= 64 && Np >= N && Np % 256 == 0 && Dp >= D && Dp % 64 == 0 && sqn && nrm && nmax2,
                "rr_rank_rows_f16: bad arguments");
     RM_REQUIRE(N < 0x7fffffff, "rr_rank_rows_f16: too many items");
-    hipStream_t s = (hipStream_t)stream;
     const _Float16* x16 = (const _Float16*)feat16;
     int rc;
+    const int64_t pass = rr_sv_pass_rows(N, Np, chunk_rows, K, S);
+    if (pass > 0) {
+        const int64_t ns = rr_sv_ns(N, S);
+        float* sqn_s = chunk;
+        float* nrm_s = chunk + ns;
+        char* pbase = (char*)(chunk + 2 * ns);
+        hipLaunchKernelGGL(rr_gather_norms_kernel, dim3((unsigned)ceil_div(ns, 256)), dim3(256), 0, s, sqn, nrm, ns, S,
+                           sqn_s, nrm_s);
+        RM_LAUNCHED();
+        for (int64_t a = lo; a < hi; a += pass) {
+            const int64_t nb = hi - a < pass ? hi - a : pass;
+            float* hs = (float*)pbase;                                          // [nb][ns]
+            int2* list = (int2*)(hs + nb * ns);                                 // [nb][cap]
+            int32_t* cnt = (int32_t*)(list + nb * RR_SV_CAP_);                  // [nb]
+            float4* thr = (float4*)(((uintptr_t)(cnt + nb) + 15) & ~(uintptr_t)15);  // [nb]
+            EpiArgs es{};
+            es.out = hs;
+            es.ldc = ns;
+            es.rr_sqn = sqn;
+            es.rr_nrm = nrm;
+            es.rr_csqn = sqn_s;
+            es.rr_cnrm = nrm_s;
+            es.rr_row0 = a;
+            es.rr_n = ns;
+            rank_select_consts((int)D, es.rr_c);
+            // the sample: W rows = every S-th item (row stride S * Dp)
+            if ((rc = gemm_f16(EPI_RRHI, x16 + a * Dp, Dp, x16, (int64_t)S * Dp, nb, ns, Dp, es, s))) return rc;
+            if ((rc = rr_sample_launch(hs, ns, ns, sqn, nrm, nmax2, a, nb, K, (int)D, thr, cnt, RR_SV_CAP_, s)))
+                return rc;
+            EpiArgs ev{};
+            ev.rr_sqn = sqn;
+            ev.rr_nrm = nrm;
+            ev.rr_row0 = a;
+            ev.rr_n = N;
+            rank_select_consts((int)D, ev.rr_c);
+            ev.rr_thr = thr;
+            ev.sv_cnt = cnt;
+            ev.sv_list = list;
+            ev.sv_cap = RR_SV_CAP_;
+            if ((rc = gemm_f16(EPI_RRSV, x16 + a * Dp, Dp, x16, Dp, nb, Np, Dp, ev, s))) return rc;
+            if ((rc = rank_select_sv_launch(cnt, list, RR_SV_CAP_, thr, feat, ldf, (int)D, sqn, a, nb, K,
+                                            rank_out + (a - lo) * K, rowmax_out + (a - lo), need + (a - lo), s)))
+                return rc;
+        }
+        return OK;
+    }
     for (int64_t a = lo; a < hi; a += chunk_rows) {
         const int64_t nb = hi - a < chunk_rows ? hi - a : chunk_rows;
         EpiArgs ea{};
@@ -1306,6 +1382,45 @@ REIDMI_API int reidmi_rr_rank_rows_f16(const float* feat, int64_t N, int64_t D, 
             return rc;
     }
     return OK;
+}
+
+// reidmi_rr_rank_rows with an fp16 pre-filter: the fp16 MFMA product of the rows with the
+// items bounds every exact distance, and only each row's candidates are recomputed with the
+// exact chain.  Same rank_out / rowmax_out bits as reidmi_rr_rank_rows for the rows with
+// need[r] = 0; rows with need[r] = 1 (concentrated or non-finite distances) are left for the
+// exact rows.  nrm = sqrt(sqn) [N]; nmax2 = reidmi_rr_norm_max of sqn, nrm.  chunk: chunk_rows x
+// Np fp32 of scratch.  The GEMM writes the rows' bounds (chunk_rows x Np) and rank_select1
+// streams them; reidmi_rr_rank_rows_f16_ex with a sample stride >= 2 runs the selection inside
+// the GEMM's epilogue instead (backend.hip, "R2 pre-filter with the selection in the GEMM";
+// same bits, slower at every N measured -- see RR_SAMPLE_STRIDE).
+REIDMI_API int reidmi_rr_rank_rows_f16(const float* feat, int64_t N, int64_t D, int64_t ldf, const float* sqn,
+                                       const float* nrm, const float* nmax2, const void* feat16, int64_t Np,
+                                       int64_t Dp, int64_t lo, int64_t hi, int K, int32_t* rank_out,
+                                       float* rowmax_out, int32_t* need, float* chunk, int64_t chunk_rows,
+                                       void* stream) {
+    return rank_rows_f16(feat, N, D, ldf, sqn, nrm, nmax2, feat16, Np, Dp, lo, hi, K, rank_out, rowmax_out, need,
+                         chunk, chunk_rows, RR_SAMPLE_STRIDE, (hipStream_t)stream);
+}
+
+// The same with the sample stride chosen (tests: 0 = the dense form at any N).
+REIDMI_API int reidmi_rr_rank_rows_f16_ex(const float* feat, int64_t N, int64_t D, int64_t ldf, const float* sqn,
+                                          const float* nrm, const float* nmax2, const void* feat16, int64_t Np,
+                                          int64_t Dp, int64_t lo, int64_t hi, int K, int32_t* rank_out,
+                                          float* rowmax_out, int32_t* need, float* chunk, int64_t chunk_rows,
+                                          int sample_stride, void* stream) {
+    RM_REQUIRE(sample_stride >= 0, "rr_rank_rows_f16_ex: sample_stride >= 0");
+    return rank_rows_f16(feat, N, D, ldf, sqn, nrm, nmax2, feat16, Np, Dp, lo, hi, K, rank_out, rowmax_out, need,
+                         chunk, chunk_rows, sample_stride, (hipStream_t)stream);
+}
+
+// Rows one pass of reidmi_rr_rank_rows_f16(_ex) takes with a chunk of chunk_rows x Np floats:
+// the sampled form's pass (> chunk_rows for large N), or chunk_rows for the dense form.
+// sample_stride < 0: the stride reidmi_rr_rank_rows_f16 uses.
+REIDMI_API int64_t reidmi_rr_rank_rows_f16_pass_rows(int64_t N, int64_t Np, int64_t chunk_rows, int K,
+                                                     int sample_stride) {
+    if (N <= 0 || Np < N || chunk_rows <= 0 || K < 1) return -1;
+    const int64_t p = rr_sv_pass_rows(N, Np, chunk_rows, K, sample_stride < 0 ? RR_SAMPLE_STRIDE : sample_stride);
+    return p > 0 ? p : chunk_rows;
 }
 
 REIDMI_API int reidmi_rr_v_rows(const float* feat, int64_t N, int64_t D, int64_t ldf, const float* sqn,

@@ -192,7 +192,11 @@ class HipStages:
                 # one row pass at a time: rows it cannot decide (distances too concentrated
                 # for its bound) go through the exact rows, and once a pass has more of those
                 # than not (a random network's embeddings) the rest skips the filter
-                cr = min(max(256, self.chunk_rows * self.N // Np // 256 * 256), hi - lo)
+                cc = min(max(256, self.chunk_rows * self.N // Np // 256 * 256),  # chunk rows of Np floats
+                         (hi - lo + 255) // 256 * 256)
+                # rows per call: one internal pass (the in-epilogue selection holds ~0.3 MB per
+                # row at N = 1M instead of 4 Np bytes, so a pass takes many more rows)
+                cr = min(int(_lib.load().reidmi_rr_rank_rows_f16_pass_rows(self.N, Np, cc, self.K, -1)), hi - lo)
                 need = torch.empty(cr, device=self.dev, dtype=torch.int32)
                 idx = torch.empty(cr, device=self.dev, dtype=torch.int32)
                 cnt = torch.empty(1, device=self.dev, dtype=torch.int32)
@@ -204,7 +208,7 @@ class HipStages:
                               _lib.ptr(self.sqn), _lib.ptr(nrm), _lib.ptr(nmax2), _lib.ptr(x16), Np, Dp, a, b,
                               self.K,
                               _lib.ptr(R[a - lo:]), _lib.ptr(rmax[a - lo:]), _lib.ptr(need),
-                              _lib.ptr(self._chunk_buf(cr, Np)), cr, self.st)
+                              _lib.ptr(self._chunk_buf(cc, Np)), cc, self.st)
                     _lib.call("reidmi_nonzero_i32", _lib.ptr(need), b - a, _lib.ptr(idx), _lib.ptr(cnt), self.st)
                     undecided, rows = int(cnt.item()), b - a
                     self._exact_rows(a, idx, undecided, R[a - lo:b - lo], rmax[a - lo:b - lo])

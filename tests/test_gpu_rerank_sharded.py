@@ -132,6 +132,79 @@ def test_rank_prefilter_bitexact(gpu, case):
     assert np.array_equal(mf.view(np.uint32), me.view(np.uint32))
 
 
+def _rank_rows_f16_direct(f, K, stride, chunk_rows):
+    """reidmi_rr_rank_rows_f16_ex over all rows with a given sample stride (0: the dense form):
+    (rank [N][K], rowmax [N], need [N]) as numpy; rows with need = 1 carry no output."""
+    from multimodal_reid_amd import _lib
+    N, D = f.shape
+    Np, Dp = (N + 255) // 256 * 256, (D + 63) // 64 * 64
+    sqn = torch.empty(N, device=f.device)  # the exact rows' squared norms (reranking.HipStages)
+    _lib.call("reidmi_row_sqnorm_f32", _lib.ptr(f), N, D, D, _lib.ptr(sqn), _lib.stream())
+    nrm = torch.sqrt(sqn)
+    x16 = torch.zeros((Np, Dp), dtype=torch.float16, device=f.device)
+    ok = torch.ones(1, dtype=torch.int32, device=f.device)
+    _lib.call("reidmi_rr_feat16", _lib.ptr(f), N, D, D, _lib.ptr(x16), Np, Dp, _lib.ptr(ok), _lib.stream())
+    nmax2 = torch.empty(2, device=f.device)
+    _lib.call("reidmi_rr_norm_max", _lib.ptr(sqn), _lib.ptr(nrm), N, _lib.ptr(nmax2), _lib.stream())
+    R = torch.full((N, K), -1, dtype=torch.int32, device=f.device)
+    rmax = torch.zeros(N, device=f.device)
+    need = torch.zeros(N, dtype=torch.int32, device=f.device)
+    chunk = torch.empty(chunk_rows * Np, device=f.device)
+    _lib.call("reidmi_rr_rank_rows_f16_ex", _lib.ptr(f), N, D, D, _lib.ptr(sqn), _lib.ptr(nrm), _lib.ptr(nmax2),
+              _lib.ptr(x16), Np, Dp, 0, N, K, _lib.ptr(R), _lib.ptr(rmax), _lib.ptr(need), _lib.ptr(chunk), chunk_rows,
+              stride, _lib.stream())
+    return R.cpu().numpy(), rmax.cpu().numpy(), need.cpu().numpy()
+
+
+@pytest.mark.parametrize("case", ["clustered", "sorted_ids", "near_dup", "tracklets", "large_norm", "gaussian_1792",
+                                  "concentrated"])
+def test_rank_prefilter_in_epilogue_bitexact(gpu, case):
+    """The in-epilogue selection (1/16 sample -> per-row thresholds -> EPI_RRSV survivor lists ->
+    rank_select_sv) equals the dense form (bounds written and streamed) and the exact rows bit
+    for bit on every row it decides, at N = 12 000-16 000 (the sampled form applies from
+    N ~ 4 096), several passes per call; 'sorted_ids' orders the items by identity so the
+    sample misses whole clusters (loose thresholds), 'near_dup' / 'tracklets' make long survivor
+    lists and dense ties, 'concentrated' sends every row to the exact path."""
+    from multimodal_reid_amd import _lib
+    r = np.random.default_rng(len(case) + 7)
+    if case in ("clustered", "sorted_ids"):
+        f = _feats(400, 11600, seed=9, ids=900)
+        if case == "sorted_ids":
+            qp, gp, _, _ = syn.labels(400, 11600, num_ids=900, num_cams=6, seed=9)
+            f = f[np.argsort(np.concatenate([qp, gp]), kind="stable")]
+    elif case == "near_dup":
+        base = r.standard_normal((300, 384)).astype(np.float32)
+        f = oracle.l2norm(np.repeat(base, 40, axis=0) + 1e-4 * r.standard_normal((12000, 384)).astype(np.float32))
+    elif case == "tracklets":
+        f = _feats(500, 13500, seed=11, dim=512, ids=1200, noise=2.0)
+        f = oracle.l2norm(f[::24].repeat(24, axis=0)[:14000] + 1e-3 * r.standard_normal((14000, 512)).astype(np.float32))
+    elif case == "large_norm":
+        f = (r.standard_normal((12500, 320)) * 40).astype(np.float32)
+    elif case == "gaussian_1792":
+        f = oracle.l2norm(r.standard_normal((16000, 1792)).astype(np.float32))
+    else:
+        f = oracle.l2norm(np.ones((12000, 512), np.float32) + 1e-3 * r.standard_normal((12000, 512)).astype(np.float32))
+    f = torch.from_numpy(np.ascontiguousarray(f)).to(gpu)
+    N, K = f.shape[0], 51
+    pass_rows = _lib.load().reidmi_rr_rank_rows_f16_pass_rows
+    assert int(pass_rows(N, (N + 255) // 256 * 256, 256, K, 16)) > 256  # several rows' lists per pass
+    assert int(pass_rows(N, (N + 255) // 256 * 256, 256, K, -1)) == 256  # the default: the dense form
+    Rs, ms, ns = _rank_rows_f16_direct(f, K, 16, 256)
+    Rd, md, nd = _rank_rows_f16_direct(f, K, 0, 256)
+    Re, me, _ = _rank_rows(f, 100, False, 4 * N * 300)
+    both = (ns == 0) & (nd == 0)
+    for R, m, need in ((Rs, ms, ns), (Rd, md, nd)):
+        ok = need == 0
+        assert np.array_equal(R[ok], Re[ok, :K])
+        assert np.array_equal(m[ok].view(np.uint32), me[ok].view(np.uint32))
+    assert np.array_equal(Rs[both], Rd[both])
+    if case == "concentrated":
+        assert ns.all() and nd.all()
+    elif case in ("clustered", "sorted_ids", "gaussian_1792", "large_norm"):
+        assert ns.mean() < 0.05, ns.mean()  # the sampled form decides the rows itself
+    print(f"{case}: sampled form decides {1 - ns.mean():.3f} of the rows, dense form {1 - nd.mean():.3f}")
+
+
 def _one_call(feat, Q, k1, k2, lam):
     """reidmi_rerank itself (N x N fp32 distance materialised), whatever N."""
     from multimodal_reid_amd import _lib, reranking
