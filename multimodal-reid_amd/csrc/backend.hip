@@ -793,8 +793,8 @@ __global__ __launch_bounds__(256) void rr_sample_kernel(const float* __restrict_
                                                         const float* __restrict__ sqn, const float* __restrict__ nrm,
                                                         const float* __restrict__ nmax2, int64_t row0, int K,
                                                         float c_rel, float c_abs, float c_d,
-                                                        float4* __restrict__ thr, int32_t* __restrict__ cnt,
-                                                        int cap) {
+                                                        float4* __restrict__ meta, float* __restrict__ wrow,
+                                                        int32_t* __restrict__ cnt, int cap) {
     __shared__ TkLds L;
     __shared__ float red[4];
     const int64_t r = blockIdx.x, i = row0 + r;
@@ -817,14 +817,15 @@ __global__ __launch_bounds__(256) void rr_sample_kernel(const float* __restrict_
         // lo = fl(hi - w) is <= thr(U) (the widening covers the roundings of hi - w and of T + w)
         const float T = U + fabsf(U) * 0x1p-21f + 1e-37f;
         const float hmax = (T + w) + (fabsf(T) + w) * 0x1p-20f + 1e-37f;
-        thr[r] = make_float4(hmax, mx - w, w, 0.0f);
+        meta[r] = make_float4(sqn[i], nrm[i], hmax, mx - w);  // the survivor epilogue's row record
+        wrow[r] = w;
         cnt[r] = ok ? 0 : cap + 1;
     }
 }
 
 __global__ __launch_bounds__(256) void rank_select_sv_kernel(const int32_t* __restrict__ cnt,
                                                              const int2* __restrict__ list, int cap,
-                                                             const float4* __restrict__ thr,
+                                                             const float* __restrict__ wrow,
                                                              const float* __restrict__ feat, int64_t ldf, int D,
                                                              const float* __restrict__ sqn, int64_t row0, int K,
                                                              int32_t* __restrict__ rank_out,
@@ -860,7 +861,7 @@ __global__ __launch_bounds__(256) void rank_select_sv_kernel(const int32_t* __re
         return;
     }
     bitonic_sort_kv(sv, si, P);  // ascending (hi, index)
-    const float w = thr[r].z;
+    const float w = wrow[r];
     const float tau = sv[K - 1];
     const float th = tau + fabsf(tau) * 0x1p-21f + 1e-37f;  // rank_select1's thr_of
     const float mlo = sv[n - 1] - w;                         // the row's largest lo
@@ -909,23 +910,24 @@ __global__ __launch_bounds__(256) void rank_select_sv_kernel(const int32_t* __re
 void rank_select_consts(int D, float c[3]);
 
 int rr_sample_launch(const float* hs, int64_t lds, int64_t ns, const float* sqn, const float* nrm, const float* nmax2,
-                     int64_t row0, int64_t rows, int K, int D, float4* thr, int32_t* cnt, int cap, hipStream_t s) {
+                     int64_t row0, int64_t rows, int K, int D, float4* meta, float* wrow, int32_t* cnt, int cap,
+                     hipStream_t s) {
     RM_REQUIRE(K >= 1 && K <= 64 && ns >= K && rows >= 0 && nmax2, "rr_sample: bad arguments");
     if (rows == 0) return OK;
     float c[3];
     rank_select_consts(D, c);
     hipLaunchKernelGGL(rr_sample_kernel, dim3((unsigned)rows), dim3(256), 0, s, hs, lds, ns, sqn, nrm, nmax2, row0, K,
-                       c[0], c[1], c[2], thr, cnt, cap);
+                       c[0], c[1], c[2], meta, wrow, cnt, cap);
     RM_LAUNCHED();
     return OK;
 }
 
-int rank_select_sv_launch(const int32_t* cnt, const int2* list, int cap, const float4* thr, const float* feat,
+int rank_select_sv_launch(const int32_t* cnt, const int2* list, int cap, const float* wrow, const float* feat,
                           int64_t ldf, int D, const float* sqn, int64_t row0, int64_t rows, int K, int32_t* rank_out,
                           float* rowmax_out, int32_t* need, hipStream_t s) {
     RM_REQUIRE(K >= 1 && K <= 64 && cap >= 1 && cap <= RR_SV_CAP && rows >= 0, "rank_select_sv: bad arguments");
     if (rows == 0) return OK;
-    hipLaunchKernelGGL(rank_select_sv_kernel, dim3((unsigned)rows), dim3(256), 0, s, cnt, list, cap, thr, feat, ldf, D,
+    hipLaunchKernelGGL(rank_select_sv_kernel, dim3((unsigned)rows), dim3(256), 0, s, cnt, list, cap, wrow, feat, ldf, D,
                        sqn, row0, K, rank_out, rowmax_out, need);
     RM_LAUNCHED();
     return OK;

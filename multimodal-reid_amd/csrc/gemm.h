@@ -69,12 +69,21 @@ struct EpiArgs {
     float rr_c[3];
     const float* rr_csqn;  // the columns' squared norms / norms when they are not items 0..rr_n-1
     const float* rr_cnrm;  // (a sampled item set); null: rr_sqn / rr_nrm
-    // EPI_RRSV: per row m (rr_thr[m].x = hi_max: a pair with hi <= hi_max can be a candidate
-    // of the K smallest, .y = lb: a pair with hi >= lb can hold the row's largest distance), the
-    // survivor counters and lists [m * sv_cap + p] = (column, hi bits) of the pairs with
+    // EPI_RRSV: per row m the record rr_rowmeta[m] = (s_m, n_m, hi_max, lb) -- a pair with
+    // hi <= hi_max can be a candidate of the K smallest, a pair with hi >= lb can hold the row's
+    // largest distance -- padded to whole 256-row tiles; per column c < Np the record
+    // rr_colrec[c] = (s_c, n_c, hi_max, lb) (thresholds used with rr_tri only); the survivor
+    // counters and lists [m * sv_cap + p] = (column, hi bits) of the pairs with
     // !(hi_max < hi < lb) (a NaN survives); counts past sv_cap are kept (the row then takes the
-    // exact path).  (rr_thr[m].z = the row's bound width w, .w unused: rank_select_sv.)
-    const float4* rr_thr;
+    // exact path).  rr_tiles (optional): the tiles to run, (M-tile << 16 | N-tile), rr_ntiles
+    // of them; rr_tri: rows and columns are the same items (A = W), the list holds tiles with
+    // M-tile <= N-tile, and a tile above the diagonal also tests each pair as (column, row)
+    // against the column item's thresholds (its row of the symmetric product)
+    const float4* rr_rowmeta;
+    const float4* rr_colrec;
+    const int* rr_tiles;
+    int64_t rr_ntiles;
+    int rr_tri;
     int* sv_cnt;
     int2* sv_list;
     int sv_cap;
@@ -99,6 +108,7 @@ __device__ __forceinline__ float rr_hi(float dot, float si, float sj, float crn_
 struct GemmOpts {
     int tile = 0;
     int ngroups = 0;
+    int band = -1;  // persistent walk: M-tiles per band (0 = M-major, -1 = auto; gemm.hip tile_mn)
 };
 
 // Launch C = A . W^T with epilogue `epi`.  Requires N % 128 == 0, K % 64 == 0, lda/ldw

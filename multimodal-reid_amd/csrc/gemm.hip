@@ -13,6 +13,7 @@
 // holding one output row and 4 consecutive output columns: epilogue loads/stores are 8-16 B
 // per lane.
 #include "gemm.h"
+#include <type_traits>
 
 #include <mutex>
 #include <vector>
@@ -299,115 +300,6 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
         }
         return;
     }
-    if constexpr (EPI == EPI_RRSV) {
-        // survivors of the R2 pre-filter (gemm.h): per row group i, a lane's 16 candidate bits
-        // (hi overwrites the accumulator in place, so the pass that writes the pairs needs only
-        // acc), the row's count over its 4 lanes (lane groups q = lane >> 4 share a row), one
-        // atomic add per row for the wave's 64 columns (all row groups' atomics in flight
-        // together: one round trip per tile), then each lane writes its pairs at base + the
-        // exclusive prefix over the row's lanes
-        const int64_t n = ea.rr_n;
-        const int q = lane >> 4;
-        const float* csq = ea.rr_csqn ? ea.rr_csqn : ea.rr_sqn;
-        const float* cnr = ea.rr_cnrm ? ea.rr_cnrm : ea.rr_nrm;
-        // phase 1: the survivor bits (acc is left as it is: phase 2 recomputes hi).  A pair
-        // survives unless lb' < hi < hi_max' (rr_thr: x = hi_max', y = lb, gemm.h), so a NaN or
-        // infinite bound survives too and sends the row to the exact path (rank_select_sv).
-        float sj[4][4], nj[4][4];
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int64_t c0 = ncol + j * 16 + cq;
-            if (c0 + 3 < n) {
-                const float4 x = *(const float4*)(csq + c0), y = *(const float4*)(cnr + c0);
-                sj[j][0] = x.x, sj[j][1] = x.y, sj[j][2] = x.z, sj[j][3] = x.w;
-                nj[j][0] = y.x, nj[j][1] = y.y, nj[j][2] = y.z, nj[j][3] = y.w;
-            } else {
-#pragma unroll
-                for (int e = 0; e < 4; e++) {
-                    const int64_t c = c0 + e < n ? c0 + e : n - 1;
-                    sj[j][e] = csq[c];
-                    nj[j][e] = cnr[c];
-                }
-            }
-        }
-        uint32_t msk[NI];
-#pragma unroll
-        for (int i = 0; i < NI; i++) {
-            const int64_t m = mrow + i * 16 + (lane & 15);
-            const int64_t mm = m < M ? m : M - 1;
-            const float si = ea.rr_sqn[ea.rr_row0 + mm], ni = ea.rr_nrm[ea.rr_row0 + mm];
-            const float2 th = *(const float2*)(ea.rr_thr + mm);
-            uint32_t b = 0;
-#pragma unroll
-            for (int j = 0; j < 4; j++)
-#pragma unroll
-                for (int e = 0; e < 4; e++) {
-                    const float h = rr_hi(acc[i][j][e], si, sj[j][e], ea.rr_c[0] * ni, ni, nj[j][e], ea.rr_c);
-                    b |= (uint32_t)(m < M && ncol + j * 16 + cq + e < n && !(h > th.x && h < th.y)) << (j * 4 + e);
-                }
-            msk[i] = b;
-        }
-        bool any = false;
-#pragma unroll
-        for (int i = 0; i < NI; i++) any = any || msk[i] != 0;
-        if (!__builtin_amdgcn_ballot_w64(any)) return;  // (nearly every tile)
-        // phase 2 (rare: a tile with survivors): per row group, the row's count over its 4 lanes
-        // (inclusive prefix over lane groups q), one atomic add per row — all row groups'
-        // atomics issued before the first result is used (one round trip) — then each lane
-        // writes its pairs (column, hi bits) at base + its exclusive prefix
-        auto row_prefix = [&](int i, int& pre, int& tot) {
-            const int c = __builtin_popcount(msk[i]);
-            int s = c;
-            const int u1 = __shfl_up(s, 16, 64);
-            s += q >= 1 ? u1 : 0;
-            const int u2 = __shfl_up(s, 32, 64);
-            s += q >= 2 ? u2 : 0;
-            pre = s - c;
-            tot = __shfl(s, (lane & 15) + 48, 64);
-        };
-        // phase 1's column norms are not kept for this (rare) phase: opaque copies of the
-        // pointers keep the compiler from reusing them, which spilled the K-loop's registers
-        const float* csq2 = csq;
-        const float* cnr2 = cnr;
-        const float* rsq2 = ea.rr_sqn;
-        const float* rnr2 = ea.rr_nrm;
-        asm volatile("" : "+s"(csq2), "+s"(cnr2), "+s"(rsq2), "+s"(rnr2));
-        int base[NI];
-#pragma unroll
-        for (int i = 0; i < NI; i++) {
-            int pre, tot;
-            row_prefix(i, pre, tot);
-            const int add = tot;
-            const int64_t m = mrow + i * 16 + (lane & 15);
-            base[i] = 0;
-            if (q == 0 && add != 0) base[i] = atomicAdd(ea.sv_cnt + m, add);
-        }
-#pragma unroll
-        for (int i = 0; i < NI; i++) {
-            // one row group at a time: without the fence the scheduler hoists every group's
-            // addresses and loads, which spilled the K-loop's registers
-            __builtin_amdgcn_sched_barrier(0);
-            const int64_t m = mrow + i * 16 + (lane & 15);
-            int pre, tot;
-            row_prefix(i, pre, tot);
-            int p = __shfl(base[i], lane & 15, 64) + pre;
-            if (msk[i] == 0) continue;
-            const int64_t mm = m < M ? m : M - 1;
-            const float si = rsq2[ea.rr_row0 + mm], ni = rnr2[ea.rr_row0 + mm];
-            // static (j, e) walk: a run-time register index would go through scratch
-#pragma unroll
-            for (int j = 0; j < 4; j++)
-#pragma unroll
-                for (int e = 0; e < 4; e++)
-                    if ((msk[i] >> (j * 4 + e)) & 1u) {
-                        const int c = ncol + j * 16 + cq + e;
-                        const float h = rr_hi(acc[i][j][e], si, csq2[c], ea.rr_c[0] * ni, ni, cnr2[c], ea.rr_c);
-                        if (p < ea.sv_cap) ea.sv_list[m * ea.sv_cap + p] = make_int2(c, __builtin_bit_cast(int, h));
-                        p++;
-                    }
-        }
-        return;
-    }
     if constexpr (EPI == EPI_F32) {
 #pragma unroll
         for (int i = 0; i < NI; i++) {
@@ -649,6 +541,172 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 // inline ds_read (the compiler would insert a vmcnt(0) before a ds_read of an LDS-DMA'd
 // slot, draining the in-flight DMA every tile).  All tilings run the same MFMA chain per
 // output element -> bit-identical results.
+// ---- EPI_RRSV (the R2 pre-filter's survivors, gemm.h) in the persistent kernel.  Per row
+// group i and column group j a lane holds 4 pairs; their hi = rr_hi(acc) (packed fp32, the
+// same roundings as rr_hi) is compared with the row's thresholds, and the survivors are
+// appended to a per-wave buffer in LDS: 8-byte entries (tile sequence number << 13 | row in
+// the wave's 128 << 6 | column in its 64, bit 31 = the pair as (column, row); hi bits), lane
+// offsets from ballots.  The row and
+// column records (norms, thresholds) arrive by LDS-DMA at the tile's first K-step, into one
+// of two buffers by tile parity (a wave still reading tile t's records cannot be overtaken by
+// tile t+2's DMA: every wave passes tile t+1's barriers in between).  So the epilogue issues
+// no global memory instruction; a flush (one atomic add per entry on the row's counter, the
+// pair stored at the returned position) runs when the next (i, j) group could overflow the
+// buffer and once after the workgroup's last tile: typical tiles hold ~10 survivors per wave,
+// so the atomic round trip is paid every few dozen tiles, not per tile.
+// LDS, after the two operand stages: row records [2][256] float4 (8 KiB), column records
+// [2][256] float4 (8 KiB), survivor buffers [8 waves][kRrsvWaveCap] int2 (16 KiB).
+// A group's tile sequence t -> (M-tile, N-tile within the group): band = 0, M-major (t / tnk,
+// t % tnk); band > 0, bands of `band` M-tiles walked N-major, so the tiles one XCD runs at
+// once form a band x (32 / band) block and share both operands' panels in its L2 (the
+// re-rank's N x N products, where neither operand fits a cache; gemm_f16).
+template <bool LIST = false>
+__device__ __forceinline__ void tile_mn(int t, int tnk, int band, int tiles_m, const int* list, int& mt, int& nt) {
+    if constexpr (LIST) {  // EPI_RRSV's tile list (gemm.h rr_tiles)
+        // constant address space: a scalar load (lgkmcnt), not a vector load whose wait would
+        // drain the operand DMA in flight
+        const int v = ((const __attribute__((address_space(4))) int*)list)[t];
+        mt = v >> 16;
+        nt = v & 0xffff;
+        return;
+    }
+    if (band <= 0) {
+        mt = t / tnk;
+        nt = t - mt * tnk;
+        return;
+    }
+    const int per = band * tnk, b = t / per, r = t - b * per;
+    const int rows = tiles_m - b * band < band ? tiles_m - b * band : band;
+    nt = r / rows;
+    mt = b * band + (r - nt * rows);
+}
+
+#ifndef RR_GEMM_BAND
+#define RR_GEMM_BAND 8
+#endif
+constexpr int kRrsvWaveCap = 256;  // >= one (i, j) group: 16 rows x 16 columns
+constexpr int kRrsvSlotBytes = 8192 + 8192 + 8 * kRrsvWaveCap * 8;
+struct RrsvWalk {
+    int first, gx, wr, wc;  // the persistent walk (tile = first + seq * gx) over the tile list
+    const int* list;
+};
+
+__device__ __forceinline__ void rrsv_flush(const EpiArgs& ea, uint32_t sv_lds, int& sv_n, int lane,
+                                           const RrsvWalk& w) {
+    for (int t0 = 0; t0 < sv_n; t0 += 64) {
+        const int t = t0 + lane;
+        int2 e;
+        // inline ds_read: the compiler would wait for the operand DMA in flight (vmcnt(0))
+        // before a plain LDS read
+        asm volatile("ds_read_b64 %0, %1" : "=v"(e) : "v"(sv_lds + 8u * (uint32_t)(t < sv_n ? t : 0)) : "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(e)::"memory");
+        if (t < sv_n) {
+            int mt, nt;
+            tile_mn<true>(w.first + (int)(((uint32_t)e.x >> 13) & 0x3ffff) * w.gx, 1, 0, 0, w.list, mt, nt);
+            const int64_t mi = (int64_t)mt * 256 + w.wr * 128 + ((e.x >> 6) & 127);
+            const int ci = nt * 256 + w.wc * 64 + (e.x & 63);
+            const bool tr = e.x < 0;  // bit 31: the pair belongs to the column item's row
+            const int64_t m = tr ? ci : mi;
+            const int col = tr ? (int)mi : ci;
+            const int p = atomicAdd(ea.sv_cnt + m, 1);
+            if (p < ea.sv_cap) ea.sv_list[m * ea.sv_cap + p] = make_int2(col, e.y);
+        }
+    }
+    sv_n = 0;
+}
+
+// rows_lds / cols_lds: LDS byte addresses of this tile's record buffers (parity applied);
+// both: the tile is above the diagonal of a symmetric product (rr_tri), so each pair is also
+// tested as (column, row)
+__device__ __forceinline__ void rrsv_tile(const EpiArgs& ea, const f32x4 (&acc)[8][4], int64_t mrow, int ncol,
+                                          int64_t M, int seq, bool both, uint32_t rows_lds, uint32_t cols_lds,
+                                          uint32_t sv_lds, int& sv_n, int lane, const RrsvWalk& w) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const int64_t n = ea.rr_n;
+    const int cq = (lane >> 4) * 4;
+    const uint64_t below = (1ull << lane) - 1;
+    // appends the lane's pairs e with bit e of b: the group's total and the lanes' offsets
+    // from ballots (counts 0..4), a flush first when the buffer could overflow
+    auto append = [&](uint32_t b, int key, f32x4 h) {
+        const uint64_t v1 = __builtin_amdgcn_ballot_w64(b != 0);
+        if (v1 == 0) return;
+        const int c = __builtin_popcount(b);
+        const uint64_t v2 = __builtin_amdgcn_ballot_w64(c > 1), v3 = __builtin_amdgcn_ballot_w64(c > 2),
+                       v4 = __builtin_amdgcn_ballot_w64(c > 3);
+        const int tot = __builtin_popcountll(v1) + __builtin_popcountll(v2) + __builtin_popcountll(v3) +
+                        __builtin_popcountll(v4);
+        if (sv_n + tot > kRrsvWaveCap) rrsv_flush(ea, sv_lds, sv_n, lane, w);  // tot <= 256
+        int p = sv_n + __builtin_popcountll(v1 & below) + __builtin_popcountll(v2 & below) +
+                __builtin_popcountll(v3 & below) + __builtin_popcountll(v4 & below);
+        // the whole vector reinterpreted at once: a bit_cast of one element of a float vector
+        // read element 0 (hipcc 7.2)
+        typedef int i32x4 __attribute__((ext_vector_type(4)));
+        const i32x4 hb = __builtin_bit_cast(i32x4, h);
+#pragma unroll
+        for (int e = 0; e < 4; e++)
+            if ((b >> e) & 1u) {
+                const int2 ent = make_int2(key + e, hb[e]);
+                asm volatile("ds_write_b64 %0, %1" ::"v"(sv_lds + 8u * (uint32_t)p), "v"(ent) : "memory");
+                p++;
+            }
+        sv_n += tot;
+    };
+    const uint32_t ca = cols_lds + 16u * (uint32_t)(w.wc * 64 + cq);
+    const uint32_t ra = rows_lds + 16u * (uint32_t)(w.wr * 128 + (lane & 15));
+    // one sweep over the lane's pairs; TR: as (column, row) against the column item's
+    // thresholds.  Two separate loop nests (one sweep each): a single nest with both appends
+    // is too large to unroll, and the accumulators would go to scratch.
+    auto sweep = [&](auto tr_c) {
+        constexpr bool TR = decltype(tr_c)::value;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            // columns cq + 16 j + e: (s_c, n_c, hi_max_c, lb_c)
+            f32x4 cr[4];
+            const uint32_t caj = ca + 256u * j;
+            asm volatile("ds_read_b128 %0, %1" : "=v"(cr[0]) : "v"(caj) : "memory");
+            asm volatile("ds_read_b128 %0, %1 offset:16" : "=v"(cr[1]) : "v"(caj) : "memory");
+            asm volatile("ds_read_b128 %0, %1 offset:32" : "=v"(cr[2]) : "v"(caj) : "memory");
+            asm volatile("ds_read_b128 %0, %1 offset:48" : "=v"(cr[3]) : "v"(caj) : "memory");
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(cr[0]), "+v"(cr[1]), "+v"(cr[2]), "+v"(cr[3])::"memory");
+            const f2 sj0 = {cr[0][0], cr[1][0]}, sj1 = {cr[2][0], cr[3][0]};
+            const f2 nj0 = {cr[0][1], cr[1][1]}, nj1 = {cr[2][1], cr[3][1]};
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const int64_t m = mrow + i * 16 + (lane & 15);
+                f32x4 rm;  // (s_m, n_m, hi_max, lb)
+                asm volatile("ds_read_b128 %0, %1" : "=v"(rm) : "v"(ra + 256u * i) : "memory");
+                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(rm)::"memory");
+                const f2 si = {rm[0], rm[0]}, ni = {rm[1], rm[1]};
+                // hi of the pairs: rr_hi's operations on two lanes of packed fp32; as (column,
+                // row) it is rr_hi with the roles swapped (the product term c_rel n_c . n_m)
+                auto hi2 = [&](f2 sj, f2 nj, f2 dot) -> f2 {
+                    const f2 sum = si + sj;
+                    const f2 dt = __builtin_elementwise_fma(f2{-2.0f, -2.0f}, dot, sum);
+                    return TR ? dt + 1.01f * (__builtin_elementwise_fma(ea.rr_c[0] * nj, ni, 0x1p-23f * sum) +
+                                              ea.rr_c[1] * (nj + ni) + ea.rr_c[2])
+                              : dt + 1.01f * (__builtin_elementwise_fma(ea.rr_c[0] * ni, nj, 0x1p-23f * sum) +
+                                              ea.rr_c[1] * (ni + nj) + ea.rr_c[2]);
+                };
+                const f2 h01 = hi2(sj0, nj0, f2{acc[i][j][0], acc[i][j][1]});
+                const f2 h23 = hi2(sj1, nj1, f2{acc[i][j][2], acc[i][j][3]});
+                const f32x4 h = {h01.x, h01.y, h23.x, h23.y};
+                // a pair survives unless lb < hi < hi_max, so a NaN or infinite bound survives
+                // too and sends the row to the exact path (rank_select_sv)
+                uint32_t b = 0;
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    const float hx = TR ? cr[e][2] : rm[2], lb = TR ? cr[e][3] : rm[3];
+                    b |= (uint32_t)(m < M && ncol + j * 16 + cq + e < n && !(h[e] > hx && h[e] < lb)) << e;
+                }
+                const int key = (seq << 13) | ((i * 16 + (lane & 15)) << 6) | (j * 16 + cq);
+                append(b, TR ? key | (int)0x80000000u : key, h);
+            }
+        }
+    };
+    sweep(std::false_type{});
+    if (both) sweep(std::true_type{});
+}
+
 template <int EPI>
 struct EpiVm {  // vector-memory instructions of one full-tile epilogue_tile<EPI, 8> per wave
                 // (EPI_RRHI: its 32 stores; its norm loads complete before the first store)
@@ -661,7 +719,7 @@ template <int EPI>
 __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16* __restrict__ A, int64_t lda,
                                                                  const _Float16* __restrict__ W, int64_t ldw,
                                                                  int64_t M, int N, int K, EpiArgs ea, int tiles_m,
-                                                                 int tiles_n, int ngroups) {
+                                                                 int tiles_n, int ngroups, int band) {
     extern __shared__ __attribute__((aligned(16))) _Float16 lds[];
     const int G = gridDim.x;
     const int bid = blockIdx.x;
@@ -697,6 +755,8 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
             offA[h][u] = ra * GB_K;
             offW[h][u] = G2_M * GB_K + rb * GB_K;
         }
+    const int* const rr_list = EPI == EPI_RRSV ? ea.rr_tiles : nullptr;  // (gemm.h rr_tiles)
+    if constexpr (EPI != EPI_RRHI) band = 0;  // bands: the re-rank's dense product only
     // a DMA stream position: tile (m0, n0), K-step, and whether all 256 A rows exist
     struct Pos {
         int tile, kt;
@@ -707,8 +767,10 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
     auto set_tile = [&](Pos& p, int tile) {
         p.tile = tile;
         p.kt = 0;
-        p.m0 = (int64_t)(tile / tnk) * G2_M;
-        p.n0 = (nb0 + tile % tnk) * G2_N;
+        int mt, nt;
+        tile_mn<EPI == EPI_RRSV>(tile, tnk, band, tiles_m, rr_list, mt, nt);
+        p.m0 = (int64_t)mt * G2_M;
+        p.n0 = (nb0 + nt) * G2_N;
         p.full = p.m0 + G2_M <= M;
     };
     auto advance = [&](Pos& p) {
@@ -804,10 +866,18 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
     }
     __syncthreads();
     if (wr == 1) G5_BARRIER();
+    // EPI_RRSV (rrsv_tile): record buffers and the wave's survivor buffer after the stages
+    char* const rr_slot = (char*)(lds + 2 * G2_STAGE);
+    const uint32_t rr_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)rr_slot;
+    const uint32_t sv_lds = rr_lds + 8192 + 8192 + 8u * kRrsvWaveCap * (uint32_t)wid;
+    int sv_n = 0;  // wave-uniform
+    int seq = 0;   // tiles done by this workgroup
     int buf = 0;
     constexpr bool CAN_DEFER = EpiVm<EPI>::count > 0;
     bool deferred = false;  // the previous tile's epilogue stores may still be in flight
     for (int tile = first; tile < hi; tile += gx) {
+        int tmt, tnt;  // this tile's M-tile and N-tile (within the group)
+        tile_mn<EPI == EPI_RRSV>(tile, tnk, band, tiles_m, rr_list, tmt, tnt);
 #pragma unroll
         for (int i = 0; i < 8; i++)
 #pragma unroll
@@ -821,14 +891,27 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
             load_a(sA, 0);
             load_b(sW, 0);
             if (kt == 0 && has_bias)
-                __builtin_amdgcn_global_load_lds(ea.bias + (nb0 + tile % tnk) * G2_N + lane * 4, (lds_ptr_t)bias_slot,
+                __builtin_amdgcn_global_load_lds(ea.bias + (nb0 + tnt) * G2_N + lane * 4, (lds_ptr_t)bias_slot,
                                                  16, 0, 0);
             if (kt == 0 && fold) {
-                __builtin_amdgcn_global_load_lds(ea.colsum + (nb0 + tile % tnk) * G2_N + lane * 4, (lds_ptr_t)cs_slot,
+                __builtin_amdgcn_global_load_lds(ea.colsum + (nb0 + tnt) * G2_N + lane * 4, (lds_ptr_t)cs_slot,
                                                  16, 0, 0);
-                __builtin_amdgcn_global_load_lds((const float*)(ea.rowstat + (int64_t)(tile / tnk) * G2_M + wr * 128) +
+                __builtin_amdgcn_global_load_lds((const float*)(ea.rowstat + (int64_t)tmt * G2_M + wr * 128) +
                                                      lane * 4,
                                                  (lds_ptr_t)rs_slot, 16, 0, 0);
+            }
+            if constexpr (EPI == EPI_RRSV) {
+                // this tile's row / column records (rrsv_tile), one 1 KiB piece per wave
+                if (kt == 0) {
+                    const int par = seq & 1;
+                    if (wid < 4)
+                        __builtin_amdgcn_global_load_lds(ea.rr_rowmeta + (int64_t)tmt * G2_M + wid * 64 + lane,
+                                                         (lds_ptr_t)(rr_slot + par * 4096 + wid * 1024), 16, 0, 0);
+                    else
+                        __builtin_amdgcn_global_load_lds(ea.rr_colrec + (int64_t)(nb0 + tnt) * G2_N + (wid - 4) * 64 + lane,
+                                                         (lds_ptr_t)(rr_slot + 8192 + par * 4096 + (wid - 4) * 1024),
+                                                         16, 0, 0);
+                }
             }
             if (has1 && !b0_early) issue_w(buf ^ 1, 0, p1);
             G5_LDS_DONE();
@@ -884,8 +967,8 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
         // in the K-loop, waits here for group B's last COMPUTE; B catches up after it), so the
         // two groups' store tails overlap instead of running back to back
         if (wr == 0) G5_BARRIER();
-        const int64_t m0 = (int64_t)(tile / tnk) * G2_M;
-        const int n0 = (nb0 + tile % tnk) * G2_N;
+        const int64_t m0 = (int64_t)tmt * G2_M;
+        const int n0 = (nb0 + tnt) * G2_N;
         if constexpr (CAN_DEFER) {
             deferred = false;
             if (p1.tile < hi) {  // a next tile exists: issue its K-step 1 B0 (skipped in its LOAD 0)
@@ -948,9 +1031,17 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
                     acc[i][j][3] = __builtin_fmaf(rs[i].x, acc[i][j][3], __builtin_fmaf(rs[i].y, sn[j].w, b[j].w));
                 }
         }
-        epilogue_tile<EPI, 8, true>(ea, acc, m0 + wr * 128, n0 + wc * 64, M, N);
+        if constexpr (EPI == EPI_RRSV)
+            rrsv_tile(ea, acc, m0 + wr * 128, n0 + wc * 64, M, seq, ea.rr_tri && tmt < tnt, rr_lds + (seq & 1) * 4096,
+                      rr_lds + 8192 + (seq & 1) * 4096, sv_lds, sv_n, lane,
+                      RrsvWalk{first, gx, wr, wc, rr_list});
+        else
+            epilogue_tile<EPI, 8, true>(ea, acc, m0 + wr * 128, n0 + wc * 64, M, N);
+        seq++;
         if (wr == 1) G5_BARRIER();
     }
+    if constexpr (EPI == EPI_RRSV)
+        rrsv_flush(ea, sv_lds, sv_n, lane, RrsvWalk{first, gx, wr, wc, rr_list});
     if (wr == 0) G5_BARRIER();
 #undef G5_BARRIER
 #undef G5_LDS_DONE
@@ -959,13 +1050,20 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
 template <int EPI>
 static int launch(const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N, int64_t K,
                   const EpiArgs& ea, hipStream_t s, const GemmOpts& opt) {
-    const int64_t tiles256 = (int64_t)ceil_div(M, G2_M) * (N / G2_N);
+    const bool listed = EPI == EPI_RRSV;  // walks a tile list (gemm.h rr_tiles)
+    RM_REQUIRE(!listed || (ea.rr_tiles && ea.rr_ntiles > 0), "gemm: the survivor epilogue needs its tile list");
+    const int64_t tiles256 = listed ? ea.rr_ntiles : (int64_t)ceil_div(M, G2_M) * (N / G2_N);
     const bool fits = N % G2_N == 0 && K >= 2 * GB_K && lda * G2_M < (1ll << 31) && ldw * G2_N < (1ll << 31);
     if (fits && (opt.tile == 2 || (opt.tile == 0 && tiles256 >= 256))) {
-        const int tiles_m = ceil_div(M, G2_M), tiles_n = (int)(N / G2_N);
+        // a tile list is walked as tiles_m = its length x 1 N-tile, one XCD group
+        const int tiles_m = listed ? (int)tiles256 : ceil_div(M, G2_M), tiles_n = listed ? 1 : (int)(N / G2_N);
         RM_REQUIRE(tiles256 < (1ll << 31), "gemm: grid too large");
+        RM_REQUIRE(!listed || (ceil_div(M, G2_M) <= 65536 && N / G2_N <= 65536), "gemm: tile list: too many tiles");
+        RM_REQUIRE(EPI != EPI_RRSV || tiles256 / (tiles256 < 256 ? tiles256 : 256) < (1 << 18),
+                   "gemm: survivor epilogue: too many tiles per workgroup");
         // two operand stages + bias / colsum / rowstat slots (8 waves x 1 KiB each)
-        const size_t lds = 2 * (size_t)G2_STAGE * 2 + 3 * 8 * 256 * sizeof(float);
+        // (EPI_RRSV: its record and survivor buffers instead, rrsv_tile)
+        const size_t lds = 2 * (size_t)G2_STAGE * 2 + (EPI == EPI_RRSV ? kRrsvSlotBytes : 3 * 8 * 256 * sizeof(float));
         static bool attr = false;
         if (!attr) {
             RM_CHECK_HIP(hipFuncSetAttribute((const void*)gemm_persistent_kernel<EPI>,
@@ -976,12 +1074,21 @@ static int launch(const void* A, int64_t lda, const void* W, int64_t ldw, int64_
         // XCD N-groups: auto = 2 when the N-tiles split evenly and there are >= 8 of them
         // (c_fc: 12 tiles, +2 %, 15 % less L2 fetch; an uneven split idles the XCDs of the
         // smaller group), else 1 (profiles/r02/walk_ab.txt)
-        const int ngroups = opt.ngroups > 0 ? opt.ngroups : (tiles_n % 2 == 0 && tiles_n >= 8 ? 2 : 1);
+        const int ngroups =
+            listed ? 1 : opt.ngroups > 0 ? opt.ngroups : (tiles_n % 2 == 0 && tiles_n >= 8 ? 2 : 1);
+        // bands of M-tiles: auto = 8 for the re-rank's dense N x N product (both operands
+        // stream from HBM; the survivor epilogue's tile list is in band order too), else
+        // M-major (the encoder's weights stay in L2 / MALL)
+        const int band = EPI != EPI_RRHI ? 0 : opt.band >= 0 ? opt.band : RR_GEMM_BAND;
         hipLaunchKernelGGL((gemm_persistent_kernel<EPI>), dim3((unsigned)grid), dim3(512), lds, s, (const _Float16*)A,
-                           lda, (const _Float16*)W, ldw, M, (int)N, (int)K, ea, tiles_m, tiles_n, ngroups);
+                           lda, (const _Float16*)W, ldw, M, (int)N, (int)K, ea, tiles_m, tiles_n, ngroups, band);
         RM_LAUNCHED();
         return OK;
     }
+    if constexpr (EPI == EPI_RRSV) {
+        return fail(EINVAL_, "gemm: the survivor epilogue runs on the persistent 256 x 256 tile only "
+                             "(N % 256 == 0, K >= 128, >= 256 tiles)");
+    } else {
     const int tiles_m = ceil_div(M, GB_M), tiles_n = (int)(N / GB_N);
     const int64_t nwg = (int64_t)tiles_m * tiles_n;
     RM_REQUIRE(nwg < (1ll << 31), "gemm: grid too large");
@@ -989,11 +1096,13 @@ static int launch(const void* A, int64_t lda, const void* W, int64_t ldw, int64_
                        (const _Float16*)W, ldw, M, (int)N, (int)K, ea, tiles_n, (int)nwg);
     RM_LAUNCHED();
     return OK;
+    }
 }
 
 int gemm_f16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N, int64_t K,
              const EpiArgs& ea, hipStream_t s, const GemmOpts& opt) {
     RM_REQUIRE(opt.tile >= 0 && opt.tile <= 2, "gemm tile: 0 auto, 1 128x128, 2 persistent 256x256");
+    RM_REQUIRE(opt.band >= -1 && opt.band <= 64, "gemm walk: band in -1 (auto) .. 64");
     RM_REQUIRE(opt.ngroups == 0 || opt.ngroups == 1 || opt.ngroups == 2 || opt.ngroups == 4 || opt.ngroups == 8,
                "gemm walk: ngroups in {0 (auto), 1, 2, 4, 8}");
     RM_REQUIRE(M >= 0 && N > 0 && K > 0, "gemm: bad shape");

@@ -15,6 +15,7 @@
 // so memory is O(N * nnz) and every stage is a data-parallel kernel.
 // Arithmetic mirrors numpy exactly: float32 exp = numpy's AVX512F/AVX2 polynomial
 // (pinned against numpy 2.2.6), float32 pairwise sum, fp16 ufuncs = op in fp32 then RNE.
+#include <algorithm>
 #include "common.h"
 #include "gemm.h"
 
@@ -27,8 +28,9 @@ int rank_select_launch(float* dot, int64_t ldd, const float* feat, int64_t ldf, 
 void rank_select_consts(int D, float c[3]);
 int norm_max_launch(const float* sqn, const float* nrm, int64_t N, float* out2, hipStream_t s);
 int rr_sample_launch(const float* hs, int64_t lds, int64_t ns, const float* sqn, const float* nrm, const float* nmax2,
-                     int64_t row0, int64_t rows, int K, int D, float4* thr, int32_t* cnt, int cap, hipStream_t s);
-int rank_select_sv_launch(const int32_t* cnt, const int2* list, int cap, const float4* thr, const float* feat,
+                     int64_t row0, int64_t rows, int K, int D, float4* meta, float* wrow, int32_t* cnt, int cap,
+                     hipStream_t s);
+int rank_select_sv_launch(const int32_t* cnt, const int2* list, int cap, const float* wrow, const float* feat,
                           int64_t ldf, int D, const float* sqn, int64_t row0, int64_t rows, int K, int32_t* rank_out,
                           float* rowmax_out, int32_t* need, hipStream_t s);
 int feat16_launch(const float* x, int64_t N, int64_t D, int64_t ldx, void* y, int64_t Np, int64_t Dp,
@@ -1280,13 +1282,14 @@ REIDMI_API int reidmi_rr_norm_max(const float* sqn, const float* nrm, int64_t N,
 // Sampled survivor form of the pre-filter (backend.hip rr_sample_kernel / rank_select_sv_kernel):
 // the sample is every S-th item, ns = floor(N / S) rounded down to whole 256-column tiles; per
 // row: the sample's bounds, then the survivor list (RR_SV_CAP pairs) instead of an N-wide row.
-// Measured at N = 1.01 M (profiles/r03/rerank_1m_in_epilogue.txt): bit-identical, but the
-// EPI_RRSV GEMM took 13.0 s against 3.8 s for the dense form's GEMM + 1.7 s of streaming
-// selection -- every 256 x 256 tile holds survivors (~1 000 per row spread over 3 946 column
-// tiles), so the append phase (an atomic round trip per row group, and its registers next to
-// the accumulators spill the K-loop) runs in every tile.  The dense form stays the default
-// (RR_SAMPLE_STRIDE 0); reidmi_rr_rank_rows_f16_ex selects the sampled one.
-constexpr int RR_SAMPLE_STRIDE = 0, RR_SV_CAP_ = 4096;
+// The selection runs inside the GEMM's epilogue (gemm.hip rrsv_tile): survivors staged in LDS,
+// row / column records by LDS-DMA, no global memory instruction per tile.  A first version
+// appended straight to the rows' lists (an atomic round trip per row group and tile, its
+// registers spilling the K-loop): 13.0 s at N = 1.01 M against 3.9 + 1.7 s for the dense form
+// (profiles/r03/rerank_1m_in_epilogue.txt).  Staged in LDS: 3.7 s for all row passes; over
+// the symmetric product's upper triangle (each pair tested for both its rows, one call):
+// 1.98 s, the 1M re-rank 7.1 -> 4.3 s (profiles/r03/rerank_1m_triangle.txt).
+constexpr int RR_SAMPLE_STRIDE = 16, RR_SV_CAP_ = 4096;
 
 __global__ void rr_gather_norms_kernel(const float* __restrict__ sqn, const float* __restrict__ nrm, int64_t ns,
                                        int S, float* __restrict__ sqn_s, float* __restrict__ nrm_s) {
@@ -1297,17 +1300,84 @@ __global__ void rr_gather_norms_kernel(const float* __restrict__ sqn, const floa
     }
 }
 
-// bytes of chunk the sampled form needs: the sample's norms once, then per row the sample
-// bounds, the survivor list, its counter and thresholds
+// the survivor epilogue's column records (gemm.hip rrsv_tile) of the rectangular form: (squared
+// norm, norm, -, -) of item c, zero past N
+__global__ void rr_colrec_kernel(const float* __restrict__ sqn, const float* __restrict__ nrm, int64_t N, int64_t Np,
+                                 float4* __restrict__ out) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < Np) out[t] = t < N ? make_float4(sqn[t], nrm[t], 0.f, 0.f) : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+// The survivor GEMM's tile lists (gemm.h rr_tiles: M-tile << 16 | N-tile), bands of RR_BAND
+// M-tiles walked N-major (the 32 tiles an XCD runs at once share 8 A and 4 W panels).
+// Rectangular: tm x tn tiles.  Triangle (A = W, the whole symmetric product): the tiles with
+// M-tile <= N-tile; band b (rows r0 = b B .. r0 + r - 1) holds, for N-tile nt >= r0,
+// min(r, nt - r0 + 1) tiles.
+constexpr int RR_BAND = 8;
+__global__ void rr_rect_tiles_kernel(int tm, int tn, int* __restrict__ out) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (int64_t)tm * tn) return;
+    const int per = RR_BAND * tn, b = (int)(t / per), r = (int)(t - (int64_t)b * per);
+    const int rows = tm - b * RR_BAND < RR_BAND ? tm - b * RR_BAND : RR_BAND;
+    const int nt = r / rows, mt = b * RR_BAND + r - nt * rows;
+    out[t] = mt << 16 | nt;
+}
+
+__host__ __device__ inline int64_t rr_tri_band_count(int T, int b) {
+    const int64_t r0 = (int64_t)b * RR_BAND, r = T - r0 < RR_BAND ? T - r0 : RR_BAND;
+    return r * (r + 1) / 2 + (T - r0 - r) * r;
+}
+
+static int64_t rr_tri_tiles(int T) {
+    int64_t n = 0;
+    for (int b = 0; b * RR_BAND < T; b++) n += rr_tri_band_count(T, b);
+    return n;
+}
+
+__global__ void rr_tri_tiles_kernel(int T, int* __restrict__ out) {
+    const int b = blockIdx.x;
+    __shared__ int64_t s_off;
+    if (threadIdx.x == 0) {
+        int64_t o = 0;
+        for (int c = 0; c < b; c++) o += rr_tri_band_count(T, c);
+        s_off = o;
+    }
+    __syncthreads();
+    const int r0 = b * RR_BAND, r = T - r0 < RR_BAND ? T - r0 : RR_BAND;
+    for (int nt = r0 + threadIdx.x; nt < T; nt += blockDim.x) {
+        const int64_t k = nt - r0;
+        const int64_t pos = s_off + (k < r ? k * (k + 1) / 2 : (int64_t)r * (r + 1) / 2 + (k - r) * r);
+        const int c = k + 1 < r ? (int)k + 1 : r;
+        for (int q = 0; q < c; q++) out[pos + q] = (r0 + q) << 16 | nt;
+    }
+}
+
+// bytes of chunk the sampled form needs.  Rectangular (row passes): the column records, the
+// sample's norms and the pass's tile list once, then per row the sample bounds, the survivor
+// list, its counter, bound width and row record (the records padded to whole 256-row tiles:
+// the epilogue's DMA reads them by tile).  Triangle (all rows in one call): the records of all
+// items, the sample's norms, the tile list, the counters and widths, and the survivor lists of
+// all rows (the sample bounds of a pass of rows overlay the lists before they are written).
 static int64_t rr_sv_ns(int64_t N, int S) { return S >= 2 ? N / S / 256 * 256 : 0; }
-static int64_t rr_sv_row_bytes(int64_t ns) { return 4 * ns + 8 * (int64_t)RR_SV_CAP_ + 4 + 16; }
-// rows per pass of the sampled form in a chunk of chunk_rows x Np floats (0: not applicable)
+static int64_t rr_sv_row_bytes(int64_t ns) { return 4 * ns + 8 * (int64_t)RR_SV_CAP_ + 4 + 4 + 16; }
+// rows per pass of the rectangular form in a chunk of chunk_rows x Np floats (0: not applicable)
 static int64_t rr_sv_pass_rows(int64_t N, int64_t Np, int64_t chunk_rows, int K, int S) {
     const int64_t ns = rr_sv_ns(N, S);
     if (ns < 256 || ns < 4 * K) return 0;
-    const int64_t avail = chunk_rows * Np * 4 - 8 * ns - 64;
-    const int64_t r = avail / rr_sv_row_bytes(ns);
-    return r >= 64 ? (r < 65536 ? r : 65536) : 0;
+    // (the tile list of a pass of up to 65536 rows: 256 x Np / 256 ints = 4 Np bytes)
+    const int64_t avail = chunk_rows * Np * 4 - 16 * Np - 8 * ns - 4 * Np - 256 * 16 - 256;
+    int64_t r = avail / rr_sv_row_bytes(ns);
+    r = r < 65536 ? r : 65536;
+    return r >= 256 ? r / 256 * 256 : r >= 64 ? r : 0;  // whole 256-row tiles per pass when possible
+}
+// survivor capacity per row of the triangle form (0: not applicable: a list below 1024 pairs)
+static int64_t rr_tri_cap(int64_t N, int64_t Np, int64_t chunk_rows, int K, int S) {
+    const int64_t ns = rr_sv_ns(N, S);
+    if (ns < 256 || ns < 4 * K || Np / 256 > 65536) return 0;
+    const int64_t avail = chunk_rows * Np * 4 - 16 * Np - 8 * ns - 4 * rr_tri_tiles((int)(Np / 256)) - 8 * N - 1024;
+    int64_t cap = avail / (8 * N) / 64 * 64;
+    cap = cap < RR_SV_CAP_ ? cap : RR_SV_CAP_;
+    return cap >= 1024 && 8 * N * cap >= 4 * ns * 256 ? cap : 0;
 }
 
 static int rank_rows_f16(const float* feat, int64_t N, int64_t D, int64_t ldf, const float* sqn, const float* nrm,
@@ -1320,47 +1390,104 @@ static int rank_rows_f16(const float* feat, int64_t N, int64_t D, int64_t ldf, c
     RM_REQUIRE(N < 0x7fffffff, "rr_rank_rows_f16: too many items");
     const _Float16* x16 = (const _Float16*)feat16;
     int rc;
-    const int64_t pass = rr_sv_pass_rows(N, Np, chunk_rows, K, S);
-    if (pass > 0) {
-        const int64_t ns = rr_sv_ns(N, S);
-        float* sqn_s = chunk;
-        float* nrm_s = chunk + ns;
-        char* pbase = (char*)(chunk + 2 * ns);
+    // (the survivor epilogue needs K >= 2 K-steps of the persistent tile: Dp >= 128)
+    const bool sampled = Dp >= 128 && rr_sv_pass_rows(N, Np, chunk_rows, K, S) > 0;
+    const int64_t tcap = sampled && lo == 0 && hi == N ? rr_tri_cap(N, Np, chunk_rows, K, S) : 0;
+    GemmOpts persistent;
+    persistent.tile = 2;  // the survivor epilogue's LDS buffers live in the 256 x 256 tile
+    const int T = (int)(Np / 256);
+    // the sample's bounds of rows [a, a + nb) -> their records, widths and counters
+    auto sample = [&](float* hs, const float* sqn_s, const float* nrm_s, int64_t ns, int64_t a, int64_t nb,
+                      float4* meta, float* wrow, int32_t* cnt, int cap) -> int {
+        EpiArgs es{};
+        es.out = hs;
+        es.ldc = ns;
+        es.rr_sqn = sqn;
+        es.rr_nrm = nrm;
+        es.rr_csqn = sqn_s;
+        es.rr_cnrm = nrm_s;
+        es.rr_row0 = a;
+        es.rr_n = ns;
+        rank_select_consts((int)D, es.rr_c);
+        // the sample: W rows = every S-th item (row stride S * Dp)
+        int r = gemm_f16(EPI_RRHI, x16 + a * Dp, Dp, x16, (int64_t)S * Dp, nb, ns, Dp, es, s);
+        return r ? r : rr_sample_launch(hs, ns, ns, sqn, nrm, nmax2, a, nb, K, (int)D, meta, wrow, cnt, cap, s);
+    };
+    auto survivors = [&](int64_t a, int64_t M, const float4* rowmeta, const float4* colrec, const int* tiles,
+                         int64_t ntiles, bool tri, int32_t* cnt, int2* list, int cap) -> int {
+        EpiArgs ev{};
+        ev.rr_sqn = sqn;
+        ev.rr_nrm = nrm;
+        ev.rr_row0 = a;
+        ev.rr_n = N;
+        rank_select_consts((int)D, ev.rr_c);
+        ev.rr_rowmeta = rowmeta;
+        ev.rr_colrec = colrec;
+        ev.rr_tiles = tiles;
+        ev.rr_ntiles = ntiles;
+        ev.rr_tri = tri;
+        ev.sv_cnt = cnt;
+        ev.sv_list = list;
+        ev.sv_cap = cap;
+        return gemm_f16(EPI_RRSV, x16 + a * Dp, Dp, x16, Dp, M, Np, Dp, ev, s, persistent);
+    };
+    if (tcap > 0) {
+        // triangle: every pair once (tiles with M-tile <= N-tile), tested for both its rows
+        const int64_t ns = rr_sv_ns(N, S), ntri = rr_tri_tiles(T);
+        float4* meta = (float4*)chunk;  // [Np]: row records = column records
+        float* sqn_s = (float*)(meta + Np);
+        float* nrm_s = sqn_s + ns;
+        int* tiles = (int*)(nrm_s + ns);
+        int32_t* cnt = (int32_t*)(tiles + ntri);
+        float* wrow = (float*)(cnt + N);
+        int2* list = (int2*)(((uintptr_t)(wrow + N) + 15) & ~(uintptr_t)15);  // [N][tcap]
         hipLaunchKernelGGL(rr_gather_norms_kernel, dim3((unsigned)ceil_div(ns, 256)), dim3(256), 0, s, sqn, nrm, ns, S,
                            sqn_s, nrm_s);
         RM_LAUNCHED();
+        hipLaunchKernelGGL(rr_tri_tiles_kernel, dim3((unsigned)ceil_div(T, RR_BAND)), dim3(256), 0, s, T, tiles);
+        RM_LAUNCHED();
+        RM_CHECK_HIP(hipMemsetAsync(meta + N, 0, (Np - N) * sizeof(float4), s));
+        const int64_t sp = std::min<int64_t>(65536, 8 * N * tcap / (4 * ns) / 256 * 256);  // rows per sample pass
+        for (int64_t a = 0; a < N; a += sp) {
+            const int64_t nb = N - a < sp ? N - a : sp;
+            if ((rc = sample((float*)list, sqn_s, nrm_s, ns, a, nb, meta + a, wrow + a, cnt + a, (int)tcap))) return rc;
+        }
+        if ((rc = survivors(0, N, meta, meta, tiles, ntri, true, cnt, list, (int)tcap))) return rc;
+        return rank_select_sv_launch(cnt, list, (int)tcap, wrow, feat, ldf, (int)D, sqn, 0, N, K, rank_out, rowmax_out,
+                                     need, s);
+    }
+    if (sampled) {
+        const int64_t pass = rr_sv_pass_rows(N, Np, chunk_rows, K, S);
+        const int64_t ns = rr_sv_ns(N, S);
+        float4* colrec = (float4*)chunk;  // [Np]
+        float* sqn_s = (float*)(colrec + Np);
+        float* nrm_s = sqn_s + ns;
+        int* tiles = (int*)(nrm_s + ns);  // [pass / 256 (rounded up) x T]
+        char* pbase = (char*)(((uintptr_t)(tiles + ceil_div(pass, 256) * (int64_t)T) + 15) & ~(uintptr_t)15);
+        hipLaunchKernelGGL(rr_gather_norms_kernel, dim3((unsigned)ceil_div(ns, 256)), dim3(256), 0, s, sqn, nrm, ns, S,
+                           sqn_s, nrm_s);
+        RM_LAUNCHED();
+        hipLaunchKernelGGL(rr_colrec_kernel, dim3((unsigned)ceil_div(Np, 256)), dim3(256), 0, s, sqn, nrm, N, Np,
+                           colrec);
+        RM_LAUNCHED();
+        int tm_listed = -1;
         for (int64_t a = lo; a < hi; a += pass) {
             const int64_t nb = hi - a < pass ? hi - a : pass;
             float* hs = (float*)pbase;                                          // [nb][ns]
             int2* list = (int2*)(hs + nb * ns);                                 // [nb][cap]
             int32_t* cnt = (int32_t*)(list + nb * RR_SV_CAP_);                  // [nb]
-            float4* thr = (float4*)(((uintptr_t)(cnt + nb) + 15) & ~(uintptr_t)15);  // [nb]
-            EpiArgs es{};
-            es.out = hs;
-            es.ldc = ns;
-            es.rr_sqn = sqn;
-            es.rr_nrm = nrm;
-            es.rr_csqn = sqn_s;
-            es.rr_cnrm = nrm_s;
-            es.rr_row0 = a;
-            es.rr_n = ns;
-            rank_select_consts((int)D, es.rr_c);
-            // the sample: W rows = every S-th item (row stride S * Dp)
-            if ((rc = gemm_f16(EPI_RRHI, x16 + a * Dp, Dp, x16, (int64_t)S * Dp, nb, ns, Dp, es, s))) return rc;
-            if ((rc = rr_sample_launch(hs, ns, ns, sqn, nrm, nmax2, a, nb, K, (int)D, thr, cnt, RR_SV_CAP_, s)))
-                return rc;
-            EpiArgs ev{};
-            ev.rr_sqn = sqn;
-            ev.rr_nrm = nrm;
-            ev.rr_row0 = a;
-            ev.rr_n = N;
-            rank_select_consts((int)D, ev.rr_c);
-            ev.rr_thr = thr;
-            ev.sv_cnt = cnt;
-            ev.sv_list = list;
-            ev.sv_cap = RR_SV_CAP_;
-            if ((rc = gemm_f16(EPI_RRSV, x16 + a * Dp, Dp, x16, Dp, nb, Np, Dp, ev, s))) return rc;
-            if ((rc = rank_select_sv_launch(cnt, list, RR_SV_CAP_, thr, feat, ldf, (int)D, sqn, a, nb, K,
+            float* wrow = (float*)(cnt + nb);                                   // [nb]
+            float4* meta = (float4*)(((uintptr_t)(wrow + nb) + 15) & ~(uintptr_t)15);  // [nb, padded to 256]
+            const int tm = (int)ceil_div(nb, 256);
+            if (tm != tm_listed) {
+                hipLaunchKernelGGL(rr_rect_tiles_kernel, dim3((unsigned)ceil_div((int64_t)tm * T, 256)), dim3(256), 0, s,
+                                   tm, T, tiles);
+                RM_LAUNCHED();
+                tm_listed = tm;
+            }
+            if ((rc = sample(hs, sqn_s, nrm_s, ns, a, nb, meta, wrow, cnt, RR_SV_CAP_))) return rc;
+            if ((rc = survivors(a, nb, meta, colrec, tiles, (int64_t)tm * T, false, cnt, list, RR_SV_CAP_))) return rc;
+            if ((rc = rank_select_sv_launch(cnt, list, RR_SV_CAP_, wrow, feat, ldf, (int)D, sqn, a, nb, K,
                                             rank_out + (a - lo) * K, rowmax_out + (a - lo), need + (a - lo), s)))
                 return rc;
         }
@@ -1419,7 +1546,9 @@ REIDMI_API int reidmi_rr_rank_rows_f16_ex(const float* feat, int64_t N, int64_t 
 REIDMI_API int64_t reidmi_rr_rank_rows_f16_pass_rows(int64_t N, int64_t Np, int64_t chunk_rows, int K,
                                                      int sample_stride) {
     if (N <= 0 || Np < N || chunk_rows <= 0 || K < 1) return -1;
-    const int64_t p = rr_sv_pass_rows(N, Np, chunk_rows, K, sample_stride < 0 ? RR_SAMPLE_STRIDE : sample_stride);
+    const int S = sample_stride < 0 ? RR_SAMPLE_STRIDE : sample_stride;
+    if (rr_tri_cap(N, Np, chunk_rows, K, S) > 0) return N;  // one call over all rows: the triangle form
+    const int64_t p = rr_sv_pass_rows(N, Np, chunk_rows, K, S);
     return p > 0 ? p : chunk_rows;
 }
 

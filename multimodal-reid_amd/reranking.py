@@ -195,14 +195,20 @@ class HipStages:
                 cc = min(max(256, self.chunk_rows * self.N // Np // 256 * 256),  # chunk rows of Np floats
                          (hi - lo + 255) // 256 * 256)
                 # rows per call: one internal pass (the in-epilogue selection holds ~0.3 MB per
-                # row at N = 1M instead of 4 Np bytes, so a pass takes many more rows)
-                cr = min(int(_lib.load().reidmi_rr_rank_rows_f16_pass_rows(self.N, Np, cc, self.K, -1)), hi - lo)
+                # row at N = 1M instead of 4 Np bytes, so a pass takes many more rows); N: the
+                # whole problem in one call (the symmetric product's upper triangle, each pair
+                # tested for both its rows), after the probe pass
+                cr = int(_lib.load().reidmi_rr_rank_rows_f16_pass_rows(self.N, Np, cc, self.K, -1))
+                tri = cr >= self.N and lo == 0 and hi == self.N
+                cr = min(cr, hi - lo)
                 need = torch.empty(cr, device=self.dev, dtype=torch.int32)
                 idx = torch.empty(cr, device=self.dev, dtype=torch.int32)
                 cnt = torch.empty(1, device=self.dev, dtype=torch.int32)
                 first = True
                 while a < hi:
                     b = min(a + (min(cr, 512) if first else cr), hi)  # a small probe pass first
+                    if tri and not first:
+                        a, b = 0, hi  # the triangle form takes all rows (the probe's again)
                     first = False
                     _lib.call("reidmi_rr_rank_rows_f16", _lib.ptr(self.feat), self.N, self.D, self.D,
                               _lib.ptr(self.sqn), _lib.ptr(nrm), _lib.ptr(nmax2), _lib.ptr(x16), Np, Dp, a, b,

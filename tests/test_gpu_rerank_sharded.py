@@ -160,9 +160,10 @@ def _rank_rows_f16_direct(f, K, stride, chunk_rows):
                                   "concentrated"])
 def test_rank_prefilter_in_epilogue_bitexact(gpu, case):
     """The in-epilogue selection (1/16 sample -> per-row thresholds -> EPI_RRSV survivor lists ->
-    rank_select_sv) equals the dense form (bounds written and streamed) and the exact rows bit
-    for bit on every row it decides, at N = 12 000-16 000 (the sampled form applies from
-    N ~ 4 096), several passes per call; 'sorted_ids' orders the items by identity so the
+    rank_select_sv), in row passes (rectangular) and in one call over the symmetric product's
+    upper triangle (each pair tested for both its rows), equals the dense form (bounds written
+    and streamed) and the exact rows bit for bit on every row it decides, at N = 12 000-16 000
+    (the sampled form applies from N ~ 4 096); 'sorted_ids' orders the items by identity so the
     sample misses whole clusters (loose thresholds), 'near_dup' / 'tracklets' make long survivor
     lists and dense ties, 'concentrated' sends every row to the exact path."""
     from multimodal_reid_amd import _lib
@@ -187,22 +188,24 @@ def test_rank_prefilter_in_epilogue_bitexact(gpu, case):
     f = torch.from_numpy(np.ascontiguousarray(f)).to(gpu)
     N, K = f.shape[0], 51
     pass_rows = _lib.load().reidmi_rr_rank_rows_f16_pass_rows
-    assert int(pass_rows(N, (N + 255) // 256 * 256, 256, K, 16)) > 256  # several rows' lists per pass
-    assert int(pass_rows(N, (N + 255) // 256 * 256, 256, K, -1)) == 256  # the default: the dense form
+    Np = (N + 255) // 256 * 256
+    assert 256 <= int(pass_rows(N, Np, 256, K, 16)) < N  # rectangular: row passes (whole 256-row tiles)
+    assert int(pass_rows(N, Np, 4096, K, 16)) == N  # the triangle form: all rows in one call
+    assert int(pass_rows(N, Np, 256, K, 0)) == 256  # the dense form: chunk_rows
     Rs, ms, ns = _rank_rows_f16_direct(f, K, 16, 256)
+    Rt, mt, nt = _rank_rows_f16_direct(f, K, 16, 4096)
     Rd, md, nd = _rank_rows_f16_direct(f, K, 0, 256)
     Re, me, _ = _rank_rows(f, 100, False, 4 * N * 300)
-    both = (ns == 0) & (nd == 0)
-    for R, m, need in ((Rs, ms, ns), (Rd, md, nd)):
+    for R, m, need in ((Rs, ms, ns), (Rt, mt, nt), (Rd, md, nd)):
         ok = need == 0
         assert np.array_equal(R[ok], Re[ok, :K])
         assert np.array_equal(m[ok].view(np.uint32), me[ok].view(np.uint32))
-    assert np.array_equal(Rs[both], Rd[both])
     if case == "concentrated":
-        assert ns.all() and nd.all()
+        assert ns.all() and nt.all() and nd.all()
     elif case in ("clustered", "sorted_ids", "gaussian_1792", "large_norm"):
-        assert ns.mean() < 0.05, ns.mean()  # the sampled form decides the rows itself
-    print(f"{case}: sampled form decides {1 - ns.mean():.3f} of the rows, dense form {1 - nd.mean():.3f}")
+        assert ns.mean() < 0.05 and nt.mean() < 0.05, (ns.mean(), nt.mean())  # the sampled forms decide the rows
+    print(f"{case}: sampled form decides {1 - ns.mean():.3f} of the rows (triangle {1 - nt.mean():.3f}), "
+          f"dense form {1 - nd.mean():.3f}")
 
 
 def _one_call(feat, Q, k1, k2, lam):
