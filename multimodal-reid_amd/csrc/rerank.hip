@@ -96,7 +96,7 @@ static RrCaps rr_caps(int64_t N, int k1, int k2) {
     c.vcap = vb < N ? vb : N;
     c.tcap = (int64_t)c.k2e * c.vcap;
     c.qcap = c.tcap < N ? c.tcap : N;
-    c.kr_fast = c.kf <= 64 && vb <= KR_LST;
+    c.kr_fast = c.kf <= 64 && c.kh1 <= 32 && vb <= KR_LST;  // (kreciprocal_kernel's masks)
     return c;
 }
 
@@ -306,21 +306,37 @@ __device__ __forceinline__ int pow2_ceil_i(int n) {
     return p;
 }
 
+// v in R[row][0, kk): every load issued before any compare (no early exit: the loads of a
+// scan are independent, so they share one memory round trip per unrolled group)
+__device__ __forceinline__ bool row_has_all(const int32_t* R, int64_t ldr, int32_t row, int kk, int32_t v) {
+    const int32_t* p = R + (int64_t)row * ldr;
+    bool hit = false;
+#pragma unroll 16
+    for (int b = 0; b < kk; b++) hit |= p[b] == v;
+    return hit;
+}
+
 // One 256-thread workgroup per row i = row0 + blockIdx.x of od (output row blockIdx.x).
-// R: initial_rank [N][ldr] (stable argsort prefix), rowdiv[N] the od divisors.
+// R: initial_rank [N][ldr] (stable argsort prefix), rowdiv[N] the od divisors.  kf <= 64,
+// kh1 <= 32 (rr_caps kr_fast).  The membership scans are spread over the workgroup: one
+// (candidate a, depth f) pair per thread for the expansion's half-depth sets (bit f of a
+// per-candidate mask), instead of one thread walking a's 26 x 26 scans one load at a time.
 __global__ __launch_bounds__(256) void kreciprocal_kernel(DistSrc ds, const float* __restrict__ rowdiv,
                                                           const int32_t* __restrict__ R, int64_t ldr, int64_t row0,
                                                           int kf, int kh1, int32_t* __restrict__ vcol,
                                                           uint16_t* __restrict__ vval, int32_t* __restrict__ vnnz,
                                                           int64_t vcap, int32_t* __restrict__ flags) {
     __shared__ int32_t kr[64];
+    __shared__ int32_t cand[64][32];          // R[a][f] of the k-reciprocal items a
+    __shared__ uint32_t mpass[64], minkr[64];  // bit f: a in R[R[a][f]][:kh1]; and R[a][f] in kr
     __shared__ int32_t lst[KR_LST];
     __shared__ float w[KR_LST];
+    __shared__ int wsum[4];
     __shared__ int s_nk, s_n, s_nu;
     __shared__ float s_sum;
     const int64_t b = blockIdx.x;
     const int64_t i = row0 + b;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     // k-reciprocal set of i at depth k1 (reranking.py:53-56), kept in forward order
     if (tid < 64) {
         const int f = tid;
@@ -328,35 +344,42 @@ __global__ __launch_bounds__(256) void kreciprocal_kernel(DistSrc ds, const floa
         int32_t c = -1;
         if (f < kf) {
             c = R[i * ldr + f];
-            keep = row_has(R, ldr, c, kf, (int32_t)i);
+            keep = row_has_all(R, ldr, c, kf, (int32_t)i);
         }
         const unsigned long long m = __ballot(keep);
         const int pos = __popcll(m & ((1ull << f) - 1ull));
         if (keep) kr[pos] = c;
         if (f == 0) s_nk = __popcll(m);
+        mpass[f] = 0;
+        minkr[f] = 0;
     }
     __syncthreads();
     const int nk = s_nk;
     for (int t = tid; t < nk; t += blockDim.x) lst[t] = kr[t];
     if (tid == 0) s_n = nk;
-    __syncthreads();
-    // expansion (reranking.py:57-65): candidate a's half-depth reciprocal set is appended when
-    // |set ∩ k_reciprocal| > 2/3 |set|; order is irrelevant (np.unique sorts)
-    if (tid < nk) {
-        const int32_t a = kr[tid];
-        int32_t cset[64];
-        int nc = 0;
-        for (int f = 0; f < kh1; f++) {
-            const int32_t c = R[(int64_t)a * ldr + f];
-            if (row_has(R, ldr, c, kh1, a)) cset[nc++] = c;
+    // expansion (reranking.py:57-65): candidate a's half-depth reciprocal set
+    // {c = R[a][f], f < kh1 : a in R[c][:kh1]} is appended when more than 2/3 of it lies in the
+    // k-reciprocal set; order is irrelevant (np.unique sorts)
+    for (int p = tid; p < nk * kh1; p += blockDim.x) {
+        const int ai = p / kh1, f = p - ai * kh1;
+        const int32_t a = kr[ai];
+        const int32_t c = R[(int64_t)a * ldr + f];
+        cand[ai][f] = c;
+        if (row_has_all(R, ldr, c, kh1, a)) {
+            bool in = false;
+            for (int q = 0; q < nk; q++) in |= kr[q] == c;
+            atomicOr(&mpass[ai], 1u << f);
+            if (in) atomicOr(&minkr[ai], 1u << f);
         }
-        int inter = 0;
-        for (int q = 0; q < nc; q++)
-            for (int c = 0; c < nk; c++)
-                if (cset[q] == kr[c]) { inter++; break; }
+    }
+    __syncthreads();
+    if (tid < nk) {
+        const uint32_t mp = mpass[tid];
+        const int nc = __popc(mp), inter = __popc(minkr[tid]);
         if ((double)inter > 2.0 / 3.0 * (double)nc) {
-            const int base = atomicAdd(&s_n, nc);
-            for (int q = 0; q < nc; q++) lst[base + q] = cset[q];
+            int q = atomicAdd(&s_n, nc);
+            for (int f = 0; f < kh1; f++)
+                if ((mp >> f) & 1u) lst[q++] = cand[tid][f];
         }
     }
     __syncthreads();
@@ -365,14 +388,31 @@ __global__ __launch_bounds__(256) void kreciprocal_kernel(DistSrc ds, const floa
     for (int t = n + tid; t < P; t += blockDim.x) lst[t] = 0x7fffffff;
     __syncthreads();
     bitonic_sort_i32(lst, P);
-    // unique (np.unique) by one thread, weights, pairwise sum
-    if (tid == 0) {
-        int nu = 0;
-        for (int t = 0; t < n; t++)
-            if (nu == 0 || lst[t] != lst[nu - 1]) lst[nu++] = lst[t];
-        s_nu = nu;
+    // unique (np.unique): thread t owns a contiguous segment, counts its first occurrences,
+    // and writes them at the exclusive prefix of the counts (into w's storage, then back)
+    {
+        const int seg = (n + 255) >> 8, s0 = tid * seg, s1 = s0 + seg < n ? s0 + seg : n;
+        int cnt = 0;
+        for (int t = s0; t < s1; t++) cnt += (t == 0 || lst[t] != lst[t - 1]);
+        int incl = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int u = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += u;
+        }
+        if (lane == 63) wsum[wv] = incl;
+        __syncthreads();
+        int pos = incl - cnt;
+        for (int q = 0; q < wv; q++) pos += wsum[q];
+        int32_t* u = (int32_t*)w;
+        for (int t = s0; t < s1; t++)
+            if (t == 0 || lst[t] != lst[t - 1]) u[pos++] = lst[t];
+        if (tid == 255) s_nu = pos;  // (the last segment ends the list)
+        __syncthreads();
+        const int nu0 = s_nu;
+        for (int t = tid; t < nu0; t += blockDim.x) lst[t] = u[t];
+        __syncthreads();
     }
-    __syncthreads();
     const int nu = s_nu;
     const float dv = rowdiv[i];
     for (int t = tid; t < nu; t += blockDim.x) w[t] = np_expf(-(dist_at(ds, i, lst[t]) / dv));
