@@ -185,9 +185,11 @@ def rerank_leg(dev, cpu=True, threads=1):
     """configs[2]'s back end: DukeMTMC-size k-reciprocal re-rank (k1=50, k2=15, lambda=0.3;
     reranking.py:29-100, evaluate.py:124-132) + CMC/mAP on identity-clustered synthetic
     features, timed on its own after the Market steps (not part of `value`).
-    Roofline: the stage chain is bound by the exact-fp32 N x N distance GEMM (2 N^2 D FLOP on
-    the 157 TF/s fp32 matrix peak) — far above its HBM floor (4 N^2 distance bytes + 4 Q G
-    final bytes at 8 TB/s); frac = max(floors) / wall.  cpu_port: the C restatement on the
+    Roofline: the reference's formulation is bound by the exact-fp32 N x N distance GEMM
+    (2 N^2 D FLOP on the 157 TF/s fp32 matrix peak) — far above its HBM floor (4 N^2 distance
+    bytes + 4 Q G final bytes at 8 TB/s); frac = max(floors) / wall.  (N >= STAGED_MIN_N runs
+    the staged path, whose R2 goes through the fp16 pre-filter: fewer fp32 FLOPs than that
+    floor, the same bits.)  cpu_port: the C restatement on the
     full configuration, `threads` host threads."""
     from multimodal_reid_amd import reranking
     sp = syn.DATASET_SPLITS["dukemtmc"]
