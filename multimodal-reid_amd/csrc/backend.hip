@@ -16,13 +16,55 @@
 namespace reidmi {
 
 // --------------------------------------------------------------------------- norms
-__global__ void row_sqnorm_kernel(const float* __restrict__ x, int64_t n, int64_t d, int64_t ld,
-                                  float* __restrict__ out) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// 256 rows per 256-thread workgroup, one row's fmaf chain per thread (k ascending, the
+// distance kernel's arithmetic).  With 16-byte rows the row segments are staged through LDS
+// 32 columns at a time by coalesced float4 loads (the next segment in flight while the
+// current one is summed), instead of 256 threads each walking its own row (uncoalesced).
+constexpr int RSQ_K = 32;
+__global__ __launch_bounds__(256) void row_sqnorm_kernel(const float* __restrict__ x, int64_t n, int64_t d,
+                                                         int64_t ld, float* __restrict__ out) {
+    __shared__ float tile[256][RSQ_K + 1];
+    const int64_t r0 = (int64_t)blockIdx.x * 256, i = r0 + threadIdx.x;
+    if ((ld & 3) != 0 || ((uintptr_t)x & 15) != 0 || d < RSQ_K) {  // uniform
+        if (i >= n) return;
+        const float* r = x + i * ld;
+        float acc = 0.0f;
+        for (int64_t k = 0; k < d; k++) acc = __builtin_fmaf(r[k], r[k], acc);
+        out[i] = acc;
+        return;
+    }
+    // float4 f = threadIdx.x + 256 u of a segment: row f / 8, columns 4 (f % 8) .. + 3
+    constexpr int U = 256 * RSQ_K / 4 / 256;
+    float4 v[U];
+    auto load = [&](int64_t k0) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int f = threadIdx.x + 256 * u, row = f >> 3, c = (f & 7) * 4;
+            const int64_t gi = r0 + row < n ? r0 + row : n - 1;
+            v[u] = *(const float4*)(x + gi * ld + k0 + c);
+        }
+    };
+    const int64_t nk = d / RSQ_K;
+    float acc = 0.0f;
+    load(0);
+    for (int64_t kt = 0; kt < nk; kt++) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int f = threadIdx.x + 256 * u, row = f >> 3, c = (f & 7) * 4;
+            tile[row][c] = v[u].x;
+            tile[row][c + 1] = v[u].y;
+            tile[row][c + 2] = v[u].z;
+            tile[row][c + 3] = v[u].w;
+        }
+        __syncthreads();
+        if (kt + 1 < nk) load((kt + 1) * RSQ_K);
+#pragma unroll
+        for (int k = 0; k < RSQ_K; k++) acc = __builtin_fmaf(tile[threadIdx.x][k], tile[threadIdx.x][k], acc);
+        __syncthreads();
+    }
     if (i >= n) return;
     const float* r = x + i * ld;
-    float acc = 0.0f;
-    for (int64_t k = 0; k < d; k++) acc = __builtin_fmaf(r[k], r[k], acc);
+    for (int64_t k = nk * RSQ_K; k < d; k++) acc = __builtin_fmaf(r[k], r[k], acc);
     out[i] = acc;
 }
 
@@ -117,6 +159,9 @@ __global__ __launch_bounds__(256) void distmat_f32_kernel(
 #ifndef DM2_MINWG_
 #define DM2_MINWG_ 4
 #endif
+#ifndef DM2_BAND
+#define DM2_BAND 4
+#endif
 constexpr int DM2_BK = DM2_BK_, DM2_LD = DM_BM + 1;
 constexpr int DM2_F4 = DM2_BK / 4;            // float4 per operand row and K-step
 constexpr int DM2_U = DM_BM * DM2_F4 / 256;   // float4 staging slots per thread and operand
@@ -148,6 +193,13 @@ __global__ __launch_bounds__(256, DM2_MINWG_) void distmat2_f32_kernel(
         while (tn * (tn + 1) / 2 > wg) tn--;
         bm = (wg - tn * (tn + 1) / 2) * DM_BM;
         bn = tn * DM_BN;
+    } else if (DM2_BAND > 0 && tiles_m > DM2_BAND) {
+        // bands of DM2_BAND row tiles walked column-major: the tiles an XCD runs at once
+        // form a DM2_BAND x (32 / DM2_BAND) block, so their output rows are few and long
+        const int64_t per = (int64_t)DM2_BAND * ((G + DM_BN - 1) / DM_BN), band = wg / per, r = wg - band * per;
+        const int64_t rows = tiles_m - band * DM2_BAND < DM2_BAND ? tiles_m - band * DM2_BAND : DM2_BAND;
+        bm = (band * DM2_BAND + r % rows) * DM_BM;
+        bn = (r / rows) * DM_BN;
     } else {
         bm = (wg % tiles_m) * DM_BM;
         bn = (wg / tiles_m) * DM_BN;

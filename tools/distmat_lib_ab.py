@@ -21,7 +21,8 @@ def main():
     libs = [(os.path.basename(p), open_lib(p)) for p in sys.argv[1].split(",")]
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 3
     dev = torch.device("cuda")
-    shapes = [("market", 3368, 15913, 1280), ("msmt17", 11659, 82161, 1280), ("rr-chunk", 5592, 93820, 1280)]
+    shapes = [("market", 3368, 15913, 1280), ("msmt17", 11659, 82161, 1280), ("rr-chunk", 5592, 93820, 1280),
+              ("1m-gallery", 4096, 1000000, 768)]
     data = []
     for name, Q, G, D in shapes:
         g = torch.Generator(device=dev).manual_seed(Q)
