@@ -30,7 +30,8 @@ def test_l2norm_bitexact(gpu):
     assert np.array_equal(y.view(np.uint32), oracle.l2norm(x).view(np.uint32))
 
 
-@pytest.mark.parametrize("Q,G,D", [(100, 500, 1280), (37, 259, 768), (1, 1, 2), (130, 129, 1792), (5, 300, 513)])
+@pytest.mark.parametrize("Q,G,D", [(100, 500, 1280), (37, 259, 768), (1, 1, 2), (130, 129, 1792), (5, 300, 513),
+                                   (300, 700, 100), (1200, 257, 36)])  # row-norm tails; banded walk, partial band
 def test_distmat_bitexact(gpu, Q, G, D):
     r = np.random.default_rng(Q * 7 + G)
     q = r.standard_normal((Q, D)).astype(np.float32)
