@@ -208,6 +208,30 @@ def test_rank_prefilter_in_epilogue_bitexact(gpu, case):
           f"dense form {1 - nd.mean():.3f}")
 
 
+def test_rank_prefilter_triangle_list_overflow(gpu):
+    """The triangle form with a chunk that leaves 1 024 survivor slots per row, on 8 clusters of
+    1 500 near-duplicates (every cluster member survives for every row): the rows whose lists
+    overflow come back marked in need[] (the 1M run marks a few), the others bit-exact; through
+    the Python driver (HipStages.rank_rows: marked rows go through the exact rows) initial_rank
+    and the row maxima equal the exact rows for every row."""
+    from multimodal_reid_amd import _lib
+    r = np.random.default_rng(5)
+    base = r.standard_normal((8, 384)).astype(np.float32)
+    f = oracle.l2norm(np.repeat(base, 1500, axis=0) + 1e-4 * r.standard_normal((12000, 384)).astype(np.float32))
+    f = torch.from_numpy(np.ascontiguousarray(f)).to(gpu)
+    N, K = f.shape[0], 51
+    Np = (N + 255) // 256 * 256
+    cr = 2060  # chunk rows of Np floats: a 1 024-pair list per row
+    assert int(_lib.load().reidmi_rr_rank_rows_f16_pass_rows(N, Np, cr, K, 16)) == N
+    Rt, mt, nt = _rank_rows_f16_direct(f, K, 16, cr)
+    Re, me, _ = _rank_rows(f, 100, False, 4 * N * 300)
+    assert nt.sum() > N // 2  # the lists overflowed
+    ok = nt == 0
+    assert np.array_equal(Rt[ok], Re[ok, :K]) and np.array_equal(mt[ok].view(np.uint32), me[ok].view(np.uint32))
+    Rp, mp, _ = _rank_rows(f, 100, True, 4 * N * 2304)
+    assert np.array_equal(Rp, Re) and np.array_equal(mp.view(np.uint32), me.view(np.uint32))
+
+
 def _one_call(feat, Q, k1, k2, lam):
     """reidmi_rerank itself (N x N fp32 distance materialised), whatever N."""
     from multimodal_reid_amd import _lib, reranking
