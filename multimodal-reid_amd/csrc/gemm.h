@@ -15,8 +15,10 @@
 //                 fp16 product (the k-reciprocal re-rank's pre-filter, rerank.hip): only the bound
 //                 reaches HBM, and the selection reads 4 bytes per pair instead of 12
 //   EPI_RRSV      no dense output: the pairs of row i that can still matter to its R2 selection
-//                 (hi - w_i <= thr_i or hi >= lb_i, per-row thresholds from a sampled pass) are
-//                 appended to the row's survivor list, a few hundred of the N columns
+//                 (hi <= hi_max_i or hi >= lb_i, per-row thresholds from a sampled pass) are
+//                 appended to the row's survivor list, ~1 000 of the N columns (persistent tile
+//                 only; with rr_tri the upper triangle of a symmetric product, each pair tested
+//                 for both its rows)
 #pragma once
 #include "common.h"
 
