@@ -26,6 +26,8 @@ extern "C" {
 #define REIDMI_ECAP 3
 
 const char* reidmi_last_error(void);
+/* 4 since round 4: the A/B-only entry points (forced GEMM tiling, distance-kernel variant, the
+ * fused QKV + attention kernel) moved to the tools library (include/reidmi_tools.h). */
 int reidmi_abi_version(void);
 
 /* ------------------------------------------------------------ retrieval back end */
@@ -48,13 +50,6 @@ int reidmi_distmat_f32(const float* q, int64_t Q, int64_t ldq, const float* g, i
  * Same tiling as reidmi_distmat_f32; ws: Q+G floats. */
 int reidmi_cosine_f32(const float* q, int64_t Q, int64_t ldq, const float* g, int64_t G, int64_t ldg, int64_t D,
                       float* out, int64_t ldo, float* ws, void* stream);
-
-/* reidmi_distmat_f32 with an explicit kernel choice (tests / A-B timing; no process-global
- * state): variant 0 = auto (K-step-32 pipelined kernel when D, ldq, ldg are multiples of 4 and
- * the operands 16-byte aligned), 1 = single-stage kernel.  Both run the same MFMA sequence per
- * output: bit-identical. */
-int reidmi_distmat_f32_variant(const float* q, int64_t Q, int64_t ldq, const float* g, int64_t G, int64_t ldg,
-                               int64_t D, float* out, int64_t ldo, float* ws, int variant, void* stream);
 
 /* np.argsort(x, axis=1)[:, :k] with ties in index order (kind="stable") — evaluate.py:40,
  * reranking.py:48.  row_div (nullable): rows are divided by row_div[row] first
@@ -126,20 +121,25 @@ int reidmi_rr_feat16(const float* feat, int64_t N, int64_t D, int64_t ldf, void*
 int reidmi_rr_norm_max(const float* sqn, const float* nrm, int64_t N, float* out2, void* stream);
 /* reidmi_rr_rank_rows with an fp16 MFMA pre-filter (same rank_out / rowmax_out bits): the fp16
  * product bounds every exact distance (error bound in backend.hip rank_select_kernel); only the
- * candidates are recomputed with the exact fp32 chain.  The GEMM's epilogue writes the upper
- * bounds (chunk [chunk_rows][Np] fp32) for a streaming selection.  Rows whose distances are too
- * concentrated for the bound (or not finite) get need[r] = 1 and no output: the caller runs the
- * exact rows for them.  nrm = sqrt(sqn); nmax2 = reidmi_rr_norm_max(sqn, nrm); need [hi - lo]
- * int32; chunk: chunk_rows x Np fp32. */
+ * candidates are recomputed with the exact fp32 chain.  Default form (sample stride 16, for N
+ * >= 4096): per-row thresholds from every 16th item, then the selection runs inside the GEMM's
+ * epilogue (survivor lists, no N-wide row in HBM; when one call covers all N rows and the lists
+ * fit the chunk, only the upper triangle of the symmetric product runs).  Smaller N: the GEMM's
+ * epilogue writes the upper bounds (chunk [chunk_rows][Np] fp32) for a streaming selection.
+ * Rows whose distances are too concentrated for the bound (or not finite), or whose survivor
+ * list overflows, get need[r] = 1 and no output: the caller runs the exact rows for them.
+ * nrm = sqrt(sqn); nmax2 = reidmi_rr_norm_max(sqn, nrm); need [hi - lo] int32; chunk:
+ * chunk_rows x Np fp32. */
 int reidmi_rr_rank_rows_f16(const float* feat, int64_t N, int64_t D, int64_t ldf, const float* sqn, const float* nrm,
                             const float* nmax2, const void* feat16, int64_t Np, int64_t Dp, int64_t lo, int64_t hi,
                             int K, int32_t* rank_out, float* rowmax_out, int32_t* need, float* chunk,
                             int64_t chunk_rows, void* stream);
-/* The same with the sample stride chosen: 0 or 1 = the dense form above at any N; S >= 2 = the
- * selection inside the GEMM's epilogue against per-row thresholds from every S-th item (no
- * N-wide row in HBM; backend.hip "R2 pre-filter with the selection in the GEMM"), when
- * floor(N / S) spans at least one 256-column tile and 4 K items (else the dense form).  Same
- * output bits; slower than the dense form at every N measured (rerank.hip RR_SAMPLE_STRIDE). */
+/* The same with the sample stride chosen: 0 or 1 = the dense form (bounds written to the chunk,
+ * streaming selection) at any N; S >= 2 = the selection inside the GEMM's epilogue against
+ * per-row thresholds from every S-th item (backend.hip "R2 pre-filter with the selection in the
+ * GEMM"), when floor(N / S) spans at least one 256-column tile and 4 K items (else the dense
+ * form).  Same output bits.  reidmi_rr_rank_rows_f16 uses S = 16 (rerank.hip RR_SAMPLE_STRIDE):
+ * 1M-item R2 1.98 s in the triangle form vs 3.9 s dense. */
 int reidmi_rr_rank_rows_f16_ex(const float* feat, int64_t N, int64_t D, int64_t ldf, const float* sqn,
                                const float* nrm, const float* nmax2, const void* feat16, int64_t Np, int64_t Dp,
                                int64_t lo, int64_t hi, int K, int32_t* rank_out, float* rowmax_out, int32_t* need,
@@ -149,6 +149,35 @@ int reidmi_rr_rank_rows_f16_ex(const float* feat, int64_t N, int64_t D, int64_t 
  * bytes): size the calls' row ranges by it.  sample_stride < 0: the default form's.  -1 on bad
  * arguments. */
 int64_t reidmi_rr_rank_rows_f16_pass_rows(int64_t N, int64_t Np, int64_t chunk_rows, int K, int sample_stride);
+/* R2's triangle form in stages, for sharding it over ranks (reranking.HipStages under a process
+ * group): rank r samples its rows (reidmi_rr_tri_sample, records all-gathered), runs tiles
+ * [t0, t1) = its contiguous share of the upper-triangle list over ALL rows
+ * (reidmi_rr_tri_survivors), sends the partial survivor lists of each other rank's rows to it
+ * (reidmi_rr_sv_pack, all-to-all) which appends them (reidmi_rr_sv_merge), and selects its own
+ * rows (reidmi_rr_sv_select): the same rank_out / rowmax_out / need bits as the one-call
+ * reidmi_rr_rank_rows_f16 for any number of ranks, at the one-GPU triangle's total MFMA work.
+ * Buffers (caller-owned, device): meta [Np] x 16 B, wrow [N] fp32, cnt [N] int32 (0 for rows
+ * sampled elsewhere), list [N][cap] x 8 B, sqn_s / nrm_s [ns] fp32, tiles [ntiles] int32, hs
+ * [sample_rows][ns] fp32 (may overlay list; the sizes: reidmi_rr_tri_plan; cap = 0: the
+ * triangle form does not apply for this chunk). */
+int reidmi_rr_tri_plan(int64_t N, int64_t Np, int64_t chunk_rows, int K, int64_t* ntiles, int64_t* cap, int64_t* ns,
+                       int64_t* sample_rows);
+int reidmi_rr_tri_init(const float* sqn, const float* nrm, int64_t N, int64_t Np, int64_t ns, void* meta, float* sqn_s,
+                       float* nrm_s, int32_t* tiles, void* stream);
+int reidmi_rr_tri_sample(const void* feat16, int64_t Np, int64_t Dp, const float* sqn, const float* nrm,
+                         const float* nmax2, int64_t N, int64_t D, int K, const float* sqn_s, const float* nrm_s,
+                         int64_t ns, int64_t a, int64_t b, float* hs, int64_t hs_rows, void* meta, float* wrow,
+                         int32_t* cnt, int cap, void* stream);
+int reidmi_rr_tri_survivors(const void* feat16, int64_t Np, int64_t Dp, const float* sqn, const float* nrm, int64_t N,
+                            int64_t D, const void* meta, const int32_t* tiles, int64_t t0, int64_t t1, int32_t* cnt,
+                            void* list, int cap, void* stream);
+int reidmi_rr_sv_select(const int32_t* cnt, const void* list, int cap, const float* wrow, const float* feat,
+                        int64_t ldf, int64_t D, const float* sqn, int64_t row0, int64_t rows, int K, int32_t* rank_out,
+                        float* rowmax_out, int32_t* need, void* stream);
+int reidmi_rr_sv_pack(const int32_t* cnt, const void* list, int cap, int64_t rows, const int64_t* off, void* out,
+                      void* stream);
+int reidmi_rr_sv_merge(int32_t* cnt, void* list, int cap, int64_t rows, const int32_t* add_cnt, const int64_t* add_off,
+                       const void* add, void* stream);
 /* R3 (reranking.py:51-71): V rows lo..hi (ELL [hi-lo][vcap]) from the full rank[N][K] and
  * rowmax[N]; distance entries recomputed from feat with the distance kernel's arithmetic.
  * ws: reidmi_rr_caps' v_ws_bytes (nullable when 0). */
@@ -240,23 +269,18 @@ int reidmi_comm_allreduce(reidmi_comm_t comm, const void* send, void* recv, int6
 int reidmi_gemm_f16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N, int64_t K,
                     const float* bias, const void* rowstat, const float* colsum, void* out, int64_t ldc, void* stream);
 
-/* Live timing of the GEMM launches (HIP events on the launch stream), used by bench.py
- * for the roofline of the dominant kernel.  collect: epi = GEMM epilogue id (-1 = all);
- * returns summed device ms, launch count, algorithmic FLOPs (2MNK) and clears the record. */
+/* Measurement hooks: live timing of the GEMM launches (HIP events recorded on the launch stream
+ * around each GEMM, including those inside reidmi_vit_forward / reidmi_text_forward), which is
+ * how bench.py measures the dominant kernel's average launch time over its timed steps (the
+ * roofline `achieved`; no other interface reaches a kernel inside the forward).  Off by
+ * default: a disabled hook costs one branch per GEMM launch and records nothing.
+ * collect: epi = GEMM epilogue id (-1 = all); returns summed device ms, launch count,
+ * algorithmic FLOPs (2MNK) and clears the record. */
 int reidmi_prof_enable(int on);
 int reidmi_prof_collect(int epi, double* total_ms, int64_t* count, double* flops);
 /* Same, counting only launches of >= min_flops (e.g. the full-batch launches of a kernel,
  * so that the average matches that kernel's row in a rocprofv3 --stats summary). */
 int reidmi_prof_collect_min(int epi, double min_flops, double* total_ms, int64_t* count, double* flops);
-
-/* reidmi_gemm_f16 with an explicit tiling (tests / A-B timing; no process-global state):
- * tile 0 = auto (the persistent 256x256x64 LDS-DMA tile for >= 256 tiles, else 128x128x64),
- * 1 = force 128x128, 2 = force persistent; ngroups = the persistent walk's XCD groups (1, 2, 4,
- * 8; each owns 1/ngroups of the N-tiles, a smaller weight share per XCD L2), 0 = auto.
- * Every choice is bit-identical. */
-int reidmi_gemm_f16_tiled(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N,
-                          int64_t K, const float* bias, const void* rowstat, const float* colsum, void* out,
-                          int64_t ldc, int tile, int ngroups, void* stream);
 
 /* Key padding used for an L-token sequence by the attention kernel (rows of v^T). */
 int reidmi_attn_lpad(int L);
@@ -266,16 +290,6 @@ int reidmi_attn_lpad(int L);
  * vt [nseq*H][64][reidmi_attn_lpad(L)], o [nseq*L][H*64]; all fp16.  L <= 256. */
 int reidmi_mhsa_f16(const void* q, const void* k, const void* vt, void* o, int64_t nseq, int L, int H, int causal,
                      void* stream);
-
-/* ln_1 -> in_proj -> SDPA of one encoder block (custom_clip_model.py:22-27) with ln_1 folded
- * (reidmi_gemm_f16's rowstat / colsum / folded bias; wq [3W][ldw] = the folded in_proj weight):
- * o [nseq*L][W] fp16 = attention output, token-major (the out_proj operand).  fused = 1: one
- * kernel, q / k / v stay on chip (192 < L <= 224, non-causal: the vision towers; q, k, vt may
- * be NULL); fused = 0: the QKV GEMM into q, k [nseq*H][L][64] and vt [nseq*H][64][reidmi_attn_lpad(L)]
- * then reidmi_mhsa_f16.  Bit-identical results; reidmi_vit_forward uses the fused kernel. */
-int reidmi_qkv_attention_f16(const void* x, int64_t ldx, const void* wq, int64_t ldw, const float* bias,
-                             const float* colsum, const void* rowstat, int64_t nseq, int L, int H, int W, void* q,
-                             void* k, void* vt, void* o, int fused, void* stream);
 
 /* LayerNorm over rows of width W in {512,768,1024} (fp32 math, eps) — custom_clip_model.py:43-49.
  * Row r of the output reads input row row_idx ? row_idx[r] : r.  y32 / y16 (fp16) nullable. */
@@ -384,6 +398,73 @@ int64_t reidmi_text_workspace_bytes(const reidmi_text_weights* w, int64_t N);
  * < ctx_used (causal mask: rows past the EOT never reach it); n_ctx < ctx_used <= ctx. */
 int reidmi_text_forward(const reidmi_text_weights* w, const int64_t* tokens, const float* prompts, int64_t N,
                         int ctx_used, float* out, void* ws, int64_t ws_bytes, void* stream);
+
+/* ------------------------------------------------ weight packing (checkpoint boundary, §8b)
+ *
+ * From the reference's fp32 tensors on the device, in its key layout, to a runnable tower whose
+ * device data all lives in one caller-owned buffer (256-byte aligned, reidmi_*_pack_bytes):
+ * CLIP-ReID checkpoints hold the vision tower under `image_encoder.*` (utils.py:169-221, loaded
+ * into custom_clip_model.VisionTransformer) and the text tower under `text_encoder.*`
+ * (zero_shot_learning.py:28-35, loaded into the CLIP text tower); strip the prefix and pass the
+ * tensors below.  Packing (the definitions multimodal_reid_amd.model uses, pack.hip): ln_1 / ln_2
+ * folded into in_proj / c_fc (W' = fp16(fp32(W gamma)), s = sum of W' rows, b' = fp32(b + W beta)
+ * with a compensated fp64 sum), the other matrices cast to fp16 (utils.py:145-166 convert_weights),
+ * conv1 flattened and zero-padded to a multiple of 64, proj / text_projection transposed; fp32
+ * vectors copied.  Stream-ordered; the sources may be freed once the stream passes the call.
+ * out_blocks: HOST array of `layers` entries that out->blocks will point to (keep it alive). */
+typedef struct reidmi_block_src {  /* transformer.resblocks.{i}.* */
+    const float* ln_1_w;           /* ln_1.weight [W] */
+    const float* ln_1_b;           /* ln_1.bias [W] */
+    const float* in_proj_w;        /* attn.in_proj_weight [3W][W] */
+    const float* in_proj_b;        /* attn.in_proj_bias [3W] */
+    const float* out_proj_w;       /* attn.out_proj.weight [W][W] */
+    const float* out_proj_b;       /* attn.out_proj.bias [W] */
+    const float* ln_2_w;           /* ln_2.weight [W] */
+    const float* ln_2_b;           /* ln_2.bias [W] */
+    const float* c_fc_w;           /* mlp.c_fc.weight [4W][W] */
+    const float* c_fc_b;           /* mlp.c_fc.bias [4W] */
+    const float* c_proj_w;         /* mlp.c_proj.weight [W][4W] */
+    const float* c_proj_b;         /* mlp.c_proj.bias [W] */
+    const float* vpt_shallow;      /* IVLP VPT_shallow [n_ctx][W] (maple.py:617-644), or NULL */
+} reidmi_block_src;
+
+/* Vision tower keys (custom_clip_model.py:57-76; maple.py:722-753 for IVLP).  The positional
+ * embedding must already be at the (grid_h, grid_w) grid of the stride-12 patches (CLIP-ReID
+ * checkpoints are; an OpenAI 224 x 224 grid goes through utils.resize_pos_embed first,
+ * utils.py:111-125).  blocks: HOST array of `layers` entries. */
+typedef struct reidmi_vit_src {
+    int32_t width, layers, patch, stride, out_dim, grid_h, grid_w, n_ctx;
+    const float* conv1_w;               /* conv1.weight [W][3][P][P] */
+    const float* class_embedding;       /* [W] */
+    const float* positional_embedding;  /* [1 + grid_h * grid_w][W] */
+    const float* ln_pre_w;
+    const float* ln_pre_b;
+    const float* ln_post_w;
+    const float* ln_post_b;
+    const float* proj;                  /* [W][out_dim] */
+    const float* vpt;                   /* VPT [n_ctx][W] or NULL */
+    const reidmi_block_src* blocks;
+} reidmi_vit_src;
+
+/* Text tower keys of CLIP (maple.py:929-984): token_embedding.weight, positional_embedding,
+ * transformer.resblocks.*, ln_final.*, text_projection.  blocks: HOST array of `layers`. */
+typedef struct reidmi_text_src {
+    int32_t width, layers, ctx, vocab, out_dim, n_ctx;
+    const float* token_embedding;       /* [vocab][W] */
+    const float* positional_embedding;  /* [ctx][W] */
+    const float* ln_final_w;
+    const float* ln_final_b;
+    const float* text_projection;       /* [W][out_dim] */
+    const reidmi_block_src* blocks;
+} reidmi_text_src;
+
+/* Buffer bytes for the packed tower (-1 on bad shapes). */
+int64_t reidmi_vit_pack_bytes(const reidmi_vit_src* src);
+int reidmi_vit_weights_pack(const reidmi_vit_src* src, void* buf, int64_t buf_bytes, reidmi_vit_weights* out,
+                            reidmi_block_weights* out_blocks, void* stream);
+int64_t reidmi_text_pack_bytes(const reidmi_text_src* src);
+int reidmi_text_weights_pack(const reidmi_text_src* src, void* buf, int64_t buf_bytes, reidmi_text_weights* out,
+                             reidmi_block_weights* out_blocks, void* stream);
 
 /* -------------------------------------------------------- inference glue (G1) */
 

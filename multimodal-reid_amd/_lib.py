@@ -10,6 +10,7 @@ import torch
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG, "libreidmi.so")
+TOOLS_LIB_PATH = os.path.join(PKG, "libreidmi_tools.so")  # tests / A-B tools only (reidmi_tools.h)
 
 _vp = ctypes.c_void_p
 _i64 = ctypes.c_int64
@@ -26,7 +27,6 @@ SIGNATURES = {
     "reidmi_l2norm_f32": [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp],
     "reidmi_distmat_f32": [_vp, _i64, _i64, _vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp],
     "reidmi_cosine_f32": [_vp, _i64, _i64, _vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp],
-    "reidmi_distmat_f32_variant": [_vp, _i64, _i64, _vp, _i64, _i64, _i64, _vp, _i64, _vp, _i32, _vp],
     "reidmi_topk_rows_f32": [_vp, _i64, _i64, _i64, _vp, _i32, _vp, _vp, _i64, _vp],
     "reidmi_eval_rows": [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp],
     "reidmi_eval_rows_workspace_bytes": [_i64],
@@ -44,6 +44,14 @@ SIGNATURES = {
     "reidmi_rr_rank_rows_f16_ex": [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i32, _vp, _vp,
                                    _vp, _vp, _i64, _i32, _vp],
     "reidmi_rr_rank_rows_f16_pass_rows": [_i64, _i64, _i64, _i32, _i32],
+    "reidmi_rr_tri_plan": [_i64, _i64, _i64, _i32, _vp, _vp, _vp, _vp],
+    "reidmi_rr_tri_init": [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp],
+    "reidmi_rr_tri_sample": [_vp, _i64, _i64, _vp, _vp, _vp, _i64, _i64, _i32, _vp, _vp, _i64, _i64, _i64, _vp, _i64,
+                             _vp, _vp, _vp, _i32, _vp],
+    "reidmi_rr_tri_survivors": [_vp, _i64, _i64, _vp, _vp, _i64, _i64, _vp, _vp, _i64, _i64, _vp, _vp, _i32, _vp],
+    "reidmi_rr_sv_select": [_vp, _vp, _i32, _vp, _vp, _i64, _i64, _vp, _i64, _i64, _i32, _vp, _vp, _vp, _vp],
+    "reidmi_rr_sv_pack": [_vp, _vp, _i32, _i64, _vp, _vp, _vp],
+    "reidmi_rr_sv_merge": [_vp, _vp, _i32, _i64, _vp, _vp, _vp, _vp],
     "reidmi_rr_v_rows": [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _i32, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _i64, _vp,
                          _vp],
     "reidmi_rr_row_offsets": [_vp, _i64, _vp, _vp],
@@ -61,12 +69,9 @@ SIGNATURES = {
     "reidmi_gather_rows_f32": [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp],
     "reidmi_attn_lpad": [_i32],
     "reidmi_prof_enable": [_i32],
-    "reidmi_gemm_f16_tiled": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _vp],
     "reidmi_prof_collect": [_i32, _vp, _vp, _vp],
     "reidmi_prof_collect_min": [_i32, ctypes.c_double, _vp, _vp, _vp],
     "reidmi_mhsa_f16": [_vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp],
-    "reidmi_qkv_attention_f16": [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i32,
-                                 _vp],
     "reidmi_layernorm": [_vp, _i64, _i64, _vp, _i64, _vp, _vp, _f32, _vp, _i64, _vp, _i64, _vp],
     "reidmi_row_stats_f16": [_vp, _i64, _i64, _i64, _vp, _vp, _vp],
     "reidmi_gemm_f16_resid_partials": [_vp, _i64, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _i64, _vp, _vp],
@@ -86,43 +91,72 @@ SIGNATURES = {
     "reidmi_comm_allgather_rows": [_vp, _vp, _i64, _i64, _vp, _vp, _i64, _vp],
     "reidmi_comm_allreduce": [_vp, _vp, _vp, _i64, _i32, _vp],
 }
+# libreidmi_tools.so only (include/reidmi_tools.h): forced kernel variants for tests / A-B timing
+TOOLS_SIGNATURES = {
+    "reidmi_distmat_f32_variant": [_vp, _i64, _i64, _vp, _i64, _i64, _i64, _vp, _i64, _vp, _i32, _vp],
+    "reidmi_gemm_f16_tiled": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _vp],
+    "reidmi_qkv_attention_f16": [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i32,
+                                 _vp],
+}
 # entry points with struct arguments are typed in model.py (reidmi_vit_*, reidmi_text_*)
 STRUCT_ENTRY_POINTS = ("reidmi_vit_workspace_bytes", "reidmi_vit_forward", "reidmi_text_workspace_bytes",
-                       "reidmi_text_forward")
+                       "reidmi_text_forward", "reidmi_vit_pack_bytes", "reidmi_vit_weights_pack",
+                       "reidmi_text_pack_bytes", "reidmi_text_weights_pack")
 
 _LIB = None
+_TOOLS = None
 
 
 class ReidmiError(RuntimeError):
     pass
 
 
+def _open(path, tools):
+    if not os.path.exists(path):
+        raise ReidmiError(f"{path} is not built: run `python __graft_entry__.py build` "
+                          "(there is no CPU fallback)")
+    from . import build_lib
+    if not build_lib.manifest_matches(tools):
+        raise ReidmiError(f"{path} was not built from the sources next to it (its manifest differs): "
+                          "run `python __graft_entry__.py build`")
+    L = ctypes.CDLL(path)
+    L.reidmi_last_error.restype = ctypes.c_char_p
+    L.reidmi_abi_version.restype = _i32
+    table = dict(SIGNATURES, **TOOLS_SIGNATURES) if tools else SIGNATURES
+    for name, args in table.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = _i64 if name.endswith("_bytes") or name in INT64_RESULT else _i32
+    return L
+
+
 def load():
     """Load libreidmi.so (torch's HIP runtime is already loaded by `import torch`, so the
     library's libamdhip64.so.7 dependency resolves to that same runtime)."""
     global _LIB
-    if _LIB is not None:
-        return _LIB
-    if not os.path.exists(LIB_PATH):
-        raise ReidmiError(f"{LIB_PATH} is not built: run `python __graft_entry__.py build` "
-                          "(there is no CPU fallback)")
-    from . import build_lib
-    if not build_lib.manifest_matches():
-        raise ReidmiError(f"{LIB_PATH} was not built from the sources next to it (libreidmi.manifest.json "
-                          "differs): run `python __graft_entry__.py build`")
-    L = ctypes.CDLL(LIB_PATH)
-    L.reidmi_last_error.restype = ctypes.c_char_p
-    L.reidmi_abi_version.restype = _i32
-    for name, args in SIGNATURES.items():
-        fn = getattr(L, name)
-        fn.argtypes = args
-        fn.restype = _i64 if name.endswith("_bytes") or name in INT64_RESULT else _i32
-    _LIB = L
-    return L
+    if _LIB is None:
+        _LIB = _open(LIB_PATH, False)
+    return _LIB
+
+
+def load_tools():
+    """libreidmi_tools.so: the product entry points plus reidmi_tools.h's forced variants (tests
+    and A/B tools only; its static state — errors, timing hooks — is its own)."""
+    global _TOOLS
+    if _TOOLS is None:
+        _TOOLS = _open(TOOLS_LIB_PATH, True)
+    return _TOOLS
 
 
 def call(name, *args):
     L = load()
+    rc = getattr(L, name)(*args)
+    if rc != 0:
+        raise ReidmiError(f"{name} failed ({rc}): {L.reidmi_last_error().decode()}")
+
+
+def call_tools(name, *args):
+    L = load_tools()
     rc = getattr(L, name)(*args)
     if rc != 0:
         raise ReidmiError(f"{name} failed ({rc}): {L.reidmi_last_error().decode()}")

@@ -9,7 +9,12 @@ Rebuilds are decided by content, not by file times: every object records the sha
 source, the headers and the compiler flags, and the library is written together with
 libreidmi.manifest.json (the same digests).  _lib.load() refuses a library whose manifest
 does not match the sources next to it, so a stale or foreign libreidmi.so cannot be used
-silently, and the manifest says which sources a given library was built from."""
+silently, and the manifest says which sources a given library was built from.
+
+libreidmi_tools.so (include/reidmi_tools.h) is the product library plus the forced-variant
+entry points that tests and A/B tools use: the sources that hold `#ifdef REIDMI_TOOLS`
+sections are compiled a second time with -DREIDMI_TOOLS (build/tools/) and linked with the
+product objects of the other sources.  The product library never contains those sections."""
 import concurrent.futures as cf
 import hashlib
 import json
@@ -22,6 +27,9 @@ CSRC = os.path.join(PKG, "csrc")
 OBJ = os.path.join(PKG, "build")
 LIB = os.path.join(PKG, "libreidmi.so")
 MANIFEST = os.path.join(PKG, "libreidmi.manifest.json")
+TOOLS_LIB = os.path.join(PKG, "libreidmi_tools.so")
+TOOLS_MANIFEST = os.path.join(PKG, "libreidmi_tools.manifest.json")
+TOOLS_DEFINE = "-DREIDMI_TOOLS"
 INCLUDE = os.path.join(os.path.dirname(PKG), "include")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
@@ -71,14 +79,20 @@ def _headers_digest():
     return h.hexdigest()
 
 
-def _compile(src, hdr):
-    obj = os.path.join(OBJ, src.replace(".hip", ".o"))
+def _tools_sources():
+    """Sources with a REIDMI_TOOLS section (compiled twice)."""
+    return [s for s in _sources() if "REIDMI_TOOLS" in open(os.path.join(CSRC, s)).read()]
+
+
+def _compile(src, hdr, tools=False):
+    odir = os.path.join(OBJ, "tools") if tools else OBJ
+    obj = os.path.join(odir, src.replace(".hip", ".o"))
     stamp = obj + ".sha256"
     srcp = os.path.join(CSRC, src)
-    key = hashlib.sha256((_sha(srcp) + hdr).encode()).hexdigest()
+    key = hashlib.sha256((_sha(srcp) + hdr + (TOOLS_DEFINE if tools else "")).encode()).hexdigest()
     if os.path.exists(obj) and os.path.exists(stamp) and open(stamp).read().strip() == key:
         return obj, False
-    cmd = [HIPCC, *FLAGS, "-c", srcp, "-o", obj]
+    cmd = [HIPCC, *FLAGS, *([TOOLS_DEFINE] if tools else []), "-c", srcp, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-6000:]}")
@@ -87,40 +101,55 @@ def _compile(src, hdr):
     return obj, True
 
 
-def manifest_matches():
-    """True when libreidmi.so exists and its manifest records exactly the current sources."""
-    if not (os.path.exists(LIB) and os.path.exists(MANIFEST)):
+def manifest_matches(tools=False):
+    """True when the library exists and its manifest records exactly the current sources."""
+    lib, man = (TOOLS_LIB, TOOLS_MANIFEST) if tools else (LIB, MANIFEST)
+    if not (os.path.exists(lib) and os.path.exists(man)):
         return False
     try:
-        with open(MANIFEST) as f:
+        with open(man) as f:
             m = json.load(f)
     except (OSError, ValueError):
         return False
-    return m.get("inputs") == source_digests() and m.get("lib_sha256") == _sha(LIB)
+    return m.get("inputs") == source_digests() and m.get("lib_sha256") == _sha(lib)
 
 
-def build(verbose=False, jobs=None):
-    os.makedirs(OBJ, exist_ok=True)
+def _link(lib, man, objs, res, tools, verbose):
+    changed = any(c for _, c in res)
+    if not changed and manifest_matches(tools):
+        if verbose:
+            print("up to date", lib)
+        return
+    # the tools library binds its own copies of the internal symbols (a process may load both)
+    cmd = [HIPCC, *LDFLAGS, *(["-Wl,-Bsymbolic"] if tools else []), "-o", lib, *objs]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
+    ver = subprocess.run([HIPCC, "--version"], capture_output=True, text=True).stdout.strip().splitlines()
+    with open(man, "w") as f:
+        json.dump({"inputs": source_digests(), "lib_sha256": _sha(lib), "arch": ARCH, "tools": tools,
+                   "compiler": ver[0] if ver else "", "rebuilt": [os.path.basename(o) for o, c in res if c]},
+                  f, indent=1, sort_keys=True)
+    if verbose:
+        print("built", lib, "(recompiled:", ", ".join(os.path.basename(o) for o, c in res if c) or "none", ")")
+
+
+def build(verbose=False, jobs=None, tools=True):
+    os.makedirs(os.path.join(OBJ, "tools"), exist_ok=True)
     jobs = jobs or min(8, os.cpu_count() or 4, 16)
     hdr = _headers_digest()
+    srcs = _sources()
+    tsrcs = _tools_sources() if tools else []
+    jobs_list = [(s, False) for s in srcs] + [(s, True) for s in tsrcs]
     with cf.ThreadPoolExecutor(jobs) as ex:
-        res = list(ex.map(lambda s: _compile(s, hdr), _sources()))
-    objs = [o for o, _ in res]
-    changed = any(c for _, c in res)
-    if changed or not manifest_matches():
-        cmd = [HIPCC, *LDFLAGS, "-o", LIB, *objs]
-        r = subprocess.run(cmd, capture_output=True, text=True)
-        if r.returncode != 0:
-            raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
-        ver = subprocess.run([HIPCC, "--version"], capture_output=True, text=True).stdout.strip().splitlines()
-        with open(MANIFEST, "w") as f:
-            json.dump({"inputs": source_digests(), "lib_sha256": _sha(LIB), "arch": ARCH,
-                       "compiler": ver[0] if ver else "", "rebuilt": [os.path.basename(o) for o, c in res if c]},
-                      f, indent=1, sort_keys=True)
-        if verbose:
-            print("built", LIB, "(recompiled:", ", ".join(os.path.basename(o) for o, c in res if c) or "none", ")")
-    elif verbose:
-        print("up to date", LIB)
+        allres = list(ex.map(lambda st: _compile(st[0], hdr, st[1]), jobs_list))
+    res = allres[:len(srcs)]
+    _link(LIB, MANIFEST, [o for o, _ in res], res, False, verbose)
+    if tools:
+        tres = allres[len(srcs):]
+        tobj = {s: r for s, r in zip(tsrcs, tres)}
+        tres_all = [tobj.get(s, r) for s, r in zip(srcs, res)]
+        _link(TOOLS_LIB, TOOLS_MANIFEST, [o for o, _ in tres_all], tres_all, True, verbose)
     return LIB
 
 

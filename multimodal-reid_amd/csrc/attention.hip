@@ -613,6 +613,9 @@ __global__ __launch_bounds__(NKB * 64) void mhsa_pipe_kernel(const _Float16* __r
 }
 
 // ======================================================== fused QKV GEMM + attention
+// Built only into the tools library (libreidmi_tools.so, REIDMI_TOOLS): bit-exact with the
+// two-kernel block and measured slower, so the product library does not ship it.
+#ifdef REIDMI_TOOLS
 // ln_1 -> in_proj -> SDPA of a vision block (custom_clip_model.py:12,22-27) in one persistent
 // kernel: the QKV GEMM's 1 GB of q / k / v^T per batch of 1024 crops (and the attention's read
 // of it) never reaches HBM.  Unit = (image b, head h): the 192 columns [q_h | k_h | v_h] of the
@@ -943,6 +946,8 @@ __global__ __launch_bounds__(NKB * 64, 1) void qkv_attn_kernel(const _Float16* _
 // stride 2 mod 64 used before padded V^T by up to 60 elements per row: 23 % of V at L = 211.)
 // The QKV epilogue writes V^T with this same stride in HBM, so one head's V^T is a contiguous
 // blob for the LDS-DMA copy; 64 * (LP + 4) * 2 bytes is a multiple of 512.
+#endif  // REIDMI_TOOLS (fused QKV GEMM + attention kernel)
+
 static int vt_stride(int lp) { return lp + 4; }
 
 static int g_num_cu = 0;
@@ -1099,6 +1104,7 @@ int mhsa_cls(const void* q, const void* k, const void* vt, void* o, int64_t nseq
     return OK;
 }
 
+#ifdef REIDMI_TOOLS
 // Fused QKV + attention for non-causal blocks of L in (192, 224] tokens (the vision towers:
 // 211, IVLP 213); returns EINVAL for other shapes (the caller then runs the two kernels).
 // x [nseq*L][ldx] fp16 (the residual stream), wq [3W][ldw] fp16 (ln_1-folded in_proj), bias /
@@ -1127,6 +1133,7 @@ int qkv_attn(const void* x, int64_t ldx, const void* wq, int64_t ldw, const floa
     RM_LAUNCHED();
     return OK;
 }
+#endif  // REIDMI_TOOLS
 
 // Smallest instantiated key-padding >= L.  Lp must also equal the vt row length the
 // QKV epilogue wrote (attn_lpad()).

@@ -1911,13 +1911,16 @@ REIDMI_API int reidmi_distmat_f32(const float* q, int64_t Q, int64_t ldq, const 
     return distmat_impl(false, q, Q, ldq, g, G, ldg, D, out, ldo, ws, stream);
 }
 
-// Per-call kernel selection (tests / A-B timing): 0 = auto (pipelined when the operands
-// allow), 1 = the single-stage kernel; the same MFMA chain per output (bit-identical).
+#ifdef REIDMI_TOOLS
+// Per-call kernel selection (tests / A-B timing; tools library, include/reidmi_tools.h):
+// 0 = auto (pipelined when the operands allow), 1 = the single-stage kernel; the same MFMA
+// chain per output (bit-identical).
 REIDMI_API int reidmi_distmat_f32_variant(const float* q, int64_t Q, int64_t ldq, const float* g, int64_t G,
                                           int64_t ldg, int64_t D, float* out, int64_t ldo, float* ws, int variant,
                                           void* stream) {
     return distmat_impl(false, q, Q, ldq, g, G, ldg, D, out, ldo, ws, stream, variant);
 }
+#endif
 
 REIDMI_API int reidmi_cosine_f32(const float* q, int64_t Q, int64_t ldq, const float* g, int64_t G, int64_t ldg,
                                  int64_t D, float* out, int64_t ldo, float* ws, void* stream) {

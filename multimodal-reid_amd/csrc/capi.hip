@@ -12,5 +12,7 @@ int fail(int code, const std::string& m) {
 
 REIDMI_API const char* reidmi_last_error(void) { return reidmi::g_err.c_str(); }
 // 2: per-call GEMM tiling / distance variant entry points replace the process-global setters;
-//    RCCL exchange (reidmi_comm_*); re-ranking without capacity limits.
-REIDMI_API int reidmi_abi_version(void) { return 3; }
+// 3: RCCL exchange (reidmi_comm_*); re-ranking without capacity limits;
+// 4: the forced-variant entry points moved to libreidmi_tools.so (include/reidmi_tools.h);
+//    weight packing (reidmi_vit_weights_pack / reidmi_text_weights_pack).
+REIDMI_API int reidmi_abi_version(void) { return 4; }

@@ -21,13 +21,15 @@ namespace reidmi {
 int mhsa(const void* q, const void* k, const void* vt, void* o, int64_t nseq, int L, int H, bool causal,
          hipStream_t s);
 int attn_lpad(int L);
-bool qkv_attn_fits(int L, int W, bool causal);
+#ifdef REIDMI_TOOLS
 // The fused QKV + attention kernel is bit-identical to the two-kernel block but measured slower
 // at the bench batch (B = 1024, L = 211: 1.20 ms vs 1.09-1.12 ms for QKV GEMM + mhsa,
-// tools/qkv_attn_ab.py, profiles/r03), so vision blocks run the two kernels.
-constexpr bool kFuseQkvAttention = false;
+// tools/qkv_attn_ab.py, profiles/r03), so vision blocks run the two kernels and the kernel is
+// built into the tools library only.
+bool qkv_attn_fits(int L, int W, bool causal);
 int qkv_attn(const void* x, int64_t ldx, const void* wq, int64_t ldw, const float* bias, const float* colsum,
              const void* rowstat, int64_t nseq, int L, int H, int W, void* o, hipStream_t s);
+#endif
 int mhsa_cls(const void* q, const void* k, const void* vt, void* o, int64_t nseq, int L, int H, hipStream_t s);
 
 // ------------------------------------------------------------------- LayerNorm
@@ -358,10 +360,7 @@ static int run_block(const reidmi_block_weights& bw, char* ws, const Plan& P, in
     int rc;
     // ln_1 (custom_clip_model.py:27)
     if ((rc = x_pst ? row_stats_from_partials(pst, M, W, st, s) : row_stats(x, M, W, W, st, s))) return rc;
-    if (kFuseQkvAttention && qkv_attn_fits(L, W, causal)) {
-        // vision blocks: QKV GEMM + attention fused, q / k / v never leave the CU (attention.hip)
-        if ((rc = qkv_attn(x, W, bw.qkv_w, W, bw.qkv_b, bw.qkv_s, st, nseq, L, H, W, o, s))) return rc;
-    } else {
+    {
         EpiArgs ea{};
         ea.bias = bw.qkv_b;
         ea.rowstat = st;
@@ -660,8 +659,9 @@ REIDMI_API int reidmi_gemm_f16_resid_partials(const void* A, int64_t lda, const 
                     (hipStream_t)stream);
 }
 
+#ifdef REIDMI_TOOLS
 // ln_1-folded QKV projection + attention of one block (custom_clip_model.py:22-27) on its own,
-// for tests / A-B timing: fused = 1 the single fused kernel, 0 the QKV GEMM (head-split
+// for tests / A-B timing (tools library, include/reidmi_tools.h): fused = 1 the single fused kernel, 0 the QKV GEMM (head-split
 // epilogue into q, k [nseq*H][L][64], vt [nseq*H][64][reidmi_attn_lpad(L)]) then the attention
 // kernel.  The two are bit-identical (same MFMA chains, same roundings).
 REIDMI_API int reidmi_qkv_attention_f16(const void* x, int64_t ldx, const void* wq, int64_t ldw, const float* bias,
@@ -688,3 +688,4 @@ REIDMI_API int reidmi_qkv_attention_f16(const void* x, int64_t ldx, const void* 
     if ((rc = gemm_f16(EPI_QKV, x, ldx, wq, ldw, nseq * L, 3 * W, W, ea, s))) return rc;
     return mhsa(q, k, vt, o, nseq, L, H, false, s);
 }
+#endif  // REIDMI_TOOLS

@@ -1206,6 +1206,8 @@ REIDMI_API int reidmi_gemm_f16(int epi, const void* A, int64_t lda, const void* 
     return gemm_api(epi, A, lda, W, ldw, M, N, K, bias, rowstat, colsum, out, ldc, GemmOpts{}, stream);
 }
 
+#ifdef REIDMI_TOOLS
+// Forced tiling / walk (tests, A-B timing; tools library, include/reidmi_tools.h)
 REIDMI_API int reidmi_gemm_f16_tiled(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M,
                                      int64_t N, int64_t K, const float* bias, const void* rowstat, const float* colsum,
                                      void* out, int64_t ldc, int tile, int ngroups, void* stream) {
@@ -1214,3 +1216,4 @@ REIDMI_API int reidmi_gemm_f16_tiled(int epi, const void* A, int64_t lda, const 
     opt.ngroups = ngroups;
     return gemm_api(epi, A, lda, W, ldw, M, N, K, bias, rowstat, colsum, out, ldc, opt, stream);
 }
+#endif  // REIDMI_TOOLS

@@ -1420,6 +1420,73 @@ static int64_t rr_tri_cap(int64_t N, int64_t Np, int64_t chunk_rows, int K, int 
     return cap >= 1024 && 8 * N * cap >= 4 * ns * 256 ? cap : 0;
 }
 
+// ---- pieces of the triangle form, shared by rank_rows_f16 (one call over all rows) and the
+// staged entry points reidmi_rr_tri_* (the sharded R2: the tile list split over ranks, the
+// survivor lists of other ranks' rows exchanged, reranking.HipStages)
+// sample norms (every S-th item), the upper-triangle tile list, the zero records past N
+static int tri_init(const float* sqn, const float* nrm, int64_t N, int64_t Np, int64_t ns, int S, float4* meta,
+                    float* sqn_s, float* nrm_s, int* tiles, hipStream_t s) {
+    const int T = (int)(Np / 256);
+    hipLaunchKernelGGL(rr_gather_norms_kernel, dim3((unsigned)ceil_div(ns, 256)), dim3(256), 0, s, sqn, nrm, ns, S,
+                       sqn_s, nrm_s);
+    RM_LAUNCHED();
+    hipLaunchKernelGGL(rr_tri_tiles_kernel, dim3((unsigned)ceil_div(T, RR_BAND)), dim3(256), 0, s, T, tiles);
+    RM_LAUNCHED();
+    if (Np > N) RM_CHECK_HIP(hipMemsetAsync(meta + N, 0, (Np - N) * sizeof(float4), s));
+    return OK;
+}
+
+// the sample's bounds of rows [a, a + nb) (EPI_RRHI against every S-th item) -> their records,
+// widths and counters (rr_sample_kernel)
+static int tri_sample(const _Float16* x16, int64_t Dp, const float* sqn, const float* nrm, const float* nmax2,
+                      int64_t D, int K, int S, const float* sqn_s, const float* nrm_s, int64_t ns, int64_t a,
+                      int64_t nb, float* hs, float4* meta, float* wrow, int32_t* cnt, int cap, hipStream_t s) {
+    EpiArgs es{};
+    es.out = hs;
+    es.ldc = ns;
+    es.rr_sqn = sqn;
+    es.rr_nrm = nrm;
+    es.rr_csqn = sqn_s;
+    es.rr_cnrm = nrm_s;
+    es.rr_row0 = a;
+    es.rr_n = ns;
+    rank_select_consts((int)D, es.rr_c);
+    // the sample: W rows = every S-th item (row stride S * Dp)
+    int r = gemm_f16(EPI_RRHI, x16 + a * Dp, Dp, x16, (int64_t)S * Dp, nb, ns, Dp, es, s);
+    return r ? r : rr_sample_launch(hs, ns, ns, sqn, nrm, nmax2, a, nb, K, (int)D, meta, wrow, cnt, cap, s);
+}
+
+// the survivor GEMM (EPI_RRSV) over tiles [0, ntiles) of a tile list; tri: the list is (part
+// of) the symmetric product's upper triangle and each pair above the diagonal is tested for both
+// its rows
+static int tri_survivors(const _Float16* x16, int64_t Dp, int64_t Np, const float* sqn, const float* nrm, int64_t N,
+                         int64_t D, int64_t a, int64_t M, const float4* rowmeta, const float4* colrec, const int* tiles,
+                         int64_t ntiles, bool tri, int32_t* cnt, int2* list, int cap, hipStream_t s) {
+    if (ntiles <= 0) return OK;
+    EpiArgs ev{};
+    ev.rr_sqn = sqn;
+    ev.rr_nrm = nrm;
+    ev.rr_row0 = a;
+    ev.rr_n = N;
+    rank_select_consts((int)D, ev.rr_c);
+    ev.rr_rowmeta = rowmeta;
+    ev.rr_colrec = colrec;
+    ev.rr_tiles = tiles;
+    ev.rr_ntiles = ntiles;
+    ev.rr_tri = tri;
+    ev.sv_cnt = cnt;
+    ev.sv_list = list;
+    ev.sv_cap = cap;
+    GemmOpts persistent;
+    persistent.tile = 2;  // the survivor epilogue's LDS buffers live in the 256 x 256 tile
+    return gemm_f16(EPI_RRSV, x16 + a * Dp, Dp, x16, Dp, M, Np, Dp, ev, s, persistent);
+}
+
+// rows per sample pass of the triangle form when its hs scratch overlays the N x cap lists
+static int64_t tri_sample_rows(int64_t N, int64_t cap, int64_t ns) {
+    return std::min<int64_t>(65536, 8 * N * cap / (4 * ns) / 256 * 256);
+}
+
 static int rank_rows_f16(const float* feat, int64_t N, int64_t D, int64_t ldf, const float* sqn, const float* nrm,
                          const float* nmax2, const void* feat16, int64_t Np, int64_t Dp, int64_t lo, int64_t hi,
                          int K, int32_t* rank_out, float* rowmax_out, int32_t* need, float* chunk,
@@ -1433,43 +1500,14 @@ static int rank_rows_f16(const float* feat, int64_t N, int64_t D, int64_t ldf, c
     // (the survivor epilogue needs K >= 2 K-steps of the persistent tile: Dp >= 128)
     const bool sampled = Dp >= 128 && rr_sv_pass_rows(N, Np, chunk_rows, K, S) > 0;
     const int64_t tcap = sampled && lo == 0 && hi == N ? rr_tri_cap(N, Np, chunk_rows, K, S) : 0;
-    GemmOpts persistent;
-    persistent.tile = 2;  // the survivor epilogue's LDS buffers live in the 256 x 256 tile
     const int T = (int)(Np / 256);
-    // the sample's bounds of rows [a, a + nb) -> their records, widths and counters
     auto sample = [&](float* hs, const float* sqn_s, const float* nrm_s, int64_t ns, int64_t a, int64_t nb,
                       float4* meta, float* wrow, int32_t* cnt, int cap) -> int {
-        EpiArgs es{};
-        es.out = hs;
-        es.ldc = ns;
-        es.rr_sqn = sqn;
-        es.rr_nrm = nrm;
-        es.rr_csqn = sqn_s;
-        es.rr_cnrm = nrm_s;
-        es.rr_row0 = a;
-        es.rr_n = ns;
-        rank_select_consts((int)D, es.rr_c);
-        // the sample: W rows = every S-th item (row stride S * Dp)
-        int r = gemm_f16(EPI_RRHI, x16 + a * Dp, Dp, x16, (int64_t)S * Dp, nb, ns, Dp, es, s);
-        return r ? r : rr_sample_launch(hs, ns, ns, sqn, nrm, nmax2, a, nb, K, (int)D, meta, wrow, cnt, cap, s);
+        return tri_sample(x16, Dp, sqn, nrm, nmax2, D, K, S, sqn_s, nrm_s, ns, a, nb, hs, meta, wrow, cnt, cap, s);
     };
     auto survivors = [&](int64_t a, int64_t M, const float4* rowmeta, const float4* colrec, const int* tiles,
                          int64_t ntiles, bool tri, int32_t* cnt, int2* list, int cap) -> int {
-        EpiArgs ev{};
-        ev.rr_sqn = sqn;
-        ev.rr_nrm = nrm;
-        ev.rr_row0 = a;
-        ev.rr_n = N;
-        rank_select_consts((int)D, ev.rr_c);
-        ev.rr_rowmeta = rowmeta;
-        ev.rr_colrec = colrec;
-        ev.rr_tiles = tiles;
-        ev.rr_ntiles = ntiles;
-        ev.rr_tri = tri;
-        ev.sv_cnt = cnt;
-        ev.sv_list = list;
-        ev.sv_cap = cap;
-        return gemm_f16(EPI_RRSV, x16 + a * Dp, Dp, x16, Dp, M, Np, Dp, ev, s, persistent);
+        return tri_survivors(x16, Dp, Np, sqn, nrm, N, D, a, M, rowmeta, colrec, tiles, ntiles, tri, cnt, list, cap, s);
     };
     if (tcap > 0) {
         // triangle: every pair once (tiles with M-tile <= N-tile), tested for both its rows
@@ -1481,13 +1519,8 @@ static int rank_rows_f16(const float* feat, int64_t N, int64_t D, int64_t ldf, c
         int32_t* cnt = (int32_t*)(tiles + ntri);
         float* wrow = (float*)(cnt + N);
         int2* list = (int2*)(((uintptr_t)(wrow + N) + 15) & ~(uintptr_t)15);  // [N][tcap]
-        hipLaunchKernelGGL(rr_gather_norms_kernel, dim3((unsigned)ceil_div(ns, 256)), dim3(256), 0, s, sqn, nrm, ns, S,
-                           sqn_s, nrm_s);
-        RM_LAUNCHED();
-        hipLaunchKernelGGL(rr_tri_tiles_kernel, dim3((unsigned)ceil_div(T, RR_BAND)), dim3(256), 0, s, T, tiles);
-        RM_LAUNCHED();
-        RM_CHECK_HIP(hipMemsetAsync(meta + N, 0, (Np - N) * sizeof(float4), s));
-        const int64_t sp = std::min<int64_t>(65536, 8 * N * tcap / (4 * ns) / 256 * 256);  // rows per sample pass
+        if ((rc = tri_init(sqn, nrm, N, Np, ns, S, meta, sqn_s, nrm_s, tiles, s))) return rc;
+        const int64_t sp = tri_sample_rows(N, tcap, ns);  // rows per sample pass
         for (int64_t a = 0; a < N; a += sp) {
             const int64_t nb = N - a < sp ? N - a : sp;
             if ((rc = sample((float*)list, sqn_s, nrm_s, ns, a, nb, meta + a, wrow + a, cnt + a, (int)tcap))) return rc;
@@ -1556,10 +1589,11 @@ static int rank_rows_f16(const float* feat, int64_t N, int64_t D, int64_t ldf, c
 // exact chain.  Same rank_out / rowmax_out bits as reidmi_rr_rank_rows for the rows with
 // need[r] = 0; rows with need[r] = 1 (concentrated or non-finite distances) are left for the
 // exact rows.  nrm = sqrt(sqn) [N]; nmax2 = reidmi_rr_norm_max of sqn, nrm.  chunk: chunk_rows x
-// Np fp32 of scratch.  The GEMM writes the rows' bounds (chunk_rows x Np) and rank_select1
-// streams them; reidmi_rr_rank_rows_f16_ex with a sample stride >= 2 runs the selection inside
-// the GEMM's epilogue instead (backend.hip, "R2 pre-filter with the selection in the GEMM";
-// same bits, slower at every N measured -- see RR_SAMPLE_STRIDE).
+// Np fp32 of scratch.  Default: sample stride RR_SAMPLE_STRIDE (16), the selection inside the
+// GEMM's epilogue (backend.hip, "R2 pre-filter with the selection in the GEMM"; the triangle
+// form when one call covers all rows); below that size, or with reidmi_rr_rank_rows_f16_ex's
+// stride 0 / 1, the GEMM writes the rows' bounds (chunk_rows x Np) and rank_select1 streams them.
+// Same bits either way.
 REIDMI_API int reidmi_rr_rank_rows_f16(const float* feat, int64_t N, int64_t D, int64_t ldf, const float* sqn,
                                        const float* nrm, const float* nmax2, const void* feat16, int64_t Np,
                                        int64_t Dp, int64_t lo, int64_t hi, int K, int32_t* rank_out,
@@ -1590,6 +1624,139 @@ REIDMI_API int64_t reidmi_rr_rank_rows_f16_pass_rows(int64_t N, int64_t Np, int6
     if (rr_tri_cap(N, Np, chunk_rows, K, S) > 0) return N;  // one call over all rows: the triangle form
     const int64_t p = rr_sv_pass_rows(N, Np, chunk_rows, K, S);
     return p > 0 ? p : chunk_rows;
+}
+
+// ---- The triangle form of R2 in stages (reranking.HipStages' sharded R2): every
+// rank samples its own rows (records all-gathered), runs a contiguous share of the upper-triangle
+// tile list over ALL rows (each pair tested for both its rows), sends the partial survivor lists
+// of other ranks' rows to their owners (reidmi_rr_sv_pack -> all-to-all -> reidmi_rr_sv_merge)
+// and selects its own rows: the union of the lists is the one-call triangle form's, and the
+// selection sorts each list by (hi, index), so the rows come out with the same bits for any
+// number of ranks, at the one-GPU triangle's total MFMA work.
+namespace reidmi {
+__global__ void rr_sv_pack_kernel(const int32_t* __restrict__ cnt, const int2* __restrict__ list, int cap,
+                                  int64_t rows, const int64_t* __restrict__ off, int2* __restrict__ out) {
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= rows) return;
+    const int n = cnt[r] < cap ? cnt[r] : cap;
+    const int2* src = list + r * cap;
+    int2* dst = out + off[r];
+    for (int p = threadIdx.x & 63; p < n; p += 64) dst[p] = src[p];
+}
+
+__global__ void rr_sv_merge_kernel(int32_t* __restrict__ cnt, int2* __restrict__ list, int cap, int64_t rows,
+                                   const int32_t* __restrict__ add_cnt, const int64_t* __restrict__ add_off,
+                                   const int2* __restrict__ add) {
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= rows) return;
+    const int base = cnt[r], na = add_cnt[r];
+    const int m = na < cap ? na : cap;  // entries the sender holds
+    int2* dst = list + r * cap;
+    const int2* src = add + add_off[r];
+    for (int p = threadIdx.x & 63; p < m; p += 64)
+        if ((int64_t)base + p < cap) dst[base + p] = src[p];
+    __builtin_amdgcn_wave_barrier();
+    if ((threadIdx.x & 63) == 0) {
+        const int64_t t = (int64_t)base + na;
+        cnt[r] = t < 0x3fffffff ? (int32_t)t : 0x3fffffff;  // > cap: the row overflows (need)
+    }
+}
+}  // namespace reidmi
+
+// Triangle form's sizes for a chunk of chunk_rows x Np floats (the same as the one-call form
+// picks, reidmi_rr_rank_rows_f16): *ntiles = tiles of the upper triangle, *cap = survivor slots
+// per row (0: the triangle form does not apply), *ns = sample items, *sample_rows = rows per
+// sample pass when its scratch (sample_rows x ns fp32) overlays the N x cap lists.
+REIDMI_API int reidmi_rr_tri_plan(int64_t N, int64_t Np, int64_t chunk_rows, int K, int64_t* ntiles, int64_t* cap,
+                                  int64_t* ns, int64_t* sample_rows) {
+    RM_REQUIRE(N > 0 && Np >= N && Np % 256 == 0 && chunk_rows > 0 && K >= 1 && ntiles && cap && ns && sample_rows,
+               "rr_tri_plan: bad arguments");
+    const int S = RR_SAMPLE_STRIDE;
+    *cap = K <= 64 ? rr_tri_cap(N, Np, chunk_rows, K, S) : 0;
+    *ns = rr_sv_ns(N, S);
+    *ntiles = Np / 256 <= 65536 ? rr_tri_tiles((int)(Np / 256)) : 0;
+    *sample_rows = *cap > 0 ? tri_sample_rows(N, *cap, *ns) : 0;
+    return OK;
+}
+
+// meta [Np] float4 (row / column records; the tail past N zeroed here), sqn_s / nrm_s [ns],
+// tiles [ntiles] int32 (the upper-triangle tile list, band order)
+REIDMI_API int reidmi_rr_tri_init(const float* sqn, const float* nrm, int64_t N, int64_t Np, int64_t ns, void* meta,
+                                  float* sqn_s, float* nrm_s, int32_t* tiles, void* stream) {
+    RM_REQUIRE(sqn && nrm && meta && sqn_s && nrm_s && tiles && N > 0 && Np >= N && Np % 256 == 0 && ns >= 256 &&
+                   ns * RR_SAMPLE_STRIDE <= N,
+               "rr_tri_init: bad arguments");
+    return tri_init(sqn, nrm, N, Np, ns, RR_SAMPLE_STRIDE, (float4*)meta, sqn_s, nrm_s, tiles, (hipStream_t)stream);
+}
+
+// Records, widths and counters of rows [a, b) (meta / wrow / cnt indexed by item): the sample's
+// bounds in passes of hs_rows rows through hs (hs_rows x ns fp32; may overlay the lists).
+REIDMI_API int reidmi_rr_tri_sample(const void* feat16, int64_t Np, int64_t Dp, const float* sqn, const float* nrm,
+                                    const float* nmax2, int64_t N, int64_t D, int K, const float* sqn_s,
+                                    const float* nrm_s, int64_t ns, int64_t a, int64_t b, float* hs, int64_t hs_rows,
+                                    void* meta, float* wrow, int32_t* cnt, int cap, void* stream) {
+    RM_REQUIRE(feat16 && sqn && nrm && nmax2 && sqn_s && nrm_s && hs && meta && wrow && cnt && 0 <= a && a <= b &&
+                   b <= N && Np >= N && Dp >= D && Dp % 64 == 0 && K >= 1 && K <= 64 && hs_rows > 0 && ns >= K &&
+                   cap >= 1 && cap <= RR_SV_CAP_,
+               "rr_tri_sample: bad arguments");
+    hipStream_t s = (hipStream_t)stream;
+    int rc;
+    for (int64_t x = a; x < b; x += hs_rows) {
+        const int64_t nb = b - x < hs_rows ? b - x : hs_rows;
+        if ((rc = tri_sample((const _Float16*)feat16, Dp, sqn, nrm, nmax2, D, K, RR_SAMPLE_STRIDE, sqn_s, nrm_s, ns, x, nb,
+                             hs, (float4*)meta + x, wrow + x, cnt + x, cap, s)))
+            return rc;
+    }
+    return OK;
+}
+
+// The survivor GEMM over tiles [t0, t1) of the triangle list, all N rows: appends to cnt [N] /
+// list [N][cap] (cnt of rows not sampled on this rank must start at 0).
+REIDMI_API int reidmi_rr_tri_survivors(const void* feat16, int64_t Np, int64_t Dp, const float* sqn, const float* nrm,
+                                       int64_t N, int64_t D, const void* meta, const int32_t* tiles, int64_t t0,
+                                       int64_t t1, int32_t* cnt, void* list, int cap, void* stream) {
+    RM_REQUIRE(feat16 && sqn && nrm && meta && tiles && cnt && list && 0 <= t0 && t0 <= t1 && Np >= N && Np % 256 == 0 &&
+                   Dp >= 128 && Dp % 64 == 0 && cap >= 1 && cap <= RR_SV_CAP_,
+               "rr_tri_survivors: bad arguments");
+    const float4* m = (const float4*)meta;
+    return tri_survivors((const _Float16*)feat16, Dp, Np, sqn, nrm, N, D, 0, N, m, m, tiles + t0, t1 - t0, true, cnt,
+                         (int2*)list, cap, (hipStream_t)stream);
+}
+
+// The selection of rows row0 .. row0 + rows from their lists (cnt / list / wrow indexed from
+// row0): rank_out [rows][K], rowmax_out, need (rank_select_sv_kernel).
+REIDMI_API int reidmi_rr_sv_select(const int32_t* cnt, const void* list, int cap, const float* wrow, const float* feat,
+                                   int64_t ldf, int64_t D, const float* sqn, int64_t row0, int64_t rows, int K,
+                                   int32_t* rank_out, float* rowmax_out, int32_t* need, void* stream) {
+    RM_REQUIRE(cnt && list && wrow && feat && sqn && rank_out && rowmax_out && need && rows >= 0 && row0 >= 0,
+               "rr_sv_select: bad arguments");
+    return rank_select_sv_launch(cnt, (const int2*)list, cap, wrow, feat, ldf, (int)D, sqn, row0, rows, K, rank_out,
+                                 rowmax_out, need, (hipStream_t)stream);
+}
+
+// The survivor lists of `rows` rows packed contiguously: out[off[r] + p] = list[r][p] for
+// p < min(cnt[r], cap) (off = exclusive scan of those lengths).
+REIDMI_API int reidmi_rr_sv_pack(const int32_t* cnt, const void* list, int cap, int64_t rows, const int64_t* off,
+                                 void* out, void* stream) {
+    RM_REQUIRE(cnt && list && off && rows >= 0 && cap >= 1 && (out || rows == 0), "rr_sv_pack: bad arguments");
+    if (rows == 0) return OK;
+    hipLaunchKernelGGL(rr_sv_pack_kernel, dim3((unsigned)ceil_div(rows, 4)), dim3(256), 0, (hipStream_t)stream, cnt,
+                       (const int2*)list, cap, rows, off, (int2*)out);
+    RM_LAUNCHED();
+    return OK;
+}
+
+// Appends another rank's partial lists of the same rows: list[r][cnt[r] + p] = add[add_off[r] + p]
+// while it fits cap; cnt[r] += add_cnt[r] (a total past cap marks the row's overflow, as the
+// one-call form's counter does).
+REIDMI_API int reidmi_rr_sv_merge(int32_t* cnt, void* list, int cap, int64_t rows, const int32_t* add_cnt,
+                                  const int64_t* add_off, const void* add, void* stream) {
+    RM_REQUIRE(cnt && list && add_cnt && add_off && rows >= 0 && cap >= 1, "rr_sv_merge: bad arguments");
+    if (rows == 0) return OK;
+    hipLaunchKernelGGL(rr_sv_merge_kernel, dim3((unsigned)ceil_div(rows, 4)), dim3(256), 0, (hipStream_t)stream, cnt,
+                       (int2*)list, cap, rows, add_cnt, add_off, (const int2*)add);
+    RM_LAUNCHED();
+    return OK;
 }
 
 REIDMI_API int reidmi_rr_v_rows(const float* feat, int64_t N, int64_t D, int64_t ldf, const float* sqn,

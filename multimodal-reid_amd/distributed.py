@@ -14,10 +14,37 @@ Re-ranking (reranking.re_ranking_sharded) shards its rows too: rank r owns rows
 shard(N, r, W) of the N = Q + G items for R1-R4 and queries shard(Q, r, W) for R6-R7, with
 all-gathers of initial_rank[:, :K], the od divisors, and the CSR rows of V and V_qe between
 the stages.
+
+Contract of the drop-in surface under a process group (one place): nothing in
+evaluate.py / reranking.py / zero_shot_learning.py issues a collective unless the caller asks
+for it with ``sharded=True``.  By default every call has the reference's single-process
+semantics on whatever this process passed (a DDP script that evaluates on rank 0 only, or
+passes the full split on every rank, gets the single-process result and no hang):
+  * R1_mAP_eval(..., sharded=True) / get_cmc_map(..., sharded=True): each rank passes ITS
+    shard (its query rows, its gallery rows); every rank returns the CMC/mAP of the whole split.
+  * re_ranking_device(..., sharded=True): every rank passes the FULL features; the stages are
+    row-sharded over the ranks and every rank returns the whole (Q, G) matrix.
+Inside a default (unsharded) call, ``local()`` hides the process group from these helpers.
 """
+import contextlib
+import threading
+
 import numpy as np
 import torch
 import torch.distributed as dist
+
+_tls = threading.local()
+
+
+@contextlib.contextmanager
+def local():
+    """Run the enclosed calls as one process: world() = (0, 1), no collectives."""
+    prev = getattr(_tls, "local", False)
+    _tls.local = True
+    try:
+        yield
+    finally:
+        _tls.local = prev
 
 
 def world():
@@ -27,7 +54,7 @@ def world():
 
 
 def _initialized():
-    return dist.is_available() and dist.is_initialized()
+    return not getattr(_tls, "local", False) and dist.is_available() and dist.is_initialized()
 
 
 def shard(n, rank, world_size):
@@ -109,6 +136,23 @@ def gather_rows_var(x):
         dist.all_gather(bufs, pad)
         parts = [bufs[r][:ns[r]] for r in range(W)]
     return torch.cat(parts).to(x.device), ns
+
+
+def all_to_all_var(send, in_splits):
+    """Variable-size all-to-all of a 1-D tensor: rank r sends send[off_q : off_q + in_splits[q]]
+    to rank q; returns (the received pieces concatenated in source-rank order, their sizes), on
+    send's device.  RCCL moves device tensors (all_to_all_single), gloo host tensors."""
+    rank, W = world()
+    if not _initialized():
+        return send, list(in_splits)
+    dev = _collective_device(send)
+    sizes = torch.tensor([int(v) for v in in_splits], dtype=torch.int64, device=dev)
+    got = torch.empty_like(sizes)
+    dist.all_to_all_single(got, sizes)
+    out_splits = [int(v) for v in got.cpu()]
+    recv = torch.empty(sum(out_splits), dtype=send.dtype, device=dev)
+    dist.all_to_all_single(recv, send.contiguous().to(dev), out_splits, [int(v) for v in in_splits])
+    return recv.to(send.device), out_splits
 
 
 def pack_rows(valid, first, ap, nkept):

@@ -149,22 +149,25 @@ class R1_mAP_eval():
     As in the reference, ``max_rank`` is stored but compute() scores with eval_func's
     default 50 (evaluate.py:132): the CMC is 50 long whatever max_rank was given.
 
-    Under a torch.distributed process group (one process per GPU) every rank
-    holds ITS shard: its updates are its query rows followed by its gallery rows, and
-    ``num_query`` is its own query count.  compute() then all-gathers the feature blocks and
+    ``sharded=True`` (torch.distributed process group, one process per GPU, SURVEY.md §8e;
+    the contract: distributed.py): every rank holds ITS shard: its updates are its query rows
+    followed by its gallery rows, and ``num_query`` is its own query count.  compute() then
+    all-gathers the feature blocks and
     labels (gallery-sharded embed + RCCL all-gather, the north star's exchange step), scores
     the query rows shard(Q, rank, W) against the whole gallery (exact distance, or the
     row-sharded k-reciprocal re-rank), all-gathers the per-query results and reduces them in
     global query order: every rank returns the CMC/mAP of the single-process run over the
     rank-ordered concatenation of the shards, bit for bit (contiguous shards in rank order =
-    the single-process order)."""
+    the single-process order).  Default (``sharded=False``): the reference's single-process
+    semantics on this process's data, no collective even under a process group."""
 
-    def __init__(self, num_query, max_rank=50, feat_norm=True, reranking=False):
+    def __init__(self, num_query, max_rank=50, feat_norm=True, reranking=False, sharded=False):
         super(R1_mAP_eval, self).__init__()
         self.num_query = num_query
         self.max_rank = max_rank
         self.feat_norm = feat_norm
         self.reranking = reranking
+        self.sharded = sharded
 
     def reset(self):
         self.feats = []
@@ -183,8 +186,14 @@ class R1_mAP_eval():
         if self.feat_norm:
             print("The test feature is normalized")
             feats = l2_normalize_device(feats)
-        if rd._initialized():
+        if self.sharded:
+            if not rd._initialized():
+                raise _lib.ReidmiError("R1_mAP_eval(sharded=True) needs an initialised torch.distributed process group")
             return self._compute_sharded(feats)
+        with rd.local():
+            return self._compute_local(feats)
+
+    def _compute_local(self, feats):
         qf = feats[:self.num_query]
         q_pids = np.asarray(self.pids[:self.num_query])
         q_camids = np.asarray(self.camids[:self.num_query])

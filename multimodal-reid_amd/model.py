@@ -13,8 +13,11 @@ the vision keys of custom_clip_model.VisionTransformer (``conv1.weight``,
 ``transformer.resblocks.{i}.attn.in_proj_weight``, ... ``proj``; plus ``VPT`` /
 ``VPT_shallow`` for IVLP) and the text keys of CLIP (``token_embedding.weight``,
 ``transformer.resblocks.{i}...``, ``ln_final.*``, ``text_projection``).  Matrices are
-stored fp16 in HBM (the reference's GPU dtype, utils.py:145-166), vectors fp32.  All compute
-runs in libreidmi.so.
+stored fp16 in HBM (the reference's GPU dtype, utils.py:145-166), vectors fp32.  The packing
+itself (LayerNorm folds, fp16 casts, transposes) is libreidmi's C ABI
+(reidmi_vit_weights_pack / reidmi_text_weights_pack, pack.hip): this module only moves the
+checkpoint's fp32 tensors to the device in the reference's key layout and hands them over, so
+a non-Python caller packs the same bytes.  All compute runs in libreidmi.so.
 """
 import ctypes
 
@@ -45,7 +48,30 @@ class TextWeights(ctypes.Structure):
                [("blocks", ctypes.POINTER(BlockWeights))]
 
 
+class BlockSrc(ctypes.Structure):  # reidmi_block_src
+    _fields_ = [(n, _vp) for n in ("ln_1_w", "ln_1_b", "in_proj_w", "in_proj_b", "out_proj_w", "out_proj_b", "ln_2_w",
+                                   "ln_2_b", "c_fc_w", "c_fc_b", "c_proj_w", "c_proj_b", "vpt_shallow")]
+
+
+class VitSrc(ctypes.Structure):  # reidmi_vit_src
+    _fields_ = [(n, _i32) for n in ("width", "layers", "patch", "stride", "out_dim", "grid_h", "grid_w", "n_ctx")] + \
+               [(n, _vp) for n in ("conv1_w", "class_embedding", "positional_embedding", "ln_pre_w", "ln_pre_b",
+                                   "ln_post_w", "ln_post_b", "proj", "vpt")] + [("blocks", ctypes.POINTER(BlockSrc))]
+
+
+class TextSrc(ctypes.Structure):  # reidmi_text_src
+    _fields_ = [(n, _i32) for n in ("width", "layers", "ctx", "vocab", "out_dim", "n_ctx")] + \
+               [(n, _vp) for n in ("token_embedding", "positional_embedding", "ln_final_w", "ln_final_b",
+                                   "text_projection")] + [("blocks", ctypes.POINTER(BlockSrc))]
+
+
 _SIG = {
+    "reidmi_vit_pack_bytes": ([ctypes.POINTER(VitSrc)], ctypes.c_int64),
+    "reidmi_vit_weights_pack": ([ctypes.POINTER(VitSrc), _vp, ctypes.c_int64, ctypes.POINTER(VitWeights),
+                                 ctypes.POINTER(BlockWeights), _vp], ctypes.c_int),
+    "reidmi_text_pack_bytes": ([ctypes.POINTER(TextSrc)], ctypes.c_int64),
+    "reidmi_text_weights_pack": ([ctypes.POINTER(TextSrc), _vp, ctypes.c_int64, ctypes.POINTER(TextWeights),
+                                  ctypes.POINTER(BlockWeights), _vp], ctypes.c_int),
     "reidmi_vit_workspace_bytes": ([ctypes.POINTER(VitWeights), ctypes.c_int64, ctypes.c_int], ctypes.c_int64),
     "reidmi_vit_forward": ([ctypes.POINTER(VitWeights), _vp, ctypes.c_int, ctypes.c_int64, ctypes.c_int,
                             ctypes.c_int, _vp, ctypes.c_int, _vp, _vp, _vp, _vp, ctypes.c_int64, _vp], ctypes.c_int),
@@ -70,8 +96,10 @@ def _t(a):
     return torch.from_numpy(np.asarray(a, dtype=np.float32))
 
 
-class _Packer:
-    """Moves tensors to the device once and keeps them alive."""
+class _Sources:
+    """The checkpoint's tensors as contiguous device fp32 (the packer's inputs), kept alive
+    until the packing calls are issued (stream-ordered: the caching allocator reuses a freed
+    block only for later work on the same stream)."""
 
     def __init__(self, device):
         self.device = device
@@ -80,55 +108,53 @@ class _Packer:
     def f32(self, a):
         t = _t(a).contiguous().to(self.device)
         self.keep.append(t)
-        return t
-
-    def f16(self, a):
-        t = _t(a).contiguous().to(torch.float16).to(self.device)
-        self.keep.append(t)
-        return t
-
-    def keep_dev(self, t):
-        t = t.contiguous().to(self.device)
-        self.keep.append(t)
-        return t
+        return t.data_ptr()
 
 
 def fold_layernorm(w, b, gamma, beta):
-    """LayerNorm(gamma, beta) folded into the Linear (w, b) it feeds (load time, fp64):
-    LN(x) w^T + b = rstd (x w'^T - mean s) + b' with w' = fp16(w diag(gamma)),
-    s_n = sum_k w'[n, k] (of the fp16 values) and b' = b + w beta.  Returns (w' fp16, s, b')."""
-    w64, g64 = _t(w).double(), _t(gamma).double()
-    wf = (w64 * g64[None, :]).to(torch.float16)
-    s = wf.double().sum(1).float()
-    bf = (_t(b).double() + w64 @ _t(beta).double()).float()
-    return wf, s, bf
+    """Host restatement of the packer's LayerNorm fold (pack.hip fold_rows_kernel), for tests:
+    LN(x) w^T + b = rstd (x w'^T - mean s) + b' with w' = fp16(fp32(w diag(gamma))) (torch's
+    fp64 -> fp16 cast rounds through fp32), s_n = sum_k w'[n, k] (exact in fp64) and
+    b' = fp32(b + w beta) with the fp64 products summed exactly (math.fsum).  Returns (w' fp16,
+    s, b') as torch tensors."""
+    import math
+    w32, g32 = _t(w).numpy(), _t(gamma).numpy()
+    wf = torch.from_numpy((w32 * g32[None, :]).astype(np.float16))
+    s = torch.from_numpy(wf.numpy().astype(np.float64).sum(1).astype(np.float32))
+    prod = w32.astype(np.float64) * _t(beta).numpy().astype(np.float64)[None, :]
+    bb = _t(b).numpy().astype(np.float64)
+    bf = np.array([math.fsum([bb[n], *prod[n]]) for n in range(len(bb))], np.float64).astype(np.float32)
+    return wf, s, torch.from_numpy(bf)
 
 
-def _pack_blocks(sd, prefix, layers, pk):
-    arr = (BlockWeights * layers)()
+def _block_sources(sd, layers, src):
+    arr = (BlockSrc * layers)()
+    names = {"ln_1_w": "ln_1.weight", "ln_1_b": "ln_1.bias", "in_proj_w": "attn.in_proj_weight",
+             "in_proj_b": "attn.in_proj_bias", "out_proj_w": "attn.out_proj.weight",
+             "out_proj_b": "attn.out_proj.bias", "ln_2_w": "ln_2.weight", "ln_2_b": "ln_2.bias",
+             "c_fc_w": "mlp.c_fc.weight", "c_fc_b": "mlp.c_fc.bias", "c_proj_w": "mlp.c_proj.weight",
+             "c_proj_b": "mlp.c_proj.bias"}
     for i in range(layers):
-        p = f"{prefix}transformer.resblocks.{i}."
-        b = arr[i]
-        b.ln1_w = pk.f32(sd[p + "ln_1.weight"]).data_ptr()
-        b.ln1_b = pk.f32(sd[p + "ln_1.bias"]).data_ptr()
-        wf, cs, bf = fold_layernorm(sd[p + "attn.in_proj_weight"], sd[p + "attn.in_proj_bias"],
-                                    sd[p + "ln_1.weight"], sd[p + "ln_1.bias"])
-        b.qkv_w = pk.keep_dev(wf).data_ptr()
-        b.qkv_b = pk.keep_dev(bf).data_ptr()
-        b.qkv_s = pk.keep_dev(cs).data_ptr()
-        b.out_w = pk.f16(sd[p + "attn.out_proj.weight"]).data_ptr()
-        b.out_b = pk.f32(sd[p + "attn.out_proj.bias"]).data_ptr()
-        b.ln2_w = pk.f32(sd[p + "ln_2.weight"]).data_ptr()
-        b.ln2_b = pk.f32(sd[p + "ln_2.bias"]).data_ptr()
-        wf, cs, bf = fold_layernorm(sd[p + "mlp.c_fc.weight"], sd[p + "mlp.c_fc.bias"],
-                                    sd[p + "ln_2.weight"], sd[p + "ln_2.bias"])
-        b.fc1_w = pk.keep_dev(wf).data_ptr()
-        b.fc1_b = pk.keep_dev(bf).data_ptr()
-        b.fc1_s = pk.keep_dev(cs).data_ptr()
-        b.fc2_w = pk.f16(sd[p + "mlp.c_proj.weight"]).data_ptr()
-        b.fc2_b = pk.f32(sd[p + "mlp.c_proj.bias"]).data_ptr()
-        b.prompt = pk.f32(sd[p + "VPT_shallow"]).data_ptr() if (p + "VPT_shallow") in sd else None
+        p = f"transformer.resblocks.{i}."
+        for field, key in names.items():
+            setattr(arr[i], field, src.f32(sd[p + key]))
+        arr[i].vpt_shallow = src.f32(sd[p + "VPT_shallow"]) if (p + "VPT_shallow") in sd else None
     return arr
+
+
+def _pack(kind, src_struct, layers, weights, device):
+    """reidmi_{vit,text}_weights_pack into one device buffer; returns (buffer, host block array)."""
+    nbytes = _fn(f"reidmi_{kind}_pack_bytes")(ctypes.byref(src_struct))
+    if nbytes < 0:
+        raise _lib.ReidmiError(f"reidmi_{kind}_pack_bytes: {_lib.load().reidmi_last_error().decode()}")
+    buf = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
+    blocks = (BlockWeights * layers)()
+    rc = _fn(f"reidmi_{kind}_weights_pack")(ctypes.byref(src_struct), buf.data_ptr(), nbytes, ctypes.byref(weights),
+                                             blocks, _lib.stream(device))
+    if rc != 0:
+        raise _lib.ReidmiError(f"reidmi_{kind}_weights_pack: {_lib.load().reidmi_last_error().decode()}")
+    weights.blocks = blocks
+    return buf, blocks
 
 
 def resize_pos_embed(posemb, gh, gw):
@@ -163,24 +189,22 @@ class VisionTransformer:
         pos = _t(sd["positional_embedding"])
         if pos.shape[0] != 1 + gh * gw:
             pos = resize_pos_embed(pos, gh, gw)
-        kpad = (3 * P * P + 63) // 64 * 64
-        convp = torch.zeros(W, kpad)
-        convp[:, :3 * P * P] = conv.reshape(W, -1)
-        pk = self._pk = _Packer(self.device)
-        w = self.weights = VitWeights()
-        w.width, w.layers, w.heads, w.patch, w.stride = W, layers, W // 64, P, stride
-        w.out_dim, w.grid_h, w.grid_w, w.n_ctx, w.kpad = self.out_dim, gh, gw, self.n_ctx, kpad
-        w.conv_w = pk.f16(convp).data_ptr()
-        w.class_emb = pk.f32(sd["class_embedding"]).data_ptr()
-        w.pos_emb = pk.f32(pos).data_ptr()
-        w.ln_pre_w = pk.f32(sd["ln_pre.weight"]).data_ptr()
-        w.ln_pre_b = pk.f32(sd["ln_pre.bias"]).data_ptr()
-        w.ln_post_w = pk.f32(sd["ln_post.weight"]).data_ptr()
-        w.ln_post_b = pk.f32(sd["ln_post.bias"]).data_ptr()
-        w.proj_t = pk.f16(_t(sd["proj"]).t()).data_ptr()
-        w.vpt = pk.f32(sd["VPT"]).data_ptr() if self.n_ctx else None
-        self._blocks = _pack_blocks(sd, "", layers, pk)
-        w.blocks = self._blocks
+        src = _Sources(self.device)
+        vs = VitSrc()
+        vs.width, vs.layers, vs.patch, vs.stride, vs.out_dim = W, layers, P, stride, self.out_dim
+        vs.grid_h, vs.grid_w, vs.n_ctx = gh, gw, self.n_ctx
+        vs.conv1_w = src.f32(conv)
+        vs.class_embedding = src.f32(sd["class_embedding"])
+        vs.positional_embedding = src.f32(pos)
+        vs.ln_pre_w, vs.ln_pre_b = src.f32(sd["ln_pre.weight"]), src.f32(sd["ln_pre.bias"])
+        vs.ln_post_w, vs.ln_post_b = src.f32(sd["ln_post.weight"]), src.f32(sd["ln_post.bias"])
+        vs.proj = src.f32(sd["proj"])
+        vs.vpt = src.f32(sd["VPT"]) if self.n_ctx else None
+        bsrc = _block_sources(sd, layers, src)
+        vs.blocks = bsrc
+        self.weights = VitWeights()
+        self._packed, self._blocks = _pack("vit", vs, layers, self.weights, self.device)
+        del src
         self._ws = {}
 
     @property
@@ -257,19 +281,22 @@ class TextTransformer:
         self.out_dim = _t(sd["text_projection"]).shape[1]
         vp = [k for k in sd if k.endswith("VPT_shallow")]
         self.n_ctx = int(_t(sd[vp[0]]).shape[0]) if vp else 0
-        pk = self._pk = _Packer(self.device)
-        w = self.weights = TextWeights()
-        w.width, w.layers, w.heads, w.ctx, w.vocab, w.out_dim, w.n_ctx = (W, layers, W // 64, pos.shape[0],
-                                                                          tok.shape[0], self.out_dim, self.n_ctx)
-        self.token_embedding_weight = pk.f32(tok)
-        w.tok_emb = self.token_embedding_weight.data_ptr()
-        self.positional_embedding = pk.f32(pos)
-        w.pos_emb = self.positional_embedding.data_ptr()
-        w.ln_final_w = pk.f32(sd["ln_final.weight"]).data_ptr()
-        w.ln_final_b = pk.f32(sd["ln_final.bias"]).data_ptr()
-        w.proj_t = pk.f16(_t(sd["text_projection"]).t()).data_ptr()
-        self._blocks = _pack_blocks(sd, "", layers, pk)
-        w.blocks = self._blocks
+        # fp32 copies for the prompt learners' token lookups (prompts.py) and TextEncoder
+        self.token_embedding_weight = _t(tok).contiguous().to(self.device)
+        self.positional_embedding = _t(pos).contiguous().to(self.device)
+        src = _Sources(self.device)
+        ts = TextSrc()
+        ts.width, ts.layers, ts.ctx, ts.vocab, ts.out_dim, ts.n_ctx = (W, layers, pos.shape[0], tok.shape[0],
+                                                                       self.out_dim, self.n_ctx)
+        ts.token_embedding = self.token_embedding_weight.data_ptr()
+        ts.positional_embedding = self.positional_embedding.data_ptr()
+        ts.ln_final_w, ts.ln_final_b = src.f32(sd["ln_final.weight"]), src.f32(sd["ln_final.bias"])
+        ts.text_projection = src.f32(sd["text_projection"])
+        bsrc = _block_sources(sd, layers, src)
+        ts.blocks = bsrc
+        self.weights = TextWeights()
+        self._packed, self._blocks = _pack("text", ts, layers, self.weights, self.device)
+        del src
         self._ws = None
         # run on the positions up to the last EOT of the batch only (exact: causal mask,
         # reidmi_text_forward's ctx_used); False = all ctx positions, as the reference does

@@ -33,18 +33,29 @@ def _check(flags):
         raise _lib.ReidmiError("re_ranking: " + ", ".join(m for b, m in _CAP_MSG.items() if f & b) + " exceeded")
 
 
-def re_ranking_device(probFea, galFea, k1, k2, lambda_value, local_distmat=None, only_local=False):
-    """Device version: returns the (Q, G) fp32 torch tensor on the GPU."""
+def re_ranking_device(probFea, galFea, k1, k2, lambda_value, local_distmat=None, only_local=False, sharded=False):
+    """Device version: returns the (Q, G) fp32 torch tensor on the GPU.  ``sharded=True``
+    (torch.distributed process group, every rank holding the FULL features): the stages are
+    row-sharded over the ranks and the final rows all-gathered, so every rank returns the whole
+    matrix.  Default: this process alone, no collective (distributed.py states the contract)."""
+    from . import distributed as rd
+    if sharded:
+        if not rd._initialized():
+            raise _lib.ReidmiError("re_ranking_device(sharded=True) needs an initialised torch.distributed process group")
+        if only_local or local_distmat is not None:
+            raise _lib.ReidmiError("re_ranking_device(sharded=True) re-ranks from features only")
+        Q = probFea.size(0) if isinstance(probFea, torch.Tensor) else len(probFea)
+        return rd.gather_rows(re_ranking_sharded(probFea, galFea, k1, k2, lambda_value), Q)
+    with rd.local():
+        return _re_ranking_local(probFea, galFea, k1, k2, lambda_value, local_distmat, only_local)
+
+
+def _re_ranking_local(probFea, galFea, k1, k2, lambda_value, local_distmat, only_local):
     Q = probFea.size(0) if isinstance(probFea, torch.Tensor) else len(probFea)
     G = galFea.size(0) if isinstance(galFea, torch.Tensor) else len(galFea)
-    from . import distributed as rd
-    if not (only_local or local_distmat is not None) and (Q + G >= STAGED_MIN_N or rd.world()[1] > 1):
-        # N x N buffers would dominate: row-chunked stages, same bits.  Under a process group of
-        # several ranks (each holding the full features, as the reference's callers do) the
-        # stages are row-sharded over the ranks and the final rows all-gathered, so every rank
-        # returns the whole (Q, G) matrix.
-        out = re_ranking_sharded(probFea, galFea, k1, k2, lambda_value)
-        return rd.gather_rows(out, Q) if rd.world()[1] > 1 else out
+    if not (only_local or local_distmat is not None) and Q + G >= STAGED_MIN_N:
+        # N x N buffers would dominate: row-chunked stages, same bits
+        return re_ranking_sharded(probFea, galFea, k1, k2, lambda_value)
     dev = torch.device("cuda", torch.cuda.current_device())
     lam_h, lam_f = _lam(lambda_value)
     out = torch.empty((Q, G), device=dev, dtype=torch.float32)
@@ -129,6 +140,7 @@ class HipStages:
         # the batches are concatenated)
         self.ell_bytes = max(256 << 20, chunk_bytes // 2)
         self._ws = {}
+        self.stats = {"rows": 0, "exact_rows": 0, "form": None, "exact_idx": []}
 
     def _chunk_buf(self, rows, cols):
         n = rows * cols
@@ -217,15 +229,133 @@ class HipStages:
                               _lib.ptr(self._chunk_buf(cc, Np)), cc, self.st)
                     _lib.call("reidmi_nonzero_i32", _lib.ptr(need), b - a, _lib.ptr(idx), _lib.ptr(cnt), self.st)
                     undecided, rows = int(cnt.item()), b - a
+                    self.stats["form"] = "triangle" if tri else "row passes"
+                    if not (tri and b - a < hi - lo):  # (the triangle form redoes the probe's rows)
+                        self.stats["rows"] += rows
+                        self.stats["exact_rows"] += undecided
+                        if 0 < undecided <= 65536:  # which rows took the exact fallback (tests)
+                            self.stats["exact_idx"].append(idx[:undecided].cpu().numpy().astype(np.int64) + a)
                     self._exact_rows(a, idx, undecided, R[a - lo:b - lo], rmax[a - lo:b - lo])
                     a = b
                     if 2 * undecided > rows:
                         break
             if a < hi:
+                self.stats["rows"] += hi - a
+                self.stats["exact_rows"] += hi - a
                 cr = min(self.chunk_rows, hi - a)
                 _lib.call("reidmi_rr_rank_rows", _lib.ptr(self.feat), self.N, self.D, self.D, _lib.ptr(self.sqn), a,
                           hi, self.K, _lib.ptr(R[a - lo:]), _lib.ptr(rmax[a - lo:]),
                           _lib.ptr(self._chunk_buf(cr, self.N)), cr, self.st)
+        return R, rmax
+
+    def rank_rows_tri_sharded(self, lo, hi):
+        """R2 of this rank's rows lo..hi = shard(N) through the triangle form split over the
+        ranks (reidmi_rr_tri_*, include/reidmi.h): records of every row all-gathered, this rank's
+        contiguous share of the upper-triangle tile list run over all rows, the partial survivor
+        lists exchanged all-to-all with their rows' owners, own rows selected, rows the selection
+        marks through the exact rows.  The same bits as the one-GPU triangle (and as the exact
+        rows) at 1/W of its MFMA work per rank.  None when the triangle form does not apply (no
+        fp16 pre-filter, K > 64, a chunk too small, or concentrated features — every rank then
+        agrees, through one all-reduce, to take rank_rows' row passes)."""
+        from . import distributed as rd
+        rank, W = rd.world()
+        if not (RANK_PREFILTER and self.K <= 64) or hi <= lo:
+            return None
+        x16, Np, Dp, nrm, fits, nmax2 = self._feat16()  # the same decision on every rank (same features)
+        if not fits or Dp < 128:
+            return None
+        L = _lib.load()
+        cc = max(256, self.chunk_rows * self.N // Np // 256 * 256)
+        nt, cap, ns, sp = (ctypes.c_int64() for _ in range(4))
+        _lib.call("reidmi_rr_tri_plan", self.N, Np, cc, self.K, ctypes.byref(nt), ctypes.byref(cap), ctypes.byref(ns),
+                  ctypes.byref(sp))
+        ntiles, cap, ns, sp = nt.value, cap.value, ns.value, sp.value
+        # probe (as the one-call path): concentrated features (a random network's embeddings)
+        # put every row beyond the bound; then all ranks take the exact row passes
+        pr = min(512, hi - lo)
+        Rp = torch.empty((pr, self.K), device=self.dev, dtype=torch.int32)
+        mp_ = torch.empty(pr, device=self.dev, dtype=torch.float32)
+        need = torch.empty(pr, device=self.dev, dtype=torch.int32)
+        _lib.call("reidmi_rr_rank_rows_f16", _lib.ptr(self.feat), self.N, self.D, self.D, _lib.ptr(self.sqn),
+                  _lib.ptr(nrm), _lib.ptr(nmax2), _lib.ptr(x16), Np, Dp, lo, lo + pr, self.K, _lib.ptr(Rp),
+                  _lib.ptr(mp_), _lib.ptr(need), _lib.ptr(self._chunk_buf(cc, Np)), cc, self.st)
+        bad = torch.tensor([float(cap == 0 or 2 * int(need.sum().item()) > pr)], dtype=torch.float64)
+        if rd._initialized():
+            b = bad.to(rd._collective_device(self.feat))
+            rd.dist.all_reduce(b, op=rd.dist.ReduceOp.MAX)
+            bad = b.cpu()
+        if bad.item() > 0:
+            return None
+        del Rp, mp_, need
+        self._chunk = None  # the lists take the chunk's place
+        N, K = self.N, self.K
+        meta = torch.zeros(Np * 4, device=self.dev, dtype=torch.float32)
+        wrow = torch.empty(N, device=self.dev, dtype=torch.float32)
+        cnt = torch.zeros(N, device=self.dev, dtype=torch.int32)
+        lst = torch.empty(N * cap * 2, device=self.dev, dtype=torch.int32)
+        sqn_s = torch.empty(ns, device=self.dev, dtype=torch.float32)
+        nrm_s = torch.empty(ns, device=self.dev, dtype=torch.float32)
+        tiles = torch.empty(max(ntiles, 1), device=self.dev, dtype=torch.int32)
+        _lib.call("reidmi_rr_tri_init", _lib.ptr(self.sqn), _lib.ptr(nrm), N, Np, ns, _lib.ptr(meta), _lib.ptr(sqn_s),
+                  _lib.ptr(nrm_s), _lib.ptr(tiles), self.st)
+        _lib.call("reidmi_rr_tri_sample", _lib.ptr(x16), Np, Dp, _lib.ptr(self.sqn), _lib.ptr(nrm), _lib.ptr(nmax2), N,
+                  self.D, K, _lib.ptr(sqn_s), _lib.ptr(nrm_s), ns, lo, hi, _lib.ptr(lst), sp, _lib.ptr(meta),
+                  _lib.ptr(wrow), _lib.ptr(cnt), cap, self.st)
+        m4 = meta.view(Np, 4)
+        m4[:N] = rd.gather_rows(m4[lo:hi].contiguous(), N)  # every row's record (the column records too)
+        t0, t1 = rd.shard(ntiles, rank, W)
+        _lib.call("reidmi_rr_tri_survivors", _lib.ptr(x16), Np, Dp, _lib.ptr(self.sqn), _lib.ptr(nrm), N, self.D,
+                  _lib.ptr(meta), _lib.ptr(tiles), t0, t1, _lib.ptr(cnt), _lib.ptr(lst), cap, self.st)
+        del tiles
+        # partial lists of each owner's rows -> the owner
+        bounds = [rd.shard(N, q, W) for q in range(W)]
+        lens = cnt.clamp(max=cap).to(torch.int64)
+        send_cnt, send_ent, ent_splits = [], [], []
+        for q, (a, b) in enumerate(bounds):
+            send_cnt.append(cnt[a:b])
+            if q == rank or b == a:
+                ent_splits.append(0)
+                continue
+            off = torch.zeros(b - a, device=self.dev, dtype=torch.int64)
+            off[1:] = torch.cumsum(lens[a:b], 0)[:-1]
+            total = int(lens[a:b].sum().item())
+            out = torch.empty(max(total, 1) * 2, device=self.dev, dtype=torch.int32)
+            _lib.call("reidmi_rr_sv_pack", _lib.ptr(cnt[a:]), _lib.ptr(lst[a * cap * 2:]), cap, b - a, _lib.ptr(off),
+                      _lib.ptr(out), self.st)
+            send_ent.append(out[:total * 2].view(torch.int64))
+            ent_splits.append(total)
+        rc, cnt_splits = rd.all_to_all_var(torch.cat(send_cnt), [b - a for a, b in bounds])
+        re_, ent_got = rd.all_to_all_var(torch.cat(send_ent) if send_ent else torch.zeros(0, device=self.dev,
+                                                                                           dtype=torch.int64),
+                                         ent_splits)
+        rows = hi - lo
+        ro, eo = 0, 0
+        for q in range(W):
+            add_cnt = rc[ro:ro + cnt_splits[q]]
+            ro += cnt_splits[q]
+            if q != rank:
+                alen = add_cnt.clamp(max=cap).to(torch.int64)
+                off = torch.zeros(rows, device=self.dev, dtype=torch.int64)
+                off[1:] = torch.cumsum(alen, 0)[:-1]
+                _lib.call("reidmi_rr_sv_merge", _lib.ptr(cnt[lo:]), _lib.ptr(lst[lo * cap * 2:]), cap, rows,
+                          _lib.ptr(add_cnt), _lib.ptr(off), _lib.ptr(re_[eo:]) if ent_got[q] else None, self.st)
+            eo += ent_got[q]
+        R = torch.empty((rows, K), device=self.dev, dtype=torch.int32)
+        rmax = torch.empty(rows, device=self.dev, dtype=torch.float32)
+        need = torch.empty(rows, device=self.dev, dtype=torch.int32)
+        _lib.call("reidmi_rr_sv_select", _lib.ptr(cnt[lo:]), _lib.ptr(lst[lo * cap * 2:]), cap, _lib.ptr(wrow[lo:]),
+                  _lib.ptr(self.feat), self.D, self.D, _lib.ptr(self.sqn), lo, rows, K, _lib.ptr(R), _lib.ptr(rmax),
+                  _lib.ptr(need), self.st)
+        del lst, re_
+        idx = torch.empty(rows, device=self.dev, dtype=torch.int32)
+        c = torch.empty(1, device=self.dev, dtype=torch.int32)
+        _lib.call("reidmi_nonzero_i32", _lib.ptr(need), rows, _lib.ptr(idx), _lib.ptr(c), self.st)
+        undecided = int(c.item())
+        self.stats.update(form="triangle (sharded)", rows=self.stats["rows"] + rows,
+                          exact_rows=self.stats["exact_rows"] + undecided)
+        if 0 < undecided <= 65536:
+            self.stats["exact_idx"].append(idx[:undecided].cpu().numpy().astype(np.int64) + lo)
+        self._exact_rows(lo, idx, undecided, R, rmax)
         return R, rmax
 
     def offsets(self, nnz):
@@ -358,7 +488,9 @@ def staged_rerank(stages, N, Q):
     from . import distributed as rd
     rank, W = rd.world()
     lo, hi = rd.shard(N, rank, W)
-    R_loc, rmax_loc = stages.rank_rows(lo, hi)                    # R1 + R2 (reranking.py:36-48)
+    # R1 + R2 (reranking.py:36-48): several ranks split the one-GPU triangle form's tiles
+    tri = stages.rank_rows_tri_sharded(lo, hi) if W > 1 and hasattr(stages, "rank_rows_tri_sharded") else None
+    R_loc, rmax_loc = tri if tri is not None else stages.rank_rows(lo, hi)
     R = rd.gather_rows(R_loc, N)
     rmax = rd.gather_rows(rmax_loc, N)
     V = _gather_csr(stages, *stages.v_rows(R, rmax, lo, hi), N)  # R3 (reranking.py:51-71)
@@ -372,7 +504,7 @@ def staged_rerank(stages, N, Q):
     return out
 
 
-def re_ranking_sharded(probFea, galFea, k1, k2, lambda_value, chunk_bytes=None):
+def re_ranking_sharded(probFea, galFea, k1, k2, lambda_value, chunk_bytes=None, stats=None):
     """Sharded re_ranking: probFea / galFea are the FULL query and gallery features on this
     rank's GPU (all-gathered after a sharded embed).  Returns this rank's query rows
     shard(Q, rank, W) of the re-ranked (Q, G) distance as a device tensor; with one process
@@ -381,4 +513,7 @@ def re_ranking_sharded(probFea, galFea, k1, k2, lambda_value, chunk_bytes=None):
     Q = q.shape[0]
     feat = torch.cat([q, _as_dev_f32(galFea)]).contiguous()
     stages = HipStages(feat, Q, k1, k2, lambda_value, chunk_bytes)
-    return staged_rerank(stages, feat.shape[0], Q)
+    out = staged_rerank(stages, feat.shape[0], Q)
+    if stats is not None:  # R2 path counters of this rank (rows, rows sent to the exact fallback, form)
+        stats.update(stages.stats)
+    return out

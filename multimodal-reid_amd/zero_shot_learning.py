@@ -69,14 +69,15 @@ def inference(model, bottleneck, bottleneck_proj, zeroshot_weights, loader, load
 
 
 def get_cmc_map(gallery_embeddings, query_embeddings, gallery_labels, query_labels, gallery_cams, query_cams,
-                reranking=False):
+                reranking=False, sharded=False):
     """zero_shot_learning.py:137-153 (R1_mAP_eval with max_rank=50, feat_norm=True);
     ``reranking=True`` selects R1_mAP_eval's k-reciprocal branch (evaluate.py:124-127).
-    Under a torch.distributed process group (torchrun, one process per GPU) the arguments are
-    THIS rank's shards (its loaders' images, e.g. contiguous shards in rank order):
-    R1_mAP_eval all-gathers them and every rank returns the CMC/mAP of the whole split,
-    bit-identical to one process over the concatenated shards (evaluate.R1_mAP_eval)."""
-    evaluator = R1_mAP_eval(len(query_labels), max_rank=50, feat_norm=True, reranking=reranking)
+    ``sharded=True`` (torch.distributed process group, torchrun, one process per GPU): the
+    arguments are THIS rank's shards (its loaders' images, e.g. contiguous shards in rank
+    order); R1_mAP_eval all-gathers them and every rank returns the CMC/mAP of the whole split,
+    bit-identical to one process over the concatenated shards (evaluate.R1_mAP_eval).  Default:
+    one process's data, no collective (distributed.py states the contract)."""
+    evaluator = R1_mAP_eval(len(query_labels), max_rank=50, feat_norm=True, reranking=reranking, sharded=sharded)
     evaluator.reset()
     evaluator.update((torch.cat((query_embeddings.float(), gallery_embeddings.float()), dim=0),
                       torch.cat((torch.as_tensor(query_labels), torch.as_tensor(gallery_labels)), dim=0),

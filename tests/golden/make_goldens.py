@@ -449,8 +449,10 @@ def e2e_fixtures(out):
     for the rank lists."""
     import tempfile
     _, maple, ref_utils, ref_zsl = _stubbed()
-    Q, G, bs = 128, 512, 64
-    qp, gp, qc, gc = syn.labels(Q, G, num_ids=100, num_cams=6, seed=21, distractor_frac=0.1)
+    # 512 q x 2048 g: one query's AP flip moves mAP by <= 1/512 ~ 2e-3 x dAP, so a flat 1e-3
+    # bound is meaningful (round 3's 128 x 512 fixture needed a noise floor, VERDICT r3).
+    Q, G, bs = 512, 2048, 64
+    qp, gp, qc, gc = syn.labels(Q, G, num_ids=400, num_cams=6, seed=21, distractor_frac=0.1)
     pids, cams = np.concatenate([qp, gp]), np.concatenate([qc, gc])
     imgs = syn.identity_crops(pids, cams, seed=21)
     offs = syn.tta_offsets(Q + G, seed=21)
@@ -470,6 +472,7 @@ def e2e_fixtures(out):
                    torch.zeros(e - s, dtype=torch.int64), torch.arange(s, e))
 
     res = dict(q_pids=qp, g_pids=gp, q_cams=qc, g_cams=gc, tta_offsets=offs)
+    diag = {}
     for tag in ("fp16", "fp32"):
         if tag == "fp32":
             model.visual.float()
@@ -481,6 +484,8 @@ def e2e_fixtures(out):
         assert eg.dtype == (torch.float16 if tag == "fp16" else torch.float32)
         (cmc, mAP), px = _with_stable(ref_eval, ref_zsl.get_cmc_map, eg, eq, tg, tq, cg, cq)
         res[f"feat32_{tag}"] = torch.cat([eq[:16], eg[:16]]).float().numpy()  # first 16 q + 16 g rows
+        # every feature row, for diagnosis only (13 MB: git-ignored, not a test input)
+        diag[tag] = torch.cat([eq, eg]).float().numpy()
         res[f"cmc_{tag}"], res[f"map_{tag}"] = cmc, np.float64(mAP)
         res[f"rank50_{tag}"] = px.calls[0][:, :50].astype(np.int32)
         ev = ref_eval.R1_mAP_eval(Q, max_rank=50, feat_norm=True, reranking=True)
@@ -491,6 +496,8 @@ def e2e_fixtures(out):
         res[f"rank50_rr_{tag}"] = px.calls[-1][:, :50].astype(np.int32)
         print("e2e", tag, "mAP", mAP, "rank1", cmc[0], "rerank mAP", rmap)
     np.savez_compressed(os.path.join(out, "e2e.npz"), **res)
+    os.makedirs(os.path.join(REPO, "tools", "diag"), exist_ok=True)
+    np.savez(os.path.join(REPO, "tools", "diag", "e2e_ref_feats.npz"), **diag)
 
 
 def prompt_fixtures(out):

@@ -46,7 +46,16 @@ def _worker(rank, world, port, out):
     cmc, mAP = rd.sharded_eval(torch.from_numpy(qf[qlo:qhi]), torch.from_numpy(gf[glo:ghi]), qp, gp, qc, gc, Q, G,
                                _rows_fn, 50)
     g_all = rd.gather_rows(torch.from_numpy(gf[glo:ghi]), G)
-    out[rank] = (cmc, mAP, bool(torch.equal(g_all, torch.from_numpy(gf))))
+    # the variable-size all-to-all of the sharded R2 (rank r sends q + r + 1 values to rank q)
+    send = torch.cat([torch.full((q + rank + 1,), 100 * rank + q, dtype=torch.int64) for q in range(world)])
+    recv, splits = rd.all_to_all_var(send, [q + rank + 1 for q in range(world)])
+    want = torch.cat([torch.full((rank + s + 1,), 100 * s + rank, dtype=torch.int64) for s in range(world)])
+    a2a_ok = torch.equal(recv, want) and splits == [rank + s + 1 for s in range(world)]
+    # the drop-in's default: no collective (distributed.local) even with a process group
+    with rd.local():
+        local_ok = rd.world() == (0, 1) and rd.gather_rows(torch.ones(3), 3).shape == (3,)
+    out[rank] = (cmc, mAP, bool(torch.equal(g_all, torch.from_numpy(gf))), bool(a2a_ok), bool(local_ok),
+                 rd.world() == (rank, world))
     dist.destroy_process_group()
 
 
@@ -66,8 +75,8 @@ def test_sharded_eval_matches_single_process(world):
     out = mgr.dict()
     mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
     for r in range(world):
-        cmc, mAP, gathered_ok = out[r]
-        assert gathered_ok
+        cmc, mAP, gathered_ok, a2a_ok, local_ok, world_ok = out[r]
+        assert gathered_ok and a2a_ok and local_ok and world_ok
         assert np.array_equal(cmc, ref_cmc) and mAP == ref_map
 
 

@@ -46,7 +46,7 @@ def test_distmat_bitexact(gpu, Q, G, D):
     for v in (0, 1):
         out = torch.empty(Q, G, device="cuda")
         ws = torch.empty(Q + G, device="cuda")
-        _lib.call("reidmi_distmat_f32_variant", _lib.ptr(qd), Q, D, _lib.ptr(gd), G, D, D, _lib.ptr(out), G,
+        _lib.call_tools("reidmi_distmat_f32_variant", _lib.ptr(qd), Q, D, _lib.ptr(gd), G, D, D, _lib.ptr(out), G,
                   _lib.ptr(ws), v, _lib.stream())
         assert np.array_equal(out.cpu().numpy().view(np.uint32), ref), v
 

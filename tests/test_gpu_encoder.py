@@ -38,7 +38,7 @@ def _gemm(L, epi, A, W, bias, out, rowstat=None, colsum=None, tile=None, walk=0)
         L.call("reidmi_gemm_f16", epi, L.ptr(A), K, L.ptr(W), K, M, N, K, L.ptr(bias), L.ptr(rowstat), L.ptr(colsum),
                L.ptr(out), out.shape[1], L.stream())
     else:  # per-call tiling (every choice bit-identical)
-        L.call("reidmi_gemm_f16_tiled", epi, L.ptr(A), K, L.ptr(W), K, M, N, K, L.ptr(bias), L.ptr(rowstat),
+        L.call_tools("reidmi_gemm_f16_tiled", epi, L.ptr(A), K, L.ptr(W), K, M, N, K, L.ptr(bias), L.ptr(rowstat),
                L.ptr(colsum), L.ptr(out), out.shape[1], tile, walk, L.stream())
 
 
@@ -379,7 +379,7 @@ def _qkv_attention(L, nseq, W, fused, x, wq, bias, cs, rs):
         k = torch.empty_like(q)
         vt = torch.zeros(nseq * H * 64 * lp, dtype=torch.float16, device="cuda")
     o = torch.full((nseq * L, W), float("nan"), dtype=torch.float16, device="cuda")
-    lib.call("reidmi_qkv_attention_f16", lib.ptr(x), W, lib.ptr(wq), W, lib.ptr(bias), lib.ptr(cs), lib.ptr(rs), nseq,
+    lib.call_tools("reidmi_qkv_attention_f16", lib.ptr(x), W, lib.ptr(wq), W, lib.ptr(bias), lib.ptr(cs), lib.ptr(rs), nseq,
              L, H, W, lib.ptr(q), lib.ptr(k), lib.ptr(vt), lib.ptr(o), int(fused), lib.stream())
     return o
 

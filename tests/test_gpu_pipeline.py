@@ -8,8 +8,8 @@ functions (tests/golden/make_goldens.py with the refstubs/ import stand-ins):
   * utils.model_adaptor on a CLIP-ReID checkpoint file (§8f-2; utils.py:169-262)
   * cosine_similarity (X1; evaluate.py:16-26)
   * end-to-end accuracy: model_adaptor -> inference (plain + TTA) -> get_cmc_map /
-    R1_mAP_eval(reranking=True) on identity-structured crops (north star: mAP within 1e-3,
-    rank lists)
+    R1_mAP_eval(reranking=True) on 512 q x 2048 g identity-structured crops (north star: mAP
+    within a flat 1e-3 of the reference's fp32 run, plain and re-ranked; rank lists)
 
 Feature tolerances are those of tests/test_gpu_encoder.py: max |err| against the reference's
 fp32 outputs <= 1.5 x the reference's own fp16-vs-fp32 deviation on the same inputs (the
@@ -178,30 +178,38 @@ def _topk_agree(rank_a, rank_b, k):
 
 
 def test_end_to_end_accuracy_vs_reference(gpu):
-    """North-star claim on identity-structured crops (128 q x 512 g, 2 passes each).
-    The reference ran its own pipeline twice, in fp32 (its exact arithmetic) and in its GPU
-    dtype (fp16); the two differ by dmAP_ref (~1e-3 here).  Ours must be within 1e-3 of the
-    fp32 run's mAP and within dmAP_ref + 1e-3 of the fp16 run's (plain and re-ranked), match
-    their rank-1, and agree with the fp32 run's top-10 lists at least as often as the
-    reference's fp16 run does (minus one query)."""
+    """North-star claim (BASELINE.json: mAP within 1e-3 of the reference) on identity-structured
+    crops, 512 q x 2048 g, 2 passes each (one query's AP flip moves mAP by ~2e-3 x dAP, so the
+    bound is meaningful at this size).  The reference ran its own pipeline twice
+    (tests/golden/make_goldens.py e2e_fixtures): in fp32 (its exact arithmetic) and in its GPU
+    dtype (fp16), which differ by 5.0e-4 (plain) / 7.7e-4 (re-ranked) here.  Ours must be within
+    a flat 1e-3 of the fp32 run's mAP, plain and re-ranked (R1_mAP_eval's k-reciprocal branch,
+    evaluate.py:124-127), rank-1 within the reference's own fp16 deviation plus one query, and
+    agree with the fp32 run's top-10 lists at least as often as the reference's fp16 run does
+    (minus one query)."""
     from multimodal_reid_amd import evaluate, utils
     from multimodal_reid_amd import zero_shot_learning as zsl
     g = golden("e2e.npz")
     qp, gp, qc, gc = g["q_pids"], g["g_pids"], g["q_cams"], g["g_cams"]
     Q, G = len(qp), len(gp)
+    assert (Q, G) == (512, 2048)
     imgs = syn.identity_crops(np.concatenate([qp, gp]), np.concatenate([qc, gc]), seed=21)
     offs = g["tta_offsets"]
     model, _, _ = utils.model_adaptor(None, 256, 128, syn.clipreid_checkpoint("ViT-B/16", seed=20))
     feats = _embed_all(model, imgs, offs)
     fsel = torch.cat([feats[:16], feats[Q:Q + 16]]).cpu().numpy()
     close_to_reference(fsel, {"f": g["feat32_fp32"], "f_fp16": g["feat32_fp16"]}, "f")  # TTA-averaged features
-    cmc, mAP = zsl.get_cmc_map(feats[Q:], feats[:Q], torch.from_numpy(gp), torch.from_numpy(qp),
-                               torch.from_numpy(gc), torch.from_numpy(qc))
-    d_ref = abs(float(g["map_fp16"]) - float(g["map_fp32"]))
-    for tag, tol in (("fp32", 1e-3), ("fp16", d_ref + 1e-3)):
-        assert abs(mAP - float(g[f"map_{tag}"])) <= tol, (tag, mAP, float(g[f"map_{tag}"]), tol)
-        assert cmc[0] == g[f"cmc_{tag}"][0]
-    assert cmc.shape == (50,)
+    args = (feats[Q:], feats[:Q], torch.from_numpy(gp), torch.from_numpy(qp), torch.from_numpy(gc), torch.from_numpy(qc))
+    cmc, mAP = zsl.get_cmc_map(*args)
+    rcmc, rmap = zsl.get_cmc_map(*args, reranking=True)
+    print(f"e2e: mAP {mAP:.5f} (ref fp32 {float(g['map_fp32']):.5f}, fp16 {float(g['map_fp16']):.5f}); "
+          f"re-ranked mAP {rmap:.5f} (ref fp32 {float(g['map_rr_fp32']):.5f}, fp16 {float(g['map_rr_fp16']):.5f}); "
+          f"rank-1 {cmc[0]:.5f} / {rcmc[0]:.5f} (ref fp32 {g['cmc_fp32'][0]:.5f} / {g['cmc_rr_fp32'][0]:.5f})")
+    assert cmc.shape == (50,) and rcmc.shape == (50,)
+    for c, m, key in ((cmc, mAP, ""), (rcmc, rmap, "rr_")):
+        assert abs(m - float(g[f"map_{key}fp32"])) <= 1e-3, (key, m, float(g[f"map_{key}fp32"]))
+        d_ref = abs(float(g[f"cmc_{key}fp16"][0]) - float(g[f"cmc_{key}fp32"][0]))
+        assert abs(float(c[0]) - float(g[f"cmc_{key}fp32"][0])) <= d_ref + 1.0 / Q + 1e-7, (key, c[0])
     n = evaluate.l2_normalize_device(feats)
     dist = evaluate.euclidean_distance_device(n[:Q], n[Q:])
     ours = evaluate.topk_rows_device(dist, 50).cpu().numpy()
@@ -209,30 +217,6 @@ def test_end_to_end_accuracy_vs_reference(gpu):
     a_ours = _topk_agree(ours, g["rank50_fp32"], 10)
     assert a_ours >= a_ref - 1.0 / Q, (a_ours, a_ref)
     assert _topk_agree(ours, g["rank50_fp32"], 1) >= _topk_agree(g["rank50_fp16"], g["rank50_fp32"], 1) - 1.0 / Q
-    # k-reciprocal branch of R1_mAP_eval (evaluate.py:124-127).  The re-ranked mAP is a
-    # discontinuous function of the features (k-reciprocal sets flip): at this size three builds
-    # whose attention outputs differ in the rounding of 1 value in ~36 000 (1 fp16 ulp) gave
-    # 0.3016 / 0.3027 / 0.3038 with identical feature error (profiles/r03/e2e_rounding_ab.txt),
-    # and the reference's own fp16 run sits d_rr = 0.0013 from its fp32 run.  The bound adds the
-    # noise floor measured here: the largest re-ranked mAP change that a relative perturbation
-    # of 2^-12 (half an fp16 ulp) of our own features produces, over 3 seeds.
-    def rr_map(f):
-        return zsl.get_cmc_map(f[Q:], f[:Q], torch.from_numpy(gp), torch.from_numpy(qp), torch.from_numpy(gc),
-                               torch.from_numpy(qc), reranking=True)[1]
-    rmap = rr_map(feats)
-    floor = 0.0
-    for seed in range(3):
-        gen = torch.Generator(device=feats.device).manual_seed(seed)
-        eps = (torch.rand(feats.shape, generator=gen, device=feats.device) * 2 - 1) * 2.0 ** -12
-        floor = max(floor, abs(rr_map(feats * (1 + eps)) - rmap))
-    assert floor < 5e-3, floor  # a perturbation this small must not move the metric further
-    d_rr = abs(float(g["map_rr_fp16"]) - float(g["map_rr_fp32"]))
-    for tag, tol in (("fp32", 1e-3 + floor), ("fp16", d_rr + 1e-3 + floor)):
-        assert abs(rmap - float(g[f"map_rr_{tag}"])) <= tol, (tag, rmap, float(g[f"map_rr_{tag}"]), tol, floor)
-    print(f"e2e: mAP {mAP:.5f} (ref fp32 {float(g['map_fp32']):.5f}, fp16 {float(g['map_fp16']):.5f}); "
-          f"top-10 agreement with ref fp32 {a_ours:.3f} (ref fp16 {a_ref:.3f}); "
-          f"re-rank mAP {rmap:.5f} (ref {float(g['map_rr_fp32']):.5f} / {float(g['map_rr_fp16']):.5f}; "
-          f"half-ulp noise floor {floor:.5f})")
 
 
 @pytest.mark.parametrize("kind", ["coop", "vl"])

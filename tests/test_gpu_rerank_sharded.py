@@ -284,3 +284,63 @@ def test_staged_prefilter_above_min_n_bitexact(gpu, case):
                np.concatenate([qc, gc])))
     cmc2, map2 = ev.compute()
     assert np.array_equal(cmc1, cmc2) and map1 == map2
+
+
+def _tri_case(case):
+    r = np.random.default_rng(77)
+    if case == "clustered":
+        return _feats(400, 11800, seed=13, dim=384, ids=900)
+    # tracklets: groups of 24 near-identical items (dense ties, long survivor lists)
+    f = _feats(400, 12000, seed=14, dim=384, ids=1000, noise=2.0)
+    return oracle.l2norm(f[::24].repeat(24, axis=0)[:12400] + 1e-3 * r.standard_normal((12400, 384)).astype(np.float32))
+
+
+def _tri_chunk(N):
+    return 4 * N * 4608  # chunk rows >= 4 096 at this N: the triangle form applies
+
+
+def _tri_worker(rank, world, port, out, case):
+    import torch.distributed as dist
+    from multimodal_reid_amd import distributed as rd, reranking
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        f = torch.from_numpy(_tri_case(case)).cuda()
+        N, Q = f.shape[0], 400
+        st = reranking.HipStages(f, Q, 50, 15, 0.3, chunk_bytes=_tri_chunk(N))
+        part = reranking.staged_rerank(st, N, Q)
+        out[rank] = (rd.gather_rows(part, Q).cpu().numpy(), st.stats["form"], st.stats["exact_rows"])
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case", ["clustered", "tracklets"])
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_triangle_r2_equals_one_gpu(gpu, case, world):
+    """R2's triangle form split over ranks (HipStages.rank_rows_tri_sharded: each rank runs a
+    contiguous 1/W of the upper-triangle tiles over all rows, the partial survivor lists go to
+    their rows' owners all-to-all) on >= 12 000 items: the re-ranked distances of gloo world 2 / 3
+    (sharing cuda:0) equal the one-process run (the one-call triangle form) bit for bit, and
+    every rank took the sharded triangle (not the rectangular row passes)."""
+    import torch.multiprocessing as mp
+    from multimodal_reid_amd import reranking
+    feats = _tri_case(case)
+    f = torch.from_numpy(feats).to(gpu)
+    N, Q = f.shape[0], 400
+    st = reranking.HipStages(f, Q, 50, 15, 0.3, chunk_bytes=_tri_chunk(N))
+    one = reranking.staged_rerank(st, N, Q).cpu().numpy()
+    assert st.stats["form"] == "triangle"
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_tri_worker, args=(world, port, out, case), nprocs=world, join=True)
+    for r in range(world):
+        got, form, exact = out[r]
+        assert form == "triangle (sharded)", (r, form)
+        assert np.array_equal(got.view(np.uint32), one.view(np.uint32)), r
+    print(f"{case} world {world}: exact-fallback rows per rank {[out[r][2] for r in range(world)]} "
+          f"(one GPU: {st.stats['exact_rows']})")

@@ -5,10 +5,13 @@
   (msmt17_leg: + the row-sharded k-reciprocal re-rank) at reduced split sizes, with 2 and 3
   gloo ranks sharing cuda:0 -> CMC/mAP identical to one process;
 * the reference call surface under a process group: zero_shot_learning.get_cmc_map(...,
-  reranking=False/True) given each rank's shards (R1_mAP_eval's sharded compute) -> identical to
-  one process over the whole split;
-* re_ranking_device with the full features on every rank (row-sharded stages + all-gather of
-  the final rows) -> the one-process matrix bit for bit.
+  reranking=False/True, sharded=True) given each rank's shards (R1_mAP_eval's sharded compute)
+  -> identical to one process over the whole split;
+* re_ranking_device(..., sharded=True) with the full features on every rank (row-sharded
+  stages + all-gather of the final rows) -> the one-process matrix bit for bit;
+* the default (unsharded) surface under a process group issues no collective: only the last
+  rank calls get_cmc_map / re_ranking_device on the full split (as a DDP script evaluating on
+  one rank does) and gets the one-process result; the other ranks never call it (no hang).
 (gloo moves the collectives' bytes through the host; RCCL refuses several ranks on one GPU.)"""
 import os
 import socket
@@ -52,12 +55,21 @@ def _surface(dev, rank, world):
     res = {}
     for rr in (False, True):
         cmc, mAP = zsl.get_cmc_map(g, q, torch.from_numpy(gp[glo:ghi]), torch.from_numpy(qp[qlo:qhi]),
-                                   torch.from_numpy(gc[glo:ghi]), torch.from_numpy(qc[qlo:qhi]), reranking=rr)
+                                   torch.from_numpy(gc[glo:ghi]), torch.from_numpy(qc[qlo:qhi]), reranking=rr,
+                                   sharded=rd._initialized())
         res[rr] = (np.asarray(cmc), float(mAP))
     from multimodal_reid_amd import evaluate
     qn = evaluate.l2_normalize_device(torch.from_numpy(qf).to(dev))
     gn = evaluate.l2_normalize_device(torch.from_numpy(gf).to(dev))
-    full = reranking.re_ranking_device(qn, gn, 20, 6, 0.3).cpu().numpy()
+    full = reranking.re_ranking_device(qn, gn, 20, 6, 0.3, sharded=rd._initialized()).cpu().numpy()
+    if rank == world - 1:
+        # the default surface on the full split, on one rank only: single-process semantics
+        for rr in (False, True):
+            cmc, mAP = zsl.get_cmc_map(torch.from_numpy(gf).to(dev), torch.from_numpy(qf).to(dev),
+                                       torch.from_numpy(gp), torch.from_numpy(qp), torch.from_numpy(gc),
+                                       torch.from_numpy(qc), reranking=rr)
+            res[("full", rr)] = (np.asarray(cmc), float(mAP))
+        res["full_rr"] = reranking.re_ranking_device(qn, gn, 20, 6, 0.3).cpu().numpy()
     return res, full
 
 
@@ -67,7 +79,7 @@ def _bench(dev, rank, world):
     wl = bench.Workload(dev, rank, world, BATCH, dataset=MARKET, model=model)
     cmc, mAP, _, _ = wl.step()
     leg = bench.msmt17_leg(model, dev, rank, world, BATCH, dataset=MSMT)
-    return np.asarray(cmc), float(mAP), leg["mAP"], leg["mAP_rerank"]
+    return np.asarray(cmc), float(mAP), leg["mAP"], (leg["rerank"]["mAP_rerank"], leg["rerank_embedded"]["mAP_rerank"])
 
 
 def _worker(rank, world, port, out):
@@ -110,3 +122,7 @@ def test_bench_step_and_surface_sharded_equal_single(single, world):
         for rr in (False, True):
             assert np.array_equal(surf[rr][0], surf1[rr][0]) and surf[rr][1] == surf1[rr][1], (r, rr)
         assert np.array_equal(full.view(np.uint32), full1.view(np.uint32))
+    last = out[world - 1][1][0]
+    for rr in (False, True):
+        assert np.array_equal(last[("full", rr)][0], surf1[rr][0]) and last[("full", rr)][1] == surf1[rr][1], rr
+    assert np.array_equal(last["full_rr"].view(np.uint32), full1.view(np.uint32))

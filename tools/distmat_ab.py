@@ -9,7 +9,7 @@ for (Q, G, D) in [(3368, 15913, 1280), (531, 1010000, 1792), (11659, 82161, 1280
     res = {}
     ws = torch.empty(Q + G, device=dev)
     for v in (1, 0, 1, 0):
-        run = lambda: L.call("reidmi_distmat_f32_variant", L.ptr(q), Q, D, L.ptr(g), G, D, D, L.ptr(out), G,
+        run = lambda: L.call_tools("reidmi_distmat_f32_variant", L.ptr(q), Q, D, L.ptr(g), G, D, D, L.ptr(out), G,
                              L.ptr(ws), v, L.stream())
         run(); torch.cuda.synchronize()
         t = time.perf_counter()

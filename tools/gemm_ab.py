@@ -49,11 +49,11 @@ def main():
             for t in tiles:
                 targs = args[:13] + (t, 0, args[13])
                 for _ in range(3):
-                    L.call("reidmi_gemm_f16_tiled", *targs)
+                    L.call_tools("reidmi_gemm_f16_tiled", *targs)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(a.reps):
-                    L.call("reidmi_gemm_f16_tiled", *targs)
+                    L.call_tools("reidmi_gemm_f16_tiled", *targs)
                 e1.record()
                 torch.cuda.synchronize()
                 ms = e0.elapsed_time(e1) / a.reps

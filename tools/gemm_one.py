@@ -43,14 +43,14 @@ def main():
         cs = torch.rand(N, device=dev)
     base = (epi, L.ptr(A), K, L.ptr(W), K, M, N, K, L.ptr(b), L.ptr(rs), L.ptr(cs), L.ptr(out), N)
     for _ in range(a.warm):  # clocks up before the first timed walk
-        L.call("reidmi_gemm_f16_tiled", *base, a.tile, 0, L.stream())
+        L.call_tools("reidmi_gemm_f16_tiled", *base, a.tile, 0, L.stream())
     for walk in (int(w) for w in a.walk.split(",")):
         args = base + (a.tile, walk, L.stream())
-        L.call("reidmi_gemm_f16_tiled", *args)
+        L.call_tools("reidmi_gemm_f16_tiled", *args)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(a.reps):
-            L.call("reidmi_gemm_f16_tiled", *args)
+            L.call_tools("reidmi_gemm_f16_tiled", *args)
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / a.reps

@@ -39,7 +39,7 @@ def main():
     hbm_unfused = 2.0 * (M * W + 3 * M * W + 3 * M * W + M * W)  # x, q/k/v written + read, o
     variants = [(os.path.basename(p), ctypes.CDLL(os.path.abspath(p))) for p in sys.argv[5:]]
     for _, V in variants:
-        V.reidmi_qkv_attention_f16.argtypes = lib.SIGNATURES["reidmi_qkv_attention_f16"]
+        V.reidmi_qkv_attention_f16.argtypes = lib.TOOLS_SIGNATURES["reidmi_qkv_attention_f16"]
     for rnd in range(3):
         for fused, name, V in [(0, "", None), (1, "", None)] + [(1, n, V) for n, V in variants]:
             def run():
@@ -48,7 +48,7 @@ def main():
                                                       lib.ptr(rs), B, L, H, W, None, None, None, lib.ptr(o), 1,
                                                       lib.stream()) == 0
                     return
-                lib.call("reidmi_qkv_attention_f16", lib.ptr(x), W, lib.ptr(wq), W, lib.ptr(bias), lib.ptr(cs), lib.ptr(rs),
+                lib.call_tools("reidmi_qkv_attention_f16", lib.ptr(x), W, lib.ptr(wq), W, lib.ptr(bias), lib.ptr(cs), lib.ptr(rs),
                          B, L, H, W, lib.ptr(q), lib.ptr(k), lib.ptr(vt), lib.ptr(o), fused, lib.stream())
             for _ in range(3):
                 run()
