@@ -134,7 +134,7 @@ class IdentityCrops:
 
 
 class Workload:
-    def __init__(self, dev, rank, world, batch, dataset="market1501", model=None, crops="uniform"):
+    def __init__(self, dev, rank, world, batch, dataset="market1501", model=None, crops="uniform", streams=1):
         # dataset: a name of synthetic.DATASET_SPLITS, or such a dict (tests run reduced splits)
         sp = syn.DATASET_SPLITS[dataset] if isinstance(dataset, str) else dataset
         self.Q, self.G = sp["num_query"], sp["num_gallery"]
@@ -162,11 +162,21 @@ class Workload:
         self.q_emb = torch.empty(self.qhi - self.qlo, D, device=dev)
         self.g_emb = torch.empty(self.ghi - self.glo, D, device=dev)
         self.dist = torch.empty(self.qhi - self.qlo, self.G, device=dev)
+        # encoder batches alternate over `streams` HIP streams: one batch's kernels fill the CUs a
+        # neighbour's leave idle (the last partial round of tiles of each persistent GEMM launch,
+        # the short LayerNorm / attention launches, launch gaps); each stream has its workspace
+        self.streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(streams - 1)]
 
     def embed(self, imgs, tta, out):
-        for s in range(0, imgs.shape[0], self.batch):
+        main = torch.cuda.current_stream(self.dev)
+        for st in self.streams[1:]:
+            st.wait_stream(main)
+        for i, s in enumerate(range(0, imgs.shape[0], self.batch)):
             e = min(s + self.batch, imgs.shape[0])
-            zsl.embed_pair(self.model, imgs[s:e], tta=tta[s:e], out=out[s:e])
+            with torch.cuda.stream(self.streams[i % len(self.streams)]):
+                zsl.embed_pair(self.model, imgs[s:e], tta=tta[s:e], out=out[s:e])
+        for st in self.streams[1:]:
+            main.wait_stream(st)
 
     def step(self):
         t0 = time.perf_counter()
@@ -582,6 +592,7 @@ def main():
     # 4096 crops per encoder call (M = 864 256 token rows per GEMM): fewer launches and a
     # smaller partial last round of tiles per launch than 1024 (+1.5-2 %, profiles/r03/bench_batch_ab.txt)
     ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--streams", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-rerank", action="store_true")
     ap.add_argument("--no-msmt17", action="store_true")
@@ -595,7 +606,7 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
-    wl = Workload(dev, rank, world, a.batch)
+    wl = Workload(dev, rank, world, a.batch, streams=a.streams)
     L = _lib.load()
     for _ in range(a.warmup):
         wl.step()

@@ -38,6 +38,24 @@ static size_t used = 0;
 
 constexpr int GB_M = 128, GB_N = 128, GB_K = 64;
 
+// Timing variants (tools/build_variant.py -D...=1; never set in the product or tools builds):
+// epilogue pieces compiled out with their values kept live, to price each piece in A/B runs.
+#ifndef GEMM_VAR_NOSTORE
+#define GEMM_VAR_NOSTORE 0
+#endif
+#ifndef GEMM_VAR_NOGELU
+#define GEMM_VAR_NOGELU 0
+#endif
+#ifndef GEMM_VAR_NOPSTAT
+#define GEMM_VAR_NOPSTAT 0
+#endif
+#ifndef GEMM_VAR_NORESLOAD
+#define GEMM_VAR_NORESLOAD 0
+#endif
+#ifndef GEMM_VAR_STAGGER  // s_sleep(127) rounds (~8k cycles each) before odd workgroups start
+#define GEMM_VAR_STAGGER 0
+#endif
+
 __device__ __forceinline__ int swz(int r, int kc) { return r * GB_K + ((kc ^ ((r >> 1) & 7)) << 3); }
 
 typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
@@ -150,9 +168,10 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
                     const f32x4 a = acc[i0 + ii][2 * jp], b = acc[i0 + ii][2 * jp + 1];
                     h[jp] = f16x8{(_Float16)a[0], (_Float16)a[1], (_Float16)a[2], (_Float16)a[3],
                                   (_Float16)b[0], (_Float16)b[1], (_Float16)b[2], (_Float16)b[3]};
-                    if (live) *(f16x8*)(xo + m * ea.ldc + colp(jp)) = h[jp];
+                    if constexpr (GEMM_VAR_NOSTORE) asm volatile("" ::"v"(h[jp]));
+                    else if (live) *(f16x8*)(xo + m * ea.ldc + colp(jp)) = h[jp];
                 }
-                if (ea.pstat) {
+                if (!GEMM_VAR_NOPSTAT && ea.pstat) {
                     // LayerNorm partials of the new fp16 row values over this wave's 64 columns
                     // (the 4 lane groups hold 16 each): sum, then the centred sum of squares
                     f32x2v sp = {0.f, 0.f};
@@ -187,7 +206,14 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
                 int64_t m = mrow + (i0 + ii) * 16 + (lane & 15);
                 m = m < M ? m : M - 1;  // clamped rows are loaded but not stored
 #pragma unroll
-                for (int jp = 0; jp < 2; jp++) xv[ii][jp] = *(const f16x8*)(xo + m * ea.ldc + colp(jp));
+                for (int jp = 0; jp < 2; jp++) {
+                    if constexpr (GEMM_VAR_NORESLOAD) {  // timing variant: no residual read
+                        xv[ii][jp] = f16x8{};
+                        asm volatile("" : "+v"(xv[ii][jp]));
+                    } else {
+                        xv[ii][jp] = *(const f16x8*)(xo + m * ea.ldc + colp(jp));
+                    }
+                }
             }
             if (i0 > 0) store_batch(i0 - NB);
 #pragma unroll
@@ -364,7 +390,7 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
 #pragma unroll
         for (int jp = 0; jp < 2; jp++) {
             f32x4 a = acc[i][2 * jp], c = acc[i][2 * jp + 1];
-            if constexpr (EPI == EPI_GELU_H16) {
+            if constexpr (EPI == EPI_GELU_H16 && !GEMM_VAR_NOGELU) {
 #pragma unroll
                 for (int e = 0; e < 4; e += 2) {
                     const f32x2v ga = quick_gelu2(f32x2v{a[e], a[e + 1]});
@@ -384,7 +410,11 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
                 const int hd = qkv_c0 + (col - ncol);  // h * 64 + d
                 *(uint4*)(qkrow + (int64_t)(hd >> 6) * ea.seq * 64 + (hd & 63)) = v;
             } else {
-                *(uint4*)((_Float16*)ea.out + m * ea.ldc + col) = v;
+                if constexpr (GEMM_VAR_NOSTORE) {  // timing variant: value kept, no store
+                    typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+                    asm volatile("" ::"v"(__builtin_bit_cast(u32x4v, v)));
+                }
+                else *(uint4*)((_Float16*)ea.out + m * ea.ldc + col) = v;
             }
         }
     }
@@ -732,6 +762,10 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
     const int lo = (int)(sub * xs / xper), hi = (int)(sub * (xs + 1) / xper);
     const int first = lo + bid / ng;
     if (first >= hi) return;
+    if constexpr (GEMM_VAR_STAGGER > 0) {  // timing variant: odd workgroups start later (desynchronised epilogues)
+        if (bid & 1)
+            for (int i = 0; i < GEMM_VAR_STAGGER; i++) __builtin_amdgcn_s_sleep(127);
+    }
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wr = wid >> 2, wc = wid & 3;

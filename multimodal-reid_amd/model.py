@@ -212,13 +212,17 @@ class VisionTransformer:
         return torch.float32
 
     def _workspace(self, B, full):
+        """Workspace of the current stream (one per stream, so batches on several streams run
+        concurrently; the caching allocator keeps each on its stream)."""
         nbytes = _fn("reidmi_vit_workspace_bytes")(ctypes.byref(self.weights), B, int(full))
         if nbytes < 0:
             raise _lib.ReidmiError(_lib.load().reidmi_last_error().decode())
-        ws = self._ws.get("buf")
+        key = torch.cuda.current_stream(self.device).cuda_stream
+        ws = self._ws.get(key)
         if ws is None or ws.numel() < nbytes:
+            self._ws.pop(key, None)
             ws = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
-            self._ws["buf"] = ws
+            self._ws[key] = ws
         return ws, nbytes
 
     def _images(self, img):

@@ -17,7 +17,9 @@ reidmi_boot.load()
 from multimodal_reid_amd import _lib as L  # noqa: E402
 
 SHAPES = {"cfc": (3072, 768, 1, True), "qkv": (2304, 768, 0, True), "out": (768, 768, 6, False),
-          "proj": (768, 3072, 6, False)}
+          "proj": (768, 3072, 6, False), "outp": (768, 768, 6, "pst"), "projp": (768, 3072, 6, "pst")}
+# "outp" / "projp": the encoder's form of out_proj / c_proj (residual + LayerNorm partials,
+# reidmi_gemm_f16_resid_partials)
 
 
 def open_lib(path):
@@ -50,17 +52,25 @@ def main():
             b = torch.rand(N, device=dev, generator=g)
             out = (torch.rand(M, N, device=dev, generator=g) - 0.5).half()
             rs = cs = None
-            if fold:
+            pst = torch.empty((N // 64) * M * 2, device=dev) if fold == "pst" else None
+            if fold is True:
                 rs = torch.stack([torch.rand(M + 256, device=dev) + 0.5, torch.rand(M + 256, device=dev) - 0.5], 1)
                 cs = torch.rand(N, device=dev)
-            args = (epi, L.ptr(A), K, L.ptr(W), K, M, N, K, L.ptr(b), L.ptr(rs), L.ptr(cs), L.ptr(out), N, L.stream())
+            if pst is not None:
+                fn_name = "reidmi_gemm_f16_resid_partials"
+                args = (L.ptr(A), K, L.ptr(W), K, M, N, K, L.ptr(b), L.ptr(out), N, L.ptr(pst), L.stream())
+            else:
+                fn_name = "reidmi_gemm_f16"
+                args = (epi, L.ptr(A), K, L.ptr(W), K, M, N, K, L.ptr(b), L.ptr(rs), L.ptr(cs), L.ptr(out), N,
+                        L.stream())
             for lname, lib in libs:
+                fn = getattr(lib, fn_name)
                 for _ in range(3):
-                    assert lib.reidmi_gemm_f16(*args) == 0, lib.reidmi_last_error()
+                    assert fn(*args) == 0, lib.reidmi_last_error()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(a.reps):
-                    lib.reidmi_gemm_f16(*args)
+                    fn(*args)
                 e1.record()
                 torch.cuda.synchronize()
                 ms = e0.elapsed_time(e1) / a.reps
