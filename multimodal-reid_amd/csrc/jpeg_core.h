@@ -25,7 +25,7 @@ enum : int32_t {
     J_LAYOUT = 3,          // component count / sampling factors outside 1, 3 x {4:4:4, 4:2:2, 4:2:0}
     J_BAD_TABLE = 4,       // missing or malformed DQT / DHT
     J_BAD_DATA = 5,        // entropy-coded data does not decode (set by the device pass)
-    J_TRUNCATED = 6,       // the file ends before EOI (Pillow: "image file is truncated")
+    J_TRUNCATED = 6,       // libjpeg's input starves before the last MCU (Pillow: "image file is truncated")
 };
 
 enum : int32_t { CS_GRAY = 0, CS_YCC = 1, CS_RGB = 2 };
@@ -81,6 +81,8 @@ struct BitReader {
     uint64_t acc;   // MSB-aligned bit window
     int bits;       // valid bits in acc
     bool marker;    // a marker (or the end) was reached: zeros are fed from here on
+    int64_t loaded; // bits moved into acc since start() (fillers after a marker included):
+                    // the bits consumed in the segment are loaded - bits
     bool nw_ok;     // nw0/nw1: the aligned words covering >= 5 stream bytes at p, loaded one
     int nmis;       // refill ahead and first read at the next refill, so the load's latency
     uint32_t nw0, nw1;   // hides behind the symbols decoded in between
@@ -99,6 +101,7 @@ struct BitReader {
         end = e;
         acc = 0;
         bits = 0;
+        loaded = 0;
         marker = false;
         fetch();
     }
@@ -116,6 +119,7 @@ struct BitReader {
                 const uint32_t be = (v >> 24) | ((v >> 8) & 0xFF00u) | ((v << 8) & 0xFF0000u) | (v << 24);
                 acc |= (uint64_t)be << (32 - bits);
                 bits += 32;
+                loaded += 32;
                 p += 4;
             } else {
                 int pos = 0;
@@ -132,6 +136,7 @@ struct BitReader {
                     }
                     acc |= (uint64_t)c << (56 - bits);
                     bits += 8;
+                    loaded += 8;
                 }
                 p += pos;
                 if (marker) bits = 32 > bits ? 32 : bits;   // zeros from here on
@@ -161,9 +166,11 @@ struct BitReader {
             }
             acc |= (uint64_t)c << (56 - bits);
             bits += 8;
+            loaded += 8;
         }
         fetch();
     }
+    __host__ __device__ inline int64_t consumed() const { return loaded - bits; }
     __host__ __device__ inline uint32_t take(int n) {   // n in [1, 16]
         const uint32_t v = (uint32_t)(acc >> (64 - n));
         acc <<= n;
@@ -202,6 +209,99 @@ __host__ __device__ inline int32_t huff_extend(uint32_t v, int s) {   // HUFF_EX
     return (v < (1u << (s - 1))) ? (int32_t)v - (1 << s) + 1 : (int32_t)v;
 }
 
+// libjpeg-turbo's entropy-decoder input buffering (jdhuff.c), replayed beside the decode to tell
+// whether the reference's loader gets the whole image.  Pillow hands libjpeg the file's bytes as
+// a suspending source (JpegDecode.c): when a fetch of the bit buffer reaches the end of the data
+// before a marker, libjpeg suspends, and at the end of the file Pillow raises "image file is
+// truncated"; once every MCU is decoded, a missing EOI does not matter (JpegDecode.c ignores
+// jpeg_finish_decompress suspending when all rows are out).  So a file is truncated exactly when
+// a fetch during the MCUs (or the search for a restart marker) starves.  Fetch points:
+//  * slow path (decode_mcu_slow; every MCU when a restart interval is set, and every MCU that
+//    starts with fewer than 512 x blocks_in_MCU bytes left in the buffer): before a Huffman
+//    symbol when fewer than 8 bits are buffered, before a symbol's extra bits (or the rest of a
+//    code longer than 8 bits) when fewer than those are buffered; a fetch reads bytes until >= 25
+//    bits are buffered (MIN_GET_BITS), stopping at a marker (no suspension; zeros follow);
+//  * fast path (decode_mcu_fast): 6 bytes whenever <= 16 bits are buffered, before each symbol
+//    and each symbol's extra bits; never near the end of the data (the 512-byte margin).
+// F counts destuffed bytes fetched in the restart segment, C the bits consumed (BitReader).
+#ifndef LJ_MIN_GET_BITS
+#define LJ_MIN_GET_BITS 57
+#endif
+constexpr int kLjMinGetBits = LJ_MIN_GET_BITS;   // BIT_BUF_SIZE - 7 with a 64-bit bit buffer
+struct LjInput {
+    const uint8_t* p;   // libjpeg's next raw byte
+    const uint8_t* end;
+    int64_t F;
+    bool marker;        // reached a marker: no more fetches in this segment
+    bool starved;       // a fetch reached the end of the data first (the loader raises)
+    bool fast;          // the current MCU runs decode_mcu_fast
+    __host__ __device__ inline void start(const uint8_t* b, const uint8_t* e) {
+        p = b;
+        end = e;
+        F = 0;
+        marker = false;
+    }
+    __host__ __device__ inline void fetch1() {   // one destuffed byte (jpeg_fill_bit_buffer)
+        if (p >= end) {
+            starved = marker = true;
+            return;
+        }
+        if (*p != 0xFF) {
+            ++p;
+            ++F;
+            return;
+        }
+        const uint8_t* q = p + 1;
+        while (q < end && *q == 0xFF) ++q;   // fill bytes
+        if (q >= end) {
+            starved = marker = true;
+            return;
+        }
+        if (*q == 0) {
+            p = q + 1;
+            ++F;
+        } else {
+            marker = true;   // unread_marker: the bytes stay for the marker reader
+        }
+    }
+    // before reading n bits (n >= 1) at consumed position C
+    __host__ __device__ inline void need(int64_t C, int n) {
+        if (fast) {
+            if (8 * F - C <= 16)   // FILL_BIT_BUFFER_FAST: six FILL_BYTEs (no end check: the margin)
+                for (int i = 0; i < 6 && !marker; ++i) fetch1();
+        } else if (!marker && 8 * F - C < n) {
+            while (!marker && 8 * F - C < kLjMinGetBits) fetch1();
+        }
+    }
+    // a Huffman code of l > 8 bits read from C (jpeg_huff_decode: CHECK_BIT_BUFFER(9), then one
+    // bit at a time: a fetch where the buffer ran dry)
+    __host__ __device__ inline void need_long(int64_t C, int l) {
+        if (fast || marker) return;   // (the fast path's buffer holds > 16 bits here)
+        if (8 * F - C < 9) {
+            need(C, 9);
+        } else if (8 * F - C < l) {
+            const int64_t Cd = 8 * F;
+            while (!marker && 8 * F - Cd < kLjMinGetBits) fetch1();
+        }
+    }
+    // at an MCU start: decode_mcu's choice of path
+    __host__ __device__ inline void mcu(int blocks_in_mcu, bool restarts) {
+        fast = !restarts && !marker && (end - p) >= 512 * (int64_t)blocks_in_mcu;
+    }
+    // process_restart -> read_restart_marker: the next marker (skipping garbage); starves at the end
+    __host__ __device__ inline void restart() {
+        const uint8_t* q = p;
+        while (q + 1 < end && !(q[0] == 0xFF && q[1] != 0xFF && q[1] != 0)) ++q;
+        if (q + 1 >= end) {
+            starved = true;
+            q = end;
+        } else {
+            q += 2;
+        }
+        start(q, end);
+    }
+};
+
 // Where decoded coefficients go.  DirectSink writes them into zeroed blocks in place (host
 // check); the device kernel stages each block in LDS and writes it out whole (jpeg.hip).
 struct DirectSink {
@@ -212,9 +312,9 @@ struct DirectSink {
 };
 
 // Decodes one image's scan into zig-zag-order int16 coefficient blocks.  Returns J_OK,
-// J_BAD_DATA (then the blocks not yet ended are left as they were) or J_TRUNCATED (no EOI
-// follows the scan: every block is decoded, missing data as zeros, as libjpeg does, but the
-// reference's loader raises for such a file).
+// J_BAD_DATA (then the blocks not yet ended are left as they were) or J_TRUNCATED (libjpeg's
+// input would starve before the last MCU, LjInput: every block is decoded, missing data as zeros,
+// but the reference's loader raises for such a file).
 template <class Sink>
 __host__ __device__ inline int32_t entropy_decode(const uint8_t* src, const JpegImage& im, const JpegHuff* huff,
                                                   int16_t* coef, Sink& sink) {
@@ -224,6 +324,9 @@ __host__ __device__ inline int32_t entropy_decode(const uint8_t* src, const Jpeg
     // of their streams execute nearly the same instructions.
     BitReader br;
     br.start(src + im.src_off, src + im.src_off + im.src_len);
+    LjInput lj;
+    lj.starved = false;
+    lj.start(src + im.src_off, src + im.src_off + im.src_len);
     const bool gray = im.ncomp == 1;
     const int h0 = gray ? 1 : im.hs[0];
     const int n0 = gray ? 1 : im.hs[0] * im.vs[0];   // Y blocks per MCU
@@ -247,14 +350,20 @@ __host__ __device__ inline int32_t entropy_decode(const uint8_t* src, const Jpeg
     int comp = 0;
     sink.begin(org0);
     const JpegHuff* tbl = dct0;
+    lj.mcu(nb, im.ri != 0);
     while (mcu < nmcu) {
         br.refill();
+        const int64_t c0 = br.consumed();
+        lj.need(c0, 8);   // HUFF_DECODE (HUFF_DECODE_FAST)
         const int sym = br.decode(tbl);
         if (sym < 0) return J_BAD_DATA;
+        const int64_t c1 = br.consumed();
+        if (c1 - c0 > 8) lj.need_long(c0, (int)(c1 - c0));   // a code longer than the lookahead
         const bool dc = k == 0;
         const int r = dc ? 0 : sym >> 4;
         const int s = dc ? sym : sym & 15;
         if (s > 15) return J_BAD_DATA;
+        if (s) lj.need(c1, s);   // CHECK_BIT_BUFFER(s) / FILL_BIT_BUFFER_FAST
         int32_t v = s ? huff_extend(br.take(s), s) : 0;
         if (dc) {
             v += comp == 0 ? pred0 : (comp == 1 ? pred1 : pred2);
@@ -288,7 +397,9 @@ __host__ __device__ inline int32_t entropy_decode(const uint8_t* src, const Jpeg
                     togo = im.ri;
                     pred0 = pred1 = pred2 = 0;
                     br.restart();
+                    lj.restart();
                 }
+                lj.mcu(nb, im.ri != 0);
             }
             comp = b < n0 ? 0 : b - n0 + 1;
             int16_t* y = org0 + ((b & (h0 - 1)) + (int64_t)(b >> (h0 - 1)) * bw0) * 64;
@@ -296,12 +407,21 @@ __host__ __device__ inline int32_t entropy_decode(const uint8_t* src, const Jpeg
             tbl = comp == 0 ? dct0 : (comp == 1 ? dct1 : dct2);
         }
     }
-    // libjpeg then reads the markers up to EOI (jpeg_finish_decompress); a file that ends first
-    // makes the reference's loader raise "image file is truncated" (the reader never moves past
-    // a marker, so the search starts at or before it)
-    for (const uint8_t* q = br.p; q + 1 < br.end; ++q)
-        if (q[0] == 0xFF && q[1] == 0xD9) return J_OK;
-    return J_TRUNCATED;
+    // every MCU decoded: the reference's loader returns the image unless libjpeg's input starved
+    // on the way (LjInput); a missing EOI alone does not fail it.  jpeg_finish_decompress then
+    // reads the next marker (next_marker: garbage bytes skipped; suspending at the end is fine
+    // once every row is out): EOI, RSTn, TEM, APPn, COM, DQT, DHT, DRI end the image normally; a
+    // second SOI or SOF, or a reserved marker, is an error in libjpeg (Pillow: "broken data
+    // stream"), reported here as undecodable data.
+    if (lj.starved) return J_TRUNCATED;
+    const uint8_t* q = lj.p;
+    while (q + 1 < lj.end && !(q[0] == 0xFF && q[1] != 0xFF && q[1] != 0)) ++q;
+    if (q + 1 < lj.end) {
+        const int m = q[1];
+        const bool sof = m >= 0xC0 && m <= 0xCF && m != 0xC4 && m != 0xCC;
+        if (m == 0xD8 || sof || (m >= 0x02 && m <= 0xBF)) return J_BAD_DATA;
+    }
+    return J_OK;
 }
 
 // ---------------------------------------------------------------- islow IDCT (jidctint.c)

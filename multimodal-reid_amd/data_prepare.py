@@ -129,7 +129,7 @@ def _to_device(a, device):
 JPEG_STATUS = {1: "not a JPEG or truncated", 2: "progressive / lossless / arithmetic-coded / 12-bit / multi-scan",
                3: "component layout other than grayscale or 3 x {4:4:4, 4:2:2, 4:2:0}",
                4: "missing or malformed quantisation / Huffman tables", 5: "entropy-coded data does not decode",
-               6: "image file is truncated (the file ends inside the entropy-coded data)"}
+               6: "image file is truncated (libjpeg's input would run out before the last MCU)"}
 
 
 class JpegBatch:
@@ -166,10 +166,11 @@ class JpegBatch:
                              f"{JPEG_STATUS.get(int(st[i]), int(st[i]))}")
 
 
-def decode_jpeg(files, device=None, check=True):
+def decode_jpeg(files, device=None, check=True, return_status=False):
     """Image.open(f).convert("RGB") of every file (data_prepare.py:89), on the GPU.
     Returns (pix uint8 device tensor of the packed HWC images, meta int64 device tensor [B][3]
-    = (offset, h, w), JpegBatch) — the input reidmi_preprocess_u8 takes.  With check=True an
+    = (offset, h, w), JpegBatch) — the input reidmi_preprocess_u8 takes — and, with
+    return_status, the per-file device status (JPEG_STATUS codes).  With check=True an
     unsupported or undecodable file raises (there is no host fallback)."""
     device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
     jb = files if isinstance(files, JpegBatch) else JpegBatch(files)
@@ -187,7 +188,7 @@ def decode_jpeg(files, device=None, check=True):
     if check and jb.B:
         jb.raise_for_status(err[:jb.B].cpu().numpy())
     meta = torch.from_numpy(jb.meta).to(device, non_blocking=True)
-    return pix, meta, jb
+    return (pix, meta, jb, err[:jb.B]) if return_status else (pix, meta, jb)
 
 
 def preprocess_jpeg(files, height=256, width=128, model_type="vit", dtype=torch.float16, device=None, out=None):

@@ -140,6 +140,28 @@ def truncated_cases():
     return [("mid-scan", good[0][:int(len(good[0]) * 0.6)]), ("no-eoi", good[1][:-2])]
 
 
+def tail_cases():
+    """Files whose scan is followed by something other than EOI: trailing bytes
+    with no EOI, a lone 0xFF, another marker, a cut inside the last bytes — with and without
+    restart intervals, several sizes and subsamplings.  Pillow (the reference's decoder,
+    libjpeg-turbo 3.1 behind a suspending source) loads some and raises for others; what
+    decides it is whether libjpeg's bit-buffer fetches reach the end of the data before the
+    last MCU (jpeg_core.h LjInput), and which marker follows the scan."""
+    out = []
+    for i, (h, w, sub, q, kw) in enumerate([(64, 48, 2, 90, {}), (128, 64, 2, 90, {}), (37, 29, 1, 75, {}),
+                                            (128, 64, 0, 95, {}), (200, 150, 2, 50, {}), (16, 16, 2, 90, {}),
+                                            (128, 64, 2, 90, {"restart_marker_blocks": 4}),
+                                            (96, 80, 1, 80, {"restart_marker_rows": 1}), (300, 200, 2, 92, {})]):
+        body = syn.jpeg_files(1, h, w, seed=40 + i, quality=q, subsampling=sub, **kw)[0][:-2]
+        for extra in (b"", b"\x00", b"\x00" * 2, b"\x00" * 3, b"\x00" * 4, b"\x00" * 5, b"\x00" * 6, b"\x00" * 9,
+                      b"\x12\x34\x56\x78\x9a", b"\xff", b"\xff\xd9", b"\xff\xd8", b"\xff\xd0", b"\xff\xfe\x00\x02"):
+            out.append((f"{i}+{extra.hex()}", body + extra))
+        for cut in (1, 2, 3, 5, 17, 100):
+            if cut < len(body) - 700:
+                out.append((f"{i}-{cut}", body[:-cut]))
+    return out
+
+
 def test_plan_pools_tables_and_reads_paths(tmp_path):
     files = syn.jpeg_files(20, 128, 64, seed=2)   # one encoder setting: one set of tables
     for i, b in enumerate(files[:3]):
@@ -187,6 +209,20 @@ def test_core_arithmetic_on_host_vs_pillow(tmp_path):
                           tout.ctypes.data_as(vp), terr.ctypes.data_as(vp))
     assert terr.tolist() == [6] * len(tc)
     assert all(_pil_raises(b) for _, b in tc)
+    # after the scan: the device decoder returns an image exactly when Pillow does
+    ec = tail_cases()
+    je = data_prepare.JpegBatch([b for _, b in ec])
+    eout = np.zeros(max(je.out_bytes, 1), np.uint8)
+    eerr = np.zeros(je.B, np.int32)
+    host.jpeg_host_decode(je.buf.ctypes.data_as(vp), je.plan.ctypes.data_as(vp), je.info.ctypes.data_as(vp),
+                          eout.ctypes.data_as(vp), eerr.ctypes.data_as(vp))
+    mism = [(name, int(eerr[k])) for k, (name, b) in enumerate(ec) if (eerr[k] == 0) == _pil_raises(b)]
+    assert not mism, mism
+    assert 0 < int((eerr == 0).sum()) < len(ec)  # both kinds occur
+    for k, (name, b) in enumerate(ec):  # and the images it returns are Pillow's pixels
+        if eerr[k] == 0:
+            off, h, w = je.meta[k]
+            assert np.array_equal(eout[off:off + h * w * 3].reshape(h, w, 3), pil_rgb(b)), name
     bad = [name for i, (name, b) in enumerate(cases)
            if not np.array_equal(out[jb.meta[i, 0]:jb.meta[i, 0] + jb.meta[i, 1] * jb.meta[i, 2] * 3]
                                  .reshape(jb.meta[i, 1], jb.meta[i, 2], 3), pil_rgb(b))]
@@ -265,3 +301,14 @@ def test_decode_reports_truncated_files(gpu):
     pix, _, jb = data_prepare.decode_jpeg([good] + [b for _, b in tc], check=False)
     torch.cuda.synchronize()
     assert np.array_equal(pix.cpu().numpy()[:40 * 24 * 3].reshape(40, 24, 3), pil_rgb(good))
+    # what follows the scan (no EOI, trailing bytes, another marker): the device decoder returns
+    # an image exactly when Pillow does, with Pillow's pixels
+    ec = tail_cases()
+    pix, _, jb, err = data_prepare.decode_jpeg([b for _, b in ec], check=False, return_status=True)
+    torch.cuda.synchronize()
+    err, pix = err.cpu().numpy()[:len(ec)], pix.cpu().numpy()
+    for k, (name, b) in enumerate(ec):
+        assert (err[k] == 0) != _pil_raises(b), name
+        if err[k] == 0:
+            off, h, w = jb.meta[k]
+            assert np.array_equal(pix[off:off + h * w * 3].reshape(h, w, 3), pil_rgb(b)), name
