@@ -3,6 +3,8 @@
     model_adaptor(model, height, width, weights=None, model_type="vit", training_mode="coop",
                   vision_stride_size=12) -> (model, bottleneck, bottleneck_proj)   utils.py:169-262
     load_clip(state_dict, height, width, ...) -> model.CLIP                       maple.py:1044-1098
+    load_model(model, classnames, templates, weights, ...) -> (zeroshot_weights, model)
+                                                                   zero_shot_learning.py:15-58
     resize_pos_embed                                                              utils.py:111-125
 
 CLIP-ReID checkpoints store the towers under ``image_encoder.*`` / ``text_encoder.*``
@@ -14,6 +16,7 @@ refused here: re-save its ``state_dict()`` with ``torch.save``).
 BNNeck (utils.py:128-142) is constructed and loaded but, as in the reference's eval
 (zero_shot_learning.py:91-92), never applied.
 """
+import numpy as np
 import torch
 
 from .model import CLIP, TextTransformer, VisionTransformer, resize_pos_embed  # noqa: F401
@@ -81,3 +84,62 @@ def load_clip(state_dict, height=256, width=128, stride=12, device=None, text=Tr
         txt = {k: v for k, v in state_dict.items() if not k.startswith("visual.")}
         tx = TextTransformer(txt, device=device)
     return CLIP(visual, tx)
+
+
+def text_encoder_overlay(base_text_sd, weights):
+    """zero_shot_learning.py:28-35: the CLIP text tower's state dict with the checkpoint's
+    ``text_encoder.*`` entries laid over it (prefix stripped, each cast to the base entry's
+    dtype, strict=False: keys the checkpoint lacks keep the base values; a ``text_encoder.*`` key
+    the tower does not have raises KeyError, as the reference's dtype lookup does, :34).
+    ``weights``: a checkpoint path (weights-only load) or state dict, or None."""
+    sd = dict(base_text_sd)
+    if weights is None:
+        return sd
+    ck = load_checkpoint(weights) if isinstance(weights, str) else weights
+    for key, v in ck.items():
+        if key.startswith("text_encoder."):
+            k = key[len("text_encoder."):]
+            base = sd[k]  # KeyError for a key the tower lacks (zero_shot_learning.py:34)
+            dt = base.dtype if isinstance(base, torch.Tensor) else torch.from_numpy(np.asarray(base)).dtype
+            sd[k] = (v if isinstance(v, torch.Tensor) else torch.from_numpy(np.asarray(v))).to(dt)
+    return sd
+
+
+def load_model(model, classnames, templates, weights, augmented_template=True, tokenize=None, device=None):
+    """zero_shot_learning.py:15-58 (coop mode): the CLIP text tower with the CLIP-ReID
+    checkpoint's ``text_encoder.*`` overlay (text_encoder_overlay), then the zero-shot
+    classifier over the class names' templates (zeroshot_classifier: augmented templates ->
+    per-class normalise / mean / normalise; plain -> one template per class, normalised).
+    ``model``: what ``clip.load(model_name)`` returns in the reference — here an OpenAI-layout
+    state dict (``clip.load`` downloads weights, which this environment cannot) or a model.CLIP
+    whose text tower's source state dict is kept (``model.text.source_state_dict``).
+    ``templates[classname]``: a list of sentences (augmented) or one sentence (plain);
+    ``tokenize``: clip.tokenize's role (tokenizer.tokenize with the BPE vocabulary, which is not
+    shipped: parity unpinned) — or pass token ids directly as the templates' values.
+    Returns (zeroshot_weights [n_cls, E] fp32 on the GPU, model.CLIP)."""
+    from .zero_shot_learning import zeroshot_classifier
+    if isinstance(model, CLIP):
+        base = getattr(model.text, "source_state_dict", None)
+        if base is None:
+            raise ValueError("load_model: the CLIP model's text tower keeps no source state dict; pass the state dict")
+        visual = model.visual
+    else:
+        base = {k: v for k, v in model.items() if not k.startswith("visual.")}
+        visual = None
+    text = TextTransformer(text_encoder_overlay(base, weights), device=device)
+    text.source_state_dict = base
+
+    def ids(t):
+        if isinstance(t, (str, list)) and (isinstance(t, str) or (t and isinstance(t[0], str))):
+            if tokenize is None:
+                raise ValueError("load_model: sentences need a tokenizer (tokenizer.tokenize with the CLIP BPE "
+                                 "vocabulary); or pass token ids")
+            return np.asarray(tokenize(t if isinstance(t, list) else [t]))
+        return np.asarray(t)
+
+    if augmented_template:
+        zw = zeroshot_classifier(text, [ids(templates[c]) for c in classnames], augmented_template=True)
+    else:
+        zw = zeroshot_classifier(text, np.concatenate([ids(templates[c]).reshape(1, -1) for c in classnames]),
+                                 augmented_template=False)
+    return zw, CLIP(visual, text)

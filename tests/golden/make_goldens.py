@@ -401,6 +401,22 @@ def glue_fixtures(out):
         ref_zsl.params = _ap.Namespace(training_mode="coop", augmented_template=False)
         zw_plain, _ = ref_zsl.load_model("ViT-B/16", classnames, plain, None)
     res.update(zeroshot_aug=zw_aug.numpy(), zeroshot_plain=zw_plain.numpy(), zeroshot_tokens=tok_all)
+    # load_model with a CLIP-ReID checkpoint FILE: its text_encoder.* entries overlay the CLIP
+    # text tower (zero_shot_learning.py:28-35, strict=False): here every block's attention
+    # weights and ln_final come from another seed, the rest stays the base model's
+    import tempfile
+    over = syn.text_state_dict(seed=33)
+    ck = {"text_encoder." + k: v for k, v in over.items() if ".attn." in k or k.startswith("ln_final")}
+    ck["image_encoder.class_embedding"] = np.zeros(768, np.float32)  # ignored by the overlay
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "ckpt.pth")
+        torch.save(_torch_sd(ck), path)
+        model2 = _small_clip(maple, text_sd)
+        clip.LOAD_HOOK = lambda name: model2
+        with _cpu_cuda():
+            ref_zsl.params = _ap.Namespace(training_mode="coop", augmented_template=True)
+            zw_over, _ = ref_zsl.load_model("ViT-B/16", classnames, templates, path)
+    res.update(zeroshot_overlay=zw_over.numpy())
     np.savez_compressed(os.path.join(out, "glue.npz"), **res)
     print("glue fixtures ok", zw_aug.shape, zw_plain.shape)
 

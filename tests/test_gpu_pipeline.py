@@ -115,6 +115,28 @@ def test_zeroshot_classifier_vs_reference(gpu):
     _close(plain, g["zeroshot_plain"], atol=5e-3)
 
 
+def test_load_model_text_encoder_overlay_vs_reference(gpu, tmp_path):
+    """zero_shot_learning.load_model (:15-58) with a CLIP-ReID checkpoint FILE: its
+    text_encoder.* entries (every block's attention and ln_final from another seed) laid over
+    the CLIP text tower (strict=False, dtype cast), then the augmented-template classifier;
+    against the reference's load_model on the same base model and file."""
+    from multimodal_reid_amd import utils
+    g = golden("glue.npz")
+    base = syn.text_state_dict(seed=8)
+    over = syn.text_state_dict(seed=33)
+    ck = {"text_encoder." + k: torch.from_numpy(np.asarray(v)) for k, v in over.items()
+          if ".attn." in k or k.startswith("ln_final")}
+    ck["image_encoder.class_embedding"] = torch.zeros(768)
+    path = tmp_path / "ckpt.pth"
+    torch.save(ck, path)
+    tok = g["zeroshot_tokens"]
+    classnames = [f"{1 + c:04d}" for c in range(6)]
+    templates = {name: tok[c * 5:(c + 1) * 5] for c, name in enumerate(classnames)}
+    zw, model = utils.load_model(base, classnames, templates, str(path))
+    _close(zw.cpu().numpy(), g["zeroshot_overlay"], atol=5e-3)
+    assert model.text is not None and model.visual is None
+
+
 @pytest.mark.parametrize("E,counts", [(512, [56, 1, 3, 17]), (768, [2, 2]), (64, [0, 5])])
 def test_class_mean_normalize_kernel(gpu, E, counts):
     """T4's per-class normalise -> mean -> normalise (zero_shot_learning.py:45-47) against
