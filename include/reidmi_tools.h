@@ -37,6 +37,12 @@ int reidmi_qkv_attention_f16(const void* x, int64_t ldx, const void* wq, int64_t
                              const float* colsum, const void* rowstat, int64_t nseq, int L, int H, int W, void* q,
                              void* k, void* vt, void* o, int fused, void* stream);
 
+/* The QKV GEMM alone (ln_1 fold + the head split reidmi_vit_forward uses): x [nseq*L][lda],
+ * W [3*H*64][ldw] -> q, k [nseq*H][L][64], vt [nseq*H][64][lpad] (lpad = reidmi_attn_lpad(L)). */
+int reidmi_gemm_f16_qkv(const void* A, int64_t lda, const void* W, int64_t ldw, int64_t nseq, int L, int H,
+                        const float* bias, const void* rowstat, const float* colsum, void* q, void* k, void* vt,
+                        int lpad, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1250,4 +1250,22 @@ REIDMI_API int reidmi_gemm_f16_tiled(int epi, const void* A, int64_t lda, const 
     opt.ngroups = ngroups;
     return gemm_api(epi, A, lda, W, ldw, M, N, K, bias, rowstat, colsum, out, ldc, opt, stream);
 }
+
+// The QKV GEMM alone (EPI_QKV: ln_1 fold + head split into q, k [nseq*H][L][64] and
+// v^T [nseq*H][64][lpad]), for pricing its epilogue against a plain fp16 output (tools/lib_ab.py)
+REIDMI_API int reidmi_gemm_f16_qkv(const void* A, int64_t lda, const void* W, int64_t ldw, int64_t nseq, int L, int H,
+                                   const float* bias, const void* rowstat, const float* colsum, void* q, void* k,
+                                   void* vt, int lpad, void* stream) {
+    EpiArgs ea{};
+    ea.bias = bias;
+    ea.rowstat = (const float2*)rowstat;
+    ea.colsum = colsum;
+    ea.q = q;
+    ea.k = k;
+    ea.vt = vt;
+    ea.seq = L;
+    ea.heads = H;
+    ea.lpad = lpad;
+    return gemm_f16(EPI_QKV, A, lda, W, ldw, nseq * L, 3 * (int64_t)H * 64, H * 64, ea, (hipStream_t)stream);
+}
 #endif  // REIDMI_TOOLS
