@@ -52,8 +52,20 @@ constexpr int GB_M = 128, GB_N = 128, GB_K = 64;
 #ifndef GEMM_VAR_NORESLOAD
 #define GEMM_VAR_NORESLOAD 0
 #endif
-#ifndef GEMM_VAR_STAGGER  // s_sleep(127) rounds (~8k cycles each) before odd workgroups start
-#define GEMM_VAR_STAGGER 0
+#ifndef GEMM_VAR_STAGGER  // s_sleep(GEMM_VAR_STAG_SLP) rounds before a workgroup starts:
+#define GEMM_VAR_STAGGER 0  // STAGGER x ((bid >> GEMM_VAR_STAG_SHIFT) & GEMM_VAR_STAG_MASK)
+#endif
+#ifndef GEMM_VAR_RPF  // residual epilogue: prefetch the tile's residual rows to L2 over RPF K-steps
+#define GEMM_VAR_RPF 0
+#endif
+#ifndef GEMM_VAR_STAG_SHIFT
+#define GEMM_VAR_STAG_SHIFT 0
+#endif
+#ifndef GEMM_VAR_STAG_MASK
+#define GEMM_VAR_STAG_MASK 1
+#endif
+#ifndef GEMM_VAR_STAG_SLP  // 64 x SLP cycles per round (127: ~8k cycles, ~4 us)
+#define GEMM_VAR_STAG_SLP 127
 #endif
 
 __device__ __forceinline__ int swz(int r, int kc) { return r * GB_K + ((kc ^ ((r >> 1) & 7)) << 3); }
@@ -745,7 +757,9 @@ struct EpiVm {  // vector-memory instructions of one full-tile epilogue_tile<EPI
                                                                                           : -1;
 };
 
-template <int EPI>
+// TAG: a symbol tag only (same code): the residual epilogue's two callers, out_proj (K = W,
+// TAG 0) and mlp.c_proj (K = 4W, TAG 1), get their own kernel names in rocprof traces
+template <int EPI, int TAG = 0>
 __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16* __restrict__ A, int64_t lda,
                                                                  const _Float16* __restrict__ W, int64_t ldw,
                                                                  int64_t M, int N, int K, EpiArgs ea, int tiles_m,
@@ -762,9 +776,9 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
     const int lo = (int)(sub * xs / xper), hi = (int)(sub * (xs + 1) / xper);
     const int first = lo + bid / ng;
     if (first >= hi) return;
-    if constexpr (GEMM_VAR_STAGGER > 0) {  // timing variant: odd workgroups start later (desynchronised epilogues)
-        if (bid & 1)
-            for (int i = 0; i < GEMM_VAR_STAGGER; i++) __builtin_amdgcn_s_sleep(127);
+    if constexpr (GEMM_VAR_STAGGER > 0) {  // timing variant: workgroups start at different times (desynchronised epilogues)
+        const int rounds = GEMM_VAR_STAGGER * ((bid >> GEMM_VAR_STAG_SHIFT) & GEMM_VAR_STAG_MASK);
+        for (int i = 0; i < rounds; i++) __builtin_amdgcn_s_sleep(GEMM_VAR_STAG_SLP);
     }
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -970,6 +984,24 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
             load_b(sW, 0);
             if (has2) {
                 issue_a(buf, 1, p2);
+                if constexpr (GEMM_VAR_RPF > 0 && EPI == EPI_RESID_F16) {
+                    // timing variant: one 4-byte LDS-DMA per lane (no VGPR destination) touching
+                    // 128 / RPF of the wave's residual rows (two 64-B halves each) in each of the
+                    // K-steps nk-1-RPF .. nk-2; retired by the next K-step's vmcnt(6)
+                    const int k0 = nk - 1 - GEMM_VAR_RPF;
+                    if (kt >= k0 && kt < nk - 1) {
+                        constexpr int RPS = 128 / (GEMM_VAR_RPF > 0 ? GEMM_VAR_RPF : 1);  // rows per K-step
+                        const int r = (kt - k0) * RPS + (lane & 31) % RPS;
+                        int64_t m = (int64_t)tmt * G2_M + wr * 128 + r;
+                        m = m < M ? m : M - 1;
+                        const _Float16* src = (const _Float16*)ea.out + m * ea.ldc + (nb0 + tnt) * G2_N + wc * 64 +
+                                              (lane >> 5) * 32;
+                        __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(lds + 2 * G2_STAGE + 3 * 8 * 512), 4, 0, 0);
+                        G5_LDS_DONE();
+                        asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+                        goto rpf_done;
+                    }
+                }
                 G5_LDS_DONE();
                 if constexpr (CAN_DEFER) {
                     constexpr int S = EpiVm<EPI>::count;
@@ -990,6 +1022,7 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
                 G5_LDS_DONE();
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
+        rpf_done:
             G5_BARRIER();
             compute(1, 0);
             G5_BARRIER();
@@ -1097,12 +1130,15 @@ static int launch(const void* A, int64_t lda, const void* W, int64_t ldw, int64_
                    "gemm: survivor epilogue: too many tiles per workgroup");
         // two operand stages + bias / colsum / rowstat slots (8 waves x 1 KiB each)
         // (EPI_RRSV: its record and survivor buffers instead, rrsv_tile)
-        const size_t lds = 2 * (size_t)G2_STAGE * 2 + (EPI == EPI_RRSV ? kRrsvSlotBytes : 3 * 8 * 256 * sizeof(float));
-        static bool attr = false;
-        if (!attr) {
-            RM_CHECK_HIP(hipFuncSetAttribute((const void*)gemm_persistent_kernel<EPI>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            attr = true;
+        const size_t lds = 2 * (size_t)G2_STAGE * 2 + (EPI == EPI_RRSV ? kRrsvSlotBytes : 3 * 8 * 256 * sizeof(float)) +
+                           (GEMM_VAR_RPF > 0 ? 256 : 0);
+        // c_proj (residual epilogue, K > N) launches the TAG 1 copy of the kernel
+        const bool tag1 = EPI == EPI_RESID_F16 && K > N;
+        auto kern = tag1 ? gemm_persistent_kernel<EPI, 1> : gemm_persistent_kernel<EPI, 0>;
+        static bool attr[2] = {false, false};
+        if (!attr[tag1]) {
+            RM_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            attr[tag1] = true;
         }
         const int grid = (int)(tiles256 < 256 ? tiles256 : 256);
         // XCD N-groups: auto = 2 when the N-tiles split evenly and there are >= 8 of them
@@ -1114,7 +1150,7 @@ static int launch(const void* A, int64_t lda, const void* W, int64_t ldw, int64_
         // stream from HBM; the survivor epilogue's tile list is in band order too), else
         // M-major (the encoder's weights stay in L2 / MALL)
         const int band = EPI != EPI_RRHI ? 0 : opt.band >= 0 ? opt.band : RR_GEMM_BAND;
-        hipLaunchKernelGGL((gemm_persistent_kernel<EPI>), dim3((unsigned)grid), dim3(512), lds, s, (const _Float16*)A,
+        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(512), lds, s, (const _Float16*)A,
                            lda, (const _Float16*)W, ldw, M, (int)N, (int)K, ea, tiles_m, tiles_n, ngroups, band);
         RM_LAUNCHED();
         return OK;
