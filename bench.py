@@ -148,7 +148,7 @@ class Workload:
         self.qlo, self.qhi = shard(self.Q, rank, world)
         self.glo, self.ghi = shard(self.G, rank, world)
         if crops == "identity":  # identity-structured (the MSMT17 leg: real-like k-reciprocal neighbourhoods)
-            ic = IdentityCrops(sp["num_ids"], sp["num_cams"], 5, dev)
+            ic = IdentityCrops(sp["num_ids"], sp["num_cams"], 5, dev, noise=0.3)
             self.q_img = ic(self.q_pids, self.q_cams, self.qlo, self.qhi)
             ic.seed = 6
             self.g_img = ic(self.g_pids, self.g_cams, self.glo, self.ghi)
@@ -199,6 +199,9 @@ class Workload:
         return cmc, mAP, t1 - t0, t2 - t1
 
 
+MSMT17_RESID_GAIN = 4.0  # synthetic.vit_state_dict resid_gain of the MSMT17 leg's network
+
+
 def msmt17_leg(model, dev, rank, world, batch, dataset="msmt17"):
     """configs[3] + the north star's target: MSMT17 (11659q x 82161g) end to end — sharded
     embed of every image (2 TTA passes), RCCL all-gather of the normalised feature blocks,
@@ -207,9 +210,17 @@ def msmt17_leg(model, dev, rank, world, batch, dataset="msmt17"):
     structured crops (IdentityCrops: 3060 ids, 15 cameras), so the embeddings have real
     k-reciprocal neighbourhoods and R2 takes the fp16 pre-filter path the way real features do
     (the U(-1,1) crops put every gallery item inside the bound and send each R2 row to the
-    exact fallback).  Timed once, after the Market steps (kernels warm); wall seconds are max
-    over ranks."""
+    exact fallback).  ``model`` None: ViT-B/16 with CLIP's init except residual-branch output
+    projections MSMT17_RESID_GAIN x larger (synthetic.vit_state_dict resid_gain): at CLIP's init
+    the blocks barely move the CLS row, every image embeds to nearly the same vector (cosine to
+    the mean 0.997) and R2 sends every row to the exact fallback; at gain 4 (0.97-0.98) the
+    embedded crops take the fp16 pre-filter path like trained features
+    (profiles/r04/feature_spread.txt).  Timed once, after the Market steps (kernels warm); wall
+    seconds are max over ranks."""
     from multimodal_reid_amd import reranking
+    model_own = model is None
+    if model_own:
+        model = VisionTransformer(syn.vit_state_dict("ViT-B/16", seed=0, resid_gain=MSMT17_RESID_GAIN), device=dev)
     wl = Workload(dev, rank, world, batch, dataset=dataset, model=model, crops="identity")
     Q, G = wl.Q, wl.G
 
@@ -244,11 +255,8 @@ def msmt17_leg(model, dev, rank, world, batch, dataset="msmt17"):
     sync()
     t3 = time.perf_counter()
     del final, qn, gn
-    # The random-init network's embeddings are concentrated (even of identity-structured crops
-    # every gallery item lies inside the fp16 bound), so R2 above ran every row through the exact
-    # fallback.  Real (trained) features have k-reciprocal neighbourhoods; the re-rank + eval is
-    # timed again on the §8d back-end features (identity-clustered Gaussians, D = 1280) of the
-    # same split: the path real features take (fp16 pre-filter, in-epilogue triangle R2).
+    # The re-rank + eval timed again on the §8d back-end features (identity-clustered Gaussians,
+    # D = 1280) of the same split, the reference point of earlier rounds.
     qf_np, gf_np = syn.features(wl.q_pids, wl.g_pids, dim=1280, seed=0)
     qs = evaluate.l2_normalize_device(torch.from_numpy(qf_np).to(dev))
     gs = evaluate.l2_normalize_device(torch.from_numpy(gf_np).to(dev))
@@ -262,12 +270,16 @@ def msmt17_leg(model, dev, rank, world, batch, dataset="msmt17"):
     t5 = time.perf_counter()
     te, tv, tr, t8 = _max_over_ranks([t1 - t0, t2 - t1, t3 - t2, t5 - t4], dev)
     N, D = Q + G, qs.shape[1]
+    wl_D = wl.model.width + wl.model.out_dim
+    tri_e = N * N * wl_D
+    fl_e = 2.0 * tri_e / (PEAK_F16_TFLOPS * 1e12)
     del wl, final, qs, gs
     torch.cuda.empty_cache()
     tri = N * N * D  # the R2 pre-filter's fp16 product over the upper triangle (2 N^2 D / 2)
     embed_flop = 2 * N * 37.90e9
     fl, hb = 2.0 * tri / (PEAK_F16_TFLOPS * 1e12), 8.0 * Q * G / (PEAK_HBM_GBPS * 1e9)
-    return {"config": f"MSMT17 {Q}q x {G}g, identity-structured crops (3060 ids, 15 cams), ViT-B/16 2 passes/img, "
+    return {"config": f"MSMT17 {Q}q x {G}g, identity-structured crops (3060 ids, 15 cams, noise 0.3), ViT-B/16 "
+                      f"(synthetic, residual gain {MSMT17_RESID_GAIN if model_own else 'caller'}) 2 passes/img, "
                       f"{world} GPU(s): sharded embed + all-gather, exact distmat + CMC/mAP, sharded k-reciprocal "
                       "re-rank (k1=50 k2=15 lambda=0.3) + CMC/mAP",
             "imgs_per_s": round((Q + G) / te, 1), "embed_wall_s": round(te, 4), "eval_wall_s": round(tv, 4),
@@ -280,10 +292,14 @@ def msmt17_leg(model, dev, rank, world, batch, dataset="msmt17"):
                        "roofline": {"bound": "mfma (R2 fp16 pre-filter, N^2 D upper-triangle product)",
                                     "algorithmic_flop": 2.0 * tri, "flop_floor_s": round(fl, 5),
                                     "hbm_floor_s": round(hb, 5), "frac": round(max(fl, hb) / t8, 4)}},
-            "rerank_embedded": {"features": "the embedded crops (random-init network: concentrated, every R2 row "
-                                            "through the exact fallback)", "wall_s": round(tr, 4),
+            "rerank_embedded": {"features": f"the embedded crops (D={wl_D}; synthetic network, residual gain "
+                                            f"{MSMT17_RESID_GAIN if model_own else 'caller'})", "wall_s": round(tr, 4),
                                 "mAP_rerank": float(mAP_rr), "rank1_rerank": float(cmc_rr[0]),
-                                "r2_rows": stats.get("rows"), "r2_exact_fallback_rows": stats.get("exact_rows")},
+                                "r2_rows": stats.get("rows"), "r2_exact_fallback_rows": stats.get("exact_rows"),
+                                "r2_form": stats.get("form"),
+                                "roofline": {"bound": "mfma (R2 fp16 pre-filter, N^2 D upper-triangle product)",
+                                             "algorithmic_flop": 2.0 * tri_e, "flop_floor_s": round(fl_e, 5),
+                                             "frac": round(max(fl_e, hb) / tr, 4)}},
             "roofline": {"embed": {"bound": "mfma", "achieved": round(embed_flop / te / 1e12, 1),
                                    "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
                                    "frac": round(embed_flop / te / 1e12 / PEAK_F16_TFLOPS, 4)}}}
@@ -634,7 +650,7 @@ def main():
                               ctypes.byref(fl))
     L.reidmi_prof_enable(0)
     elapsed = _max_over_ranks([elapsed], dev)[0]
-    ms17 = None if a.no_msmt17 else msmt17_leg(wl.model, dev, rank, world, a.batch)
+    ms17 = None if a.no_msmt17 else msmt17_leg(None, dev, rank, world, a.batch)
     if rank == 0:
         imgs = (wl.Q + wl.G) * a.steps
         avg_ms = ms.value / max(cnt.value, 1)

@@ -55,9 +55,6 @@ constexpr int GB_M = 128, GB_N = 128, GB_K = 64;
 #ifndef GEMM_VAR_STAGGER  // s_sleep(GEMM_VAR_STAG_SLP) rounds before a workgroup starts:
 #define GEMM_VAR_STAGGER 0  // STAGGER x ((bid >> GEMM_VAR_STAG_SHIFT) & GEMM_VAR_STAG_MASK)
 #endif
-#ifndef GEMM_VAR_RPF  // residual epilogue: prefetch the tile's residual rows to L2 over RPF K-steps
-#define GEMM_VAR_RPF 0
-#endif
 #ifndef GEMM_VAR_STAG_SHIFT
 #define GEMM_VAR_STAG_SHIFT 0
 #endif
@@ -779,6 +776,12 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
     if constexpr (GEMM_VAR_STAGGER > 0) {  // timing variant: workgroups start at different times (desynchronised epilogues)
         const int rounds = GEMM_VAR_STAGGER * ((bid >> GEMM_VAR_STAG_SHIFT) & GEMM_VAR_STAG_MASK);
         for (int i = 0; i < rounds; i++) __builtin_amdgcn_s_sleep(GEMM_VAR_STAG_SLP);
+    } else if constexpr (EPI == EPI_RESID_F16) {
+        // The residual epilogue reads and writes 2 x 128 KB per tile; with every workgroup in
+        // step those bursts hit HBM together.  Odd workgroups start ~8k cycles (~1/8 of an
+        // out_proj tile) late: out_proj -2.5 %, c_proj -1.7 %; no effect on the other epilogues
+        // (profiles/r04/gemm_stagger_prefetch_ab.txt)
+        if (bid & 1) __builtin_amdgcn_s_sleep(127);
     }
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -984,24 +987,6 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
             load_b(sW, 0);
             if (has2) {
                 issue_a(buf, 1, p2);
-                if constexpr (GEMM_VAR_RPF > 0 && EPI == EPI_RESID_F16) {
-                    // timing variant: one 4-byte LDS-DMA per lane (no VGPR destination) touching
-                    // 128 / RPF of the wave's residual rows (two 64-B halves each) in each of the
-                    // K-steps nk-1-RPF .. nk-2; retired by the next K-step's vmcnt(6)
-                    const int k0 = nk - 1 - GEMM_VAR_RPF;
-                    if (kt >= k0 && kt < nk - 1) {
-                        constexpr int RPS = 128 / (GEMM_VAR_RPF > 0 ? GEMM_VAR_RPF : 1);  // rows per K-step
-                        const int r = (kt - k0) * RPS + (lane & 31) % RPS;
-                        int64_t m = (int64_t)tmt * G2_M + wr * 128 + r;
-                        m = m < M ? m : M - 1;
-                        const _Float16* src = (const _Float16*)ea.out + m * ea.ldc + (nb0 + tnt) * G2_N + wc * 64 +
-                                              (lane >> 5) * 32;
-                        __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(lds + 2 * G2_STAGE + 3 * 8 * 512), 4, 0, 0);
-                        G5_LDS_DONE();
-                        asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
-                        goto rpf_done;
-                    }
-                }
                 G5_LDS_DONE();
                 if constexpr (CAN_DEFER) {
                     constexpr int S = EpiVm<EPI>::count;
@@ -1022,7 +1007,6 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
                 G5_LDS_DONE();
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
-        rpf_done:
             G5_BARRIER();
             compute(1, 0);
             G5_BARRIER();
@@ -1130,8 +1114,7 @@ static int launch(const void* A, int64_t lda, const void* W, int64_t ldw, int64_
                    "gemm: survivor epilogue: too many tiles per workgroup");
         // two operand stages + bias / colsum / rowstat slots (8 waves x 1 KiB each)
         // (EPI_RRSV: its record and survivor buffers instead, rrsv_tile)
-        const size_t lds = 2 * (size_t)G2_STAGE * 2 + (EPI == EPI_RRSV ? kRrsvSlotBytes : 3 * 8 * 256 * sizeof(float)) +
-                           (GEMM_VAR_RPF > 0 ? 256 : 0);
+        const size_t lds = 2 * (size_t)G2_STAGE * 2 + (EPI == EPI_RRSV ? kRrsvSlotBytes : 3 * 8 * 256 * sizeof(float));
         // c_proj (residual epilogue, K > N) launches the TAG 1 copy of the kernel
         const bool tag1 = EPI == EPI_RESID_F16 && K > N;
         auto kern = tag1 ? gemm_persistent_kernel<EPI, 1> : gemm_persistent_kernel<EPI, 0>;

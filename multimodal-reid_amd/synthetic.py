@@ -46,10 +46,13 @@ def vit_grid(height, width, stride=12, patch=16):
 
 
 def vit_state_dict(model="ViT-B/16", height=256, width=128, stride=12, seed=0, layers=None,
-                   width_override=None, heads_override=None, vpt_ctx=0):
+                   width_override=None, heads_override=None, vpt_ctx=0, resid_gain=1.0):
     """State dict (numpy fp32) with the key layout of custom_clip_model.VisionTransformer
     (and, with ``vpt_ctx>0``, the IVLP extras of maple.VisionTransformer: ``VPT`` and
-    per-block ``VPT_shallow`` for blocks 1..L-1, maple.py:604-611,737-743)."""
+    per-block ``VPT_shallow`` for blocks 1..L-1, maple.py:604-611,737-743).  ``resid_gain``
+    scales the residual branches' output projections (attn.out_proj, mlp.c_proj): at CLIP's
+    init (1.0) each block adds little to the residual stream, so the CLS output barely depends
+    on the image (concentrated embeddings); a trained tower's blocks do not."""
     spec = dict(VIT_SPECS[model])
     if width_override:
         spec["width"] = width_override
@@ -61,7 +64,7 @@ def vit_state_dict(model="ViT-B/16", height=256, width=128, stride=12, seed=0, l
     gh, gw = vit_grid(height, width, stride, P)
     scale = w ** -0.5
     attn_std = w ** -0.5
-    proj_std = (w ** -0.5) * ((2 * L) ** -0.5)
+    proj_std = (w ** -0.5) * ((2 * L) ** -0.5) * resid_gain
     fc_std = (2 * w) ** -0.5
     sd = {}
     sd["conv1.weight"] = _normal("conv1.weight", (w, 3, P, P), (3 * P * P) ** -0.5, seed)
@@ -291,12 +294,12 @@ def openai_state_dict(model="ViT-B/16", seed=0, vpt_ctx=0, text_ctx=0, input_res
     return sd
 
 
-def clipreid_checkpoint(model="ViT-B/16", seed=0, height=256, width=128, stride=12):
+def clipreid_checkpoint(model="ViT-B/16", seed=0, height=256, width=128, stride=12, resid_gain=1.0):
     """CLIP-ReID checkpoint key layout that utils.model_adaptor reads (utils.py:184-221):
     ``image_encoder.*`` (the stride-12 vision tower), ``text_encoder.*`` (the text tower,
     zero_shot_learning.py:31-34) and the BNNeck ``bottleneck.*`` / ``bottleneck_proj.*``
     BatchNorm1d buffers (utils.py:128-142)."""
-    vis = vit_state_dict(model, height=height, width=width, stride=stride, seed=seed)
+    vis = vit_state_dict(model, height=height, width=width, stride=stride, seed=seed, resid_gain=resid_gain)
     sd = {"image_encoder." + k: v for k, v in vis.items()}
     sd.update({"text_encoder." + k: v for k, v in text_state_dict(seed=seed).items()})
     W, E = VIT_SPECS[model]["width"], VIT_SPECS[model]["out_dim"]
