@@ -55,9 +55,9 @@ EPI_GELU = 1  # the c_fc GEMM (+QuickGELU epilogue): the largest single kernel p
 # an XCD (4 MB L2).  Other batches: not measured (null).
 #   batch 1024 (profiles/r02/pmc_c_fc_fp16_walk2_*): 736 400 / 1 296 384 KiB; algorithmic
 #     A 332 MB + W 4.7 MB + out 1 327 MB = 1.66 GB
-#   batch 4096 (profiles/r03/pmc_c_fc_b4096_*): 3 142 462 / 5 185 615 KiB; algorithmic
-#     A 1 327 MB + W 4.7 MB + out 5 310 MB = 6.64 GB
-C_FC_TRAFFIC_BYTES = {1024: (2 * 736400 + 1296384) * 1024, 4096: (2 * 3142462 + 5185615) * 1024}
+#   batch 4096 (profiles/r04/final/pmc_c_fc_b4096_*, mean of 6 launches; r03: 3 142 462 /
+#     5 185 615): 3 150 970 / 5 185 625 KiB; algorithmic A 1 327 MB + W 4.7 MB + out 5 310 MB = 6.64 GB
+C_FC_TRAFFIC_BYTES = {1024: (2 * 736400 + 1296384) * 1024, 4096: (2 * 3150970 + 5185625) * 1024}
 
 
 def _max_over_ranks(values, dev):
@@ -676,7 +676,7 @@ def main():
             "embed_wall_s": round(embed_s / a.steps, 4),
             "mAP": round(float(mAP), 6),
             "rank1": round(float(cmc[0]), 6),
-            "roofline": {"bound": "mfma", "kernel": "gemm_persistent_kernel<1> (ln_2-folded fp16 mlp.c_fc + QuickGELU)",
+            "roofline": {"bound": "mfma", "kernel": "gemm_persistent_kernel<1, 0> (ln_2-folded fp16 mlp.c_fc + QuickGELU)",
                          "achieved": round(achieved, 1) if achieved else None, "peak": PEAK_F16_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_F16_TFLOPS, 4) if achieved else None,
                          "traffic": C_FC_TRAFFIC_BYTES.get(a.batch), "traffic_unit": "bytes/launch (PMC)", "avg_launch_ms": round(avg_ms, 4), "launches": cnt.value,

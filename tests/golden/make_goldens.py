@@ -455,10 +455,10 @@ def adaptor_fixtures(out):
     print("adaptor fixtures ok")
 
 
-# 1024 q x 3072 g, 600 ids, crop noise 0.3: the reference's fp16 and fp32 runs agree to 2.4e-5
-# (plain) / 1.7e-4 (re-ranked) in mAP.  At 512 x 2048 with noise 0.6 (mAP 0.18) they differed by
-# 5e-4 / 7.7e-4 and one query's flip moved mAP by ~2e-3: a flat 1e-3 bound was a coin toss there.
-# ~25 min on the container's 8 cores.
+# 1024 q x 3072 g, 600 ids, crop noise 0.3, residual gain 4: the reference's fp16 and fp32 runs
+# agree to 1.9e-4 (plain) / 3.4e-4 (re-ranked) in mAP.  At 512 x 2048 with noise 0.6 (mAP 0.18)
+# they differed by 5e-4 / 7.7e-4 and one query's flip moved mAP by ~2e-3: a flat 1e-3 bound was a
+# coin toss there.  ~29 min on the container's 8 cores.
 E2E_Q, E2E_G = int(os.environ.get("E2E_Q", 1024)), int(os.environ.get("E2E_G", 3072))
 E2E_IDS = int(os.environ.get("E2E_IDS", 600))
 E2E_NOISE = float(os.environ.get("E2E_NOISE", 0.3))
