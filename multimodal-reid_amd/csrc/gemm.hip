@@ -1117,7 +1117,7 @@ static int launch(const void* A, int64_t lda, const void* W, int64_t ldw, int64_
         const size_t lds = 2 * (size_t)G2_STAGE * 2 + (EPI == EPI_RRSV ? kRrsvSlotBytes : 3 * 8 * 256 * sizeof(float));
         // c_proj (residual epilogue, K > N) launches the TAG 1 copy of the kernel
         const bool tag1 = EPI == EPI_RESID_F16 && K > N;
-        auto kern = tag1 ? gemm_persistent_kernel<EPI, 1> : gemm_persistent_kernel<EPI, 0>;
+        auto kern = tag1 ? gemm_persistent_kernel<EPI, EPI == EPI_RESID_F16 ? 1 : 0> : gemm_persistent_kernel<EPI, 0>;
         static bool attr[2] = {false, false};
         if (!attr[tag1]) {
             RM_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
