@@ -159,6 +159,9 @@ __device__ __forceinline__ void attn_block(const _Float16* sK, const _Float16* s
 //  * O^T is widened to 16-byte stores by one v_permlane32_swap per dword (4 stores per lane
 //    instead of 8 half-width ones): kAttnPipeStores vector-memory ops per wave.
 constexpr int kAttnPipeStores = 4;
+#ifndef ATTN_TEXT_STAGES  // LDS stages of the causal mhsa_kernel at NKB <= 4 (2: the plain double buffer)
+#define ATTN_TEXT_STAGES 3
+#endif
 #ifndef ATTN_PIPE
 #define ATTN_PIPE 1
 #endif
@@ -396,7 +399,10 @@ __device__ __forceinline__ void attn_block_pipe(const _Float16* sK, const _Float
 //     of O^T = V^T P^T (accumulator-as-operand), V^T read with the same key permutation;
 //   O^T[d][q] comes out as 4 runs of 4 consecutive d per lane -> 8-byte stores.
 
-template <int NKB, bool CAUSAL>
+//   NS = 3 (the causal text shapes, NKB <= 4): a ring of three LDS stages, K/V two heads ahead
+//   and Q one head ahead — short text heads are bound by the latency of their loads (one head
+//   in flight per workgroup left the CU waiting).
+template <int NKB, bool CAUSAL, int NS = 2>
 __global__ __launch_bounds__(512) void mhsa_kernel(const _Float16* __restrict__ q, const _Float16* __restrict__ k,
                                                    const _Float16* __restrict__ vt, _Float16* __restrict__ o, int L,
                                                    int H, int vstride, int64_t nbh, float scale_log2) {
@@ -452,6 +458,62 @@ __global__ __launch_bounds__(512) void mhsa_kernel(const _Float16* __restrict__ 
 
     int64_t bh = blockIdx.x;
     if (bh >= nbh) return;
+    if constexpr (NS == 3) {
+        // Every wave issues LP/8/nw = 4 K pieces and 4 V^T pieces per head, wave 0 one more
+        // (the blob's half last piece): nw == NKB waves, V^T blob = 4 NKB + 1/2 KiB (launcher
+        // checks vstride == LP + 4).  The counted waits below rely on these counts and on the
+        // 8 O stores of attn_block.
+        const int64_t G = gridDim.x;
+        issue(bh, 0);
+        f16x8 qf[4];
+        load_q(bh, qf);
+        const bool second = bh + G < nbh;
+        if (second) issue(bh + G, 1);
+        // the first head's K / V^T and Q have landed; the second head's K / V^T stays in flight
+        if (!second)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else if (wid == 0)
+            asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        pin(qf);
+        __builtin_amdgcn_s_barrier();
+        zero_pad(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        int stage = 0;
+        for (; bh < nbh; bh += G) {
+            const int64_t nxt = bh + G, nxt2 = bh + 2 * G;
+            f16x8 qn[4];
+            if (nxt < nbh) load_q(nxt, qn);  // issued before the K/V of nxt2: retired with nxt's
+            if (nxt2 < nbh) issue(nxt2, stage == 0 ? 2 : stage - 1);  // the stage head bh-G used
+            const _Float16* sK = lds + stage * stage_elems;
+            const _Float16* sV = sK + LP * 64;
+            if (wid * 32 < L) attn_block<NKB, CAUSAL>(sK, sV, vstride, qf, qi, L, bh, H, o, scale_log2);
+            // nxt's K / V^T (issued one head ago) and Q have landed; nxt2's K / V^T and this
+            // head's O stores (the youngest ops) stay in flight
+            if (wid * 32 >= L)
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            else if (nxt2 >= nbh)
+                asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+            else if (wid == 0)
+                asm volatile("s_waitcnt vmcnt(17) lgkmcnt(0)" ::: "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            const int nstage = stage == 2 ? 0 : stage + 1;
+            if (nxt < nbh) {
+                zero_pad(nstage);
+                pin(qn);
+#pragma unroll
+                for (int ks = 0; ks < 4; ks++) qf[ks] = qn[ks];
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            stage = nstage;
+        }
+        return;
+    }
     int stage = 0;
     issue(bh, 0);
     f16x8 qf[4];
@@ -996,15 +1058,18 @@ static int launch_mhsa(const void* q, const void* k, const void* vt, void* o, in
         return launch_mhsa_pipe<NKB>(q, k, vt, o, nseq, L, H, s);
     }
     constexpr int LP = NKB * 32;
+    // three LDS stages for the short causal (text) shapes (mhsa_kernel NS), two otherwise
+    constexpr int NS = CAUSAL && NKB <= 4 ? ATTN_TEXT_STAGES : 2;
     const int vs = vt_stride(LP);
     RM_REQUIRE(lpad_g == vs, "mhsa: v^T row stride must be reidmi_attn_lpad(L)");
+    RM_REQUIRE(NS == 2 || (vs == LP + 4 && (L + 31) / 32 == NKB), "mhsa: ring counts assume V^T rows of LP + 4");
     const size_t stage = (size_t)LP * 64 * 2 + (size_t)64 * vs * 2;
-    const size_t lds = 2 * stage;
+    const size_t lds = NS * stage;
     const float scale_log2 = 0.125f * 1.4426950408889634f;  // 1/sqrt(64) * log2(e)
+    auto kern = mhsa_kernel<NKB, CAUSAL, NS>;
     static bool attr = false;
     if (!attr) {
-        RM_CHECK_HIP(hipFuncSetAttribute((const void*)mhsa_kernel<NKB, CAUSAL>,
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        RM_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         attr = true;
     }
     const int64_t nbh = nseq * H;
@@ -1015,14 +1080,13 @@ static int launch_mhsa(const void* q, const void* k, const void* vt, void* o, in
     static int occ_waves = -1, occ = 1;
     if (occ_waves != waves) {
         int n = 0;
-        RM_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)mhsa_kernel<NKB, CAUSAL>,
-                                                                  64 * waves, lds));
+        RM_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)kern, 64 * waves, lds));
         occ = n > 0 ? n : 1;
         occ_waves = waves;
     }
     const int64_t slots = (int64_t)num_cu() * occ;
     const int64_t grid = nbh < slots ? nbh : slots;
-    hipLaunchKernelGGL((mhsa_kernel<NKB, CAUSAL>), dim3((unsigned)grid), dim3(64 * waves), lds, s,
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * waves), lds, s,
                        (const _Float16*)q, (const _Float16*)k, (const _Float16*)vt, (_Float16*)o, L, H, vs, nbh,
                        scale_log2);
     RM_LAUNCHED();
