@@ -211,6 +211,39 @@ def test_mhsa(gpu, L, causal):
     assert (got - ref).abs().max() < 5e-3  # fp16 P and O (bf16 needed 3e-2)
 
 
+@pytest.mark.parametrize("L,causal,nseq,H", [(20, True, 700, 8), (50, True, 700, 8), (77, True, 500, 8),
+                                            (128, True, 300, 8), (211, False, 300, 12)])
+def test_mhsa_many_heads(gpu, L, causal, nseq, H):
+    """More (sequence, head) pairs than the persistent grid has workgroups, so every workgroup
+    walks several heads: the prefetch rings (three LDS stages for the causal text shapes,
+    NKB 1-4; the pipelined two-stage vision kernel) rotate and their counted waits are
+    exercised.  Reference: torch fp32 softmax attention on the device, same bound as test_mhsa."""
+    lib = _lib()
+    lp = lib.load().reidmi_attn_lpad(L)
+    g = torch.Generator(device="cuda").manual_seed(1000 + L)
+    n = nseq * H
+    q = (torch.randn(n, L, 64, generator=g, device="cuda") * 2).half()
+    k = (torch.randn(n, L, 64, generator=g, device="cuda") * 2).half()
+    v = torch.randn(n, L, 64, generator=g, device="cuda").half()
+    vt = torch.full((n, 64, lp), float("nan"), dtype=torch.float16, device="cuda")
+    vt[:, :, :L] = v.transpose(1, 2)
+    o = torch.empty(nseq * L, H * 64, dtype=torch.float16, device="cuda")
+    lib.call("reidmi_mhsa_f16", lib.ptr(q), lib.ptr(k), lib.ptr(vt), lib.ptr(o), nseq, L, H, int(causal),
+             lib.stream())
+    worst = 0.0
+    for a in range(0, n, 512):  # reference in slices (fp32 scores of 512 heads at a time)
+        z = min(n, a + 512)
+        s = (q[a:z].float() @ k[a:z].float().transpose(1, 2)) * 0.125
+        if causal:
+            s = s + torch.full((L, L), float("-inf"), device="cuda").triu(1)
+        ref = torch.softmax(s, -1) @ v[a:z].float()  # [heads, L, 64], head index = b * H + h
+        b0, b1 = a // H, (z + H - 1) // H
+        got = o.view(nseq, L, H, 64)[b0:b1].permute(0, 2, 1, 3).reshape(-1, L, 64)[a - b0 * H:z - b0 * H]
+        assert torch.isfinite(got).all()
+        worst = max(worst, float((got.float() - ref).abs().max()))
+    assert worst < 5e-3, worst
+
+
 @pytest.fixture(scope="module")
 def vit_b16(gpu):
     from multimodal_reid_amd.model import VisionTransformer
