@@ -382,6 +382,7 @@ def backend_rooflines(wl, reps=10):
 
     dist_buf = torch.empty(Q, G, device=wl.dev)
     gp, gc = wl.g_pids[wl.glo:wl.ghi], wl.g_cams[wl.glo:wl.ghi]
+    td16 = timed(lambda: evaluate.euclidean_distance_device(qn, gn, out=dist_buf, precision="fp16"))
     td = timed(lambda: evaluate.euclidean_distance_device(qn, gn, out=dist_buf))
     args = [torch.from_numpy(np.ascontiguousarray(a)).to(wl.dev) for a in (qp, gp, qc, gc)]
     te = timed(lambda: evaluate.eval_rows_device(dist_buf, *args))
@@ -389,6 +390,12 @@ def backend_rooflines(wl, reps=10):
     return {"distmat": {"bound": "mfma-fp32", "achieved": round(2.0 * Q * G * D / td / 1e12, 1),
                         "peak": PEAK_F32_MATRIX_TFLOPS, "unit": "TFLOP/s",
                         "frac": round(2.0 * Q * G * D / td / 1e12 / PEAK_F32_MATRIX_TFLOPS, 4), "ms": round(td * 1e3, 3)},
+            # the §8b reduced-precision mode (fp16 operands, not bit-exact; not the step's path):
+            # casts + fp16 GEMM + the Q x G distance pass
+            "distmat_f16": {"bound": "mfma-fp16 + hbm", "achieved": round(2.0 * Q * G * D / td16 / 1e12, 1),
+                            "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
+                            "frac": round(2.0 * Q * G * D / td16 / 1e12 / PEAK_F16_TFLOPS, 4),
+                            "ms": round(td16 * 1e3, 3)},
             "eval_rows": {"bound": "hbm", "achieved": round(eb / te / 1e9, 1), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                           "frac": round(eb / te / 1e9 / PEAK_HBM_GBPS, 4), "ms": round(te * 1e3, 3),
                           "algorithmic_bytes": eb}}

@@ -27,6 +27,8 @@ SIGNATURES = {
     "reidmi_l2norm_f32": [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp],
     "reidmi_distmat_f32": [_vp, _i64, _i64, _vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp],
     "reidmi_cosine_f32": [_vp, _i64, _i64, _vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp],
+    "reidmi_distmat_f16_workspace_bytes": [_i64, _i64, _i64],
+    "reidmi_distmat_f16": [_vp, _i64, _i64, _vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp],
     "reidmi_topk_rows_f32": [_vp, _i64, _i64, _i64, _vp, _i32, _vp, _vp, _i64, _vp],
     "reidmi_eval_rows": [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp],
     "reidmi_eval_rows_workspace_bytes": [_i64],

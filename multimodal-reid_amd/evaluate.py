@@ -49,13 +49,23 @@ def l2_normalize_device(x):
     return y
 
 
-def euclidean_distance_device(qf, gf, out=None):
-    """(Q,G) fp32 tensor: ||q||^2 + ||g||^2 - 2 q.g, exact fp32 (fmaf chain over k)."""
+def euclidean_distance_device(qf, gf, out=None, precision="fp32"):
+    """(Q,G) fp32 tensor: ||q||^2 + ||g||^2 - 2 q.g.  precision "fp32" (default): exact fp32
+    (fmaf chain over k), the reference's distances up to BLAS order; "fp16": the q.g products on
+    the fp16 MFMA GEMM (reidmi_distmat_f16, the §8b reduced-precision mode; not bit-exact)."""
+    if precision not in ("fp32", "fp16"):
+        raise ValueError(f"euclidean_distance_device: precision must be 'fp32' or 'fp16', not {precision!r}")
     qf, gf = _as_dev_f32(qf), _as_dev_f32(gf)
     Q, D = qf.shape
     G = gf.shape[0]
     if out is None:
         out = torch.empty((Q, G), device=qf.device, dtype=torch.float32)
+    if precision == "fp16":
+        nb = _lib.load().reidmi_distmat_f16_workspace_bytes(Q, G, D)
+        ws = torch.empty(max(nb, 1), device=qf.device, dtype=torch.uint8)
+        _lib.call("reidmi_distmat_f16", _lib.ptr(qf), Q, qf.stride(0), _lib.ptr(gf), G, gf.stride(0), D,
+                  _lib.ptr(out), out.stride(0), _lib.ptr(ws), nb, _lib.stream())
+        return out
     ws = torch.empty(Q + G, device=qf.device, dtype=torch.float32)
     _lib.call("reidmi_distmat_f32", _lib.ptr(qf), Q, qf.stride(0), _lib.ptr(gf), G, gf.stride(0), D,
               _lib.ptr(out), out.stride(0), _lib.ptr(ws), _lib.stream())

@@ -51,6 +51,51 @@ def test_distmat_bitexact(gpu, Q, G, D):
         assert np.array_equal(out.cpu().numpy().view(np.uint32), ref), v
 
 
+@pytest.mark.parametrize("Q,G,D", [(100, 500, 1280), (37, 259, 768), (1, 1, 2), (130, 129, 1792), (5, 300, 513),
+                                   (700, 3000, 1280)])
+def test_distmat_f16_mode_bound(gpu, Q, G, D):
+    """The §8b reduced-precision mode (reidmi_distmat_f16): every entry within
+    2^-8 ||q|| ||g|| of the exact distance (fp16 operands: 2^-11 relative per element, the
+    dot's error <= 2^-10 ||q|| ||g|| by Cauchy-Schwarz, doubled by the -2 q.g term, plus fp32
+    accumulation), on unnormalised and on L2-normalised rows; padding of D to the GEMM's K step
+    and of G to its tile never leaks into the result."""
+    r = np.random.default_rng(Q * 11 + G)
+    q = r.standard_normal((Q, D)).astype(np.float32)
+    g = r.standard_normal((G, D)).astype(np.float32)
+    ev = _ev()
+    for norm in (False, True):
+        qd, gd = torch.from_numpy(q).cuda(), torch.from_numpy(g).cuda()
+        if norm:
+            qd, gd = ev.l2_normalize_device(qd), ev.l2_normalize_device(gd)
+        exact = ev.euclidean_distance_device(qd, gd)
+        low = ev.euclidean_distance_device(qd, gd, precision="fp16")
+        bound = 2.0 ** -8 * qd.norm(dim=1)[:, None] * gd.norm(dim=1)[None, :] + 1e-6
+        assert torch.isfinite(low).all()
+        assert bool(((low - exact).abs() <= bound).all()), float(((low - exact).abs() / bound).max())
+    with pytest.raises(ValueError):
+        ev.euclidean_distance_device(qd, gd, precision="bf16")
+
+
+def test_distmat_f16_mode_ranking(gpu):
+    """mAP / rank-1 through the reduced-precision mode against the exact one on identity-clustered
+    features of 800 q x 6000 g (normalised, as R1_mAP_eval feeds the distance): the retrieval
+    metrics agree to 2e-3 (measured: profiles/r04/distmat_f16_mode.txt)."""
+    ev = _ev()
+    qf, gf, qp, gp, qc, gc = _inputs(seed=9, Q=800, G=6000, junk=0.02)
+    qn = ev.l2_normalize_device(torch.from_numpy(qf).cuda())
+    gn = ev.l2_normalize_device(torch.from_numpy(gf).cuda())
+    res = {}
+    for prec in ("fp32", "fp16"):
+        d = ev.euclidean_distance_device(qn, gn, precision=prec)
+        valid, first, ap, nkept, _ = ev.eval_rows_device(d, qp, gp, qc, gc)
+        cmc, mAP = ev.aggregate_cmc_map(valid.cpu().numpy(), first.cpu().numpy(), ap.cpu().numpy(),
+                                        nkept.cpu().numpy(), len(gp), 50)
+        res[prec] = (float(cmc[0]), float(mAP))
+    print("distmat modes (rank-1, mAP):", res)
+    assert abs(res["fp16"][1] - res["fp32"][1]) <= 2e-3
+    assert abs(res["fp16"][0] - res["fp32"][0]) <= 2e-3
+
+
 def test_distmat_matches_reference_fixture(gpu):
     g = golden("backend_small.npz")
     qf, gf, *_ = _inputs()
