@@ -876,14 +876,21 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
             for (int ks = 0; ks < 2; ks++)
                 fb[j][ks] = *(const f16x8*)(sW + swz(wc * 64 + qn * 32 + j * 16 + (lane & 15), ks * 4 + (lane >> 4)));
     };
-    auto compute = [&](int qm, int qn) {
+    // FIRST: the tile's first K-step starts every accumulator chain from an inline-constant 0
+    // C operand, so no zeroing moves run between tiles (64 v_mov_b64 per wave and tile)
+    auto compute = [&](int qm, int qn, auto firstc) {
 #pragma unroll
         for (int ks = 0; ks < 2; ks++)
 #pragma unroll
             for (int i = 0; i < 4; i++)
 #pragma unroll
-                for (int j = 0; j < 2; j++)
-                    acc[qm * 4 + i][qn * 2 + j] = mfma16(fb[j][ks], fa[i][ks], acc[qm * 4 + i][qn * 2 + j]);
+                for (int j = 0; j < 2; j++) {
+                    f32x4& c = acc[qm * 4 + i][qn * 2 + j];
+                    if constexpr (decltype(firstc)::value)
+                        c = mfma16(fb[j][ks], fa[i][ks], ks == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : c);
+                    else
+                        c = mfma16(fb[j][ks], fa[i][ks], c);
+                }
     };
 
     // Bias of the current tile: one LDS-DMA per wave at the tile's first K-step into the
@@ -929,11 +936,7 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
     for (int tile = first; tile < hi; tile += gx) {
         int tmt, tnt;  // this tile's M-tile and N-tile (within the group)
         tile_mn<EPI == EPI_RRSV>(tile, tnk, band, tiles_m, rr_list, tmt, tnt);
-#pragma unroll
-        for (int i = 0; i < 8; i++)
-#pragma unroll
-            for (int j = 0; j < 4; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        for (int kt = 0; kt < nk; ++kt) {
+        auto kstep = [&](int kt, auto firstc) {
             const bool has1 = p1.tile < hi, has2 = p2.tile < hi;
             const bool b0_early = CAN_DEFER && kt == 0 && tile != first;  // issued before the epilogue
             const _Float16* sA = lds + buf * G2_STAGE;
@@ -967,21 +970,21 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
             if (has1 && !b0_early) issue_w(buf ^ 1, 0, p1);
             G5_LDS_DONE();
             G5_BARRIER();
-            compute(0, 0);
+            compute(0, 0, firstc);
             G5_BARRIER();
             // LOAD 1 / COMPUTE (0,1)
             load_b(sW, 1);
             if (has2) issue_a(buf, 0, p2);
             G5_LDS_DONE();
             G5_BARRIER();
-            compute(0, 1);
+            compute(0, 1, firstc);
             G5_BARRIER();
             // LOAD 2 / COMPUTE (1,1)
             load_a(sA, 1);
             if (has2) issue_w(buf, 1, p2);
             G5_LDS_DONE();
             G5_BARRIER();
-            compute(1, 1);
+            compute(1, 1, firstc);
             G5_BARRIER();
             // LOAD 3 / COMPUTE (1,0)
             load_b(sW, 0);
@@ -1008,12 +1011,14 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
             G5_BARRIER();
-            compute(1, 0);
+            compute(1, 0, firstc);
             G5_BARRIER();
             advance(p1);
             advance(p2);
             buf ^= 1;
-        }
+        };
+        kstep(0, std::true_type{});  // nk >= 2 (launch: K >= 2 * GB_K)
+        for (int kt = 1; kt < nk; ++kt) kstep(kt, std::false_type{});
         // both wave groups run the epilogue in the same barrier slot (group A, one barrier ahead
         // in the K-loop, waits here for group B's last COMPUTE; B catches up after it), so the
         // two groups' store tails overlap instead of running back to back
