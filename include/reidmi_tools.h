@@ -39,6 +39,12 @@ int reidmi_qkv_attention_f16(const void* x, int64_t ldx, const void* wq, int64_t
 
 /* The QKV GEMM alone (ln_1 fold + the head split reidmi_vit_forward uses): x [nseq*L][lda],
  * W [3*H*64][ldw] -> q, k [nseq*H][L][64], vt [nseq*H][64][lpad] (lpad = reidmi_attn_lpad(L)). */
+/* One-wave-per-SIMD GEMM prototype (gemm.hip gemm_w4_kernel): out fp16 = A.W^T + bias, same MFMA
+ * chain as reidmi_gemm_f16 epi 0 (bit-identical); nostore: the values are computed, not stored.
+ * N % 256 == 0, K % 64 == 0, K >= 128. */
+int reidmi_gemm_f16_w4(const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N, int64_t K,
+                       const float* bias, void* out, int64_t ldc, int nostore, void* stream);
+
 int reidmi_gemm_f16_qkv(const void* A, int64_t lda, const void* W, int64_t ldw, int64_t nseq, int L, int H,
                         const float* bias, const void* rowstat, const float* colsum, void* q, void* k, void* vt,
                         int lpad, void* stream);

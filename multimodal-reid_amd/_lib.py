@@ -99,6 +99,7 @@ TOOLS_SIGNATURES = {
     "reidmi_gemm_f16_tiled": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _vp],
     "reidmi_qkv_attention_f16": [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i32,
                                  _vp],
+    "reidmi_gemm_f16_w4": [_vp, _i64, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _i64, _i32, _vp],
     "reidmi_gemm_f16_qkv": [_vp, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp],
 }
 # entry points with struct arguments are typed in model.py (reidmi_vit_*, reidmi_text_*)

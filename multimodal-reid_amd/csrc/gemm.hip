@@ -1265,6 +1265,165 @@ REIDMI_API int reidmi_gemm_f16(int epi, const void* A, int64_t lda, const void* 
 }
 
 #ifdef REIDMI_TOOLS
+// ================================================ one-wave-per-SIMD prototype (W4, tools only)
+// The next GEMM design of DESIGN.md §5 (design (c), hipBLASLt's shape), measured before it is
+// built out: 256 threads = 4 waves, one per SIMD (up to 512 registers each), 256 x 256 x 64
+// tile; wave (wr, wc) owns rows 128 wr.. and columns 128 wc.. (8 x 8 fragments of 16 x 16:
+// 256 accumulator registers).  Two LDS stages; the next K-step's operands are DMA'd during the
+// current one (16 one-KiB pieces per wave, one per 8 MFMAs); one barrier per K-step.  Same
+// MFMA chain per output element as gemm_persistent_kernel (bit-identical).  Plain fp16 +
+// bias epilogue (NOSTORE: values kept, no stores) — a mainloop measurement.
+namespace reidmi {
+template <bool NOSTORE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm_w4_kernel(
+    const _Float16* __restrict__ A, int64_t lda, const _Float16* __restrict__ W, int64_t ldw, int64_t M, int N, int K,
+    EpiArgs ea, int tiles_n, int ntiles) {
+    extern __shared__ __attribute__((aligned(16))) _Float16 lds[];
+    constexpr int STAGE = (G2_M + G2_N) * GB_K;  // fp16 elements: A 256 x 64, then W 256 x 64
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wr = wid >> 1, wc = wid & 1;
+    const int nk = K / GB_K;
+    const int G = gridDim.x;
+    // DMA: waves 0, 1 bring A (pieces of 8 rows x 128 B), waves 2, 3 bring W; 16 pieces each.
+    // Piece u covers rows prow0 + 8u + (lane >> 3); its source chunk is swizzled by
+    // ((row >> 1) & 7) = (4u + (lane >> 4)) & 7: two per-lane chunk offsets (u even / odd).
+    // Every K-step issues all 16 pieces (past the workgroup's last K-step they re-read a valid
+    // K-step into the stage nobody reads again): no branches in the loop.
+    const bool isA = wid < 2;
+    const int prow0 = (wid & 1) * 128;
+    const int ld = (int)(isA ? lda : ldw);
+    const int l3 = lane >> 3;
+    const uint32_t chk_e = (uint32_t)(((lane & 7) ^ ((l3 >> 1) & 7)) << 3);
+    const uint32_t chk_o = (uint32_t)(((lane & 7) ^ (((l3 >> 1) + 4) & 7)) << 3);
+    _Float16* const dst0 = lds + (isA ? 0 : G2_M * GB_K) + prow0 * GB_K;
+    f32x4 accL[8][4], accR[8][4];  // columns wc*128 + [0, 64) and [64, 128)
+    f16x8 fa[8], fb[2][8];         // A fragments of one k-half (reused per row group), W of both
+    int tile = blockIdx.x;
+    if (tile >= ntiles) return;
+    // source of K-step kt of tile t for this wave's 128 operand rows, and how many of them exist
+    auto src_of = [&](int t, int kt, int& lim) -> const _Float16* {
+        const int64_t m0 = (int64_t)(t / tiles_n) * G2_M;
+        const int n0 = (t % tiles_n) * G2_N;
+        if (isA) {
+            const int64_t left = M - m0 - prow0;
+            lim = left < 128 ? (int)(left > 0 ? left : 1) : 128;
+            return A + (m0 + (left > 0 ? prow0 : 0)) * lda + kt * GB_K;
+        }
+        lim = 128;
+        return W + ((int64_t)n0 + prow0) * ldw + kt * GB_K;
+    };
+    auto issue = [&](const _Float16* src, int lim, int stage, int u) {
+        const int rmax = lim - 1 - 8 * u;  // rows past the matrix read its last row (never stored)
+        const int rr = l3 < rmax ? l3 : rmax;  // may be negative: row lim-1 of src, a valid row
+        const int o = rr * ld + (int)((u & 1) ? chk_o : chk_e);
+        __builtin_amdgcn_global_load_lds(src + ((int64_t)(8 * u) * ld + o),
+                                         (lds_ptr_t)(dst0 + stage * STAGE + 8 * u * GB_K), 16, 0, 0);
+    };
+    auto read_b = [&](const _Float16* sW, int ks, int b) {
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+            fb[b][j] = *(const f16x8*)(sW + swz(wc * 128 + j * 16 + (lane & 15), ks * 4 + (lane >> 4)));
+    };
+    auto read_a = [&](const _Float16* sA, int ks, int i) {
+        fa[i] = *(const f16x8*)(sA + swz(wr * 128 + i * 16 + (lane & 15), ks * 4 + (lane >> 4)));
+    };
+    // prologue: K-step 0 of the first tile
+    {
+        int lim;
+        const _Float16* src = src_of(tile, 0, lim);
+#pragma unroll
+        for (int u = 0; u < 16; u++) issue(src, lim, 0, u);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int buf = 0;
+    for (; tile < ntiles; tile += G) {
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) accL[i][j] = accR[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int kt = 0; kt < nk; kt++) {
+            // the next K-step in the workgroup's stream (this tile's, or the next tile's first)
+            const bool last = kt + 1 == nk;
+            const int nt = last && tile + G < ntiles ? tile + G : tile;
+            const int nkt = last ? 0 : kt + 1;
+            int nlim;
+            const _Float16* nsrc = src_of(nt, nkt, nlim);
+            const _Float16* sA = lds + buf * STAGE;
+            const _Float16* sW = sA + G2_M * GB_K;
+            read_b(sW, 0, 0);
+#pragma unroll
+            for (int i = 0; i < 8; i++) read_a(sA, 0, i);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            // k-half 0: row group g's MFMAs, then its A fragment of k-half 1 (the register is
+            // free after them); W of k-half 1 read behind group 0; one DMA piece per group
+#pragma unroll
+            for (int g = 0; g < 8; g++) {
+                issue(nsrc, nlim, buf ^ 1, g);
+                if (g == 0) read_b(sW, 1, 1);
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    accL[g][j] = mfma16(fb[0][j], fa[g], accL[g][j]);
+                    accR[g][j] = mfma16(fb[0][4 + j], fa[g], accR[g][j]);
+                }
+                read_a(sA, 1, g);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int g = 0; g < 8; g++) {
+                issue(nsrc, nlim, buf ^ 1, 8 + g);
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    accL[g][j] = mfma16(fb[1][j], fa[g], accL[g][j]);
+                    accR[g][j] = mfma16(fb[1][4 + j], fa[g], accR[g][j]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            // the next K-step's operands landed (every wave's: barrier); this stage is free
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            buf ^= 1;
+        }
+        const int64_t m0 = (int64_t)(tile / tiles_n) * G2_M;
+        const int n0 = (tile % tiles_n) * G2_N;
+        if constexpr (NOSTORE) {
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) asm volatile("" ::"v"(accL[i][j]), "v"(accR[i][j]));
+        } else {
+            epilogue_tile<EPI_H16, 8>(ea, accL, m0 + wr * 128, n0 + wc * 128, M, N);
+            epilogue_tile<EPI_H16, 8>(ea, accR, m0 + wr * 128, n0 + wc * 128 + 64, M, N);
+        }
+    }
+}
+}  // namespace reidmi
+
+REIDMI_API int reidmi_gemm_f16_w4(const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N,
+                                  int64_t K, const float* bias, void* out, int64_t ldc, int nostore, void* stream) {
+    RM_REQUIRE(M > 0 && N % G2_N == 0 && K % GB_K == 0 && K >= 2 * GB_K, "gemm_w4: needs N % 256 == 0, K % 64 == 0");
+    RM_REQUIRE(lda % 8 == 0 && ldw % 8 == 0 && ldc % 8 == 0 && lda * G2_M < (1ll << 31) && ldw * G2_N < (1ll << 31),
+               "gemm_w4: strides");
+    const int tiles_n = (int)(N / G2_N);
+    const int64_t ntiles = (int64_t)ceil_div(M, G2_M) * tiles_n;
+    RM_REQUIRE(ntiles < (1ll << 31), "gemm_w4: too many tiles");
+    EpiArgs ea{};
+    ea.out = out;
+    ea.ldc = ldc;
+    ea.bias = bias;
+    const size_t lds = 2 * (size_t)(G2_M + G2_N) * GB_K * 2;
+    auto kern = nostore ? gemm_w4_kernel<true> : gemm_w4_kernel<false>;
+    RM_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const int grid = (int)(ntiles < 256 ? ntiles : 256);
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(256), lds, (hipStream_t)stream, (const _Float16*)A, lda,
+                       (const _Float16*)W, ldw, M, (int)N, (int)K, ea, tiles_n, (int)ntiles);
+    RM_LAUNCHED();
+    return OK;
+}
+
 // Forced tiling / walk (tests, A-B timing; tools library, include/reidmi_tools.h)
 REIDMI_API int reidmi_gemm_f16_tiled(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M,
                                      int64_t N, int64_t K, const float* bias, const void* rowstat, const float* colsum,
