@@ -1273,6 +1273,12 @@ REIDMI_API int reidmi_gemm_f16(int epi, const void* A, int64_t lda, const void* 
 // current one (16 one-KiB pieces per wave, one per 8 MFMAs); one barrier per K-step.  Same
 // MFMA chain per output element as gemm_persistent_kernel (bit-identical).  Plain fp16 +
 // bias epilogue (NOSTORE: values kept, no stores) — a mainloop measurement.
+#ifndef W4_VAR_NODMA  // timing variants of the prototype (wrong results): no operand DMA in the K-loop
+#define W4_VAR_NODMA 0
+#endif
+#ifndef W4_VAR_NOBARRIER  // ... no barrier per K-step
+#define W4_VAR_NOBARRIER 0
+#endif
 namespace reidmi {
 template <bool NOSTORE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm_w4_kernel(
@@ -1361,7 +1367,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             // free after them); W of k-half 1 read behind group 0; one DMA piece per group
 #pragma unroll
             for (int g = 0; g < 8; g++) {
-                issue(nsrc, nlim, buf ^ 1, g);
+                if (!W4_VAR_NODMA) issue(nsrc, nlim, buf ^ 1, g);
                 if (g == 0) read_b(sW, 1, 1);
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
@@ -1374,7 +1380,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
             for (int g = 0; g < 8; g++) {
-                issue(nsrc, nlim, buf ^ 1, 8 + g);
+                if (!W4_VAR_NODMA) issue(nsrc, nlim, buf ^ 1, 8 + g);
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     accL[g][j] = mfma16(fb[1][j], fa[g], accL[g][j]);
@@ -1384,7 +1390,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             }
             // the next K-step's operands landed (every wave's: barrier); this stage is free
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
+            if (!W4_VAR_NOBARRIER) __builtin_amdgcn_s_barrier();
             buf ^= 1;
         }
         const int64_t m0 = (int64_t)(tile / tiles_n) * G2_M;
