@@ -1276,6 +1276,9 @@ REIDMI_API int reidmi_gemm_f16(int epi, const void* A, int64_t lda, const void* 
 #ifndef W4_VAR_NODMA  // timing variants of the prototype (wrong results): no operand DMA in the K-loop
 #define W4_VAR_NODMA 0
 #endif
+#ifndef W4_VAR_NOWAIT  // ... the DMA issued but never waited for in the K-loop
+#define W4_VAR_NOWAIT 0
+#endif
 #ifndef W4_VAR_NOBARRIER  // ... no barrier per K-step
 #define W4_VAR_NOBARRIER 0
 #endif
@@ -1389,7 +1392,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                 __builtin_amdgcn_sched_barrier(0);
             }
             // the next K-step's operands landed (every wave's: barrier); this stage is free
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (!W4_VAR_NOWAIT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (!W4_VAR_NOBARRIER) __builtin_amdgcn_s_barrier();
             buf ^= 1;
         }
