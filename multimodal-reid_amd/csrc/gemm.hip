@@ -1322,11 +1322,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         lim = 128;
         return W + ((int64_t)n0 + prow0) * ldw + kt * GB_K;
     };
+    // SGPR base + unsigned VGPR byte offset per piece (no 64-bit VALU address arithmetic): a
+    // piece past the matrix's last row reads the last 8 rows (or, with fewer than 8, the last
+    // row in every lane) -- valid addresses; those rows are never stored
+    const uint32_t loff_e = (uint32_t)(l3 * ld + (int)chk_e) * 2u, loff_o = (uint32_t)(l3 * ld + (int)chk_o) * 2u;
     auto issue = [&](const _Float16* src, int lim, int stage, int u) {
-        const int rmax = lim - 1 - 8 * u;  // rows past the matrix read its last row (never stored)
-        const int rr = l3 < rmax ? l3 : rmax;  // may be negative: row lim-1 of src, a valid row
-        const int o = rr * ld + (int)((u & 1) ? chk_o : chk_e);
-        __builtin_amdgcn_global_load_lds(src + ((int64_t)(8 * u) * ld + o),
+        const bool whole = 8 * u + 8 <= lim;  // wave-uniform
+        const int brow = whole ? 8 * u : (lim >= 8 ? lim - 8 : lim - 1);
+        const uint32_t voff = (whole || lim >= 8) ? ((u & 1) ? loff_o : loff_e) : ((u & 1) ? chk_o : chk_e) * 2u;
+        __builtin_amdgcn_global_load_lds((const char*)(src + (int64_t)brow * ld) + voff,
                                          (lds_ptr_t)(dst0 + stage * STAGE + 8 * u * GB_K), 16, 0, 0);
     };
     auto read_b = [&](const _Float16* sW, int ks, int b) {
