@@ -1418,6 +1418,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 REIDMI_API int reidmi_gemm_f16_w4(const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N,
                                   int64_t K, const float* bias, void* out, int64_t ldc, int nostore, void* stream) {
     RM_REQUIRE(M > 0 && N % G2_N == 0 && K % GB_K == 0 && K >= 2 * GB_K, "gemm_w4: needs N % 256 == 0, K % 64 == 0");
+    RM_REQUIRE(nostore == 0 || nostore == 1, "gemm_w4: nostore is 0 or 1");
     RM_REQUIRE(lda % 8 == 0 && ldw % 8 == 0 && ldc % 8 == 0 && lda * G2_M < (1ll << 31) && ldw * G2_N < (1ll << 31),
                "gemm_w4: strides");
     const int tiles_n = (int)(N / G2_N);

@@ -211,6 +211,23 @@ def test_mhsa(gpu, L, causal):
     assert (got - ref).abs().max() < 5e-3  # fp16 P and O (bf16 needed 3e-2)
 
 
+@pytest.mark.parametrize("M,N,K", [(3000, 768, 3072), (513, 2304, 768), (256, 256, 128)])
+def test_gemm_w4_prototype_bitexact(gpu, M, N, K):
+    """The one-wave-per-SIMD GEMM prototype of the tools library gives the shipped
+    persistent kernel's bits (same MFMA chain per element), partial last row tiles included."""
+    from multimodal_reid_amd import _lib as L
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    A = (torch.rand(M, K, device="cuda", generator=g) * 2 - 1).half()
+    W = ((torch.rand(N, K, device="cuda", generator=g) * 2 - 1) / K ** 0.5).half()
+    b = torch.rand(N, device="cuda", generator=g)
+    o1 = torch.empty(M, N, device="cuda", dtype=torch.float16)
+    o2 = torch.full((M, N), float("nan"), device="cuda", dtype=torch.float16)
+    L.call_tools("reidmi_gemm_f16_tiled", 0, L.ptr(A), K, L.ptr(W), K, M, N, K, L.ptr(b), None, None, L.ptr(o1), N, 2,
+                 0, L.stream())
+    L.call_tools("reidmi_gemm_f16_w4", L.ptr(A), K, L.ptr(W), K, M, N, K, L.ptr(b), L.ptr(o2), N, 0, L.stream())
+    assert torch.equal(o1, o2)
+
+
 @pytest.mark.parametrize("L,causal,nseq,H", [(20, True, 700, 8), (50, True, 700, 8), (77, True, 500, 8),
                                             (128, True, 300, 8), (211, False, 300, 12)])
 def test_mhsa_many_heads(gpu, L, causal, nseq, H):
