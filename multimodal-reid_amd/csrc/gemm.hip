@@ -64,6 +64,9 @@ constexpr int GB_M = 128, GB_N = 128, GB_K = 64;
 #ifndef GEMM_VAR_STAG_SLP  // 64 x SLP cycles per round (127: ~8k cycles, ~4 us)
 #define GEMM_VAR_STAG_SLP 127
 #endif
+#ifndef GEMM_VAR_FB2  // persistent tile: keep both column halves' W fragments (LOAD 3 reads none)
+#define GEMM_VAR_FB2 1
+#endif
 
 __device__ __forceinline__ int swz(int r, int kc) { return r * GB_K + ((kc ^ ((r >> 1) & 7)) << 3); }
 
@@ -860,7 +863,12 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
     } while (0)
 #define G5_LDS_DONE() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
 
-    f16x8 fa[4][2], fb[2][2];
+    // FB2: both column halves' W fragments stay in registers (6 more VGPRs as allocated), so
+    // LOAD 3 reads nothing: the K-step's W fragments are read from LDS once, not 1.5 times
+    // (-14 % LDS read bytes; c_fc / QKV / c_proj +1 %, out_proj even,
+    // profiles/r04/gemm_fb2_ab.txt)
+    constexpr bool FB2 = GEMM_VAR_FB2 != 0;
+    f16x8 fa[4][2], fbq[FB2 ? 2 : 1][2][2];
     f32x4 acc[8][4];
     auto load_a = [&](const _Float16* sA, int qm) {
 #pragma unroll
@@ -874,7 +882,8 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
         for (int j = 0; j < 2; j++)
 #pragma unroll
             for (int ks = 0; ks < 2; ks++)
-                fb[j][ks] = *(const f16x8*)(sW + swz(wc * 64 + qn * 32 + j * 16 + (lane & 15), ks * 4 + (lane >> 4)));
+                fbq[FB2 ? qn : 0][j][ks] =
+                    *(const f16x8*)(sW + swz(wc * 64 + qn * 32 + j * 16 + (lane & 15), ks * 4 + (lane >> 4)));
     };
     // FIRST: the tile's first K-step starts every accumulator chain from an inline-constant 0
     // C operand, so no zeroing moves run between tiles (64 v_mov_b64 per wave and tile)
@@ -886,10 +895,11 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
 #pragma unroll
                 for (int j = 0; j < 2; j++) {
                     f32x4& c = acc[qm * 4 + i][qn * 2 + j];
+                    const f16x8& b = fbq[FB2 ? qn : 0][j][ks];
                     if constexpr (decltype(firstc)::value)
-                        c = mfma16(fb[j][ks], fa[i][ks], ks == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : c);
+                        c = mfma16(b, fa[i][ks], ks == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : c);
                     else
-                        c = mfma16(fb[j][ks], fa[i][ks], c);
+                        c = mfma16(b, fa[i][ks], c);
                 }
     };
 
@@ -987,7 +997,7 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
             compute(1, 1, firstc);
             G5_BARRIER();
             // LOAD 3 / COMPUTE (1,0)
-            load_b(sW, 0);
+            if constexpr (!FB2) load_b(sW, 0);
             if (has2) {
                 issue_a(buf, 1, p2);
                 G5_LDS_DONE();
