@@ -812,11 +812,16 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
     const int* const rr_list = EPI == EPI_RRSV ? ea.rr_tiles : nullptr;  // (gemm.h rr_tiles)
     if constexpr (EPI != EPI_RRHI) band = 0;  // bands: the re-rank's dense product only
     // a DMA stream position: tile (m0, n0), K-step, and whether all 256 A rows exist
+    // a: byte address of A[m0][kt * GB_K], w: of W[n0][kt * GB_K] -- computed once per tile
+    // and stepped by one K-step's bytes, so a DMA issue costs no 64-bit multiply (scalar
+    // instructions of the LOAD phases, which run beside the partner wave's MFMAs)
     struct Pos {
         int tile, kt;
         int64_t m0;
         int n0;
         bool full;
+        const char* a;
+        const char* w;
     };
     auto set_tile = [&](Pos& p, int tile) {
         p.tile = tile;
@@ -826,33 +831,40 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
         p.m0 = (int64_t)mt * G2_M;
         p.n0 = (nb0 + nt) * G2_N;
         p.full = p.m0 + G2_M <= M;
+        p.a = (const char*)(A + p.m0 * lda);
+        p.w = (const char*)(W + (int64_t)p.n0 * ldw);
     };
     auto advance = [&](Pos& p) {
-        if (++p.kt == nk) set_tile(p, p.tile + gx);
+        if (++p.kt == nk) {
+            set_tile(p, p.tile + gx);
+        } else {
+            p.a += GB_K * 2;
+            p.w += GB_K * 2;
+        }
     };
-    // uniform tile base + per-lane 32-bit element offset (SGPR base + VGPR offset form)
+    // uniform tile base + per-lane 32-bit byte offset (SGPR base + VGPR offset form)
     auto issue_a = [&](int stage, int h, const Pos& p) {
-        const _Float16* base = A + p.m0 * lda + p.kt * GB_K;
+        const char* base = p.a;
         if (p.full) {
 #pragma unroll
             for (int u = 0; u < 2; u++)
-                __builtin_amdgcn_global_load_lds((const char*)base + offAb[h][u],
+                __builtin_amdgcn_global_load_lds(base + offAb[h][u],
                                                  (lds_ptr_t)(lds + stage * G2_STAGE + offA[h][u]), 16, 0, 0);
         } else {  // partial last row tile: rows >= M read row M-1 (never stored)
             const int lim = (int)(M - p.m0);
 #pragma unroll
             for (int u = 0; u < 2; u++) {
                 const int r = rowA[h][u] < lim ? rowA[h][u] : lim - 1;
-                __builtin_amdgcn_global_load_lds((const char*)base + (uint32_t)(r * (int)lda + kcA[h][u]) * 2u,
+                __builtin_amdgcn_global_load_lds(base + (uint32_t)(r * (int)lda + kcA[h][u]) * 2u,
                                                  (lds_ptr_t)(lds + stage * G2_STAGE + offA[h][u]), 16, 0, 0);
             }
         }
     };
     auto issue_w = [&](int stage, int h, const Pos& p) {
-        const _Float16* base = W + (int64_t)p.n0 * ldw + p.kt * GB_K;
+        const char* base = p.w;
 #pragma unroll
         for (int u = 0; u < 2; u++)
-            __builtin_amdgcn_global_load_lds((const char*)base + offWb[h][u],
+            __builtin_amdgcn_global_load_lds(base + offWb[h][u],
                                              (lds_ptr_t)(lds + stage * G2_STAGE + offW[h][u]), 16, 0, 0);
     };
 #define G5_BARRIER()                              \

@@ -13,6 +13,15 @@ for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 90 rocprofv3 --pmc $c --kernel-trace --output-format csv -d gpurun_out/pmc_$c -o p -- \
     python tools/gemm_one.py $M 3072 768 1 5 fold > gpurun_out/pmc_$c.log 2>&1
 done
+# c_fc SQ / GRBM passes: MFMA busy and the clock the chip holds under this load
+# (GRBM_GUI_ACTIVE / 8 XCDs / dispatch wall, MI355X_MICROARCH.md "DVFS give-back")
+j=0
+for cs in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES" \
+          "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE"; do
+  j=$((j + 1))
+  timeout -s KILL 90 rocprofv3 --pmc $cs --kernel-trace --output-format csv -d gpurun_out/cfc_pmc$j -o p -- \
+    python tools/gemm_one.py $M 3072 768 1 20 fold > gpurun_out/cfc_pmc$j.log 2>&1
+done
 i=0
 for cs in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES" \
           "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE" "FETCH_SIZE" "WRITE_SIZE"; do
