@@ -64,6 +64,9 @@ constexpr int GB_M = 128, GB_N = 128, GB_K = 64;
 #ifndef GEMM_VAR_STAG_SLP  // 64 x SLP cycles per round (127: ~8k cycles, ~4 us)
 #define GEMM_VAR_STAG_SLP 127
 #endif
+#ifndef GEMM_VAR_DIAG_LOAD0  // timing-only (wrong results): LOAD 0 reads no W fragments (4 of its 12 reads)
+#define GEMM_VAR_DIAG_LOAD0 0
+#endif
 #ifndef GEMM_VAR_FB2  // persistent tile: keep both column halves' W fragments (LOAD 3 reads none)
 #define GEMM_VAR_FB2 1
 #endif
@@ -965,7 +968,7 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
             const _Float16* sW = sA + G2_M * GB_K;
             // LOAD 0 / COMPUTE (0,0)
             load_a(sA, 0);
-            load_b(sW, 0);
+            if constexpr (!GEMM_VAR_DIAG_LOAD0) load_b(sW, 0);
             if (kt == 0 && has_bias)
                 __builtin_amdgcn_global_load_lds(ea.bias + (nb0 + tnt) * G2_N + lane * 4, (lds_ptr_t)bias_slot,
                                                  16, 0, 0);
