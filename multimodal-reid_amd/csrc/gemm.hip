@@ -93,6 +93,19 @@ __device__ __forceinline__ f32x4 mfma16(const f16x8& w, const f16x8& a, const f3
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(w, a, c, 0, 0, 0);
 }
 
+// x[l] + x[l ^ 16] and x[l] + x[l ^ 32] by the VALU lane swaps (no LDS round trip, unlike
+// __shfl_xor's ds_bpermute); fp32 addition is commutative, so the sums equal the shuffle's
+__device__ __forceinline__ float xor16_sum(float x) {
+    const uint32_t u = __builtin_bit_cast(uint32_t, x);
+    const auto p = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+    return __builtin_bit_cast(float, (uint32_t)p[0]) + __builtin_bit_cast(float, (uint32_t)p[1]);
+}
+__device__ __forceinline__ float xor32_sum(float x) {
+    const uint32_t u = __builtin_bit_cast(uint32_t, x);
+    const auto p = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+    return __builtin_bit_cast(float, (uint32_t)p[0]) + __builtin_bit_cast(float, (uint32_t)p[1]);
+}
+
 // LayerNorm fold (see gemm.h EpiArgs) with the bias: acc <- rstd_m * acc + (-mean_m rstd_m
 // * s_n + b'_n), two FMAs per element (bias b'_n of the lane's columns passed in bn).  Lane
 // layout as epilogue_tile; rows past M read row M-1.
@@ -195,8 +208,8 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
 #pragma unroll
                         for (int e = 0; e < 8; e += 2) sp += f32x2v{(float)h[jp][e], (float)h[jp][e + 1]};
                     float sum = sp.x + sp.y;
-                    sum += __shfl_xor(sum, 16, 64);
-                    sum += __shfl_xor(sum, 32, 64);
+                    sum = xor16_sum(sum);
+                    sum = xor32_sum(sum);
                     const f32x2v mu = {sum * (1.0f / 64), sum * (1.0f / 64)};
                     f32x2v dp = {0.f, 0.f};
 #pragma unroll
@@ -207,8 +220,8 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
                             dp = __builtin_elementwise_fma(d, d, dp);
                         }
                     float m2 = dp.x + dp.y;
-                    m2 += __shfl_xor(m2, 16, 64);
-                    m2 += __shfl_xor(m2, 32, 64);
+                    m2 = xor16_sum(m2);
+                    m2 = xor32_sum(m2);
                     if (live && (lane >> 4) == 0) ea.pstat[(ncol >> 6) * ea.ldp + m] = make_float2(sum, m2);
                 }
             }
