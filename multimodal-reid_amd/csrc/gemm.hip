@@ -146,6 +146,16 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
                                               int64_t M, int N) {
     const int lane = threadIdx.x & 63;
     const int cq = (lane >> 4) * 4;
+    // fp16 output rows: a wave-uniform base row (the wave's first row, or the last row when the
+    // wave has none) and per-lane 32-bit byte offsets from it, so a 16-byte load / store is
+    // addressed as SGPR base + VGPR offset (no 64-bit VALU address per access); rows past M
+    // read row M - 1, which is never below the base.  (m - b0) < 128, ldc < 2^24 (checked at
+    // launch).
+    [[maybe_unused]] const int64_t b0 = mrow < M ? mrow : M - 1;
+    [[maybe_unused]] char* const ob = (char*)((_Float16*)ea.out + b0 * ea.ldc);
+    [[maybe_unused]] auto obo = [&](int64_t m, int c) -> uint32_t {
+        return (uint32_t)((int)(m - b0) * (int)ea.ldc + c) * 2u;
+    };
     if (!BIAS_DONE && EPI != EPI_PATCH && ea.bias != nullptr) {
         float4 b[4];
 #pragma unroll
@@ -180,7 +190,6 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
                 acc[i][2 * jp] = __builtin_bit_cast(f32x4, make_uint4(s0[0], s1[0], s2[0], s3[0]));
                 acc[i][2 * jp + 1] = __builtin_bit_cast(f32x4, make_uint4(s0[1], s1[1], s2[1], s3[1]));
             }
-        _Float16* xo = (_Float16*)ea.out;
         auto colp = [&](int jp) { return ncol + (2 * jp + (q & 1)) * 16 + (q >> 1) * 8; };
         // the whole residual block is loaded before the first store (NI row groups, 2*NI
         // 16-byte loads in flight per lane: +6 % on out_proj at K = 768 over batches of 2)
@@ -197,7 +206,7 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
                     h[jp] = f16x8{(_Float16)a[0], (_Float16)a[1], (_Float16)a[2], (_Float16)a[3],
                                   (_Float16)b[0], (_Float16)b[1], (_Float16)b[2], (_Float16)b[3]};
                     if constexpr (GEMM_VAR_NOSTORE) asm volatile("" ::"v"(h[jp]));
-                    else if (live) *(f16x8*)(xo + m * ea.ldc + colp(jp)) = h[jp];
+                    else if (live) *(f16x8*)(ob + obo(m, colp(jp))) = h[jp];
                 }
                 if (!GEMM_VAR_NOPSTAT && ea.pstat) {
                     // LayerNorm partials of the new fp16 row values over this wave's 64 columns
@@ -239,7 +248,7 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
                         xv[ii][jp] = f16x8{};
                         asm volatile("" : "+v"(xv[ii][jp]));
                     } else {
-                        xv[ii][jp] = *(const f16x8*)(xo + m * ea.ldc + colp(jp));
+                        xv[ii][jp] = *(const f16x8*)(ob + obo(m, colp(jp)));
                     }
                 }
             }
@@ -442,7 +451,7 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
                     typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
                     asm volatile("" ::"v"(__builtin_bit_cast(u32x4v, v)));
                 }
-                else *(uint4*)((_Float16*)ea.out + m * ea.ldc + col) = v;
+                else *(uint4*)(ob + obo(m, col)) = v;
             }
         }
     }
@@ -1206,8 +1215,8 @@ int gemm_f16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, in
     RM_REQUIRE(N % GB_N == 0 && K % GB_K == 0, "gemm: needs N % 128 == 0 and K % 64 == 0");
     RM_REQUIRE(lda % 8 == 0 && ldw % 8 == 0 && lda >= K && ldw >= K, "gemm: lda/ldw must be >= K and 16-byte rows");
     RM_REQUIRE((epi != EPI_H16 && epi != EPI_GELU_H16 && epi != EPI_RESID_F16) ||
-                   (ea.ldc % 8 == 0 && ((uintptr_t)ea.out & 15) == 0),
-               "gemm: fp16 output needs ldc % 8 == 0 and a 16-byte aligned base");
+                   (ea.ldc % 8 == 0 && ((uintptr_t)ea.out & 15) == 0 && ea.ldc < (1 << 24) && N < (1 << 24)),
+               "gemm: fp16 output needs ldc % 8 == 0 (< 2^24) and a 16-byte aligned base");
     RM_REQUIRE((ea.rowstat == nullptr) == (ea.colsum == nullptr), "gemm: rowstat and colsum go together");
     RM_REQUIRE(ea.rowstat == nullptr || ea.bias != nullptr, "gemm: a folded LayerNorm needs the folded bias");
     if (M == 0) return OK;
