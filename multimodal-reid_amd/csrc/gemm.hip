@@ -95,15 +95,18 @@ __device__ __forceinline__ f32x4 mfma16(const f16x8& w, const f16x8& a, const f3
 
 // x[l] + x[l ^ 16] and x[l] + x[l ^ 32] by the VALU lane swaps (no LDS round trip, unlike
 // __shfl_xor's ds_bpermute); fp32 addition is commutative, so the sums equal the shuffle's
+// (results copied out as uint32_t before the bit_cast: attention.hip xhalf_pair)
 __device__ __forceinline__ float xor16_sum(float x) {
     const uint32_t u = __builtin_bit_cast(uint32_t, x);
     const auto p = __builtin_amdgcn_permlane16_swap(u, u, false, false);
-    return __builtin_bit_cast(float, (uint32_t)p[0]) + __builtin_bit_cast(float, (uint32_t)p[1]);
+    const uint32_t p0 = p[0], p1 = p[1];
+    return __builtin_bit_cast(float, p0) + __builtin_bit_cast(float, p1);
 }
 __device__ __forceinline__ float xor32_sum(float x) {
     const uint32_t u = __builtin_bit_cast(uint32_t, x);
     const auto p = __builtin_amdgcn_permlane32_swap(u, u, false, false);
-    return __builtin_bit_cast(float, (uint32_t)p[0]) + __builtin_bit_cast(float, (uint32_t)p[1]);
+    const uint32_t p0 = p[0], p1 = p[1];
+    return __builtin_bit_cast(float, p0) + __builtin_bit_cast(float, p1);
 }
 
 // LayerNorm fold (see gemm.h EpiArgs) with the bias: acc <- rstd_m * acc + (-mean_m rstd_m
