@@ -275,7 +275,8 @@ int reidmi_comm_allreduce(reidmi_comm_t comm, const void* send, void* recv, int6
  * A [M][lda], W [N][ldw] fp16 (Linear weight layout), N % 128 == 0, K % 64 == 0.
  * epi: 0 -> out fp16 = acc+bias; 1 -> out fp16 = QuickGELU(acc+bias); 5 -> out fp32 = acc+bias;
  *      6 -> out fp16 += acc+bias (sum in fp32, one rounding: the encoders' fp16 residual
- *      stream).  bias nullable (fp32).  fp16 outputs: ldc % 8 == 0, 16-byte aligned out. */
+ *      stream; no folded LayerNorm: rowstat / colsum NULL).  bias nullable (fp32).  fp16
+ *      outputs: ldc % 8 == 0 (< 2^24), 16-byte aligned out. */
 int reidmi_gemm_f16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N, int64_t K,
                     const float* bias, const void* rowstat, const float* colsum, void* out, int64_t ldc, void* stream);
 

@@ -67,6 +67,9 @@ constexpr int GB_M = 128, GB_N = 128, GB_K = 64;
 #ifndef GEMM_VAR_DIAG_LOAD0  // timing-only (wrong results): LOAD 0 reads no W fragments (4 of its 12 reads)
 #define GEMM_VAR_DIAG_LOAD0 0
 #endif
+#ifndef GEMM_VAR_RPRE  // persistent tile: residual rows loaded before the bias / fold arithmetic
+#define GEMM_VAR_RPRE 1
+#endif
 #ifndef GEMM_VAR_FB2  // persistent tile: keep both column halves' W fragments (LOAD 3 reads none)
 #define GEMM_VAR_FB2 1
 #endif
@@ -144,9 +147,30 @@ __device__ __forceinline__ void ln_fold(f32x4 (&acc)[NI][4], const float2* __res
 // once per tile, residual rows all at once, pos-embed rows in batches — otherwise the
 // compiler (which cannot prove `out` does not alias `bias`/`pos`) serialises one memory
 // round trip per fragment.
-template <int EPI, int NI, bool BIAS_DONE = false>
+// The residual epilogue's row reads: lane group q holds columns colp(jp) .. +7 of its row
+// after the accumulator pairing below (rows past M read row M - 1; never stored).
+template <int NI>
+__device__ __forceinline__ void resid_rows_load(const EpiArgs& ea, int64_t mrow, int ncol, int64_t M,
+                                                f16x8 (&xv)[NI][2]) {
+    const int lane = threadIdx.x & 63, q = lane >> 4;
+    const int64_t b0 = mrow < M ? mrow : M - 1;
+    const char* const ob = (const char*)((const _Float16*)ea.out + b0 * ea.ldc);
+#pragma unroll
+    for (int i = 0; i < NI; i++) {
+        int64_t m = mrow + i * 16 + (lane & 15);
+        m = m < M ? m : M - 1;
+#pragma unroll
+        for (int jp = 0; jp < 2; jp++) {
+            const int c = ncol + (2 * jp + (q & 1)) * 16 + (q >> 1) * 8;
+            xv[i][jp] = *(const f16x8*)(ob + (uint32_t)((int)(m - b0) * (int)ea.ldc + c) * 2u);
+        }
+    }
+}
+
+// PRE: the residual rows were read by resid_rows_load into *xpre (EPI_RESID_F16 only)
+template <int EPI, int NI, bool BIAS_DONE = false, bool PRE = false>
 __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI][4], int64_t mrow, int ncol,
-                                              int64_t M, int N) {
+                                              int64_t M, int N, const f16x8 (*xpre)[2] = nullptr) {
     const int lane = threadIdx.x & 63;
     const int cq = (lane >> 4) * 4;
     // fp16 output rows: a wave-uniform base row (the wave's first row, or the last row when the
@@ -250,6 +274,8 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
                     if constexpr (GEMM_VAR_NORESLOAD) {  // timing variant: no residual read
                         xv[ii][jp] = f16x8{};
                         asm volatile("" : "+v"(xv[ii][jp]));
+                    } else if constexpr (PRE) {
+                        xv[ii][jp] = xpre[i0 + ii][jp];
                     } else {
                         xv[ii][jp] = *(const f16x8*)(ob + obo(m, colp(jp)));
                     }
@@ -951,7 +977,7 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
     // Folded LayerNorm: colsum of the tile's 256 columns and (rstd, -mean rstd) of the
     // wave's 128 rows go to LDS by the same DMA at the tile's first K-step (the rowstat
     // buffer is padded to whole 256-row tiles, gemm.h).
-    const bool fold = ea.rowstat != nullptr;
+    const bool fold = EPI != EPI_RESID_F16 && ea.rowstat != nullptr;  // (gemm_f16 rejects a residual fold)
     float* cs_slot = bias_slot + 8 * 256;
     float* rs_slot = bias_slot + 16 * 256;
     // streams: p1 = step s+1 (region B0), p2 = step s+2 (A0, B1, A1); requires nk >= 2
@@ -1083,6 +1109,12 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
                 if constexpr (EPI == EPI_QKV) deferred = deferred && (n0 + ea.n_off) / (ea.heads * 64) != 2;
             }
         }
+        // residual epilogue: its row reads go out before the bias arithmetic (after the next
+        // tile's early DMA, so the deferred-store count EpiVm is unchanged), their latency
+        // then runs beside it
+        constexpr bool RPRE = EPI == EPI_RESID_F16 && GEMM_VAR_RPRE && !GEMM_VAR_NORESLOAD;
+        f16x8 xres[RPRE ? 8 : 1][2];
+        if constexpr (RPRE) resid_rows_load<8>(ea, m0 + wr * 128, n0 + wc * 64, M, xres);
         if (has_bias) {
             f32x4 b[4];
             // inline ds_read: no compiler-inserted vmcnt(0) for the LDS-DMA'd slot (retired by
@@ -1142,7 +1174,7 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
                       rr_lds + 8192 + (seq & 1) * 4096, sv_lds, sv_n, lane,
                       RrsvWalk{first, gx, wr, wc, rr_list});
         else
-            epilogue_tile<EPI, 8, true>(ea, acc, m0 + wr * 128, n0 + wc * 64, M, N);
+            epilogue_tile<EPI, 8, true, RPRE>(ea, acc, m0 + wr * 128, n0 + wc * 64, M, N, xres);
         seq++;
         if (wr == 1) G5_BARRIER();
     }
@@ -1222,6 +1254,7 @@ int gemm_f16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, in
                "gemm: fp16 output needs ldc % 8 == 0 (< 2^24) and a 16-byte aligned base");
     RM_REQUIRE((ea.rowstat == nullptr) == (ea.colsum == nullptr), "gemm: rowstat and colsum go together");
     RM_REQUIRE(ea.rowstat == nullptr || ea.bias != nullptr, "gemm: a folded LayerNorm needs the folded bias");
+    RM_REQUIRE(epi != EPI_RESID_F16 || ea.rowstat == nullptr, "gemm: the residual epilogue takes no folded LayerNorm");
     if (M == 0) return OK;
     hipEvent_t ev_b = nullptr;
     if (prof::enabled) {
