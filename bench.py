@@ -56,8 +56,8 @@ EPI_GELU = 1  # the c_fc GEMM (+QuickGELU epilogue): the largest single kernel p
 #   batch 1024 (profiles/r02/pmc_c_fc_fp16_walk2_*): 736 400 / 1 296 384 KiB; algorithmic
 #     A 332 MB + W 4.7 MB + out 1 327 MB = 1.66 GB
 #   batch 4096 (profiles/r04/final/pmc_c_fc_b4096_*, mean of 6 launches; r03: 3 142 462 /
-#     5 185 615): 3 050 303 / 5 185 663 KiB; algorithmic A 1 327 MB + W 4.7 MB + out 5 310 MB = 6.64 GB
-C_FC_TRAFFIC_BYTES = {1024: (2 * 736400 + 1296384) * 1024, 4096: (2 * 3050303 + 5185663) * 1024}
+#     5 185 615): 2 998 177 / 5 185 700 KiB; algorithmic A 1 327 MB + W 4.7 MB + out 5 310 MB = 6.64 GB
+C_FC_TRAFFIC_BYTES = {1024: (2 * 736400 + 1296384) * 1024, 4096: (2 * 2998177 + 5185700) * 1024}
 
 
 def _max_over_ranks(values, dev):
