@@ -20,8 +20,11 @@ zero-shot classifier's text side at Market size (750 x 56 token rows, TF/s); "ba
 "preprocess" = retrieval-kernel and transform rooflines; "jpeg" = the loaders' JPEG decode of
 a Market split of files on the device (and + transform), Pillow timed beside it; "cpu_baseline".
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B (default 4096)] [--no-cpu-baseline] [--no-rerank]
-                    [--no-msmt17] [--no-text] [--no-jpeg]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B (default 4096)] [--backend nccl|gloo]
+                    [--no-cpu-baseline] [--no-rerank] [--no-msmt17] [--no-text] [--no-jpeg]
+
+`--gpus N` under torchrun (WORLD_SIZE set) must equal the world size; without torchrun,
+bench.py starts the N rank processes itself (launch_ranks) and relays rank 0's line.
 """
 import argparse
 import json
@@ -67,6 +70,16 @@ def _max_over_ranks(values, dev):
     t = torch.tensor(values, dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return [float(v) for v in t.cpu()]
+
+
+def _all_ranks(values, dev):
+    """Every rank's list of host floats, in rank order (one all-gather)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [[float(v) for v in values]]
+    t = torch.tensor(values, dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
+    out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [[float(v) for v in o.cpu()] for o in out]
 
 
 def _crops(lo, hi, seed, dev, block=128):
@@ -179,11 +192,18 @@ class Workload:
             main.wait_stream(st)
 
     def step(self):
+        """One Market eval; returns (cmc, mAP, embed s, all-gather s, eval s) of this rank.  The
+        all-gather of the normalised gallery blocks (RCCL under nccl) is timed on its own: it
+        includes waiting for the slowest rank, so its minimum over ranks is the collective."""
         t0 = time.perf_counter()
         self.embed(self.q_img, self.q_tta, self.q_emb)
         self.embed(self.g_img, self.g_tta, self.g_emb)
         qn = evaluate.l2_normalize_device(self.q_emb)
-        gn = gather_rows(evaluate.l2_normalize_device(self.g_emb), self.G)
+        gl = evaluate.l2_normalize_device(self.g_emb)
+        torch.cuda.synchronize()
+        ta = time.perf_counter()
+        gn = gather_rows(gl, self.G)
+        self.gather_bytes = gn.numel() * gn.element_size() if self.world > 1 else 0
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         evaluate.euclidean_distance_device(qn, gn, out=self.dist)
@@ -196,7 +216,7 @@ class Workload:
         cmc, mAP = evaluate.aggregate_cmc_map(rows[:, 0].astype(np.int64), rows[:, 1].astype(np.int64), rows[:, 2],
                                               rows[:, 3].astype(np.int64), self.G, 50)
         t2 = time.perf_counter()
-        return cmc, mAP, t1 - t0, t2 - t1
+        return cmc, mAP, ta - t0, t1 - ta, t2 - t1
 
 
 MSMT17_RESID_GAIN = 4.0  # synthetic.vit_state_dict resid_gain of the MSMT17 leg's network
@@ -283,7 +303,9 @@ def msmt17_leg(model, dev, rank, world, batch, dataset="msmt17"):
                       f"{world} GPU(s): sharded embed + all-gather, exact distmat + CMC/mAP, sharded k-reciprocal "
                       "re-rank (k1=50 k2=15 lambda=0.3) + CMC/mAP",
             "imgs_per_s": round((Q + G) / te, 1), "embed_wall_s": round(te, 4), "eval_wall_s": round(tv, 4),
-            "rerank_eval_wall_s": round(t8, 4), "end_to_end_wall_s": round(te + tv + t8, 4),
+            # end to end = this run's own embedded features through embed, eval and re-rank + eval
+            # (ADVICE r4); the Gaussian-feature re-rank below is a separate reference number
+            "rerank_eval_wall_s": round(tr, 4), "end_to_end_wall_s": round(te + tv + tr, 4),
             "mAP": float(mAP), "rank1": float(cmc[0]),
             "rerank": {"features": "SURVEY.md §8d identity-clustered Gaussians (D=1280, sigma 4) of this split: the "
                                    "fp16 pre-filter path", "wall_s": round(t8, 4), "mAP_rerank": float(mAP8),
@@ -607,7 +629,75 @@ def cpu_baseline(wl, threads, n_img=512, bs=32):
                       f"({t_eval:.2f} s)"}
 
 
-def main():
+def rank_envs(n, port, base=None):
+    """The environment of each of the n ranks bench.py starts itself (`--gpus N` without
+    torchrun): the torchrun variables every rank reads (RANK, LOCAL_RANK, WORLD_SIZE,
+    MASTER_ADDR = 127.0.0.1, MASTER_PORT), plus the parent's own environment."""
+    base = dict(os.environ if base is None else base)
+    envs = []
+    for r in range(n):
+        e = dict(base)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), REIDMI_BENCH_CHILD="1")
+        envs.append(e)
+    return envs
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv, script=None, poll_s=0.2):
+    """Start n rank processes of `script` (default: this file) with `argv`, before this process
+    makes any GPU call (children are fresh interpreters started by Popen, never an exec of this
+    one).  Rank 0's stdout is captured and its last JSON line relayed; the others' stdout goes
+    to stderr.  If any rank fails, the others are terminated (they would wait in a collective
+    forever) and its exit code is returned."""
+    import subprocess
+    import threading
+    script = script or os.path.abspath(__file__)
+    envs = rank_envs(n, _free_port())
+    procs = []
+    for r, env in enumerate(envs):
+        procs.append(subprocess.Popen([sys.executable, "-u", script] + list(argv), env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr))
+    out0 = []
+    reader = threading.Thread(target=lambda: out0.append(procs[0].stdout.read()), daemon=True)
+    reader.start()
+    code = 0
+    while True:
+        states = [p.poll() for p in procs]  # every process polled each round (no short-circuit)
+        if all(c is not None for c in states):
+            break
+        bad = [c for c in states if c not in (None, 0)]
+        if bad:
+            code = bad[0]
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+            break
+        time.sleep(poll_s)
+    reader.join(timeout=60)
+    code = code or next((p.returncode for p in procs if p.returncode), 0)
+    text = (out0[0] if out0 else b"").decode(errors="replace")
+    lines = [ln for ln in text.splitlines() if ln.startswith("{")]
+    for ln in text.splitlines():
+        if not ln.startswith("{"):
+            print(ln, file=sys.stderr)
+    if lines:
+        print(lines[-1], flush=True)
+    return code
+
+
+def _parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -616,19 +706,39 @@ def main():
     # smaller partial last round of tiles per launch than 1024 (+1.5-2 %, profiles/r03/bench_batch_ab.txt)
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--streams", type=int, default=1)
+    # nccl = RCCL over xGMI, one GPU per rank; gloo = host collectives, ranks may share a GPU
+    # (LOCAL_RANK modulo the visible devices): the multi-rank test on a one-GPU box
+    ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-rerank", action="store_true")
     ap.add_argument("--no-msmt17", action="store_true")
     ap.add_argument("--no-text", action="store_true")
     ap.add_argument("--no-jpeg", action="store_true")
-    a = ap.parse_args()
+    ap.add_argument("--no-backend", action="store_true")
+    ap.add_argument("--no-preprocess", action="store_true")
+    return ap.parse_args(argv)
+
+
+def main():
+    a = _parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `python bench.py --gpus N`: start the N ranks here (nothing has touched the GPU yet)
+        sys.exit(launch_ranks(a.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {a.gpus}: the line would mislabel n_gpus")
+    if a.backend == "gloo":
+        local %= max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+        assert dist.get_world_size() == a.gpus
     wl = Workload(dev, rank, world, a.batch, streams=a.streams)
     L = _lib.load()
     for _ in range(a.warmup):
@@ -638,10 +748,11 @@ def main():
     torch.cuda.synchronize()
     L.reidmi_prof_enable(1)
     t0 = time.perf_counter()
-    embed_s = eval_s = 0.0
+    embed_s = gather_s = eval_s = 0.0
     for _ in range(a.steps):
-        cmc, mAP, te, tv = wl.step()
+        cmc, mAP, te, tg, tv = wl.step()
         embed_s += te
+        gather_s += tg
         eval_s += tv
     torch.cuda.synchronize()
     if world > 1:
@@ -657,6 +768,7 @@ def main():
                               ctypes.byref(fl))
     L.reidmi_prof_enable(0)
     elapsed = _max_over_ranks([elapsed], dev)[0]
+    per_rank = _all_ranks([embed_s / a.steps, gather_s / a.steps, eval_s / a.steps], dev)
     ms17 = None if a.no_msmt17 else msmt17_leg(None, dev, rank, world, a.batch)
     if rank == 0:
         imgs = (wl.Q + wl.G) * a.steps
@@ -678,7 +790,8 @@ def main():
             "config": {"workload": "Market-1501 full eval: 3368q x 15913g, ViT-B/16 stride-12 (211 tokens), "
                                    "2 passes/img (plain + flip/pad/crop TTA), exact-fp32 distmat, CMC/mAP",
                        "images_per_step": wl.Q + wl.G, "encoder_passes_per_step": 2 * (wl.Q + wl.G),
-                       "batch": a.batch, "parallelism": f"dp{world} (image shards + RCCL all-gather)"},
+                       "batch": a.batch, "parallelism": f"dp{world} (image shards + all-gather)",
+                       "backend": a.backend if world > 1 else None},
             "eval_wall_s": round(eval_s / a.steps, 4),
             "embed_wall_s": round(embed_s / a.steps, 4),
             "mAP": round(float(mAP), 6),
@@ -689,10 +802,21 @@ def main():
                          "traffic": C_FC_TRAFFIC_BYTES.get(a.batch), "traffic_unit": "bytes/launch (PMC)", "avg_launch_ms": round(avg_ms, 4), "launches": cnt.value,
                          "flops_per_launch": fl.value / max(cnt.value, 1)},
         }
+        if world > 1:
+            # per step: each rank's embed (its image shards, both passes + normalise), its wait in
+            # + the gallery all-gather (the minimum over ranks ~ the collective alone), its eval
+            line["ranks"] = {"embed_s": [round(v[0], 4) for v in per_rank],
+                             "allgather_s": [round(v[1], 5) for v in per_rank],
+                             "eval_s": [round(v[2], 4) for v in per_rank],
+                             "allgather_bytes": wl.gather_bytes,
+                             "allgather_GBps_at_min": round(wl.gather_bytes / max(min(v[1] for v in per_rank), 1e-9)
+                                                            / 1e9, 2)}
         if ms17 is not None:
             line["msmt17"] = ms17
-        line["backend"] = backend_rooflines(wl)
-        line["preprocess"] = preprocess_leg(dev)
+        if not a.no_backend:
+            line["backend"] = backend_rooflines(wl)
+        if not a.no_preprocess:
+            line["preprocess"] = preprocess_leg(dev)
         # host-side baselines at N = 1 only (the other ranks would idle at the final barrier)
         cpu = not a.no_cpu_baseline and world == 1
         if not a.no_jpeg:
@@ -704,7 +828,7 @@ def main():
             line["text"] = text_leg(dev, cpu=cpu, threads=threads)
         if cpu:
             line["cpu_baseline"] = cpu_baseline(wl, threads)
-        print(json.dumps(line))
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

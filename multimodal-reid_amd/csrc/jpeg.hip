@@ -133,6 +133,7 @@ static int32_t parse_one(const uint8_t* f, int64_t n, int64_t base, JpegImage& i
                 tq[c] = s[8 + 3 * c];
                 if (tq[c] > 3) return J_BAD_TABLE;   // jdinput.c latch_quant_tables: JERR_NO_QUANT_TABLE
             }
+            for (int c = 0; c < im.ncomp; ++c) im.cid[c] = cid[c];
             sof = true;
         } else if ((m >= 0xC2 && m <= 0xCF) && m != 0xC4 && m != 0xC8 && m != 0xCC) {
             return J_UNSUPPORTED;   // progressive, lossless, hierarchical, arithmetic
@@ -285,8 +286,15 @@ __global__ __launch_bounds__(64) void jpeg_entropy_kernel(const uint8_t* __restr
     int32_t st = im.status;
     if (st == J_OK) {
         LdsSink sink{blocks[threadIdx.x], nullptr};
-        if constexpr (kLds) st = entropy_decode(src, im, lds, coef, sink);
-        else st = entropy_decode(src, im, gh, coef, sink);
+        // the decode alone first; libjpeg's input buffering is replayed beside a second decode
+        // only for the images whose end of data decides (no marker after the scan, or restart
+        // intervals): a lane that needs it runs while the others of its wave wait
+        if constexpr (kLds) st = entropy_decode<false>(src, im, lds, coef, sink);
+        else st = entropy_decode<false>(src, im, gh, coef, sink);
+        if (st == J_REPLAY) {
+            if constexpr (kLds) st = entropy_decode<true>(src, im, lds, coef, sink);
+            else st = entropy_decode<true>(src, im, gh, coef, sink);
+        }
         // undecodable data: the image's coefficients are defined as zero (a truncated file keeps
         // what libjpeg would decode, the missing data as zeros: check=False callers get that image)
         if (st != J_OK && st != J_TRUNCATED) {

@@ -26,6 +26,7 @@ enum : int32_t {
     J_BAD_TABLE = 4,       // missing or malformed DQT / DHT
     J_BAD_DATA = 5,        // entropy-coded data does not decode (set by the device pass)
     J_TRUNCATED = 6,       // libjpeg's input starves before the last MCU (Pillow: "image file is truncated")
+    J_REPLAY = 100,        // internal: decode again with libjpeg's input buffering replayed (LjInput)
 };
 
 enum : int32_t { CS_GRAY = 0, CS_YCC = 1, CS_RGB = 2 };
@@ -52,6 +53,7 @@ struct JpegImage {
     int32_t bw[3], bh[3];       // blocks per row / column (whole MCUs)
     int32_t dw[3], dh[3];       // downsampled component size (libjpeg downsampled_width/height)
     int32_t quant[3], dc[3], ac[3];   // pool indices
+    int32_t cid[3];             // frame component identifiers (the post-scan SOS checks)
 };
 
 struct JpegPlan {
@@ -311,17 +313,118 @@ struct DirectSink {
     __host__ __device__ inline void end() {}
 };
 
+// After the scan: libjpeg's jpeg_finish_decompress reads markers until EOI (jdmarker.c
+// read_markers / next_marker; a single-scan image).  Suspension (the data ends, anywhere) is fine
+// once every row is out (Pillow's JpegDecode.c); an error is the loader raising ("broken data
+// stream").  From q: garbage bytes, 0xFF fill and 0xFF00 are skipped to the next marker; EOI ends
+// the image; SOI, any SOFn, JPG and the reserved markers are errors; RSTn / TEM take no
+// parameters; SOS is an error once its header is read (JERR_EOI_EXPECTED), or earlier when its
+// length or a component selector is invalid (get_sos, libjpeg-turbo's two component checks);
+// DQT / DHT / DAC / DRI are parsed with get_dqt / get_dht / get_dac / get_dri's checks
+// (a DQT table is read whole whatever the length says); APPn / COM / DNL are skipped by length.
+// Checked against Pillow 12.2 on fuzzed marker sequences (tests/test_jpeg.py tail_cases).
+__host__ __device__ inline int32_t post_scan_status(const uint8_t* q, const uint8_t* end, const JpegImage& im) {
+    for (;;) {
+        while (q + 1 < end && !(q[0] == 0xFF && q[1] != 0xFF && q[1] != 0)) ++q;
+        if (q + 1 >= end) return J_OK;
+        const int m = q[1];
+        q += 2;
+        if (m == 0xD9) return J_OK;
+        if (m == 0xD8 || (m >= 0xC0 && m <= 0xCF && m != 0xC4 && m != 0xCC)) return J_BAD_DATA;
+        if ((m >= 0xD0 && m <= 0xD7) || m == 0x01) continue;
+        if (m == 0xDA) {
+            if (end - q < 3) return J_OK;
+            const int len = (q[0] << 8) | q[1], ns = q[2];
+            if (len != ns * 2 + 6 || ns < 1 || ns > 4) return J_BAD_DATA;
+            const uint8_t* r = q + 3;
+            int cur[4] = {-1, -1, -1, -1};   // cinfo->cur_comp_info[i]: the component of selector i
+            const int nc = im.ncomp < 4 ? im.ncomp : 4;
+            for (int i = 0; i < ns; ++i) {
+                if (end - r < 2) return J_OK;
+                const int cc = r[0];
+                r += 2;
+                int found = -1;
+                for (int ci = 0; ci < nc && found < 0; ++ci)   // (tested at index ci, stored at i)
+                    if (im.cid[ci] == cc && cur[ci] < 0) found = ci;
+                if (found < 0) return J_BAD_DATA;
+                cur[i] = found;
+                for (int pi = 0; pi < i; ++pi)
+                    if (cur[pi] == found) return J_BAD_DATA;
+            }
+            return end - r < 3 ? J_OK : J_BAD_DATA;
+        }
+        const bool seg = m == 0xDD || m == 0xDB || m == 0xC4 || m == 0xCC || m == 0xFE || m == 0xDC ||
+                         (m >= 0xE0 && m <= 0xEF);
+        if (!seg) return J_BAD_DATA;   // DHP, EXP, JPGn, reserved: JERR_UNKNOWN_MARKER
+        if (end - q < 2) return J_OK;
+        const int len = (q[0] << 8) | q[1];
+        const uint8_t* r = q + 2;
+        int64_t length = len - 2;
+        if (m == 0xDD) {
+            if (len != 4) return J_BAD_DATA;
+            if (end - r < 2) return J_OK;
+            q = r + 2;
+        } else if (m == 0xDB) {
+            while (length > 0) {
+                --length;
+                if (r >= end) return J_OK;
+                const int t = *r++;
+                if ((t & 15) >= 4) return J_BAD_DATA;
+                const int need = (t >> 4) ? 128 : 64;
+                if (end - r < need) return J_OK;
+                r += need;
+                length -= need;
+            }
+            if (length != 0) return J_BAD_DATA;
+            q = r;
+        } else if (m == 0xC4) {
+            while (length > 16) {
+                if (end - r < 17) return J_OK;
+                int idx = r[0], count = 0;
+                for (int l = 1; l <= 16; ++l) count += r[l];
+                r += 17;
+                length -= 17;
+                if (count > 256 || count > length) return J_BAD_DATA;
+                if (end - r < count) return J_OK;
+                r += count;
+                length -= count;
+                if (idx & 0x10) idx -= 0x10;
+                if (idx >= 4) return J_BAD_DATA;
+            }
+            if (length != 0) return J_BAD_DATA;
+            q = r;
+        } else if (m == 0xCC) {
+            while (length > 0) {
+                if (end - r < 2) return J_OK;
+                const int idx = r[0], val = r[1];
+                r += 2;
+                length -= 2;
+                if (idx >= 32) return J_BAD_DATA;
+                if (idx < 16 && (val & 15) > (val >> 4)) return J_BAD_DATA;
+            }
+            if (length != 0) return J_BAD_DATA;
+            q = r;
+        } else {   // APPn, COM, DNL: skip_variable / get_interesting_appn
+            q = r + (length > 0 ? length : 0);
+        }
+    }
+}
+
 // Decodes one image's scan into zig-zag-order int16 coefficient blocks.  Returns J_OK,
 // J_BAD_DATA (then the blocks not yet ended are left as they were) or J_TRUNCATED (libjpeg's
 // input would starve before the last MCU, LjInput: every block is decoded, missing data as zeros,
-// but the reference's loader raises for such a file).
-template <class Sink>
+// but the reference's loader raises for such a file).  kReplay = false runs the decode alone and
+// returns J_REPLAY when the end of the data decides (no marker after the scan, or restart
+// intervals, whose marker search the replay follows): the caller decodes again with kReplay.
+template <bool kReplay, class Sink>
 __host__ __device__ inline int32_t entropy_decode(const uint8_t* src, const JpegImage& im, const JpegHuff* huff,
                                                   int16_t* coef, Sink& sink) {
     // One iteration = one symbol, with the DC and AC cases folded into the same arithmetic
     // (DC: run 0, size = symbol, value added to the component's predictor) and the block
     // position kept as running per-component MCU origins, so that lanes at different points
     // of their streams execute nearly the same instructions.
+    if constexpr (!kReplay)
+        if (im.ri) return J_REPLAY;
     BitReader br;
     br.start(src + im.src_off, src + im.src_off + im.src_len);
     LjInput lj;
@@ -350,20 +453,22 @@ __host__ __device__ inline int32_t entropy_decode(const uint8_t* src, const Jpeg
     int comp = 0;
     sink.begin(org0);
     const JpegHuff* tbl = dct0;
-    lj.mcu(nb, im.ri != 0);
+    if constexpr (kReplay) lj.mcu(nb, im.ri != 0);
     while (mcu < nmcu) {
         br.refill();
         const int64_t c0 = br.consumed();
-        lj.need(c0, 8);   // HUFF_DECODE (HUFF_DECODE_FAST)
+        if constexpr (kReplay) lj.need(c0, 8);   // HUFF_DECODE (HUFF_DECODE_FAST)
         const int sym = br.decode(tbl);
         if (sym < 0) return J_BAD_DATA;
         const int64_t c1 = br.consumed();
-        if (c1 - c0 > 8) lj.need_long(c0, (int)(c1 - c0));   // a code longer than the lookahead
+        if constexpr (kReplay)
+            if (c1 - c0 > 8) lj.need_long(c0, (int)(c1 - c0));   // a code longer than the lookahead
         const bool dc = k == 0;
         const int r = dc ? 0 : sym >> 4;
         const int s = dc ? sym : sym & 15;
         if (s > 15) return J_BAD_DATA;
-        if (s) lj.need(c1, s);   // CHECK_BIT_BUFFER(s) / FILL_BIT_BUFFER_FAST
+        if constexpr (kReplay)
+            if (s) lj.need(c1, s);   // CHECK_BIT_BUFFER(s) / FILL_BIT_BUFFER_FAST
         int32_t v = s ? huff_extend(br.take(s), s) : 0;
         if (dc) {
             v += comp == 0 ? pred0 : (comp == 1 ? pred1 : pred2);
@@ -397,9 +502,9 @@ __host__ __device__ inline int32_t entropy_decode(const uint8_t* src, const Jpeg
                     togo = im.ri;
                     pred0 = pred1 = pred2 = 0;
                     br.restart();
-                    lj.restart();
+                    if constexpr (kReplay) lj.restart();
                 }
-                lj.mcu(nb, im.ri != 0);
+                if constexpr (kReplay) lj.mcu(nb, im.ri != 0);
             }
             comp = b < n0 ? 0 : b - n0 + 1;
             int16_t* y = org0 + ((b & (h0 - 1)) + (int64_t)(b >> (h0 - 1)) * bw0) * 64;
@@ -408,20 +513,21 @@ __host__ __device__ inline int32_t entropy_decode(const uint8_t* src, const Jpeg
         }
     }
     // every MCU decoded: the reference's loader returns the image unless libjpeg's input starved
-    // on the way (LjInput); a missing EOI alone does not fail it.  jpeg_finish_decompress then
-    // reads the next marker (next_marker: garbage bytes skipped; suspending at the end is fine
-    // once every row is out): EOI, RSTn, TEM, APPn, COM, DQT, DHT, DRI end the image normally; a
-    // second SOI or SOF, or a reserved marker, is an error in libjpeg (Pillow: "broken data
-    // stream"), reported here as undecodable data.
-    if (lj.starved) return J_TRUNCATED;
-    const uint8_t* q = lj.p;
-    while (q + 1 < lj.end && !(q[0] == 0xFF && q[1] != 0xFF && q[1] != 0)) ++q;
-    if (q + 1 < lj.end) {
-        const int m = q[1];
-        const bool sof = m >= 0xC0 && m <= 0xCF && m != 0xC4 && m != 0xCC;
-        if (m == 0xD8 || sof || (m >= 0x02 && m <= 0xBF)) return J_BAD_DATA;
+    // on the way (LjInput); a missing EOI alone does not fail it.  Without the replay, the scan is
+    // known not to starve when a marker follows the data: with no restart interval libjpeg's
+    // fetches never pass the first marker after the scan start, and the BitReader stops at or
+    // before it, so a marker found from br.p is one libjpeg's input never reached past.
+    // Otherwise (no marker before the end) the decode runs again with the replay.
+    const uint8_t* q;
+    if constexpr (kReplay) {
+        if (lj.starved) return J_TRUNCATED;
+        q = lj.p;
+    } else {
+        q = br.p;
+        while (q + 1 < br.end && !(q[0] == 0xFF && q[1] != 0xFF && q[1] != 0)) ++q;
+        if (q + 1 >= br.end) return J_REPLAY;
     }
-    return J_OK;
+    return post_scan_status(q, br.end, im);
 }
 
 // ---------------------------------------------------------------- islow IDCT (jidctint.c)

@@ -77,7 +77,7 @@ def _bench(dev, rank, world):
     import bench
     model = _model(dev)
     wl = bench.Workload(dev, rank, world, BATCH, dataset=MARKET, model=model)
-    cmc, mAP, _, _ = wl.step()
+    cmc, mAP, _, _, _ = wl.step()
     leg = bench.msmt17_leg(model, dev, rank, world, BATCH, dataset=MSMT)
     return np.asarray(cmc), float(mAP), leg["mAP"], (leg["rerank"]["mAP_rerank"], leg["rerank_embedded"]["mAP_rerank"])
 

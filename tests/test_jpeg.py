@@ -159,6 +159,59 @@ def tail_cases():
         for cut in (1, 2, 3, 5, 17, 100):
             if cut < len(body) - 700:
                 out.append((f"{i}-{cut}", body[:-cut]))
+    return out + marker_tail_cases()
+
+
+def _marker_segments(rng):
+    """Marker segments libjpeg's read_markers may meet after the scan (jdmarker.c), valid and
+    damaged: parameterless markers, SOI / SOFn / JPG / reserved, SOS headers (whole, cut, bad
+    length or component selectors), DQT / DHT / DAC / DRI with good and bad lengths and indices,
+    APPn / COM / DNL with short lengths, garbage, 0xFF fill and stuffing."""
+    import struct
+
+    def rb(k):
+        return bytes(rng.randrange(256) for _ in range(k))
+
+    def u16(v):
+        return struct.pack(">H", v)
+
+    ch = rng.choice
+    return [b"\xff\xd9", b"\xff\xd8", b"\xff\xd0", b"\xff\x01", b"\xff\xda", b"\xff\xc0", b"\xff\xc2", b"\xff\xc8",
+            b"\xff\xde", b"\xff\xf0", b"\xff\xcc",
+            b"\xff\xfe" + u16(ch([0, 1, 2, 3, 4, 8])) + rb(ch([0, 1, 2, 6])),
+            b"\xff" + bytes([rng.randrange(0xE0, 0xF0)]) + u16(ch([0, 1, 2, 4, 16])) + b"ab",
+            b"\xff\xdb" + u16(ch([2, 3, 67, 68, 131, 60, 132, 100])) + bytes([ch([0, 1, 4, 0x10, 0x13, 0x20])])
+            + bytes(rng.randrange(1, 256) for _ in range(ch([0, 10, 64, 65, 128, 129]))),
+            b"\xff\xc4" + u16(ch([2, 19, 20, 21, 30, 18])) + bytes([ch([0, 1, 0x10, 0x13, 5, 0x15, 0x20])])
+            + bytes([ch([0, 1, 2, 3])] + [0] * 15) + rb(ch([0, 1, 2, 3])),
+            b"\xff\xcc" + u16(ch([2, 4, 6, 5, 3])) + bytes(rng.randrange(40) for _ in range(ch([0, 2, 4]))),
+            b"\xff\xdd" + u16(ch([4, 5, 3])) + b"\x00\x00",
+            b"\xff\xdc" + u16(ch([4, 2, 0])) + b"\x00\x10",
+            b"\xff\xda" + u16(ch([12, 8, 13, 10])) + bytes([ch([3, 1, 0, 2, 5])])
+            + bytes([ch([1, 2, 3, 9]), 0x11, ch([1, 2, 3]), 0x11, ch([3, 1]), 0x11, 0, 63, 0])[:ch(range(10))],
+            rb(ch([1, 2, 3])), b"\xff", b"\xff\x00", b"\xff\xff\xd9", b"\xff\xff\xd8"]
+
+
+def marker_tail_cases(n=240, seed=5):
+    """What follows a complete scan, as libjpeg's jpeg_finish_decompress reads it:
+    SOS after a single-scan image, markers after COM / APPn / tables, DQT / DHT / DAC / DRI
+    contents, sequences cut anywhere.  Seeded random sequences of 1-4 segments after two bodies
+    (4:2:0 and 4:2:2) plus the advisor's named cases; Pillow decides which load."""
+    import random
+    rng = random.Random(seed)
+    bodies = [syn.jpeg_files(1, 64, 48, seed=40)[0][:-2], syn.jpeg_files(1, 37, 29, seed=42, subsampling=1)[0][:-2]]
+    com = b"\xff\xfe\x00\x04ab"
+    sos = b"\xff\xda\x00\x0c\x03\x01\x00\x02\x11\x03\x11\x00\x3f\x00"
+    out = [("sos", bodies[0] + sos), ("sos-cut", bodies[0] + sos[:5]), ("com+sos", bodies[0] + com + sos),
+           ("com+soi", bodies[0] + com + b"\xff\xd8"), ("com+sof", bodies[0] + com + b"\xff\xc0\x00\x11"),
+           ("com+eoi+soi", bodies[0] + com + b"\xff\xd9\xff\xd8"), ("ffda", bodies[1] + b"\xff\xda")]
+    for k in range(n):
+        body = bodies[k % 2]
+        tail = b"".join(rng.choice(_marker_segments(rng)) for _ in range(rng.choice([1, 2, 3, 4])))
+        b = body + tail
+        if rng.random() < 0.3 and len(tail) > 1:
+            b = b[:len(body) + rng.randrange(1, len(tail))]
+        out.append((f"m{k}:{b[len(body):][:24].hex()}", b))
     return out
 
 
@@ -216,6 +269,13 @@ def test_core_arithmetic_on_host_vs_pillow(tmp_path):
     eerr = np.zeros(je.B, np.int32)
     host.jpeg_host_decode(je.buf.ctypes.data_as(vp), je.plan.ctypes.data_as(vp), je.info.ctypes.data_as(vp),
                           eout.ctypes.data_as(vp), eerr.ctypes.data_as(vp))
+    # the kernels' decode-only first pass (replay only where the end of the data decides) gives
+    # the statuses and pixels of replaying libjpeg's input buffering for every image
+    rout = np.zeros_like(eout)
+    rerr = np.zeros_like(eerr)
+    host.jpeg_host_decode_replay(je.buf.ctypes.data_as(vp), je.plan.ctypes.data_as(vp), je.info.ctypes.data_as(vp),
+                                 rout.ctypes.data_as(vp), rerr.ctypes.data_as(vp))
+    assert np.array_equal(eerr, rerr) and np.array_equal(eout, rout)
     mism = [(name, int(eerr[k])) for k, (name, b) in enumerate(ec) if (eerr[k] == 0) == _pil_raises(b)]
     assert not mism, mism
     assert 0 < int((eerr == 0).sum()) < len(ec)  # both kinds occur

@@ -11,8 +11,10 @@
 
 using namespace reidmi::jpeg;
 
-extern "C" int jpeg_host_decode(const uint8_t* files, const uint8_t* plan, const int64_t* info, uint8_t* out,
-                                int32_t* err) {
+// always_replay: run every image with libjpeg's input buffering replayed (the kernels take the
+// decode-only pass first and replay only when the end of the data decides): both must agree.
+static int host_decode(const uint8_t* files, const uint8_t* plan, const int64_t* info, uint8_t* out, int32_t* err,
+                       bool always_replay) {
     const JpegPlan* P = (const JpegPlan*)plan;
     const JpegImage* imgs = (const JpegImage*)(plan + P->img_off);
     const JpegHuff* huff = (const JpegHuff*)(plan + P->huff_off);
@@ -24,7 +26,8 @@ extern "C" int jpeg_host_decode(const uint8_t* files, const uint8_t* plan, const
         err[i] = im.status;
         if (im.status != J_OK) continue;
         DirectSink sink;
-        err[i] = entropy_decode(files, im, huff, coef.data(), sink);
+        err[i] = always_replay ? J_REPLAY : entropy_decode<false>(files, im, huff, coef.data(), sink);
+        if (err[i] == J_REPLAY) err[i] = entropy_decode<true>(files, im, huff, coef.data(), sink);
         for (int c = 0; c < im.ncomp; ++c) {
             const int64_t pitch = (int64_t)im.bw[c] * 8;
             for (int by = 0; by < im.bh[c]; ++by)
@@ -38,4 +41,14 @@ extern "C" int jpeg_host_decode(const uint8_t* files, const uint8_t* plan, const
             for (int x = 0; x < im.w; ++x) pixel_rgb(im, planes.data() + im.plane_off, x, y, out + im.out_off + ((int64_t)y * im.w + x) * 3);
     }
     return 0;
+}
+
+extern "C" int jpeg_host_decode(const uint8_t* files, const uint8_t* plan, const int64_t* info, uint8_t* out,
+                                int32_t* err) {
+    return host_decode(files, plan, info, out, err, false);
+}
+
+extern "C" int jpeg_host_decode_replay(const uint8_t* files, const uint8_t* plan, const int64_t* info, uint8_t* out,
+                                       int32_t* err) {
+    return host_decode(files, plan, info, out, err, true);
 }
