@@ -259,7 +259,10 @@ class HipStages:
         agrees, through one all-reduce, to take rank_rows' row passes)."""
         from . import distributed as rd
         rank, W = rd.world()
-        if not (RANK_PREFILTER and self.K <= 64) or hi <= lo:
+        # every early return below decides on rank-uniform inputs (the same features, k1, k2 on
+        # every rank); a rank-local reason (an empty shard, N < W) joins the all-reduced flag
+        # instead, so no rank skips a collective the others enter (ADVICE r4)
+        if not (RANK_PREFILTER and self.K <= 64):
             return None
         x16, Np, Dp, nrm, fits, nmax2 = self._feat16()  # the same decision on every rank (same features)
         if not fits or Dp < 128:
@@ -273,20 +276,23 @@ class HipStages:
         # probe (as the one-call path): concentrated features (a random network's embeddings)
         # put every row beyond the bound; then all ranks take the exact row passes
         pr = min(512, hi - lo)
-        Rp = torch.empty((pr, self.K), device=self.dev, dtype=torch.int32)
-        mp_ = torch.empty(pr, device=self.dev, dtype=torch.float32)
-        need = torch.empty(pr, device=self.dev, dtype=torch.int32)
-        _lib.call("reidmi_rr_rank_rows_f16", _lib.ptr(self.feat), self.N, self.D, self.D, _lib.ptr(self.sqn),
-                  _lib.ptr(nrm), _lib.ptr(nmax2), _lib.ptr(x16), Np, Dp, lo, lo + pr, self.K, _lib.ptr(Rp),
-                  _lib.ptr(mp_), _lib.ptr(need), _lib.ptr(self._chunk_buf(cc, Np)), cc, self.st)
-        bad = torch.tensor([float(cap == 0 or 2 * int(need.sum().item()) > pr)], dtype=torch.float64)
+        bad_local = hi <= lo or cap == 0 or ntiles == 0
+        if not bad_local:
+            Rp = torch.empty((pr, self.K), device=self.dev, dtype=torch.int32)
+            mp_ = torch.empty(pr, device=self.dev, dtype=torch.float32)
+            need = torch.empty(pr, device=self.dev, dtype=torch.int32)
+            _lib.call("reidmi_rr_rank_rows_f16", _lib.ptr(self.feat), self.N, self.D, self.D, _lib.ptr(self.sqn),
+                      _lib.ptr(nrm), _lib.ptr(nmax2), _lib.ptr(x16), Np, Dp, lo, lo + pr, self.K, _lib.ptr(Rp),
+                      _lib.ptr(mp_), _lib.ptr(need), _lib.ptr(self._chunk_buf(cc, Np)), cc, self.st)
+            bad_local = 2 * int(need.sum().item()) > pr
+            del Rp, mp_, need
+        bad = torch.tensor([float(bad_local)], dtype=torch.float64)
         if rd._initialized():
             b = bad.to(rd._collective_device(self.feat))
             rd.dist.all_reduce(b, op=rd.dist.ReduceOp.MAX)
             bad = b.cpu()
         if bad.item() > 0:
             return None
-        del Rp, mp_, need
         self._chunk = None  # the lists take the chunk's place
         N, K = self.N, self.K
         meta = torch.zeros(Np * 4, device=self.dev, dtype=torch.float32)
