@@ -280,7 +280,8 @@ int reidmi_comm_allreduce(reidmi_comm_t comm, const void* send, void* recv, int6
 int reidmi_gemm_f16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N, int64_t K,
                     const float* bias, const void* rowstat, const float* colsum, void* out, int64_t ldc, void* stream);
 
-/* Measurement hooks: live timing of the GEMM launches (HIP events recorded on the launch stream
+/* The product's timing hook (part of the product ABI on purpose; not an A/B variant — those live
+ * in libreidmi_tools.so, reidmi_tools.h).  Measurement hooks: live timing of the GEMM launches (HIP events recorded on the launch stream
  * around each GEMM, including those inside reidmi_vit_forward / reidmi_text_forward), which is
  * how bench.py measures the dominant kernel's average launch time over its timed steps (the
  * roofline `achieved`; no other interface reaches a kernel inside the forward).  Off by

@@ -162,6 +162,10 @@ __global__ __launch_bounds__(256) void distmat_f32_kernel(
 #ifndef DM2_BAND
 #define DM2_BAND 4
 #endif
+#if !defined(REIDMI_TOOLS) && (DM2_BK_ != 16 || DM2_MINWG_ != 4 || DM2_BAND != 4 || defined(RS_STATS) || \
+                               defined(RS_SINGLE_PASS))
+#error "backend.hip: DM2_* / RS_* variants build only with -DREIDMI_TOOLS (never into libreidmi.so)"
+#endif
 constexpr int DM2_BK = DM2_BK_, DM2_LD = DM_BM + 1;
 constexpr int DM2_F4 = DM2_BK / 4;            // float4 per operand row and K-step
 constexpr int DM2_U = DM_BM * DM2_F4 / 256;   // float4 staging slots per thread and operand

@@ -73,6 +73,15 @@ constexpr int GB_M = 128, GB_N = 128, GB_K = 64;
 #ifndef GEMM_VAR_FB2  // persistent tile: keep both column halves' W fragments (LOAD 3 reads none)
 #define GEMM_VAR_FB2 1
 #endif
+// The A/B hooks above compile other kernels (the timing-only ones give wrong results by design):
+// any value but the shipped one is refused outside a tools / variant build (-DREIDMI_TOOLS:
+// libreidmi_tools.so, tools/build_variant.py), so none can enter libreidmi.so.
+#if !defined(REIDMI_TOOLS) &&                                                                              \
+    (GEMM_VAR_NOSTORE != 0 || GEMM_VAR_NOGELU != 0 || GEMM_VAR_NOPSTAT != 0 || GEMM_VAR_NORESLOAD != 0 ||   \
+     GEMM_VAR_STAGGER != 0 || GEMM_VAR_DIAG_LOAD0 != 0 || GEMM_VAR_RPRE != 1 || GEMM_VAR_FB2 != 1 ||       \
+     GEMM_VAR_STAG_SHIFT != 0 || GEMM_VAR_STAG_MASK != 1 || GEMM_VAR_STAG_SLP != 127)
+#error "gemm.hip: GEMM_VAR_* variants build only with -DREIDMI_TOOLS (never into libreidmi.so)"
+#endif
 
 __device__ __forceinline__ int swz(int r, int kc) { return r * GB_K + ((kc ^ ((r >> 1) & 7)) << 3); }
 

@@ -93,10 +93,51 @@ struct Pools {
 
 static inline int u16be(const uint8_t* p) { return (p[0] << 8) | p[1]; }
 
+// The standard Huffman tables of ITU T.81 Annex K.3 (16 code counts, then the symbols): what
+// libjpeg-turbo's jpeg_make_d_derived_tbl substitutes (jstdhuff.c jpeg_std_huff_table) when a
+// scan names table 0 or 1 that no DHT defined (Motion-JPEG frames omit them).
+static const uint8_t kStdDcLuma[28] = {
+    0x00, 0x01, 0x05, 0x01, 0x01, 0x01, 0x01, 0x01, 0x01, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00,
+    0x00, 0x01, 0x02, 0x03, 0x04, 0x05, 0x06, 0x07, 0x08, 0x09, 0x0a, 0x0b,
+};
+static const uint8_t kStdAcLuma[178] = {
+    0x00, 0x02, 0x01, 0x03, 0x03, 0x02, 0x04, 0x03, 0x05, 0x05, 0x04, 0x04, 0x00, 0x00, 0x01, 0x7d,
+    0x01, 0x02, 0x03, 0x00, 0x04, 0x11, 0x05, 0x12, 0x21, 0x31, 0x41, 0x06, 0x13, 0x51, 0x61, 0x07,
+    0x22, 0x71, 0x14, 0x32, 0x81, 0x91, 0xa1, 0x08, 0x23, 0x42, 0xb1, 0xc1, 0x15, 0x52, 0xd1, 0xf0,
+    0x24, 0x33, 0x62, 0x72, 0x82, 0x09, 0x0a, 0x16, 0x17, 0x18, 0x19, 0x1a, 0x25, 0x26, 0x27, 0x28,
+    0x29, 0x2a, 0x34, 0x35, 0x36, 0x37, 0x38, 0x39, 0x3a, 0x43, 0x44, 0x45, 0x46, 0x47, 0x48, 0x49,
+    0x4a, 0x53, 0x54, 0x55, 0x56, 0x57, 0x58, 0x59, 0x5a, 0x63, 0x64, 0x65, 0x66, 0x67, 0x68, 0x69,
+    0x6a, 0x73, 0x74, 0x75, 0x76, 0x77, 0x78, 0x79, 0x7a, 0x83, 0x84, 0x85, 0x86, 0x87, 0x88, 0x89,
+    0x8a, 0x92, 0x93, 0x94, 0x95, 0x96, 0x97, 0x98, 0x99, 0x9a, 0xa2, 0xa3, 0xa4, 0xa5, 0xa6, 0xa7,
+    0xa8, 0xa9, 0xaa, 0xb2, 0xb3, 0xb4, 0xb5, 0xb6, 0xb7, 0xb8, 0xb9, 0xba, 0xc2, 0xc3, 0xc4, 0xc5,
+    0xc6, 0xc7, 0xc8, 0xc9, 0xca, 0xd2, 0xd3, 0xd4, 0xd5, 0xd6, 0xd7, 0xd8, 0xd9, 0xda, 0xe1, 0xe2,
+    0xe3, 0xe4, 0xe5, 0xe6, 0xe7, 0xe8, 0xe9, 0xea, 0xf1, 0xf2, 0xf3, 0xf4, 0xf5, 0xf6, 0xf7, 0xf8,
+    0xf9, 0xfa,
+};
+static const uint8_t kStdDcChroma[28] = {
+    0x00, 0x03, 0x01, 0x01, 0x01, 0x01, 0x01, 0x01, 0x01, 0x01, 0x01, 0x00, 0x00, 0x00, 0x00, 0x00,
+    0x00, 0x01, 0x02, 0x03, 0x04, 0x05, 0x06, 0x07, 0x08, 0x09, 0x0a, 0x0b,
+};
+static const uint8_t kStdAcChroma[178] = {
+    0x00, 0x02, 0x01, 0x02, 0x04, 0x04, 0x03, 0x04, 0x07, 0x05, 0x04, 0x04, 0x00, 0x01, 0x02, 0x77,
+    0x00, 0x01, 0x02, 0x03, 0x11, 0x04, 0x05, 0x21, 0x31, 0x06, 0x12, 0x41, 0x51, 0x07, 0x61, 0x71,
+    0x13, 0x22, 0x32, 0x81, 0x08, 0x14, 0x42, 0x91, 0xa1, 0xb1, 0xc1, 0x09, 0x23, 0x33, 0x52, 0xf0,
+    0x15, 0x62, 0x72, 0xd1, 0x0a, 0x16, 0x24, 0x34, 0xe1, 0x25, 0xf1, 0x17, 0x18, 0x19, 0x1a, 0x26,
+    0x27, 0x28, 0x29, 0x2a, 0x35, 0x36, 0x37, 0x38, 0x39, 0x3a, 0x43, 0x44, 0x45, 0x46, 0x47, 0x48,
+    0x49, 0x4a, 0x53, 0x54, 0x55, 0x56, 0x57, 0x58, 0x59, 0x5a, 0x63, 0x64, 0x65, 0x66, 0x67, 0x68,
+    0x69, 0x6a, 0x73, 0x74, 0x75, 0x76, 0x77, 0x78, 0x79, 0x7a, 0x82, 0x83, 0x84, 0x85, 0x86, 0x87,
+    0x88, 0x89, 0x8a, 0x92, 0x93, 0x94, 0x95, 0x96, 0x97, 0x98, 0x99, 0x9a, 0xa2, 0xa3, 0xa4, 0xa5,
+    0xa6, 0xa7, 0xa8, 0xa9, 0xaa, 0xb2, 0xb3, 0xb4, 0xb5, 0xb6, 0xb7, 0xb8, 0xb9, 0xba, 0xc2, 0xc3,
+    0xc4, 0xc5, 0xc6, 0xc7, 0xc8, 0xc9, 0xca, 0xd2, 0xd3, 0xd4, 0xd5, 0xd6, 0xd7, 0xd8, 0xd9, 0xda,
+    0xe2, 0xe3, 0xe4, 0xe5, 0xe6, 0xe7, 0xe8, 0xe9, 0xea, 0xf2, 0xf3, 0xf4, 0xf5, 0xf6, 0xf7, 0xf8,
+    0xf9, 0xfa,
+};
+
 // jdmarker.c read_markers up to the first SOS, restricted to what the device decodes.
 static int32_t parse_one(const uint8_t* f, int64_t n, int64_t base, JpegImage& im, Pools& pools) {
     memset(&im, 0, sizeof(im));   // (status is set by the caller from the return value)
-    if (n < 4 || f[0] != 0xFF || f[1] != 0xD8) return J_NOT_JPEG;
+    // Pillow's JpegImagePlugin accepts only files starting FF D8 FF (_accept)
+    if (n < 4 || f[0] != 0xFF || f[1] != 0xD8 || f[2] != 0xFF) return J_NOT_JPEG;
     int64_t p = 2;
     bool jfif = false, adobe = false, sof = false;
     int adobe_t = -1;
@@ -111,8 +152,14 @@ static int32_t parse_one(const uint8_t* f, int64_t n, int64_t base, JpegImage& i
         while (p < n && f[p] == 0xFF) ++p;   // fill bytes
         if (p >= n) return J_NOT_JPEG;
         const int m = f[p++];
-        if (m == 0x01 || m == 0xD8 || (m >= 0xD0 && m <= 0xD7)) continue;
+        if (m == 0x00) continue;   // 0xFF 0x00: skipped like garbage (next_marker)
+        // markers outside Pillow's table (TEM, 0x02-0xBF): JpegImagePlugin "no marker found"
+        if (m < 0xC0) return J_NOT_JPEG;
+        if (m >= 0xD0 && m <= 0xD7) continue;   // RSTn: no parameters
+        if (m == 0xD8) return J_NOT_JPEG;   // a second SOI (get_soi: JERR_SOI_DUPLICATE)
         if (m == 0xD9) return J_NOT_JPEG;   // EOI before any scan
+        // DHP, EXP, JPGn: skipped by Pillow's parser, then libjpeg's JERR_UNKNOWN_MARKER
+        if (m == 0xDE || m == 0xDF || (m >= 0xF0 && m <= 0xFD)) return J_NOT_JPEG;
         if (p + 2 > n) return J_NOT_JPEG;
         const int len = u16be(f + p);
         if (len < 2 || p + len > n) return J_NOT_JPEG;
@@ -125,7 +172,7 @@ static int32_t parse_one(const uint8_t* f, int64_t n, int64_t base, JpegImage& i
             im.ncomp = s[5];
             if (im.h == 0 || im.w == 0) return J_UNSUPPORTED;   // DNL-defined height
             if (im.ncomp != 1 && im.ncomp != 3) return J_LAYOUT;
-            if (sl < 6 + 3 * im.ncomp) return J_NOT_JPEG;
+            if (len != 8 + 3 * im.ncomp) return J_NOT_JPEG;   // get_sof: JERR_BAD_LENGTH
             for (int c = 0; c < im.ncomp; ++c) {
                 cid[c] = s[6 + 3 * c];
                 im.hs[c] = s[7 + 3 * c] >> 4;
@@ -137,22 +184,23 @@ static int32_t parse_one(const uint8_t* f, int64_t n, int64_t base, JpegImage& i
             sof = true;
         } else if ((m >= 0xC2 && m <= 0xCF) && m != 0xC4 && m != 0xC8 && m != 0xCC) {
             return J_UNSUPPORTED;   // progressive, lossless, hierarchical, arithmetic
-        } else if (m == 0xC4) {     // DHT
+        } else if (m == 0xC4) {     // DHT (get_dht: tables while > 16 bytes remain, then exactly none)
             int i = 0;
-            while (i + 17 <= sl) {
-                const int tc = s[i] >> 4, th = s[i] & 15;
+            while (sl - i > 16) {
+                const int tc = (s[i] >> 4) & 1, th = s[i] & 0xEF;   // (bit 4: AC; any other bit: a bad index)
                 int tot = 0;
                 for (int l = 0; l < 16; ++l) tot += s[i + 1 + l];
-                if (tc > 1 || th > 3 || tot > 256 || i + 17 + tot > sl) return J_BAD_TABLE;
+                if (th > 3 || tot > 256 || i + 17 + tot > sl) return J_BAD_TABLE;
                 (tc ? hac : hdc)[th] = s + i + 1;
                 (tc ? hac_len : hdc_len)[th] = 16 + tot;
                 i += 17 + tot;
             }
-        } else if (m == 0xDB) {     // DQT
+            if (i != sl) return J_BAD_TABLE;   // JERR_BAD_LENGTH
+        } else if (m == 0xDB) {     // DQT (get_dqt: any nonzero precision nibble means 16-bit entries)
             int i = 0;
             while (i < sl) {
-                const int pq = s[i] >> 4, t = s[i] & 15;
-                if (pq > 1 || t > 3 || i + 1 + 64 * (pq + 1) > sl) return J_BAD_TABLE;
+                const int pq = (s[i] >> 4) ? 1 : 0, t = s[i] & 15;
+                if (t > 3 || i + 1 + 64 * (pq + 1) > sl) return J_BAD_TABLE;
                 for (int k = 0; k < 64; ++k) {   // kept in zig-zag order; libjpeg's quantval is
                     const int q = pq ? u16be(s + i + 1 + 2 * k) : s[i + 1 + k];   // read as-is
                     // 16-bit entries above int16 (libjpeg keeps UINT16): not decoded here
@@ -163,31 +211,45 @@ static int32_t parse_one(const uint8_t* f, int64_t n, int64_t base, JpegImage& i
                 i += 1 + 64 * (pq + 1);
             }
         } else if (m == 0xDD) {     // DRI
-            if (sl < 2) return J_NOT_JPEG;
+            if (len != 4) return J_NOT_JPEG;   // get_dri: JERR_BAD_LENGTH
             im.ri = u16be(s);
-        } else if (m == 0xE0) {
-            if (sl >= 5 && memcmp(s, "JFIF\0", 5) == 0) jfif = true;
+        } else if (m == 0xE0) {     // examine_app0: a JFIF marker needs APP0_DATA_LEN (14) bytes
+            if (sl >= 14 && memcmp(s, "JFIF\0", 5) == 0) jfif = true;
         } else if (m == 0xEE) {
             if (sl >= 12 && memcmp(s, "Adobe", 5) == 0) {
                 adobe = true;
                 adobe_t = s[11];
             }
+        } else if (m == 0xCC) {     // DAC (get_dac: index < 32, DC bounds L <= U, exact length)
+            if (sl % 2) return J_NOT_JPEG;
+            for (int i = 0; i < sl; i += 2)
+                if (s[i] >= 32 || (s[i] < 16 && (s[i + 1] & 15) > (s[i + 1] >> 4))) return J_NOT_JPEG;
         } else if (m == 0xDA) {     // SOS
             if (!sof) return J_NOT_JPEG;
             const int ns = sl > 0 ? s[0] : 0;
+            if (len != 2 * ns + 6) return J_NOT_JPEG;   // get_sos: JERR_BAD_LENGTH
             if (ns != im.ncomp || sl < 4 + 2 * ns) return J_UNSUPPORTED;   // one interleaved scan only
             for (int j = 0; j < ns; ++j) {
                 if (s[1 + 2 * j] != cid[j]) return J_UNSUPPORTED;   // scan order = frame order
                 const int td = s[2 + 2 * j] >> 4, ta = s[2 + 2 * j] & 15;
-                if (td > 3 || ta > 3 || !hdc[td] || !hac[ta]) return J_BAD_TABLE;
+                if (td > 3 || ta > 3) return J_BAD_TABLE;
+                if (!hdc[td] && td < 2) {   // jpeg_std_huff_table
+                    hdc[td] = td ? kStdDcChroma : kStdDcLuma;
+                    hdc_len[td] = td ? (int)sizeof(kStdDcChroma) : (int)sizeof(kStdDcLuma);
+                }
+                if (!hac[ta] && ta < 2) {
+                    hac[ta] = ta ? kStdAcChroma : kStdAcLuma;
+                    hac_len[ta] = ta ? (int)sizeof(kStdAcChroma) : (int)sizeof(kStdAcLuma);
+                }
+                if (!hdc[td] || !hac[ta]) return J_BAD_TABLE;
                 if (!huff_ok(hdc[td], hdc[td] + 16, hdc_len[td] - 16, true) ||
                     !huff_ok(hac[ta], hac[ta] + 16, hac_len[ta] - 16, false))
                     return J_BAD_TABLE;
                 im.dc[j] = pools.add_huff(hdc[td], hdc_len[td]);
                 im.ac[j] = pools.add_huff(hac[ta], hac_len[ta]);
             }
-            const uint8_t* e = s + 1 + 2 * ns;
-            if (e[0] != 0 || e[1] != 63 || e[2] != 0) return J_UNSUPPORTED;   // Ss, Se, Ah/Al
+            // Ss, Se, Ah/Al of a sequential scan are only checked by a warning (jdhuff.c
+            // start_pass_huff_decoder: JWRN_NOT_SEQUENTIAL) and then ignored
             im.src_off = base + p + len;
             im.src_len = n - (p + len);
             break;

@@ -85,6 +85,7 @@ struct BitReader {
     bool marker;    // a marker (or the end) was reached: zeros are fed from here on
     int64_t loaded; // bits moved into acc since start() (fillers after a marker included):
                     // the bits consumed in the segment are loaded - bits
+    int64_t real;   // the segment's data bits (loaded when the marker was reached)
     bool nw_ok;     // nw0/nw1: the aligned words covering >= 5 stream bytes at p, loaded one
     int nmis;       // refill ahead and first read at the next refill, so the load's latency
     uint32_t nw0, nw1;   // hides behind the symbols decoded in between
@@ -104,15 +105,22 @@ struct BitReader {
         acc = 0;
         bits = 0;
         loaded = 0;
+        real = INT64_MAX;
         marker = false;
         fetch();
     }
-    // Keeps >= 32 bits in the window (a symbol plus its extra bits is at most 16 + 15).  The
+    // a decode step used bits past the segment's data (jdhuff.c jpeg_fill_bit_buffer: the
+    // request exceeds what precedes the marker -> insufficient_data)
+    __host__ __device__ inline bool past_data() const { return loaded - bits > real; }
+    // Keeps >= 32 bits in the window (a symbol plus its extra bits is at most 17 + 15).  The
     // next 4 stream bytes come from the prefetched words: all four at once when none is 0xFF,
-    // else one at a time in registers (0xFF 0x00 is a stuffed 0xFF, 0xFF + anything else a
-    // marker) — no memory access either way.  Only the last 8 bytes of a stream go byte by byte.
+    // else one at a time in registers (0xFF 0x00 is a stuffed 0xFF, 0xFF + anything but 0x00 /
+    // 0xFF a marker) — no memory access either way.  0xFF 0xFF (fill bytes, which libjpeg reads
+    // up to the byte after them: 0x00 makes them one 0xFF data byte, anything else a marker) and
+    // the last 8 bytes of a stream go byte by byte.
     __host__ __device__ inline void refill() {
         if (bits >= 32) return;
+        bool bytewise = !nw_ok;
         if (nw_ok) {
             const uint64_t win = (((uint64_t)nw1 << 32) | nw0) >> (nmis * 8);   // stream bytes, LSB first
             const uint32_t x = ~(uint32_t)win;
@@ -128,8 +136,14 @@ struct BitReader {
                 while (pos < 4 && bits < 32) {
                     const uint32_t c = (uint32_t)(win >> (8 * pos)) & 0xFF;
                     if (c == 0xFF) {
-                        if (((win >> (8 * pos + 8)) & 0xFF) != 0) {
+                        const uint32_t n = (uint32_t)(win >> (8 * pos + 8)) & 0xFF;
+                        if (n == 0xFF) {   // fill bytes: the byte loop below reads past them
+                            bytewise = true;
+                            break;
+                        }
+                        if (n != 0) {
                             marker = true;
+                            real = loaded;
                             break;
                         }
                         pos += 2;
@@ -141,24 +155,32 @@ struct BitReader {
                     loaded += 8;
                 }
                 p += pos;
-                if (marker) bits = 32 > bits ? 32 : bits;   // zeros from here on
+                if (marker && bits < 32) {   // zeros from here on
+                    loaded += 32 - bits;
+                    bits = 32;
+                }
             }
-            fetch();
-            return;
+            if (!bytewise) {
+                fetch();
+                return;
+            }
         }
         while (bits < 32) {
             uint32_t c = 0;
             if (!marker) {
                 if (p >= end) {
                     marker = true;
+                    real = loaded;
                 } else {
                     c = p[0];
                     if (c == 0xFF) {
-                        const uint32_t n = (p + 1 < end) ? p[1] : 0xD9;
-                        if (n == 0) {
-                            p += 2;
+                        const uint8_t* q = p + 1;
+                        while (q < end && *q == 0xFF) ++q;
+                        if (q < end && *q == 0) {
+                            p = q + 1;   // (0xFF)+ 0x00: one 0xFF data byte
                         } else {
-                            marker = true;
+                            marker = true;   // p stays at the first 0xFF
+                            real = loaded;
                             c = 0;
                         }
                     } else {
@@ -179,9 +201,10 @@ struct BitReader {
         bits -= n;
         return v;
     }
-    // jpeg_huff_decode: returns the symbol or -1 for an invalid code.  Codes longer than the
-    // lookahead: the length is K+1 + #{l in K+1..16 : lim[l] <= code} (lim is monotone),
-    // evaluated without a loop so that the lanes of a wave do not diverge on it.
+    // jpeg_huff_decode: returns the symbol.  Codes longer than the lookahead: the length is
+    // K+1 + #{l in K+1..16 : lim[l] <= code} (lim is monotone), evaluated without a loop so that
+    // the lanes of a wave do not diverge on it.  A code matching no table entry is libjpeg's
+    // JWRN_HUFF_BAD_CODE warning: 17 bits consumed, symbol 0 (decoding goes on).
     __host__ __device__ inline int decode(const JpegHuff* t) {
         const uint32_t e = t->lut[acc >> (64 - kLookahead)];
         if (e >> 8) {
@@ -194,16 +217,15 @@ struct BitReader {
         int l = kLookahead + 1;
 #pragma unroll
         for (int j = kLookahead + 1; j <= 16; ++j) l += code16 >= t->lim[j] ? 1 : 0;
-        if (l > 16) return -1;
+        if (l > 16) {
+            acc <<= 17;
+            bits -= 17;
+            return 0;
+        }
         const int32_t c = (int32_t)(code16 >> (16 - l));
         acc <<= l;
         bits -= l;
         return t->val[(c + t->valoff[l]) & 0xFF];
-    }
-    // skip to just past the next RSTn (jdmarker.c read_restart_marker on a valid stream)
-    __host__ __device__ inline void restart() {
-        while (p + 1 < end && !(p[0] == 0xFF && p[1] >= 0xD0 && p[1] <= 0xD7)) ++p;
-        start(p + 1 < end ? p + 2 : p, end);
     }
 };
 
@@ -234,9 +256,10 @@ struct LjInput {
     const uint8_t* p;   // libjpeg's next raw byte
     const uint8_t* end;
     int64_t F;
-    bool marker;        // reached a marker: no more fetches in this segment
+    bool marker;        // reached a marker (cinfo->unread_marker; p stays at its 0xFF): no more fetches
     bool starved;       // a fetch reached the end of the data first (the loader raises)
     bool fast;          // the current MCU runs decode_mcu_fast
+    int next_rst;       // cinfo->marker->next_restart_num
     __host__ __device__ inline void start(const uint8_t* b, const uint8_t* e) {
         p = b;
         end = e;
@@ -290,17 +313,65 @@ struct LjInput {
     __host__ __device__ inline void mcu(int blocks_in_mcu, bool restarts) {
         fast = !restarts && !marker && (end - p) >= 512 * (int64_t)blocks_in_mcu;
     }
-    // process_restart -> read_restart_marker: the next marker (skipping garbage); starves at the end
-    __host__ __device__ inline void restart() {
-        const uint8_t* q = p;
-        while (q + 1 < end && !(q[0] == 0xFF && q[1] != 0xFF && q[1] != 0)) ++q;
-        if (q + 1 >= end) {
-            starved = true;
-            q = end;
-        } else {
-            q += 2;
+    // jdmarker.c next_marker from q: garbage, 0xFF fill and 0xFF 0x00 skipped; the marker's first
+    // 0xFF at *at, its code m, the input after it at *after.  False: the data ends first.
+    __host__ __device__ static inline bool next_marker(const uint8_t* q, const uint8_t* e, const uint8_t** at, int* m,
+                                                       const uint8_t** after) {
+        for (;;) {
+            while (q < e && *q != 0xFF) ++q;
+            const uint8_t* r = q + 1;
+            while (r < e && *r == 0xFF) ++r;
+            if (r >= e) return false;
+            if (*r != 0) {
+                *at = q;
+                *m = *r;
+                *after = r + 1;
+                return true;
+            }
+            q = r + 1;
         }
-        start(q, end);
+    }
+    // jdhuff.c process_restart -> jdmarker.c read_restart_marker (+ jpeg_resync_to_restart): the
+    // marker a fetch stopped at (or the next one) is the expected RSTn and is consumed, or the
+    // resync decides: discard it and resume (1), scan on to the next marker (2), or leave it
+    // unread (3: the entropy decoder then reads zeros — an empty segment).  Starves at the end.
+    // Returns whether a marker is left unread.
+    __host__ __device__ inline bool restart() {
+        const uint8_t *at, *after;
+        int m;
+        if (!next_marker(p, end, &at, &m, &after)) {
+            starved = true;
+            start(end, end);
+            return false;
+        }
+        bool unread = false;
+        for (;;) {
+            const int d = next_rst;
+            int action;
+            if (m == 0xD0 + d) action = 1;                                                    // the expected RSTn
+            else if (m < 0xC0) action = 2;                                                    // invalid marker
+            else if (m < 0xD0 || m > 0xD7) action = 3;                                        // a non-restart marker
+            else if (m == 0xD0 + ((d + 1) & 7) || m == 0xD0 + ((d + 2) & 7)) action = 3;     // one of the next two
+            else if (m == 0xD0 + ((d + 7) & 7) || m == 0xD0 + ((d + 6) & 7)) action = 2;     // a prior one
+            else action = 1;
+            if (action == 1) {
+                start(after, end);
+                break;
+            }
+            if (action == 3) {
+                start(at, end);
+                marker = true;
+                unread = true;
+                break;
+            }
+            if (!next_marker(after, end, &at, &m, &after)) {
+                starved = true;
+                start(end, end);
+                return false;
+            }
+        }
+        next_rst = (next_rst + 1) & 7;
+        return unread;
     }
 };
 
@@ -429,6 +500,7 @@ __host__ __device__ inline int32_t entropy_decode(const uint8_t* src, const Jpeg
     br.start(src + im.src_off, src + im.src_off + im.src_len);
     LjInput lj;
     lj.starved = false;
+    lj.next_rst = 0;
     lj.start(src + im.src_off, src + im.src_off + im.src_len);
     const bool gray = im.ncomp == 1;
     const int h0 = gray ? 1 : im.hs[0];
@@ -454,36 +526,44 @@ __host__ __device__ inline int32_t entropy_decode(const uint8_t* src, const Jpeg
     sink.begin(org0);
     const JpegHuff* tbl = dct0;
     if constexpr (kReplay) lj.mcu(nb, im.ri != 0);
+    // jdhuff.c decode_mcu: once a step of the segment used bits past its data (a marker, or
+    // the end, reached too early), the MCU finishes on zero bits and the segment's later MCUs
+    // are left zero (insufficient_data, cleared at a restart): one loop iteration per block then
+    bool skip = false;
     while (mcu < nmcu) {
-        br.refill();
-        const int64_t c0 = br.consumed();
-        if constexpr (kReplay) lj.need(c0, 8);   // HUFF_DECODE (HUFF_DECODE_FAST)
-        const int sym = br.decode(tbl);
-        if (sym < 0) return J_BAD_DATA;
-        const int64_t c1 = br.consumed();
-        if constexpr (kReplay)
-            if (c1 - c0 > 8) lj.need_long(c0, (int)(c1 - c0));   // a code longer than the lookahead
-        const bool dc = k == 0;
-        const int r = dc ? 0 : sym >> 4;
-        const int s = dc ? sym : sym & 15;
-        if (s > 15) return J_BAD_DATA;
-        if constexpr (kReplay)
-            if (s) lj.need(c1, s);   // CHECK_BIT_BUFFER(s) / FILL_BIT_BUFFER_FAST
-        int32_t v = s ? huff_extend(br.take(s), s) : 0;
-        if (dc) {
-            v += comp == 0 ? pred0 : (comp == 1 ? pred1 : pred2);
-            pred0 = comp == 0 ? v : pred0;
-            pred1 = comp == 1 ? v : pred1;
-            pred2 = comp == 2 ? v : pred2;
-            tbl = comp == 0 ? act0 : (comp == 1 ? act1 : act2);
-        }
-        k += r;
-        if (s || dc) {
-            if (k > 63) return J_BAD_DATA;
-            sink.put(k, v);
-            k += 1;
+        if (skip) {
+            k = 64;
         } else {
-            k = r == 15 ? k + 1 : 64;   // ZRL: 16 zeros; EOB
+            br.refill();
+            const int64_t c0 = br.consumed();
+            if constexpr (kReplay) lj.need(c0, 8);   // HUFF_DECODE (HUFF_DECODE_FAST)
+            const int sym = br.decode(tbl);
+            const int64_t c1 = br.consumed();
+            if constexpr (kReplay)
+                if (c1 - c0 > 8) lj.need_long(c0, (int)(c1 - c0));   // a code longer than the lookahead
+            const bool dc = k == 0;
+            const int r = dc ? 0 : sym >> 4;
+            const int s = dc ? sym : sym & 15;
+            if (s > 15) return J_BAD_DATA;
+            if constexpr (kReplay)
+                if (s) lj.need(c1, s);   // CHECK_BIT_BUFFER(s) / FILL_BIT_BUFFER_FAST
+            int32_t v = s ? huff_extend(br.take(s), s) : 0;
+            if (dc) {
+                v += comp == 0 ? pred0 : (comp == 1 ? pred1 : pred2);
+                pred0 = comp == 0 ? v : pred0;
+                pred1 = comp == 1 ? v : pred1;
+                pred2 = comp == 2 ? v : pred2;
+                tbl = comp == 0 ? act0 : (comp == 1 ? act1 : act2);
+            }
+            k += r;
+            if (s || dc) {
+                // a run past the block: libjpeg's jpeg_natural_order[] extra entries map k 64..79
+                // to position 63 (damaged data)
+                sink.put(k > 63 ? 63 : k, v);
+                k += 1;
+            } else {
+                k = r == 15 ? k + 1 : 64;   // ZRL: 16 zeros; EOB
+            }
         }
         if (k >= 64) {   // block done: the next block of the MCU, or the next MCU
             sink.end();
@@ -491,6 +571,7 @@ __host__ __device__ inline int32_t entropy_decode(const uint8_t* src, const Jpeg
             if (++b == nb) {
                 b = 0;
                 ++mcu;
+                skip = skip || br.past_data();
                 org0 += h0 * 64;
                 org1 += 64;
                 org2 += 64;
@@ -501,8 +582,19 @@ __host__ __device__ inline int32_t entropy_decode(const uint8_t* src, const Jpeg
                 if (im.ri && mcu < nmcu && --togo == 0) {
                     togo = im.ri;
                     pred0 = pred1 = pred2 = 0;
-                    br.restart();
-                    if constexpr (kReplay) lj.restart();
+                    if constexpr (kReplay) {   // (restart intervals always take the replay)
+                        // libjpeg discards the buffered bits and continues where its input is;
+                        // a marker left unread feeds zeros (insufficient_data is kept then)
+                        const bool unread = lj.restart();
+                        br.start(lj.p, lj.end);
+                        if (unread) {
+                            br.marker = true;
+                            br.real = 0;
+                            br.nw_ok = false;
+                        } else {
+                            skip = false;
+                        }
+                    }
                 }
                 if constexpr (kReplay) lj.mcu(nb, im.ri != 0);
             }
@@ -535,7 +627,8 @@ constexpr int CB = 13, P1 = 2;   // CONST_BITS, PASS1_BITS
 constexpr int32_t F0298 = 2446, F0390 = 3196, F0541 = 4433, F0765 = 6270, F0899 = 7373, F1175 = 9633,
                   F1501 = 12299, F1847 = 15137, F1961 = 16069, F2053 = 16819, F2562 = 20995, F3072 = 25172;
 
-__host__ __device__ inline int32_t descale(int32_t x, int n) { return (x + (1 << (n - 1))) >> n; }
+template <typename T>
+__host__ __device__ inline T descale(T x, int n) { return (x + ((T)1 << (n - 1))) >> n; }
 
 // IDCT_range_limit[x & RANGE_MASK] of jdmaster.c prepare_range_limit_table (8-bit samples)
 __host__ __device__ inline uint8_t idct_limit(int32_t x) {
@@ -546,24 +639,26 @@ __host__ __device__ inline uint8_t idct_limit(int32_t x) {
     return (uint8_t)(v - 896);
 }
 
-// one 1-D 8-point pass of the LL&M butterfly on d[0..7] (stride st), dequantised inputs
+// one 1-D 8-point pass of the LL&M butterfly on d[0..7] (stride st), dequantised inputs.
+// libjpeg-turbo computes it in JLONG (64-bit); T = int32_t is the same arithmetic whenever no
+// intermediate leaves int32, which idct_islow checks per block (kPass1Max / kPass2Max).
+template <typename T>
 struct Idct8 {
-    int32_t t10, t11, t12, t13, o0, o1, o2, o3;
-    __host__ __device__ inline void run(int32_t d0, int32_t d1, int32_t d2, int32_t d3, int32_t d4, int32_t d5,
-                                        int32_t d6, int32_t d7) {
-        int32_t z1 = (d2 + d6) * F0541;
-        const int32_t tmp2 = z1 + d6 * (-F1847);
-        const int32_t tmp3 = z1 + d2 * F0765;
-        const int32_t tmp0 = (d0 + d4) * (1 << CB);
-        const int32_t tmp1 = (d0 - d4) * (1 << CB);
+    T t10, t11, t12, t13, o0, o1, o2, o3;
+    __host__ __device__ inline void run(T d0, T d1, T d2, T d3, T d4, T d5, T d6, T d7) {
+        T z1 = (d2 + d6) * F0541;
+        const T tmp2 = z1 + d6 * (-F1847);
+        const T tmp3 = z1 + d2 * F0765;
+        const T tmp0 = (d0 + d4) * ((T)1 << CB);
+        const T tmp1 = (d0 - d4) * ((T)1 << CB);
         t10 = tmp0 + tmp3;
         t13 = tmp0 - tmp3;
         t11 = tmp1 + tmp2;
         t12 = tmp1 - tmp2;
-        int32_t a0 = d7, a1 = d5, a2 = d3, a3 = d1;
+        T a0 = d7, a1 = d5, a2 = d3, a3 = d1;
         z1 = a0 + a3;
-        int32_t z2 = a1 + a2, z3 = a0 + a2, z4 = a1 + a3;
-        const int32_t z5 = (z3 + z4) * F1175;
+        T z2 = a1 + a2, z3 = a0 + a2, z4 = a1 + a3;
+        const T z5 = (z3 + z4) * F1175;
         a0 *= F0298;
         a1 *= F2053;
         a2 *= F3072;
@@ -581,8 +676,52 @@ struct Idct8 {
     }
 };
 
+// Every intermediate of one Idct8 pass is at most 178 219 x max|input| in magnitude (the sum of
+// the absolute butterfly constants along the longest path), so with max|input| <= these bounds
+// the int32 pass equals libjpeg's 64-bit one.  Valid images stay far below them; damaged entropy
+// data (huge coefficients) takes the 64-bit pass, as libjpeg computes it.
+constexpr int32_t kPass1Max = 12000;   // 178 219 x 12 000 < 2^31
+constexpr int32_t kPass2Max = 12000;
+
+template <typename T>
+__host__ __device__ inline void idct_pass1(const int32_t (&dq)[64], int32_t (&ws)[64]) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {   // pass 1: columns
+        Idct8<T> t;
+        t.run(dq[0 * 8 + c], dq[1 * 8 + c], dq[2 * 8 + c], dq[3 * 8 + c], dq[4 * 8 + c], dq[5 * 8 + c], dq[6 * 8 + c],
+              dq[7 * 8 + c]);
+        // (int) DESCALE(...): libjpeg stores the workspace as int (a 64-bit value truncates)
+        ws[0 * 8 + c] = (int32_t)descale<T>(t.t10 + t.o3, CB - P1);
+        ws[7 * 8 + c] = (int32_t)descale<T>(t.t10 - t.o3, CB - P1);
+        ws[1 * 8 + c] = (int32_t)descale<T>(t.t11 + t.o2, CB - P1);
+        ws[6 * 8 + c] = (int32_t)descale<T>(t.t11 - t.o2, CB - P1);
+        ws[2 * 8 + c] = (int32_t)descale<T>(t.t12 + t.o1, CB - P1);
+        ws[5 * 8 + c] = (int32_t)descale<T>(t.t12 - t.o1, CB - P1);
+        ws[3 * 8 + c] = (int32_t)descale<T>(t.t13 + t.o0, CB - P1);
+        ws[4 * 8 + c] = (int32_t)descale<T>(t.t13 - t.o0, CB - P1);
+    }
+}
+
+template <typename T>
+__host__ __device__ inline uint64_t idct_row(const int32_t* w) {
+    Idct8<T> t;
+    t.run(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7]);
+    constexpr int S = CB + P1 + 3;
+    // (int) DESCALE(...) & RANGE_MASK: the low 10 bits survive the truncation
+    const uint32_t o0 = idct_limit((int32_t)descale<T>(t.t10 + t.o3, S));
+    const uint32_t o7 = idct_limit((int32_t)descale<T>(t.t10 - t.o3, S));
+    const uint32_t o1 = idct_limit((int32_t)descale<T>(t.t11 + t.o2, S));
+    const uint32_t o6 = idct_limit((int32_t)descale<T>(t.t11 - t.o2, S));
+    const uint32_t o2 = idct_limit((int32_t)descale<T>(t.t12 + t.o1, S));
+    const uint32_t o5 = idct_limit((int32_t)descale<T>(t.t12 - t.o1, S));
+    const uint32_t o3 = idct_limit((int32_t)descale<T>(t.t13 + t.o0, S));
+    const uint32_t o4 = idct_limit((int32_t)descale<T>(t.t13 - t.o0, S));
+    return (uint64_t)(o0 | (o1 << 8) | (o2 << 16) | (o3 << 24)) | ((uint64_t)(o4 | (o5 << 8) | (o6 << 16) | (o7 << 24)) << 32);
+}
+
 // coef: 64 zig-zag-order int16, q: 64 zig-zag-order quantisers (both 16-byte aligned);
-// out: 8 rows of 8 samples (8-byte aligned rows, pitch `stride`)
+// out: 8 rows of 8 samples (8-byte aligned rows, pitch `stride`).  jidctint.c jpeg_idct_islow:
+// DEQUANTIZE in int (16 x 16 bits), both passes in JLONG, the workspace in int.
 __host__ __device__ inline void idct_islow(const int16_t* coef, const int16_t* q, uint8_t* out, int64_t stride) {
     struct V16 { uint32_t w[4]; };
     union Blk { V16 v[8]; int16_t s[64]; } cz, qz;
@@ -591,37 +730,27 @@ __host__ __device__ inline void idct_islow(const int16_t* coef, const int16_t* q
         cz.v[i] = ((const V16*)coef)[i];
         qz.v[i] = ((const V16*)q)[i];
     }
+    int32_t dq[64];
+    uint32_t m1 = 0;
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {   // natural order i = r * 8 + c
+        dq[i] = (int32_t)cz.s[kZz[i]] * qz.s[kZz[i]];
+        const uint32_t a = (uint32_t)(dq[i] < 0 ? -dq[i] : dq[i]);
+        m1 = a > m1 ? a : m1;
+    }
     int32_t ws[64];
+    if (m1 <= (uint32_t)kPass1Max) idct_pass1<int32_t>(dq, ws);
+    else idct_pass1<int64_t>(dq, ws);
+    uint32_t m2 = 0;
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {   // pass 1: columns
-        int32_t d[8];
-#pragma unroll
-        for (int r = 0; r < 8; ++r) d[r] = (int32_t)cz.s[kZz[r * 8 + c]] * qz.s[kZz[r * 8 + c]];
-        Idct8 t;
-        t.run(d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7]);
-        ws[0 * 8 + c] = descale(t.t10 + t.o3, CB - P1);
-        ws[7 * 8 + c] = descale(t.t10 - t.o3, CB - P1);
-        ws[1 * 8 + c] = descale(t.t11 + t.o2, CB - P1);
-        ws[6 * 8 + c] = descale(t.t11 - t.o2, CB - P1);
-        ws[2 * 8 + c] = descale(t.t12 + t.o1, CB - P1);
-        ws[5 * 8 + c] = descale(t.t12 - t.o1, CB - P1);
-        ws[3 * 8 + c] = descale(t.t13 + t.o0, CB - P1);
-        ws[4 * 8 + c] = descale(t.t13 - t.o0, CB - P1);
+    for (int i = 0; i < 64; ++i) {
+        const uint32_t a = ws[i] < 0 ? 0u - (uint32_t)ws[i] : (uint32_t)ws[i];
+        m2 = a > m2 ? a : m2;
     }
+    const bool narrow = m2 <= (uint32_t)kPass2Max;
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {   // pass 2: rows
-        const int32_t* w = ws + r * 8;
-        Idct8 t;
-        t.run(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7]);
-        constexpr int S = CB + P1 + 3;
-        const uint32_t o0 = idct_limit(descale(t.t10 + t.o3, S)), o7 = idct_limit(descale(t.t10 - t.o3, S));
-        const uint32_t o1 = idct_limit(descale(t.t11 + t.o2, S)), o6 = idct_limit(descale(t.t11 - t.o2, S));
-        const uint32_t o2 = idct_limit(descale(t.t12 + t.o1, S)), o5 = idct_limit(descale(t.t12 - t.o1, S));
-        const uint32_t o3 = idct_limit(descale(t.t13 + t.o0, S)), o4 = idct_limit(descale(t.t13 - t.o0, S));
-        const uint64_t row = (uint64_t)(o0 | (o1 << 8) | (o2 << 16) | (o3 << 24)) |
-                             ((uint64_t)(o4 | (o5 << 8) | (o6 << 16) | (o7 << 24)) << 32);
-        *(uint64_t*)(out + r * stride) = row;
-    }
+    for (int r = 0; r < 8; ++r)   // pass 2: rows
+        *(uint64_t*)(out + r * stride) = narrow ? idct_row<int32_t>(ws + r * 8) : idct_row<int64_t>(ws + r * 8);
 }
 
 // ---------------------------------------------------------------- upsampling + colour

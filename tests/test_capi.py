@@ -58,3 +58,21 @@ def test_tools_library_exports_variants_product_does_not():
     assert not [n for n in tools if hasattr(P, n)], "the product library must not export the A/B variants"
     missing = [n for n in tools + declared() if not hasattr(T, n)]
     assert not missing, missing
+
+
+@pytest.mark.parametrize("src,define", [("gemm.hip", "-DGEMM_VAR_NOSTORE=1"), ("gemm.hip", "-DGEMM_VAR_FB2=0"),
+                                        ("backend.hip", "-DDM2_BK_=32"), ("backend.hip", "-DRS_STATS")])
+def test_variant_macros_refused_outside_tools_builds(src, define):
+    """The A/B timing hooks (some compile kernels with wrong results by design) are an #error
+    unless the tools define is set, so no variant can be built into libreidmi.so."""
+    import shutil
+    import subprocess
+    from multimodal_reid_amd import build_lib as B
+    if not shutil.which(B.HIPCC):
+        pytest.skip("hipcc not available")
+    base = [B.HIPCC, "-E", "-x", "hip", "--offload-arch=gfx950", "--cuda-device-only", f"-I{B.CSRC}",
+            f"-I{B.INCLUDE}", os.path.join(B.CSRC, src), "-o", os.devnull]
+    bad = subprocess.run(base + [define], capture_output=True, text=True)
+    assert bad.returncode != 0 and "REIDMI_TOOLS" in bad.stderr
+    ok = subprocess.run(base + [define, B.TOOLS_DEFINE], capture_output=True, text=True)
+    assert ok.returncode == 0, ok.stderr[-2000:]

@@ -214,6 +214,68 @@ def marker_tail_cases(n=240, seed=5):
         out.append((f"m{k}:{b[len(body):][:24].hex()}", b))
     return out
 
+def _mutations(files, n, seed):
+    """Random damage of whole files: cuts anywhere, bit flips, overwritten byte runs, inserted
+    0xFF / marker bytes."""
+    r = np.random.default_rng(seed)
+    out = []
+    for k in range(n):
+        b = bytearray(files[k % len(files)])
+        kind = k % 4
+        if kind == 0:
+            b = b[:int(r.integers(1, len(b)))]
+        elif kind == 1:
+            for _ in range(int(r.integers(1, 8))):
+                i = int(r.integers(0, len(b)))
+                b[i] ^= 1 << int(r.integers(0, 8))
+        elif kind == 2:
+            i = int(r.integers(0, len(b)))
+            m = int(r.integers(1, 16))
+            b[i:i + m] = bytes(r.integers(0, 256, m, dtype=np.uint8))
+        else:
+            i = int(r.integers(2, len(b)))
+            b[i:i] = bytes([0xFF, int(r.choice([0x00, 0xD0, 0xD8, 0xD9, 0xDA, 0xC4, 0xDB, 0xDD, 0xFE, 0xFF]))])
+        out.append(bytes(b))
+    return out
+
+
+def damaged_cases(n=400, seed=7):
+    """Damaged files: random cuts, bit flips, overwritten runs and inserted 0xFF / marker bytes
+    (headers and scans alike) of 4:2:0, restart-interval and 4:2:2 files."""
+    seeds = syn.jpeg_files(6, 128, 64, seed=61) + syn.jpeg_files(2, 77, 45, seed=62, restart_marker_rows=1) + \
+        syn.jpeg_files(2, 37, 29, seed=63, subsampling=1)
+    return _mutations(seeds, n, seed)
+
+
+_PIL_C_PATH = """
+import io, sys, numpy as np
+from PIL import Image
+d = np.load(sys.argv[1], allow_pickle=False)
+out = {}
+for k in range(int(d["n"])):
+    try:
+        out[f"i{k}"] = np.asarray(Image.open(io.BytesIO(d[f"f{k}"].tobytes())).convert("RGB"))
+    except Exception:
+        pass
+np.savez(sys.argv[2], **out)
+"""
+
+
+def pillow_c_path(files, tmp_path):
+    """Pillow's decode of each file (None where it raises) with libjpeg-turbo's SIMD off
+    (JSIMD_FORCENONE=1, a fresh process): libjpeg's C islow IDCT.  Pillow's default SIMD islow
+    works in 16-bit lanes and differs from the C definition only for coefficients far outside
+    any encoder's range (damaged data); on valid files the two are bit-identical."""
+    import subprocess
+    import sys
+    src, dst = tmp_path / "files.npz", tmp_path / "pil.npz"
+    np.savez(src, n=len(files), **{f"f{k}": np.frombuffer(b, np.uint8) for k, b in enumerate(files)})
+    import os
+    subprocess.run([sys.executable, "-c", _PIL_C_PATH, str(src), str(dst)], check=True,
+                   env=dict(os.environ, JSIMD_FORCENONE="1"))
+    d = np.load(dst, allow_pickle=False)
+    return [d[f"i{k}"] if f"i{k}" in d.files else None for k in range(len(files))]
+
 
 def test_plan_pools_tables_and_reads_paths(tmp_path):
     files = syn.jpeg_files(20, 128, 64, seed=2)   # one encoder setting: one set of tables
@@ -287,6 +349,31 @@ def test_core_arithmetic_on_host_vs_pillow(tmp_path):
            if not np.array_equal(out[jb.meta[i, 0]:jb.meta[i, 0] + jb.meta[i, 1] * jb.meta[i, 2] * 3]
                                  .reshape(jb.meta[i, 1], jb.meta[i, 2], 3), pil_rgb(b))]
     assert not bad, bad
+    # damaged files (headers and scans): the same files load, with libjpeg's C-path pixels
+    dm = damaged_cases()
+    jd = data_prepare.JpegBatch(dm)
+    dout = np.zeros(max(jd.out_bytes, 1), np.uint8)
+    derr = np.zeros(jd.B, np.int32)
+    host.jpeg_host_decode(jd.buf.ctypes.data_as(vp), jd.plan.ctypes.data_as(vp), jd.info.ctypes.data_as(vp),
+                          dout.ctypes.data_as(vp), derr.ctypes.data_as(vp))
+    _check_damaged(dm, np.where(jd.status != 0, jd.status, derr), jd.meta, dout, pillow_c_path(dm, tmp_path))
+
+
+def _check_damaged(files, status, meta, pix, ref):
+    """status 0 exactly where Pillow returns an image (J_LAYOUT aside: sampling layouts the
+    device does not decode raise too), and then Pillow's C-path pixels."""
+    bad = []
+    for k, b in enumerate(files):
+        if status[k] == 3:
+            continue
+        if (status[k] == 0) != (ref[k] is not None):
+            bad.append((k, int(status[k]), ref[k] is not None))
+        elif status[k] == 0:
+            off, h, w = meta[k]
+            if not np.array_equal(pix[off:off + h * w * 3].reshape(h, w, 3), ref[k]):
+                bad.append((k, "pixels"))
+    assert not bad, bad
+    assert 100 < int((status == 0).sum()) and ((status == 5).any() or (status == 6).any())
 
 
 # ------------------------------------------------------------------ GPU: device decode vs Pillow
@@ -348,6 +435,17 @@ def test_decode_rejects_unsupported_and_reports_bad_data(gpu):
     torch.cuda.synchronize()
     got = pix.cpu().numpy()[:64 * 32 * 3].reshape(64, 32, 3)
     assert np.array_equal(got, pil_rgb(good[0]))
+
+
+@pytest.mark.gpu
+def test_decode_damaged_files_vs_pillow(gpu, tmp_path):
+    """The device decode of damaged files (cuts, bit flips, overwritten runs, inserted markers in
+    headers and scans): an image exactly where Pillow returns one, with libjpeg's C-path pixels."""
+    dm = damaged_cases(400, 8)
+    pix, _, jb, err = data_prepare.decode_jpeg(dm, check=False, return_status=True)
+    torch.cuda.synchronize()
+    st = np.where(jb.status != 0, jb.status, err.cpu().numpy()[:len(dm)])
+    _check_damaged(dm, st, jb.meta, pix.cpu().numpy(), pillow_c_path(dm, tmp_path))
 
 
 @pytest.mark.gpu

@@ -1,5 +1,6 @@
 """Build an A/B variant of libreidmi.so: one source recompiled with extra -D flags, linked
-with the in-tree objects of the others -> tools/variants/libreidmi_<name>.so.
+with the in-tree objects of the others -> tools/variants/libreidmi_<name>.so.  The source is
+compiled with -DREIDMI_TOOLS (the variant macros are an #error without it).
 
     python tools/build_variant.py NAME SOURCE.hip -DFOO=1 [-DBAR=2 ...]"""
 import os
@@ -17,7 +18,8 @@ def main():
     out_dir = os.path.join(ROOT, "tools", "variants")
     os.makedirs(out_dir, exist_ok=True)
     obj = os.path.join(out_dir, f"{name}_{src.replace('.hip', '.o')}")
-    r = subprocess.run([B.HIPCC, *B.FLAGS, *defs, "-c", os.path.join(B.CSRC, src), "-o", obj],
+    # -DREIDMI_TOOLS: the variant macros are refused without it (gemm.hip / backend.hip #error)
+    r = subprocess.run([B.HIPCC, *B.FLAGS, B.TOOLS_DEFINE, *defs, "-c", os.path.join(B.CSRC, src), "-o", obj],
                        capture_output=True, text=True)
     if r.returncode:
         sys.exit(r.stderr[-4000:])
