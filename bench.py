@@ -20,7 +20,7 @@ zero-shot classifier's text side at Market size (750 x 56 token rows, TF/s); "ba
 "preprocess" = retrieval-kernel and transform rooflines; "jpeg" = the loaders' JPEG decode of
 a Market split of files on the device (and + transform), Pillow timed beside it; "cpu_baseline".
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B (default 4096)] [--backend nccl|gloo]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B (default 20480)] [--backend nccl|gloo]
                     [--no-cpu-baseline] [--no-rerank] [--no-msmt17] [--no-text] [--no-jpeg]
 
 `--gpus N` under torchrun (WORLD_SIZE set) must equal the world size; without torchrun,
@@ -169,25 +169,36 @@ class Workload:
         else:
             self.q_img = _crops(self.qlo, self.qhi, 1000, dev)
             self.g_img = _crops(self.glo, self.ghi, 2000, dev)
-        self.q_tta = torch.from_numpy(syn.tta_offsets(self.qhi - self.qlo, seed=1, offset=self.qlo)).to(dev)
-        self.g_tta = torch.from_numpy(syn.tta_offsets(self.ghi - self.glo, seed=2, offset=self.glo)).to(dev)
+        # one image stream per rank: its query shard then its gallery shard (views of one tensor),
+        # embedded in balanced encoder calls of at most `batch` images (one call per pass at
+        # Market size: fewer, larger persistent GEMM launches; profiles/r05/bench_batch*.json)
+        nq = self.qhi - self.qlo
+        self.img = torch.cat([self.q_img, self.g_img])
+        self.q_img, self.g_img = self.img[:nq], self.img[nq:]
+        self.tta = torch.cat([torch.from_numpy(syn.tta_offsets(nq, seed=1, offset=self.qlo)),
+                              torch.from_numpy(syn.tta_offsets(self.ghi - self.glo, seed=2, offset=self.glo))]).to(dev)
+        self.q_tta, self.g_tta = self.tta[:nq], self.tta[nq:]
         D = self.model.width + self.model.out_dim
-        self.q_emb = torch.empty(self.qhi - self.qlo, D, device=dev)
-        self.g_emb = torch.empty(self.ghi - self.glo, D, device=dev)
+        self.emb = torch.empty(self.img.shape[0], D, device=dev)
+        self.q_emb, self.g_emb = self.emb[:nq], self.emb[nq:]
+        n = self.img.shape[0]
+        nb = max(1, -(-n // batch))
+        self.bounds = [n * i // nb for i in range(nb + 1)]
+        self.max_call = max((b - a for a, b in zip(self.bounds, self.bounds[1:])), default=0)
         self.dist = torch.empty(self.qhi - self.qlo, self.G, device=dev)
         # encoder batches alternate over `streams` HIP streams: one batch's kernels fill the CUs a
         # neighbour's leave idle (the last partial round of tiles of each persistent GEMM launch,
         # the short LayerNorm / attention launches, launch gaps); each stream has its workspace
         self.streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(streams - 1)]
 
-    def embed(self, imgs, tta, out):
+    def embed(self):
+        """Both TTA passes of every image of this rank (queries then gallery)."""
         main = torch.cuda.current_stream(self.dev)
         for st in self.streams[1:]:
             st.wait_stream(main)
-        for i, s in enumerate(range(0, imgs.shape[0], self.batch)):
-            e = min(s + self.batch, imgs.shape[0])
+        for i, (s, e) in enumerate(zip(self.bounds, self.bounds[1:])):
             with torch.cuda.stream(self.streams[i % len(self.streams)]):
-                zsl.embed_pair(self.model, imgs[s:e], tta=tta[s:e], out=out[s:e])
+                zsl.embed_pair(self.model, self.img[s:e], tta=self.tta[s:e], out=self.emb[s:e])
         for st in self.streams[1:]:
             main.wait_stream(st)
 
@@ -196,8 +207,7 @@ class Workload:
         all-gather of the normalised gallery blocks (RCCL under nccl) is timed on its own: it
         includes waiting for the slowest rank, so its minimum over ranks is the collective."""
         t0 = time.perf_counter()
-        self.embed(self.q_img, self.q_tta, self.q_emb)
-        self.embed(self.g_img, self.g_tta, self.g_emb)
+        self.embed()
         qn = evaluate.l2_normalize_device(self.q_emb)
         gl = evaluate.l2_normalize_device(self.g_emb)
         torch.cuda.synchronize()
@@ -259,8 +269,7 @@ def msmt17_leg(model, dev, rank, world, batch, dataset="msmt17"):
 
     sync()
     t0 = time.perf_counter()
-    wl.embed(wl.q_img, wl.q_tta, wl.q_emb)
-    wl.embed(wl.g_img, wl.g_tta, wl.g_emb)
+    wl.embed()
     qn = gather_rows(evaluate.l2_normalize_device(wl.q_emb), Q)
     gn = gather_rows(evaluate.l2_normalize_device(wl.g_emb), G)
     sync()
@@ -702,9 +711,10 @@ def _parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    # 4096 crops per encoder call (M = 864 256 token rows per GEMM): fewer launches and a
-    # smaller partial last round of tiles per launch than 1024 (+1.5-2 %, profiles/r03/bench_batch_ab.txt)
-    ap.add_argument("--batch", type=int, default=4096)
+    # at most this many crops per encoder call, in balanced calls over the rank's query + gallery
+    # stream: 19 281 (M = 4 068 291 token rows per GEMM) at Market size on one GPU.  Fewer,
+    # larger launches: 4096 -> 8192 -> 16384 +0.6 % / +0.5 % (profiles/r05/bench_batch*.json)
+    ap.add_argument("--batch", type=int, default=20480)
     ap.add_argument("--streams", type=int, default=1)
     # nccl = RCCL over xGMI, one GPU per rank; gloo = host collectives, ranks may share a GPU
     # (LOCAL_RANK modulo the visible devices): the multi-rank test on a one-GPU box
@@ -760,10 +770,10 @@ def main():
     elapsed = time.perf_counter() - t0
     import ctypes
     ms, cnt, fl = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
-    # full-batch c_fc launches only (the splits' partial last batches and the CLS-only last
-    # block's small c_fc are left out), so flops_per_launch / avg_launch_ms is the rate of the
-    # M = batch * 211 launch the PMC traffic below was measured on
-    full = 2.0 * a.batch * 211 * 3072 * 768
+    # the largest c_fc launches only (balanced calls differ by at most one image; the CLS-only
+    # last block's small c_fc is left out), so flops_per_launch / avg_launch_ms is the rate of the
+    # M = 211 * max_call launch the PMC traffic below was measured on
+    full = 2.0 * (wl.max_call - 1) * 211 * 3072 * 768
     L.reidmi_prof_collect_min(EPI_GELU, ctypes.c_double(full), ctypes.byref(ms), ctypes.byref(cnt),
                               ctypes.byref(fl))
     L.reidmi_prof_enable(0)
@@ -790,7 +800,8 @@ def main():
             "config": {"workload": "Market-1501 full eval: 3368q x 15913g, ViT-B/16 stride-12 (211 tokens), "
                                    "2 passes/img (plain + flip/pad/crop TTA), exact-fp32 distmat, CMC/mAP",
                        "images_per_step": wl.Q + wl.G, "encoder_passes_per_step": 2 * (wl.Q + wl.G),
-                       "batch": a.batch, "parallelism": f"dp{world} (image shards + all-gather)",
+                       "batch": a.batch, "images_per_encoder_call": wl.max_call,
+                       "parallelism": f"dp{world} (image shards + all-gather)",
                        "backend": a.backend if world > 1 else None},
             "eval_wall_s": round(eval_s / a.steps, 4),
             "embed_wall_s": round(embed_s / a.steps, 4),
@@ -799,7 +810,7 @@ def main():
             "roofline": {"bound": "mfma", "kernel": "gemm_persistent_kernel<1, 0> (ln_2-folded fp16 mlp.c_fc + QuickGELU)",
                          "achieved": round(achieved, 1) if achieved else None, "peak": PEAK_F16_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_F16_TFLOPS, 4) if achieved else None,
-                         "traffic": C_FC_TRAFFIC_BYTES.get(a.batch), "traffic_unit": "bytes/launch (PMC)", "avg_launch_ms": round(avg_ms, 4), "launches": cnt.value,
+                         "traffic": C_FC_TRAFFIC_BYTES.get(wl.max_call), "traffic_unit": "bytes/launch (PMC)", "avg_launch_ms": round(avg_ms, 4), "launches": cnt.value,
                          "flops_per_launch": fl.value / max(cnt.value, 1)},
         }
         if world > 1:

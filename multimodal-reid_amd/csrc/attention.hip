@@ -63,8 +63,9 @@ __device__ __forceinline__ uint32_t mul_pk_h(float a, float b, float inv) {
 //     keys kb*32 + (r&3) + 8(r>>2) + 4h in s[kb][r];
 //   P stays in registers: registers 8s'..8s'+7 of block kb are the B fragment of key-step s'
 //     of O^T = V^T P^T (accumulator-as-operand), V^T read with the same key permutation;
-//   O^T[d][q] comes out as 4 runs of 4 consecutive d per lane -> 8 8-byte stores (the wave's
-//     only vector-memory ops here; lanes with qi >= L store nothing).
+//   O^T[d][q] comes out as 4 runs of 4 consecutive d per lane -> kAttnStores 8-byte stores (the
+//     wave's only vector-memory ops here; lanes with qi >= L store nothing).
+constexpr int kAttnStores = 8;  // (2 d blocks x 4 runs; the callers' counted waits use it)
 template <int NKB, bool CAUSAL>
 __device__ __forceinline__ void attn_block(const _Float16* sK, const _Float16* sV, int vstride, const f16x8 (&qf)[4],
                                            int qi, int L, int64_t bh, int H, _Float16* __restrict__ o,
@@ -133,6 +134,7 @@ __device__ __forceinline__ void attn_block(const _Float16* sK, const _Float16* s
     if (qi < L) {
         const int64_t b = bh / H, hd = bh % H;
         _Float16* orow = o + (b * L + qi) * (int64_t)(H * 64) + hd * 64;
+        static_assert(2 * 4 == kAttnStores, "one store per (d block, run)");
 #pragma unroll
         for (int db = 0; db < 2; db++)
 #pragma unroll
@@ -459,10 +461,17 @@ __global__ __launch_bounds__(512) void mhsa_kernel(const _Float16* __restrict__ 
     int64_t bh = blockIdx.x;
     if (bh >= nbh) return;
     if constexpr (NS == 3) {
-        // Every wave issues LP/8/nw = 4 K pieces and 4 V^T pieces per head, wave 0 one more
-        // (the blob's half last piece): nw == NKB waves, V^T blob = 4 NKB + 1/2 KiB (launcher
-        // checks vstride == LP + 4).  The counted waits below rely on these counts and on the
-        // 8 O stores of attn_block.
+        // The counted waits below are derived from the per-wave vector-memory ops of a head
+        // (ADVICE r4): with nw == NKB waves and V^T rows of LP + 4 (both checked by the
+        // launcher) every wave issues kRingK K pieces and kRingV V^T pieces per head, wave 0 one
+        // more (the blob's half last piece); attn_block issues kAttnStores O stores and load_q 4
+        // loads.  Each is one instruction (1-KiB LDS-DMA pieces, 8-byte stores: nothing to merge
+        // or split), and the kernels use no scratch (tests/test_capi.py checks the ISA).
+        constexpr int kRingK = LP / 8 / NKB, kRingV = 4;
+        static_assert(kRingK == 4, "K: 4 one-KiB pieces per wave and head");
+        static_assert((64 * (LP + 4) * 2 + 1023) / 1024 == kRingV * NKB + 1, "V^T: 4 pieces per wave + wave 0's half");
+        constexpr int kIssue = kRingK + kRingV;        // one head's K / V^T pieces, waves 1..
+        constexpr int kIssue0 = kIssue + 1;            // wave 0
         const int64_t G = gridDim.x;
         issue(bh, 0);
         f16x8 qf[4];
@@ -473,9 +482,9 @@ __global__ __launch_bounds__(512) void mhsa_kernel(const _Float16* __restrict__ 
         if (!second)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         else if (wid == 0)
-            asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kIssue0) : "memory");
         else
-            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kIssue) : "memory");
         pin(qf);
         __builtin_amdgcn_s_barrier();
         zero_pad(0);
@@ -495,11 +504,11 @@ __global__ __launch_bounds__(512) void mhsa_kernel(const _Float16* __restrict__ 
             if (wid * 32 >= L)
                 asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
             else if (nxt2 >= nbh)
-                asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+                asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(kAttnStores) : "memory");
             else if (wid == 0)
-                asm volatile("s_waitcnt vmcnt(17) lgkmcnt(0)" ::: "memory");
+                asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(kIssue0 + kAttnStores) : "memory");
             else
-                asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)" ::: "memory");
+                asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(kIssue + kAttnStores) : "memory");
             __builtin_amdgcn_s_barrier();
             const int nstage = stage == 2 ? 0 : stage + 1;
             if (nxt < nbh) {
@@ -540,7 +549,7 @@ __global__ __launch_bounds__(512) void mhsa_kernel(const _Float16* __restrict__ 
         // stores) and drain them anyway.  LDS-DMA data is ordered for other waves' ds_reads
         // by each issuing wave's vmcnt + this barrier; zero_pad's ds_writes by lgkmcnt(0).
         if (wid * 32 < L)
-            asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(kAttnStores) : "memory");
         else
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
@@ -1056,7 +1065,7 @@ static int launch_mhsa(const void* q, const void* k, const void* vt, void* o, in
     if constexpr (!CAUSAL && ATTN_PIPE) {
         RM_REQUIRE(lpad_g == vt_stride(NKB * 32), "mhsa: v^T row stride must be reidmi_attn_lpad(L)");
         return launch_mhsa_pipe<NKB>(q, k, vt, o, nseq, L, H, s);
-    }
+    } else {  // (discarded for the pipelined shapes: mhsa_kernel<NKB, false> is not instantiated)
     constexpr int LP = NKB * 32;
     // three LDS stages for the short causal (text) shapes (mhsa_kernel NS), two otherwise
     constexpr int NS = CAUSAL && NKB <= 4 ? ATTN_TEXT_STAGES : 2;
@@ -1091,6 +1100,7 @@ static int launch_mhsa(const void* q, const void* k, const void* vt, void* o, in
                        scale_log2);
     RM_LAUNCHED();
     return OK;
+    }
 }
 
 // CLS query only (the last block of the inference path): one wave per (sequence, head).

@@ -46,7 +46,7 @@ def test_rank_envs():
 
 def test_parse_defaults_single_gpu():
     a = bench._parse([])
-    assert a.gpus == 1 and a.backend == "nccl" and a.batch == 4096
+    assert a.gpus == 1 and a.backend == "nccl" and a.batch == 20480
 
 
 def _child(tmp_path):

@@ -76,3 +76,38 @@ def test_variant_macros_refused_outside_tools_builds(src, define):
     assert bad.returncode != 0 and "REIDMI_TOOLS" in bad.stderr
     ok = subprocess.run(base + [define, B.TOOLS_DEFINE], capture_output=True, text=True)
     assert ok.returncode == 0, ok.stderr[-2000:]
+
+
+# the encoder's GEMM instances (EPI 0-6).  The re-rank pre-filter's EPI_RRHI / EPI_RRSV (7, 8)
+# spill 20 bytes per lane in the tile prologue, where each reload is followed by the compiler's
+# own vmcnt(0) (an over-wait: safe; their K-loops keep the plain vmcnt(6), no deferred stores)
+_GEMM_ENCODER = tuple(f"gemm_persistent_kernelILi{e}E" for e in range(7))
+
+
+@pytest.mark.parametrize("src,kernels", [("attention.hip", ("mhsa_kernel", "mhsa_pipe_kernel")),
+                                         ("gemm.hip", _GEMM_ENCODER)])
+def test_counted_wait_kernels_use_no_scratch(src, kernels):
+    """The kernels whose `s_waitcnt vmcnt(N)` counts are derived from their own vector-memory
+    instructions (attention's K/V^T rings, the GEMM's deferred epilogue stores) must not spill:
+    a scratch load or store would enter the same counter and let a wait return early.
+    Checked on the compiler's resource report of the product build flags."""
+    import shutil
+    import subprocess
+    from multimodal_reid_amd import build_lib as B
+    if not shutil.which(B.HIPCC):
+        pytest.skip("hipcc not available")
+    flags = [f for f in B.FLAGS if f not in ("-fPIC", "-fno-gpu-rdc")]
+    r = subprocess.run([B.HIPCC, *flags, "--cuda-device-only", "-c", "-Rpass-analysis=kernel-resource-usage",
+                        os.path.join(B.CSRC, src), "-o", os.devnull], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    name, seen = None, 0
+    for line in r.stderr.splitlines():
+        m = re.search(r"Function Name: (\S+)", line)
+        if m:
+            name = m.group(1)
+            continue
+        m = re.search(r"ScratchSize \[bytes/lane\]: (\d+)", line)
+        if m and name and any(k in name for k in kernels):
+            seen += 1
+            assert int(m.group(1)) == 0, f"{name} spills to scratch ({m.group(1)} bytes/lane)"
+    assert seen >= 3, r.stderr[-2000:]

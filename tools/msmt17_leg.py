@@ -18,8 +18,7 @@ torch.cuda.set_device(0)
 model = VisionTransformer(syn.vit_state_dict("ViT-B/16", seed=0), device=dev)
 print(json.dumps(bench.msmt17_leg(model, dev, 0, 1, 1024)), flush=True)
 wl = bench.Workload(dev, 0, 1, 1024, dataset="msmt17", model=model)
-wl.embed(wl.q_img, wl.q_tta, wl.q_emb)
-wl.embed(wl.g_img, wl.g_tta, wl.g_emb)
+wl.embed()
 qn, gn = evaluate.l2_normalize_device(wl.q_emb), evaluate.l2_normalize_device(wl.g_emb)
 ref = None
 for r in range(2):
