@@ -60,7 +60,11 @@ EPI_GELU = 1  # the c_fc GEMM (+QuickGELU epilogue): the largest single kernel p
 #     A 332 MB + W 4.7 MB + out 1 327 MB = 1.66 GB
 #   batch 4096 (profiles/r04/final/pmc_c_fc_b4096_*, mean of 6 launches; r03: 3 142 462 /
 #     5 185 615): 2 998 177 / 5 185 700 KiB; algorithmic A 1 327 MB + W 4.7 MB + out 5 310 MB = 6.64 GB
-C_FC_TRAFFIC_BYTES = {1024: (2 * 736400 + 1296384) * 1024, 4096: (2 * 2998177 + 5185700) * 1024}
+#   batch 19281, the one call per pass at Market size (profiles/r05/prof/pmc_c_fc_b19281_*, median
+#     of 6 launches): 13 840 234 / 24 410 478 KiB; algorithmic A 6 249 MB + W 4.7 MB + out 24 996 MB
+#     = 31.25 GB
+C_FC_TRAFFIC_BYTES = {1024: (2 * 736400 + 1296384) * 1024, 4096: (2 * 2998177 + 5185700) * 1024,
+                      19281: (2 * 13840234 + 24410478) * 1024}
 
 
 def _max_over_ranks(values, dev):

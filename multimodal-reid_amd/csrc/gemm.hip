@@ -176,8 +176,9 @@ __device__ __forceinline__ void resid_rows_load(const EpiArgs& ea, int64_t mrow,
     }
 }
 
-// PRE: the residual rows were read by resid_rows_load into *xpre (EPI_RESID_F16 only)
-template <int EPI, int NI, bool BIAS_DONE = false, bool PRE = false>
+// PRE: the residual rows were read by resid_rows_load into *xpre (EPI_RESID_F16 only);
+// FULL: every row of the wave's block exists, so the fp16 path stores without per-row checks
+template <int EPI, int NI, bool BIAS_DONE = false, bool PRE = false, bool FULL = false>
 __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI][4], int64_t mrow, int ncol,
                                               int64_t M, int N, const f16x8 (*xpre)[2] = nullptr) {
     const int lane = threadIdx.x & 63;
@@ -480,7 +481,7 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
             const auto hi = __builtin_amdgcn_permlane16_swap(cvt_pk_f16(a[2], a[3]), cvt_pk_f16(c[2], c[3]), false, false);
             const uint4 v = make_uint4(lo[0], hi[0], lo[1], hi[1]);
             const int col = ncol + (2 * jp + (q & 1)) * 16 + (q >> 1) * 8;
-            if (m >= M) continue;
+            if (!FULL && m >= M) continue;
             if constexpr (EPI == EPI_QKV) {
                 const int hd = qkv_c0 + (col - ncol);  // h * 64 + d
                 *(uint4*)(qkrow + (int64_t)(hd >> 6) * ea.seq * 64 + (hd & 63)) = v;
@@ -1182,6 +1183,8 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
             rrsv_tile(ea, acc, m0 + wr * 128, n0 + wc * 64, M, seq, ea.rr_tri && tmt < tnt, rr_lds + (seq & 1) * 4096,
                       rr_lds + 8192 + (seq & 1) * 4096, sv_lds, sv_n, lane,
                       RrsvWalk{first, gx, wr, wc, rr_list});
+        else if (EPI == EPI_GELU_H16 && m0 + G2_M <= M)  // c_fc's full tiles: no row checks
+            epilogue_tile<EPI, 8, true, RPRE, true>(ea, acc, m0 + wr * 128, n0 + wc * 64, M, N, xres);
         else
             epilogue_tile<EPI, 8, true, RPRE>(ea, acc, m0 + wr * 128, n0 + wc * 64, M, N, xres);
         seq++;
