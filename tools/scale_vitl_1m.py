@@ -9,9 +9,15 @@ Legs (each timed on its own, wall seconds max over ranks):
           D_feat = 1024 + 768 = 1792, each rank its query shard against the whole gallery
   rerank  k-reciprocal re-rank (k1=50, k2=15, lambda=0.3) over N = Q + G, row-sharded
           staged path (reranking.re_ranking_sharded) + CMC/mAP
+  embed_full (--embed-full) every one of the Q + G images embedded (not a sample): crops
+          generated on the device block by block (seeded per block, never all resident), both
+          passes, features written into the gallery / query matrices; then L2-normalise, the
+          exact distance and CMC/mAP on THOSE features (eval_embedded).  The random network's
+          embeddings carry no identity signal (mAP at chance); the leg times the whole
+          configs[4] job end to end instead of projecting the embed from a sample.
 
     python tools/scale_vitl_1m.py [--gallery 1000000] [--query 10000] [--embed-sample 4096]
-                                  [--no-rerank] [--no-embed]
+                                  [--no-rerank] [--no-embed] [--embed-full] [--batch 256]
 """
 import argparse
 import json
@@ -94,6 +100,43 @@ def embed_leg(dev, rank, world, n, batch, G):
             "frac_of_fp16_peak": round(tf / (2500.0 * world), 4), "projected_gallery_embed_s": round(G / rate, 1)}
 
 
+def embed_full_leg(dev, rank, world, Q, G, batch, block=8192):
+    """Embed this rank's shard of the Q + G images (both passes) -> (record, fp32 features of
+    the shard [n, 1792]).  Progress on stderr every block (a 1M job runs for minutes)."""
+    sd = syn.vit_state_dict("ViT-L/14", seed=0, layers=12)
+    m = VisionTransformer(sd, device=dev)
+    lo, hi = rd.shard(Q + G, rank, world)
+    n = hi - lo
+    feat = torch.empty((n, m.width + m.out_dim), device=dev)
+    gen = torch.Generator(device=dev)
+    imgs = torch.empty((block, 3, 256, 128), device=dev, dtype=torch.float16)
+    sync(world)
+    t = time.perf_counter()
+    for b0 in range(0, n, block):
+        b1 = min(b0 + block, n)
+        gen.manual_seed(1_000_003 * (lo + b0) + 17)  # seeded by global image index: any world size
+        x = imgs[:b1 - b0]
+        x.copy_(torch.rand((b1 - b0, 3, 256, 128), generator=gen, device=dev) * 2 - 1)
+        tta = torch.stack([torch.randint(0, 11, (b1 - b0,), generator=gen, device=dev),
+                           torch.randint(0, 21, (b1 - b0,), generator=gen, device=dev)], 1).to(torch.int32)
+        for s in range(0, b1 - b0, batch):
+            e = min(s + batch, b1 - b0)
+            zsl.embed_pair(m, x[s:e], tta=tta[s:e], out=feat[b0 + s:b0 + e])
+        if rank == 0 and (b0 // block) % 8 == 0:
+            torch.cuda.synchronize()
+            print(f"embed_full: {b1}/{n} images of rank 0's shard, {time.perf_counter() - t:.1f} s",
+                  file=sys.stderr, flush=True)
+    sync(world)
+    te = tmax(time.perf_counter() - t, dev, world)
+    rate = (Q + G) / te
+    tf = rate * 2 * VITL_GFLOP_PER_PASS / 1e3
+    rec = {"images": Q + G, "wall_s": round(te, 2), "imgs_per_s": round(rate, 1), "TFLOPs": round(tf, 1),
+           "frac_of_fp16_peak": round(tf / (2500.0 * world), 4), "batch": batch,
+           "finite": bool(torch.isfinite(feat).all().item())}
+    del m, imgs
+    return rec, feat
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gallery", type=int, default=1000000)
@@ -103,6 +146,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--no-rerank", action="store_true")
     ap.add_argument("--no-embed", action="store_true")
+    ap.add_argument("--embed-full", action="store_true")
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -118,6 +162,22 @@ def main():
         torch.cuda.empty_cache()
 
     qp, gp, qc, gc = syn.labels(Q, G, a.ids, 8, seed=0, distractor_frac=0.1, junk_frac=0.0)
+    if a.embed_full:
+        rec, f = embed_full_leg(dev, rank, world, Q, G, a.batch)
+        torch.cuda.empty_cache()
+        sync(world)
+        t = time.perf_counter()
+        f = rd.gather_rows(evaluate.l2_normalize_device(f), Q + G)  # images are [queries | gallery]
+        qlo, qhi = rd.shard(Q, rank, world)
+        d = evaluate.euclidean_distance_device(f[qlo:qhi], f[Q:])
+        cmc, mAP = cmc_map(d, qp[qlo:qhi], gp, qc[qlo:qhi], gc, Q, G)
+        sync(world)
+        tv = tmax(time.perf_counter() - t, dev, world)
+        out["embed_full"] = rec
+        out["eval_embedded"] = {"wall_s": round(tv, 3), "mAP": round(float(mAP), 6), "rank1": round(float(cmc[0]), 6),
+                                "end_to_end_s": round(rec["wall_s"] + tv, 2)}
+        del d, f
+        torch.cuda.empty_cache()
     feats = clustered_features(np.concatenate([qp, gp]), a.ids, D, dev, seed=11)
     qn, gn = feats[:Q], feats[Q:]
     qlo, qhi = rd.shard(Q, rank, world)
