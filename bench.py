@@ -280,6 +280,12 @@ def msmt17_leg(model, dev, rank, world, batch, dataset="msmt17"):
     t1 = time.perf_counter()
     evaluate.euclidean_distance_device(qn[wl.qlo:wl.qhi], gn, out=wl.dist)
     cmc, mAP = rows_to_map(wl.dist)
+    # The re-rank kernels' first launches in a process load their code (~0.1 s, once, whatever
+    # the size: profiles/r05/rr_first_call.txt); a small re-rank takes that before the timed
+    # call, as the Market steps' warm-up does for the encoder, and its time is reported
+    sync()
+    tw = time.perf_counter()
+    reranking.re_ranking_sharded(qn[:256], gn[:2048], 50, 15, 0.3)
     sync()
     t2 = time.perf_counter()
     stats = {}
@@ -301,16 +307,19 @@ def msmt17_leg(model, dev, rank, world, batch, dataset="msmt17"):
     cmc8, mAP8 = rows_to_map(final)
     sync()
     t5 = time.perf_counter()
-    te, tv, tr, t8 = _max_over_ranks([t1 - t0, t2 - t1, t3 - t2, t5 - t4], dev)
+    te, tv, tr, t8, twu = _max_over_ranks([t1 - t0, tw - t1, t3 - t2, t5 - t4, t2 - tw], dev)
     N, D = Q + G, qs.shape[1]
     wl_D = wl.model.width + wl.model.out_dim
     tri_e = N * N * wl_D
-    fl_e = 2.0 * tri_e / (PEAK_F16_TFLOPS * 1e12)
+    # floors: the R2 pre-filter's product at the fp16 peak, plus the blend's exact fp32 Q x G
+    # distances (original_dist, reranking.py:97-99) at the fp32 matrix peak
+    fl_e = 2.0 * tri_e / (PEAK_F16_TFLOPS * 1e12) + 2.0 * Q * G * wl_D / (PEAK_F32_MATRIX_TFLOPS * 1e12)
     del wl, final, qs, gs
     torch.cuda.empty_cache()
     tri = N * N * D  # the R2 pre-filter's fp16 product over the upper triangle (2 N^2 D / 2)
     embed_flop = 2 * N * 37.90e9
-    fl, hb = 2.0 * tri / (PEAK_F16_TFLOPS * 1e12), 8.0 * Q * G / (PEAK_HBM_GBPS * 1e9)
+    fl = 2.0 * tri / (PEAK_F16_TFLOPS * 1e12) + 2.0 * Q * G * D / (PEAK_F32_MATRIX_TFLOPS * 1e12)
+    hb = 8.0 * Q * G / (PEAK_HBM_GBPS * 1e9)
     return {"config": f"MSMT17 {Q}q x {G}g, identity-structured crops (3060 ids, 15 cams, noise 0.3), ViT-B/16 "
                       f"(synthetic, residual gain {MSMT17_RESID_GAIN if model_own else 'caller'}) 2 passes/img, "
                       f"{world} GPU(s): sharded embed + all-gather, exact distmat + CMC/mAP, sharded k-reciprocal "
@@ -319,21 +328,27 @@ def msmt17_leg(model, dev, rank, world, batch, dataset="msmt17"):
             # end to end = this run's own embedded features through embed, eval and re-rank + eval
             # (ADVICE r4); the Gaussian-feature re-rank below is a separate reference number
             "rerank_eval_wall_s": round(tr, 4), "end_to_end_wall_s": round(te + tv + tr, 4),
+            "rerank_kernel_load_warmup_s": round(twu, 4),
             "mAP": float(mAP), "rank1": float(cmc[0]),
             "rerank": {"features": "SURVEY.md §8d identity-clustered Gaussians (D=1280, sigma 4) of this split: the "
                                    "fp16 pre-filter path", "wall_s": round(t8, 4), "mAP_rerank": float(mAP8),
                        "rank1_rerank": float(cmc8[0]), "r2_rows": stats8.get("rows"), "r2_exact_fallback_rows": stats8.get("exact_rows"),
                        "r2_form": stats8.get("form"),
-                       "roofline": {"bound": "mfma (R2 fp16 pre-filter, N^2 D upper-triangle product)",
-                                    "algorithmic_flop": 2.0 * tri, "flop_floor_s": round(fl, 5),
+                       "roofline": {"bound": "mfma (R2 fp16 pre-filter 2 N^2 D at the fp16 peak + the blend's exact "
+                                             "fp32 Q x G distances 2 Q G D at the fp32 matrix peak)",
+                                    "algorithmic_flop": 2.0 * tri, "blend_distance_flop": 2.0 * Q * G * D,
+                                    "flop_floor_s": round(fl, 5),
                                     "hbm_floor_s": round(hb, 5), "frac": round(max(fl, hb) / t8, 4)}},
             "rerank_embedded": {"features": f"the embedded crops (D={wl_D}; synthetic network, residual gain "
                                             f"{MSMT17_RESID_GAIN if model_own else 'caller'})", "wall_s": round(tr, 4),
                                 "mAP_rerank": float(mAP_rr), "rank1_rerank": float(cmc_rr[0]),
                                 "r2_rows": stats.get("rows"), "r2_exact_fallback_rows": stats.get("exact_rows"),
                                 "r2_form": stats.get("form"),
-                                "roofline": {"bound": "mfma (R2 fp16 pre-filter, N^2 D upper-triangle product)",
-                                             "algorithmic_flop": 2.0 * tri_e, "flop_floor_s": round(fl_e, 5),
+                                "roofline": {"bound": "mfma (R2 fp16 pre-filter 2 N^2 D at the fp16 peak + the "
+                                                      "blend's exact fp32 Q x G distances 2 Q G D at the fp32 "
+                                                      "matrix peak)",
+                                             "algorithmic_flop": 2.0 * tri_e, "blend_distance_flop": 2.0 * Q * G * wl_D,
+                                             "flop_floor_s": round(fl_e, 5),
                                              "frac": round(max(fl_e, hb) / tr, 4)}},
             "roofline": {"embed": {"bound": "mfma", "achieved": round(embed_flop / te / 1e12, 1),
                                    "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
