@@ -136,8 +136,9 @@ class JpegBatch:
     """Host side of a JPEG batch: the file bytes, the decode plan (reidmi_jpeg_plan) and the
     per-image status / (offset, h, w) of the decoded layout.  Host only: needs no GPU."""
 
-    def __init__(self, files):
-        self.buf, self.offsets = read_files(files)
+    def __init__(self, files, buffer=None):
+        # buffer: (uint8 bytes, int64 offsets [B+1]) already joined by read_files (files unused)
+        self.buf, self.offsets = read_files(files) if buffer is None else buffer
         B = len(self.offsets) - 1
         self.B = B
         self.meta = np.zeros((B, 3), np.int64)
