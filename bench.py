@@ -700,23 +700,35 @@ def launch_ranks(n, argv, script=None, poll_s=0.2):
     reader = threading.Thread(target=lambda: out0.append(procs[0].stdout.read()), daemon=True)
     reader.start()
     code = 0
-    while True:
-        states = [p.poll() for p in procs]  # every process polled each round (no short-circuit)
-        if all(c is not None for c in states):
-            break
-        bad = [c for c in states if c not in (None, 0)]
-        if bad:
-            code = bad[0]
-            for p in procs:
-                if p.poll() is None:
-                    p.terminate()
-            for p in procs:
-                try:
-                    p.wait(timeout=30)
-                except subprocess.TimeoutExpired:
-                    p.kill()
-            break
-        time.sleep(poll_s)
+
+    def stop_all():
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+
+    import signal
+    prev = signal.signal(signal.SIGTERM, lambda *_: sys.exit(128 + signal.SIGTERM))  # -> stop_all below
+    try:
+        while True:
+            states = [p.poll() for p in procs]  # every process polled each round (no short-circuit)
+            if all(c is not None for c in states):
+                break
+            bad = [c for c in states if c not in (None, 0)]
+            if bad:
+                code = bad[0]
+                stop_all()
+                break
+            time.sleep(poll_s)
+    except BaseException:  # interrupted (Ctrl-C, SIGTERM): no orphan ranks left waiting in a collective
+        stop_all()
+        raise
+    finally:
+        signal.signal(signal.SIGTERM, prev)
     reader.join(timeout=60)
     code = code or next((p.returncode for p in procs if p.returncode), 0)
     text = (out0[0] if out0 else b"").decode(errors="replace")

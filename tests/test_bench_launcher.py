@@ -75,3 +75,34 @@ def test_launch_failing_rank_ends_job(tmp_path, bad):
     code = bench.launch_ranks(2, ["--fail-rank", bad], script=_child(tmp_path))
     assert code == 3
     assert time.perf_counter() - t < 60
+
+
+def test_terminated_launcher_ends_its_ranks(tmp_path):
+    """SIGTERM to the launching process (a driver's time limit) must not leave ranks behind."""
+    import signal
+    import subprocess
+    import time
+    pidfile = tmp_path / "pids"
+    child = tmp_path / "child.py"
+    child.write_text("import os, sys, time\n"
+                     f"open({str(pidfile)!r}, 'a').write(str(os.getpid()) + '\\n')\n"
+                     "time.sleep(600)\n")
+    parent = subprocess.Popen([sys.executable, "-c",
+                               f"import sys; sys.path.insert(0, {REPO!r}); import bench; "
+                               f"sys.exit(bench.launch_ranks(2, [], script={str(child)!r}))"])
+    t = time.time()
+    while (not pidfile.exists() or len(pidfile.read_text().split()) < 2) and time.time() - t < 60:
+        time.sleep(0.1)
+    pids = [int(x) for x in pidfile.read_text().split()]
+    assert len(pids) == 2
+    parent.send_signal(signal.SIGTERM)
+    assert parent.wait(timeout=60) != 0
+    for pid in pids:
+        for _ in range(100):
+            try:
+                os.kill(pid, 0)
+            except ProcessLookupError:
+                break
+            time.sleep(0.1)
+        else:
+            raise AssertionError(f"rank process {pid} outlived its launcher")
