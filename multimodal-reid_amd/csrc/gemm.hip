@@ -73,13 +73,16 @@ constexpr int GB_M = 128, GB_N = 128, GB_K = 64;
 #ifndef GEMM_VAR_FB2  // persistent tile: keep both column halves' W fragments (LOAD 3 reads none)
 #define GEMM_VAR_FB2 1
 #endif
+#ifndef GEMM_VAR_NODMA  // timing-only (wrong results): no operand DMA inside the K-loop
+#define GEMM_VAR_NODMA 0
+#endif
 // The A/B hooks above compile other kernels (the timing-only ones give wrong results by design):
 // any value but the shipped one is refused outside a tools / variant build (-DREIDMI_TOOLS:
 // libreidmi_tools.so, tools/build_variant.py), so none can enter libreidmi.so.
 #if !defined(REIDMI_TOOLS) &&                                                                              \
     (GEMM_VAR_NOSTORE != 0 || GEMM_VAR_NOGELU != 0 || GEMM_VAR_NOPSTAT != 0 || GEMM_VAR_NORESLOAD != 0 ||   \
      GEMM_VAR_STAGGER != 0 || GEMM_VAR_DIAG_LOAD0 != 0 || GEMM_VAR_RPRE != 1 || GEMM_VAR_FB2 != 1 ||       \
-     GEMM_VAR_STAG_SHIFT != 0 || GEMM_VAR_STAG_MASK != 1 || GEMM_VAR_STAG_SLP != 127)
+     GEMM_VAR_STAG_SHIFT != 0 || GEMM_VAR_STAG_MASK != 1 || GEMM_VAR_STAG_SLP != 127 || GEMM_VAR_NODMA != 0)
 #error "gemm.hip: GEMM_VAR_* variants build only with -DREIDMI_TOOLS (never into libreidmi.so)"
 #endif
 
@@ -1053,21 +1056,22 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
                                                          16, 0, 0);
                 }
             }
-            if (has1 && !b0_early) issue_w(buf ^ 1, 0, p1);
+            constexpr bool KDMA = GEMM_VAR_NODMA == 0;
+            if (KDMA && has1 && !b0_early) issue_w(buf ^ 1, 0, p1);
             G5_LDS_DONE();
             G5_BARRIER();
             compute(0, 0, firstc);
             G5_BARRIER();
             // LOAD 1 / COMPUTE (0,1)
             load_b(sW, 1);
-            if (has2) issue_a(buf, 0, p2);
+            if (KDMA && has2) issue_a(buf, 0, p2);
             G5_LDS_DONE();
             G5_BARRIER();
             compute(0, 1, firstc);
             G5_BARRIER();
             // LOAD 2 / COMPUTE (1,1)
             load_a(sA, 1);
-            if (has2) issue_w(buf, 1, p2);
+            if (KDMA && has2) issue_w(buf, 1, p2);
             G5_LDS_DONE();
             G5_BARRIER();
             compute(1, 1, firstc);
@@ -1075,7 +1079,7 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
             // LOAD 3 / COMPUTE (1,0)
             if constexpr (!FB2) load_b(sW, 0);
             if (has2) {
-                issue_a(buf, 1, p2);
+                if constexpr (KDMA) issue_a(buf, 1, p2);
                 G5_LDS_DONE();
                 if constexpr (CAN_DEFER) {
                     constexpr int S = EpiVm<EPI>::count;

@@ -61,6 +61,7 @@ def test_tools_library_exports_variants_product_does_not():
 
 
 @pytest.mark.parametrize("src,define", [("gemm.hip", "-DGEMM_VAR_NOSTORE=1"), ("gemm.hip", "-DGEMM_VAR_FB2=0"),
+                                        ("gemm.hip", "-DGEMM_VAR_NODMA=1"),
                                         ("backend.hip", "-DDM2_BK_=32"), ("backend.hip", "-DRS_STATS")])
 def test_variant_macros_refused_outside_tools_builds(src, define):
     """The A/B timing hooks (some compile kernels with wrong results by design) are an #error
