@@ -76,13 +76,20 @@ constexpr int GB_M = 128, GB_N = 128, GB_K = 64;
 #ifndef GEMM_VAR_NODMA  // timing-only (wrong results): no operand DMA inside the K-loop
 #define GEMM_VAR_NODMA 0
 #endif
+#ifndef GEMM_VAR_NOWAIT  // timing-only (racy results): no counted operand wait (vmcnt(6)) in the K-loop
+#define GEMM_VAR_NOWAIT 0
+#endif
+#ifndef GEMM_VAR_ASAME  // timing-only (wrong results): every tile's A operand DMA reads row tile 0 (L2-resident)
+#define GEMM_VAR_ASAME 0
+#endif
 // The A/B hooks above compile other kernels (the timing-only ones give wrong results by design):
 // any value but the shipped one is refused outside a tools / variant build (-DREIDMI_TOOLS:
 // libreidmi_tools.so, tools/build_variant.py), so none can enter libreidmi.so.
 #if !defined(REIDMI_TOOLS) &&                                                                              \
     (GEMM_VAR_NOSTORE != 0 || GEMM_VAR_NOGELU != 0 || GEMM_VAR_NOPSTAT != 0 || GEMM_VAR_NORESLOAD != 0 ||   \
      GEMM_VAR_STAGGER != 0 || GEMM_VAR_DIAG_LOAD0 != 0 || GEMM_VAR_RPRE != 1 || GEMM_VAR_FB2 != 1 ||       \
-     GEMM_VAR_STAG_SHIFT != 0 || GEMM_VAR_STAG_MASK != 1 || GEMM_VAR_STAG_SLP != 127 || GEMM_VAR_NODMA != 0)
+     GEMM_VAR_STAG_SHIFT != 0 || GEMM_VAR_STAG_MASK != 1 || GEMM_VAR_STAG_SLP != 127 || GEMM_VAR_NODMA != 0 || \
+     GEMM_VAR_ASAME != 0 || GEMM_VAR_NOWAIT != 0)
 #error "gemm.hip: GEMM_VAR_* variants build only with -DREIDMI_TOOLS (never into libreidmi.so)"
 #endif
 
@@ -898,7 +905,7 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
         p.m0 = (int64_t)mt * G2_M;
         p.n0 = (nb0 + nt) * G2_N;
         p.full = p.m0 + G2_M <= M;
-        p.a = (const char*)(A + p.m0 * lda);
+        p.a = (const char*)(A + (GEMM_VAR_ASAME ? 0 : p.m0) * lda);
         p.w = (const char*)(W + (int64_t)p.n0 * ldw);
     };
     auto advance = [&](Pos& p) {
@@ -1090,10 +1097,10 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
                             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(S + 7) : "memory");
                         else
                             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(S + 6) : "memory");
-                    } else {
+                    } else if constexpr (!GEMM_VAR_NOWAIT) {
                         asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
                     }
-                } else {
+                } else if constexpr (!GEMM_VAR_NOWAIT) {
                     asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
                 }
             } else {
