@@ -112,19 +112,22 @@ def embed_full_leg(dev, rank, world, Q, G, batch, block=8192):
     imgs = torch.empty((block, 3, 256, 128), device=dev, dtype=torch.float16)
     sync(world)
     t = time.perf_counter()
-    for b0 in range(0, n, block):
-        b1 = min(b0 + block, n)
-        gen.manual_seed(1_000_003 * (lo + b0) + 17)  # seeded by global image index: any world size
-        x = imgs[:b1 - b0]
-        x.copy_(torch.rand((b1 - b0, 3, 256, 128), generator=gen, device=dev) * 2 - 1)
-        tta = torch.stack([torch.randint(0, 11, (b1 - b0,), generator=gen, device=dev),
-                           torch.randint(0, 21, (b1 - b0,), generator=gen, device=dev)], 1).to(torch.int32)
-        for s in range(0, b1 - b0, batch):
-            e = min(s + batch, b1 - b0)
-            zsl.embed_pair(m, x[s:e], tta=tta[s:e], out=feat[b0 + s:b0 + e])
-        if rank == 0 and (b0 // block) % 8 == 0:
+    # global blocks of `block` images, each generated whole from its own seed and cut to this
+    # rank's range, so image k is the same for any world size
+    for gb in range(lo // block, -(-hi // block)):
+        g0, g1 = gb * block, min((gb + 1) * block, Q + G)
+        gen.manual_seed(1_000_003 * gb + 17)
+        x = imgs[:g1 - g0]
+        x.copy_(torch.rand((g1 - g0, 3, 256, 128), generator=gen, device=dev) * 2 - 1)
+        tta = torch.stack([torch.randint(0, 11, (g1 - g0,), generator=gen, device=dev),
+                           torch.randint(0, 21, (g1 - g0,), generator=gen, device=dev)], 1).to(torch.int32)
+        a, b = max(g0, lo), min(g1, hi)
+        for s in range(a, b, batch):
+            e = min(s + batch, b)
+            zsl.embed_pair(m, x[s - g0:e - g0], tta=tta[s - g0:e - g0], out=feat[s - lo:e - lo])
+        if rank == 0 and gb % 8 == 0:
             torch.cuda.synchronize()
-            print(f"embed_full: {b1}/{n} images of rank 0's shard, {time.perf_counter() - t:.1f} s",
+            print(f"embed_full: {b - lo}/{n} images of rank 0's shard, {time.perf_counter() - t:.1f} s",
                   file=sys.stderr, flush=True)
     sync(world)
     te = tmax(time.perf_counter() - t, dev, world)
