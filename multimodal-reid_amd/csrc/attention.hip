@@ -1178,6 +1178,327 @@ int mhsa_cls(const void* q, const void* k, const void* vt, void* o, int64_t nseq
     return OK;
 }
 
+// ------------------------------------------------- the last block's CLS attention without K, V
+// Only the CLS query's attention output is consumed in the last block (zero_shot_learning.py:
+// 85-87 reads x12[:, 0] / xproj[:, 0]).  With the ln_1 fold (gemm.h: W' = W diag(gamma), s its
+// column sums, b' = b + W beta, per row rstd_t and a_t = -mean_t rstd_t), key and value of token t
+// are k_t = rstd_t (x_t W_K'^T) + a_t s_K + b_K' and v_t alike, so for the CLS query q_h of head h
+//   q_h . k_t = rstd_t (x_t . u_h) + a_t (q_h . s_Kh) + q_h . b_Kh',        u_h = W_Kh'^T q_h
+//   sum_t p_t v_t = W_Vh' z_h + alpha_h s_Vh + b_Vh',  z_h = sum_t p_t rstd_t x_t,
+//                                                      alpha_h = sum_t p_t a_t  (sum_t p_t = 1)
+// (custom_clip_model.py:22-24 -> F.multi_head_attention_forward's in_proj + SDPA, reassociated):
+// the same function of x without K and V for every token — 2 x 768 x 768 MACs per token and
+// 2 x 324 KB of K / V^T per image never formed.  Unlike the K / V path, nothing in between is
+// rounded to fp16 (u and the weights p rstd enter the MFMAs as fp16 hi + lo pairs, fp32-exact
+// products), so the result is closer to the reference's fp32 run than the fp16 K / V it replaces.
+//   cls_u_kernel     u_h (hi, lo), q_h . s_Kh, q_h . b_Kh' for 16 images per workgroup (VALU)
+//   cls_attn_kernel  one image per workgroup: scores X u^T on MFMA, softmax, z = w^T X on MFMA
+//                    (x staged in LDS and read transposed with ds_read_b64_tr_b16), alpha
+//   cls_o_kernel     o = W_V' z + alpha s_V + b_V' -> fp16, 16 images per workgroup (VALU)
+typedef __fp16 trh4 __attribute__((__vector_size__(8)));
+constexpr int kClsImg = 16;  // images per workgroup of cls_u / cls_o
+constexpr int kClsLp = 224;  // token rows covered by cls_attn (7 x 32): L <= 224
+
+template <int W>
+__global__ __launch_bounds__(256) void cls_u_kernel(const _Float16* __restrict__ q, const _Float16* __restrict__ wk,
+                                                    const float* __restrict__ sk, const float* __restrict__ bk,
+                                                    int64_t nseq, _Float16* __restrict__ u16, float* __restrict__ qsb) {
+    constexpr int H = W / 64, J = W / 256, NP = kClsImg / 2;
+    __shared__ f32x2v sq[W][NP];  // q[k] of the workgroup's images, as image pairs
+    const int tid = threadIdx.x;
+    const int64_t b0 = (int64_t)blockIdx.x * kClsImg;
+    for (int e = tid; e < W * NP; e += 256) {
+        const int k = e / NP, p = e - k * NP;
+        const int64_t i0 = b0 + 2 * p;
+        sq[k][p] = f32x2v{i0 < nseq ? (float)q[i0 * W + k] : 0.f, i0 + 1 < nseq ? (float)q[(i0 + 1) * W + k] : 0.f};
+    }
+    __syncthreads();
+    if (tid < kClsImg * 16) {  // q_h . s_Kh and q_h . b_Kh' per (image, head)
+        const int i = tid >> 4, h = tid & 15;
+        float a = 0.f, c = 0.f;
+        if (h < H)
+            for (int d = 0; d < 64; d++) {
+                const float qv = sq[64 * h + d][i >> 1][i & 1];
+                a = __builtin_fmaf(qv, sk[64 * h + d], a);
+                c = __builtin_fmaf(qv, bk[64 * h + d], c);
+            }
+        if (b0 + i < nseq && h < H) {
+            qsb[(b0 + i) * 32 + h] = a;
+            qsb[(b0 + i) * 32 + 16 + h] = c;
+        }
+    }
+    for (int h = 0; h < H; h++) {
+        f32x2v acc[NP][J];
+#pragma unroll
+        for (int p = 0; p < NP; p++)
+#pragma unroll
+            for (int j = 0; j < J; j++) acc[p][j] = f32x2v{0.f, 0.f};
+        for (int d = 0; d < 64; d++) {
+            const _Float16* wr = wk + (int64_t)(64 * h + d) * W;  // row 64h + d of W_K'
+            float w[J];
+#pragma unroll
+            for (int j = 0; j < J; j++) w[j] = (float)wr[tid + 256 * j];
+#pragma unroll
+            for (int p = 0; p < NP; p++) {
+                const f32x2v qq = sq[64 * h + d][p];
+#pragma unroll
+                for (int j = 0; j < J; j++) acc[p][j] = __builtin_elementwise_fma(qq, f32x2v{w[j], w[j]}, acc[p][j]);
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < NP; p++)
+#pragma unroll
+            for (int e = 0; e < 2; e++) {
+                const int64_t b = b0 + 2 * p + e;
+                if (b >= nseq) continue;
+#pragma unroll
+                for (int j = 0; j < J; j++) {
+                    const float v = acc[p][j][e];
+                    const _Float16 hi = (_Float16)v;
+                    const _Float16 lo = (_Float16)(v - (float)hi);
+                    u16[((b * 2 + 0) * H + h) * (int64_t)W + tid + 256 * j] = hi;
+                    u16[((b * 2 + 1) * H + h) * (int64_t)W + tid + 256 * j] = lo;
+                }
+            }
+    }
+}
+
+template <int W>
+struct ClsLds {
+    static constexpr int US = W + 8, XS = W + 16, TS = kClsLp + 8;
+    static constexpr int R0 = (2 * 16 * US > 32 * XS ? 2 * 16 * US : 32 * XS) * 2;  // sU | sX bytes
+    static constexpr int S_OFF = R0, WT_OFF = S_OFF + 16 * kClsLp * 4, RS_OFF = WT_OFF + 2 * 16 * TS * 2;
+    static constexpr int BYTES = RS_OFF + kClsLp * 8;
+};
+
+template <int W>
+__global__ __launch_bounds__(512) void cls_attn_kernel(const _Float16* __restrict__ x, const float2* __restrict__ rs,
+                                                       const _Float16* __restrict__ u16, const float* __restrict__ qsb,
+                                                       int64_t nseq, int L, float scale_log2, float* __restrict__ z,
+                                                       float* __restrict__ alpha) {
+    constexpr int H = W / 64, KS = W / 32, CT = W / 16 / 8;  // k-steps of the scores; column tiles per wave
+    using C = ClsLds<W>;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    _Float16* sU = (_Float16*)smem;  // [2][16][US] u hi / lo (scores)
+    _Float16* sX = (_Float16*)smem;  // [32][XS] a chunk of x rows (z; the same region)
+    float* sS = (float*)(smem + C::S_OFF);        // [16][224] scores (log2 units)
+    _Float16* sWt = (_Float16*)(smem + C::WT_OFF);  // [2][16][TS] p rstd hi / lo, head-major
+    float2* sRS = (float2*)(smem + C::RS_OFF);    // [224] (rstd, -mean rstd)
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int l15 = lane & 15, g = lane >> 4;
+    for (int64_t b = blockIdx.x; b < nseq; b += gridDim.x) {
+        for (int e = tid; e < 2 * 16 * (W / 8); e += 512) {
+            const int hl = e / (16 * (W / 8)), r = e / (W / 8) % 16, c8 = e % (W / 8);
+            f16x8 v = {};
+            if (r < H) v = *(const f16x8*)(u16 + ((b * 2 + hl) * H + r) * (int64_t)W + c8 * 8);
+            *(f16x8*)(sU + (hl * 16 + r) * C::US + c8 * 8) = v;
+        }
+        for (int t = tid; t < kClsLp; t += 512) sRS[t] = t < L ? rs[b * L + t] : make_float2(0.f, 0.f);
+        __syncthreads();
+        // scores: D[h = 4g + e][t = 16 rt + l15] = sum_c u_h[c] x_t[c] (A = u rows, B = x rows)
+        for (int rt = wid; rt * 16 < L; rt += 8) {
+            const int t = rt * 16 + l15 < L ? rt * 16 + l15 : L - 1;
+            const _Float16* xr = x + (b * L + t) * (int64_t)W + g * 8;
+            f16x8 xf[KS];
+#pragma unroll
+            for (int ks = 0; ks < KS; ks++) xf[ks] = *(const f16x8*)(xr + ks * 32);
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < KS; ks++) {
+                const f16x8 uh = *(const f16x8*)(sU + l15 * C::US + ks * 32 + g * 8);
+                const f16x8 ul = *(const f16x8*)(sU + (16 + l15) * C::US + ks * 32 + g * 8);
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(uh, xf[ks], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ul, xf[ks], acc, 0, 0, 0);
+            }
+            const int tt = rt * 16 + l15;
+            const float2 st = sRS[tt];
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const int h = 4 * g + e;
+                const float v = h < H ? (st.x * acc[e] + st.y * qsb[b * 32 + h] + qsb[b * 32 + 16 + h]) * scale_log2 : 0.f;
+                sS[h * kClsLp + tt] = tt < L ? v : -__builtin_inff();
+            }
+        }
+        for (int e = tid; e < 16 * kClsLp; e += 512)  // rows the score tiles do not cover
+            if (e % kClsLp >= (L + 15) / 16 * 16) sS[e] = -__builtin_inff();
+        __syncthreads();
+        {  // softmax of head h = tid / 32 over its tokens; w = p rstd (hi, lo), alpha = sum p a
+            const int h = tid >> 5, part = tid & 31;
+            float sv[kClsLp / 32];
+            float m = -__builtin_inff();
+#pragma unroll
+            for (int i = 0; i < kClsLp / 32; i++) {
+                sv[i] = sS[h * kClsLp + part + 32 * i];
+                m = fmaxf(m, sv[i]);
+            }
+#pragma unroll
+            for (int o = 16; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 32));
+            float sum = 0.f;
+#pragma unroll
+            for (int i = 0; i < kClsLp / 32; i++) {
+                sv[i] = h < H && part + 32 * i < L ? __builtin_amdgcn_exp2f(sv[i] - m) : 0.f;
+                sum += sv[i];
+            }
+#pragma unroll
+            for (int o = 16; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, 32);
+            const float inv = h < H ? 1.0f / sum : 0.f;
+            float al = 0.f;
+#pragma unroll
+            for (int i = 0; i < kClsLp / 32; i++) {
+                const int t = part + 32 * i;
+                const float pn = sv[i] * inv;
+                const float2 st = sRS[t];
+                const float w = pn * st.x;
+                al = __builtin_fmaf(pn, st.y, al);
+                const _Float16 hi = (_Float16)w;
+                sWt[h * C::TS + t] = hi;
+                sWt[(16 + h) * C::TS + t] = (_Float16)(w - (float)hi);
+            }
+#pragma unroll
+            for (int o = 16; o >= 1; o >>= 1) al += __shfl_xor(al, o, 32);
+            if (part == 0 && h < H) alpha[b * H + h] = al;
+        }
+        __syncthreads();
+        // z: D[h = 4g + e][c = c0 + l15] = sum_t w[h][t] x_t[c] (A = w rows, B = x columns read
+        // transposed: lane 4q + p of a 16-lane group addresses row q, columns 4p..4p+3 of a 4 x 16
+        // block and receives column l15 of its 4 rows; two blocks give the 8 tokens of the operand)
+        f32x4 zacc[CT];
+#pragma unroll
+        for (int i = 0; i < CT; i++) zacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int tc = 0; tc * 32 < L; tc++) {
+            for (int e = tid; e < 32 * (W / 8); e += 512) {
+                const int r = e / (W / 8), c8 = e % (W / 8);
+                const int t = tc * 32 + r < L ? tc * 32 + r : L - 1;  // (rows >= L carry weight 0)
+                *(f16x8*)(sX + r * C::XS + c8 * 8) = *(const f16x8*)(x + (b * L + t) * (int64_t)W + c8 * 8);
+            }
+            __syncthreads();
+            const f16x8 ah = *(const f16x8*)(sWt + l15 * C::TS + tc * 32 + g * 8);
+            const f16x8 al = *(const f16x8*)(sWt + (16 + l15) * C::TS + tc * 32 + g * 8);
+#pragma unroll
+            for (int i = 0; i < CT; i++) {
+                const int c0 = (wid + 8 * i) * 16;
+                const _Float16* a0 = sX + (8 * g + (l15 >> 2)) * C::XS + c0 + 4 * (l15 & 3);
+                const trh4 r0 = __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) trh4*)a0);
+                const trh4 r1 =
+                    __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) trh4*)(a0 + 4 * C::XS));
+                const uint2 u0 = __builtin_bit_cast(uint2, r0), u1 = __builtin_bit_cast(uint2, r1);
+                const f16x8 bf = __builtin_bit_cast(f16x8, make_uint4(u0.x, u0.y, u1.x, u1.y));
+                zacc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bf, zacc[i], 0, 0, 0);
+                zacc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bf, zacc[i], 0, 0, 0);
+            }
+            __syncthreads();
+        }
+#pragma unroll
+        for (int i = 0; i < CT; i++) {
+            const int c0 = (wid + 8 * i) * 16;
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const int h = 4 * g + e;
+                if (h < H) z[(b * H + h) * (int64_t)W + c0 + l15] = zacc[i][e];
+            }
+        }
+    }
+}
+
+// o[b][n] = W_V'[n] . z[b][h(n)] + alpha[b][h] s_V[n] + b_V'[n] for 16 images per workgroup on
+// MFMA: D[n = n0 + 4g + e][image = l15] over 16-row tiles of W_V' (A, rows straight from HBM)
+// and the images' z rows (B, fp32 -> fp16 hi + lo: fp32-exact products)
+template <int W>
+__global__ __launch_bounds__(256) void cls_o_kernel(const float* __restrict__ z, const float* __restrict__ alpha,
+                                                    const _Float16* __restrict__ wv, const float* __restrict__ sv,
+                                                    const float* __restrict__ bv, int64_t nseq, _Float16* __restrict__ o) {
+    constexpr int H = W / 64, NT = W / 16, KS = W / 32;
+    const int lane = threadIdx.x & 63, l15 = lane & 15, g = lane >> 4;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t b0 = (int64_t)blockIdx.x * kClsImg;
+    const int64_t img = b0 + l15 < nseq ? b0 + l15 : nseq - 1;  // (images past nseq: not stored)
+    for (int nt = wid; nt < NT; nt += 4) {
+        const int n0 = nt * 16, h = n0 / 64;
+        const _Float16* wr = wv + (int64_t)(n0 + l15) * W + g * 8;
+        const float* zr = z + (img * H + h) * (int64_t)W + g * 8;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+        for (int ks = 0; ks < KS; ks++) {
+            const f16x8 a = *(const f16x8*)(wr + ks * 32);
+            const float4 z0 = *(const float4*)(zr + ks * 32), z1 = *(const float4*)(zr + ks * 32 + 4);
+            const float zv[8] = {z0.x, z0.y, z0.z, z0.w, z1.x, z1.y, z1.z, z1.w};
+            f16x8 bh, bl;
+#pragma unroll
+            for (int e = 0; e < 8; e++) {
+                bh[e] = (_Float16)zv[e];
+                bl[e] = (_Float16)(zv[e] - (float)bh[e]);
+            }
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bh, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bl, acc, 0, 0, 0);
+        }
+        if (b0 + l15 < nseq) {
+            const float al = alpha[img * H + h];
+            _Float16 r[4];
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const int n = n0 + 4 * g + e;
+                r[e] = (_Float16)(acc[e] + al * sv[n] + bv[n]);
+            }
+            *(uint2*)(o + img * W + n0 + 4 * g) = __builtin_bit_cast(uint2, r);
+        }
+    }
+}
+
+int64_t cls_attn_nokv_ws_bytes(int64_t nseq, int W) {
+    const int64_t H = W / 64;
+    auto al = [](int64_t v) { return (v + 255) / 256 * 256; };
+    return al(nseq * 2 * H * W * 2) + al(nseq * 32 * 4) + al(nseq * H * W * 4) + al(nseq * H * 4);
+}
+
+template <int W>
+static int launch_cls_nokv(const _Float16* x, const float2* rs, const _Float16* q, const _Float16* wqkv,
+                           const float* colsum, const float* bias, int64_t nseq, int L, char* ws, _Float16* o,
+                           hipStream_t s) {
+    constexpr int H = W / 64;
+    auto al = [](int64_t v) { return (v + 255) / 256 * 256; };
+    _Float16* u16 = (_Float16*)ws;
+    float* qsb = (float*)(ws + al(nseq * 2 * H * W * 2));
+    float* z = (float*)((char*)qsb + al(nseq * 32 * 4));
+    float* alpha = (float*)((char*)z + al(nseq * H * W * 4));
+    const unsigned nb = (unsigned)((nseq + kClsImg - 1) / kClsImg);
+    hipLaunchKernelGGL(cls_u_kernel<W>, dim3(nb), dim3(256), 0, s, q, wqkv + (int64_t)W * W, colsum + W, bias + W, nseq,
+                       u16, qsb);
+    RM_LAUNCHED();
+    static bool attr = false;
+    static int occ = 0;
+    if (!attr) {
+        RM_CHECK_HIP(hipFuncSetAttribute((const void*)cls_attn_kernel<W>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         ClsLds<W>::BYTES));
+        int n = 0;
+        RM_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)cls_attn_kernel<W>, 512,
+                                                                  ClsLds<W>::BYTES));
+        occ = n > 0 ? n : 1;
+        attr = true;
+    }
+    const int64_t slots = (int64_t)num_cu() * occ;
+    hipLaunchKernelGGL(cls_attn_kernel<W>, dim3((unsigned)(nseq < slots ? nseq : slots)), dim3(512), ClsLds<W>::BYTES, s,
+                       x, rs, (const _Float16*)u16, (const float*)qsb, nseq, L, 0.125f * 1.4426950408889634f, z, alpha);
+    RM_LAUNCHED();
+    hipLaunchKernelGGL(cls_o_kernel<W>, dim3(nb), dim3(256), 0, s, (const float*)z, (const float*)alpha,
+                       wqkv + (int64_t)2 * W * W, colsum + 2 * W, bias + 2 * W, nseq, o);
+    RM_LAUNCHED();
+    return OK;
+}
+
+// x [nseq*L][W] fp16 (the residual stream), rs [nseq*L] (rstd, -mean rstd) of its rows, q
+// [nseq][W] fp16 (the CLS rows' heads, head-major), wqkv / colsum / bias the ln_1-folded in_proj
+// ([3W][W] fp16, [3W], [3W]), ws >= cls_attn_nokv_ws_bytes -> o [nseq][W] fp16.
+int cls_attn_nokv(const void* x, const void* rs, const void* q, const void* wqkv, const float* colsum,
+                  const float* bias, int64_t nseq, int L, int H, int W, void* ws, void* o, hipStream_t s) {
+    RM_REQUIRE(H * 64 == W && (W == 768 || W == 1024), "cls_attn_nokv: width 768 or 1024, 64-wide heads");
+    RM_REQUIRE(L >= 1 && L <= kClsLp, "cls_attn_nokv: 1 <= L <= 224");
+    if (nseq <= 0) return OK;
+    auto f = W == 768 ? launch_cls_nokv<768> : launch_cls_nokv<1024>;
+    return f((const _Float16*)x, (const float2*)rs, (const _Float16*)q, (const _Float16*)wqkv, colsum, bias, nseq, L,
+             (char*)ws, (_Float16*)o, s);
+}
+
 #ifdef REIDMI_TOOLS
 // Fused QKV + attention for non-causal blocks of L in (192, 224] tokens (the vision towers:
 // 211, IVLP 213); returns EINVAL for other shapes (the caller then runs the two kernels).

@@ -31,6 +31,9 @@ int qkv_attn(const void* x, int64_t ldx, const void* wq, int64_t ldw, const floa
              const void* rowstat, int64_t nseq, int L, int H, int W, void* o, hipStream_t s);
 #endif
 int mhsa_cls(const void* q, const void* k, const void* vt, void* o, int64_t nseq, int L, int H, hipStream_t s);
+int64_t cls_attn_nokv_ws_bytes(int64_t nseq, int W);
+int cls_attn_nokv(const void* x, const void* rs, const void* q, const void* wqkv, const float* colsum,
+                  const float* bias, int64_t nseq, int L, int H, int W, void* ws, void* o, hipStream_t s);
 
 // ------------------------------------------------------------------- LayerNorm
 // One wave per row; W = NV*256, each lane holds NV groups of 4 consecutive elements.
@@ -405,13 +408,15 @@ __global__ void gather_rowstat_kernel(const float2* __restrict__ st, int64_t nse
 }
 
 // The last block when only the CLS row of its output is consumed (inference path,
-// zero_shot_learning.py:85-87 reads x12[:,0] / xproj[:,0]): K and V for every token, then
-// Q, attention, out_proj, LN2 and the MLP for the CLS rows only.  Every CLS-row value is
-// computed by the same kernels as in run_block (GEMM outputs per element), but its
-// statistics come from a pass over the CLS rows, where run_block combines the residual
-// epilogues' partials (a different fp32 summation order), and its attention is the
-// single-query kernel: equal to the full block's row 0 up to fp32 rounding
-// (tests/test_gpu_encoder.py bounds the difference).
+// zero_shot_learning.py:85-87 reads x12[:,0] / xproj[:,0]): Q, attention, out_proj, LN2 and
+// the MLP for the CLS rows only.  The CLS query's attention reads the ln_1 input x of every
+// token directly (cls_attn_nokv, attention.hip: scores and the value sum reassociated through
+// the folded in_proj, so K and V are never formed for the 211 tokens — round 5; the K / V GEMM +
+// single-query kernel path of rounds 1-4 runs with REIDMI_CLS_KV=1, the A/B and test baseline).
+// Its LayerNorm statistics come from a pass over the CLS rows, where run_block combines the
+// residual epilogues' partials (a different fp32 summation order): equal to the full block's
+// row 0 up to that rounding and the fp16 roundings of K / V it skips (tests/test_gpu_encoder.py
+// bounds the difference).
 static int run_block_cls(const reidmi_block_weights& bw, char* ws, const Plan& P, int64_t nseq, int L, int W, int H,
                          bool x_pst, hipStream_t s) {
     const int64_t M = nseq * L;
@@ -428,17 +433,8 @@ static int run_block_cls(const reidmi_block_weights& bw, char* ws, const Plan& P
     // same statistics); gathered into the padded per-sequence buffer the Q GEMM reads
     hipLaunchKernelGGL(gather_rowstat_kernel, dim3(ceil_div(nseq, 256)), dim3(256), 0, s, st, nseq, L, sc);
     RM_LAUNCHED();
-    EpiArgs kv{};
-    kv.bias = bw.qkv_b + W;
-    kv.rowstat = st;
-    kv.colsum = bw.qkv_s + W;
-    kv.k = ws + P.k;
-    kv.vt = ws + P.vt;
-    kv.seq = L;
-    kv.heads = H;
-    kv.lpad = attn_lpad(L);
-    kv.n_off = W;
-    if ((rc = gemm_f16(EPI_QKV, x, W, (const _Float16*)bw.qkv_w + (int64_t)W * W, W, M, 2 * W, W, kv, s))) return rc;
+    const char* kv_env = getenv("REIDMI_CLS_KV");  // (read per call: tests switch it in-process)
+    const bool kv_path = kv_env != nullptr && kv_env[0] == '1';
     EpiArgs qa{};
     qa.bias = bw.qkv_b;
     qa.rowstat = sc;
@@ -447,8 +443,28 @@ static int run_block_cls(const reidmi_block_weights& bw, char* ws, const Plan& P
     qa.seq = 1;  // one (CLS) row per sequence: q [nseq*H][1][64]
     qa.heads = H;
     qa.lpad = 1;
-    if ((rc = gemm_f16(EPI_QKV, x, ldc, bw.qkv_w, W, nseq, W, W, qa, s))) return rc;
-    if ((rc = mhsa_cls(ws + P.q, ws + P.k, ws + P.vt, o, nseq, L, H, s))) return rc;
+    if (!kv_path) {
+        // (P.k, nseq * L * W * 2 bytes, the K buffer of the other path, holds its scratch)
+        if ((rc = gemm_f16(EPI_QKV, x, ldc, bw.qkv_w, W, nseq, W, W, qa, s))) return rc;
+        RM_REQUIRE(cls_attn_nokv_ws_bytes(nseq, W) <= nseq * L * W * 2, "run_block_cls: scratch");
+        if ((rc = cls_attn_nokv(x, st, ws + P.q, bw.qkv_w, bw.qkv_s, bw.qkv_b, nseq, L, H, W, ws + P.k, o, s)))
+            return rc;
+    } else {  // K and V for every token, then the single-query kernel
+        EpiArgs kv{};
+        kv.bias = bw.qkv_b + W;
+        kv.rowstat = st;
+        kv.colsum = bw.qkv_s + W;
+        kv.k = ws + P.k;
+        kv.vt = ws + P.vt;
+        kv.seq = L;
+        kv.heads = H;
+        kv.lpad = attn_lpad(L);
+        kv.n_off = W;
+        if ((rc = gemm_f16(EPI_QKV, x, W, (const _Float16*)bw.qkv_w + (int64_t)W * W, W, M, 2 * W, W, kv, s)))
+            return rc;
+        if ((rc = gemm_f16(EPI_QKV, x, ldc, bw.qkv_w, W, nseq, W, W, qa, s))) return rc;
+        if ((rc = mhsa_cls(ws + P.q, ws + P.k, ws + P.vt, o, nseq, L, H, s))) return rc;
+    }
     EpiArgs er{};
     er.out = x;
     er.ldc = ldc;

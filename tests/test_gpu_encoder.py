@@ -333,6 +333,29 @@ def test_vit_cls_path_and_tta(vit_b16):
     assert torch.equal(a12, t12) and torch.equal(ap, tp)
 
 
+@pytest.mark.parametrize("arch,gain,vpt", [("ViT-B/16", 1.0, 0), ("ViT-B/16", 4.0, 0), ("ViT-B/16", 1.0, 2),
+                                            ("ViT-L/14", 1.0, 0)])
+def test_cls_attention_without_kv_matches_kv_path(gpu, monkeypatch, arch, gain, vpt):
+    """The last block's CLS attention reassociated through the folded in_proj (cls_attn_nokv:
+    K and V never formed) against the K / V GEMM + single-query kernel path it replaced
+    (REIDMI_CLS_KV=1): the same function, differing by the fp16 roundings of K and V the new path
+    skips.  37 images (a partial last group of 16), ViT-B/16 at CLIP's init and the spread
+    network, IVLP prompts (L = 213), ViT-L/14 (width 1024, 16 heads)."""
+    from multimodal_reid_amd.model import VisionTransformer
+    sd = syn.vit_state_dict(arch, seed=3, layers=12, resid_gain=gain, **({"vpt_ctx": vpt} if vpt else {}))
+    m = VisionTransformer(sd)
+    imgs = torch.from_numpy(syn.images(37, seed=9))
+    assert m.seq_len == 211 + vpt
+    monkeypatch.delenv("REIDMI_CLS_KV", raising=False)
+    n12, np_ = (t.cpu().numpy() for t in m.encode_cls(imgs))
+    monkeypatch.setenv("REIDMI_CLS_KV", "1")
+    k12, kp = (t.cpu().numpy() for t in m.encode_cls(imgs))
+    assert np.isfinite(n12).all() and np.isfinite(np_).all()
+    assert _cos(n12, k12).min() >= 0.999995 and _cos(np_, kp).min() >= 0.999995
+    scale = np.abs(k12).max()
+    assert np.abs(n12 - k12).max() <= 2e-3 * scale, (np.abs(n12 - k12).max(), scale)
+
+
 def test_vit_batch_invariance(vit_b16):
     """Each image's features are bit-identical whatever batch it is computed in."""
     sd, m = vit_b16
