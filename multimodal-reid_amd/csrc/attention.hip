@@ -1263,139 +1263,161 @@ __global__ __launch_bounds__(256) void cls_u_kernel(const _Float16* __restrict__
     }
 }
 
+// LDS of cls_attn_kernel: u (hi, lo) rows, one 32-token chunk of x rows, the 8 waves' partial
+// scores, the chunk's weights p rstd (hi, lo), its row statistics, and per head the running
+// max / normaliser / alpha and the chunk's rescale factor
 template <int W>
 struct ClsLds {
-    static constexpr int US = W + 8, XS = W + 16, TS = kClsLp + 8;
-    static constexpr int R0 = (2 * 16 * US > 32 * XS ? 2 * 16 * US : 32 * XS) * 2;  // sU | sX bytes
-    static constexpr int S_OFF = R0, WT_OFF = S_OFF + 16 * kClsLp * 4, RS_OFF = WT_OFF + 2 * 16 * TS * 2;
-    static constexpr int BYTES = RS_OFF + kClsLp * 8;
+    static constexpr int US = W + 8, XS = W + 16, TS = 32 + 8;
+    static constexpr int U_OFF = 0, X_OFF = U_OFF + 2 * 16 * US * 2, P_OFF = X_OFF + 32 * XS * 2;
+    static constexpr int WT_OFF = P_OFF + 8 * 16 * 16 * 4, RS_OFF = WT_OFF + 2 * 16 * TS * 2;
+    static constexpr int H_OFF = RS_OFF + 32 * 8, BYTES = H_OFF + 16 * 4 * 4;
 };
 
+// One image per workgroup, its tokens in 32-row chunks (online softmax, each x row read once):
+// the chunk's x rows are staged in LDS (the next chunk's are loaded into registers meanwhile);
+// scores D[h = 4g + e][t = l15] = u_h . x_t on MFMA (A = u rows, B = x rows), the two 16-token
+// tiles split over the 8 waves by K quarters and summed by the softmax threads; per head the
+// running max m, normaliser l and alpha are updated and the chunk's weights w_t = p_t rstd_t
+// (hi, lo) written; z accumulates D[h][c] = sum_t w[h][t] x_t[c] on MFMA, its rows rescaled by
+// exp2(m_old - m_new) (B = x columns read transposed: lane 4q + p of a 16-lane group addresses
+// row q, columns 4p..4p+3 of a 4 x 16 block and receives column l15 of its 4 rows).
 template <int W>
 __global__ __launch_bounds__(512) void cls_attn_kernel(const _Float16* __restrict__ x, const float2* __restrict__ rs,
                                                        const _Float16* __restrict__ u16, const float* __restrict__ qsb,
                                                        int64_t nseq, int L, float scale_log2, float* __restrict__ z,
                                                        float* __restrict__ alpha) {
-    constexpr int H = W / 64, KS = W / 32, CT = W / 16 / 8;  // k-steps of the scores; column tiles per wave
+    constexpr int H = W / 64, KQ = W / 32 / 4, CT = W / 16 / 8;  // k-steps per quarter; z column tiles per wave
+    constexpr int XV = 32 * (W / 8) / 512;                         // 16-byte pieces of a chunk per thread
+    static_assert(32 * (W / 8) % 512 == 0, "chunk pieces per thread");
     using C = ClsLds<W>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    _Float16* sU = (_Float16*)smem;  // [2][16][US] u hi / lo (scores)
-    _Float16* sX = (_Float16*)smem;  // [32][XS] a chunk of x rows (z; the same region)
-    float* sS = (float*)(smem + C::S_OFF);        // [16][224] scores (log2 units)
-    _Float16* sWt = (_Float16*)(smem + C::WT_OFF);  // [2][16][TS] p rstd hi / lo, head-major
-    float2* sRS = (float2*)(smem + C::RS_OFF);    // [224] (rstd, -mean rstd)
+    _Float16* sU = (_Float16*)(smem + C::U_OFF);    // [2][16][US]
+    _Float16* sX = (_Float16*)(smem + C::X_OFF);    // [32][XS]
+    float* sP = (float*)(smem + C::P_OFF);          // [8 waves][16 h][16 t]
+    _Float16* sWt = (_Float16*)(smem + C::WT_OFF);  // [2][16][TS]
+    float2* sRS = (float2*)(smem + C::RS_OFF);      // [32]
+    float* sH = (float*)(smem + C::H_OFF);          // [16] rescale factor, then [16] final 1 / l
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int l15 = lane & 15, g = lane >> 4;
+    const int nch = (L + 31) / 32;
     for (int64_t b = blockIdx.x; b < nseq; b += gridDim.x) {
+        const _Float16* xb = x + b * L * (int64_t)W;
+        f16x8 xr[XV];
+        auto fetch = [&](int ch) {  // piece e of the chunk: row e / (W/8), 16 bytes at column 8 (e % (W/8))
+#pragma unroll
+            for (int v = 0; v < XV; v++) {
+                const int e = tid + 512 * v, r = e / (W / 8), c8 = e % (W / 8);
+                const int t = ch * 32 + r < L ? ch * 32 + r : L - 1;  // (rows >= L carry weight 0)
+                xr[v] = *(const f16x8*)(xb + (int64_t)t * W + c8 * 8);
+            }
+        };
+        fetch(0);
         for (int e = tid; e < 2 * 16 * (W / 8); e += 512) {
             const int hl = e / (16 * (W / 8)), r = e / (W / 8) % 16, c8 = e % (W / 8);
             f16x8 v = {};
             if (r < H) v = *(const f16x8*)(u16 + ((b * 2 + hl) * H + r) * (int64_t)W + c8 * 8);
             *(f16x8*)(sU + (hl * 16 + r) * C::US + c8 * 8) = v;
         }
-        for (int t = tid; t < kClsLp; t += 512) sRS[t] = t < L ? rs[b * L + t] : make_float2(0.f, 0.f);
-        __syncthreads();
-        // scores: D[h = 4g + e][t = 16 rt + l15] = sum_c u_h[c] x_t[c] (A = u rows, B = x rows)
-        for (int rt = wid; rt * 16 < L; rt += 8) {
-            const int t = rt * 16 + l15 < L ? rt * 16 + l15 : L - 1;
-            const _Float16* xr = x + (b * L + t) * (int64_t)W + g * 8;
-            f16x8 xf[KS];
-#pragma unroll
-            for (int ks = 0; ks < KS; ks++) xf[ks] = *(const f16x8*)(xr + ks * 32);
-            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int ks = 0; ks < KS; ks++) {
-                const f16x8 uh = *(const f16x8*)(sU + l15 * C::US + ks * 32 + g * 8);
-                const f16x8 ul = *(const f16x8*)(sU + (16 + l15) * C::US + ks * 32 + g * 8);
-                acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(uh, xf[ks], acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ul, xf[ks], acc, 0, 0, 0);
-            }
-            const int tt = rt * 16 + l15;
-            const float2 st = sRS[tt];
-#pragma unroll
-            for (int e = 0; e < 4; e++) {
-                const int h = 4 * g + e;
-                const float v = h < H ? (st.x * acc[e] + st.y * qsb[b * 32 + h] + qsb[b * 32 + 16 + h]) * scale_log2 : 0.f;
-                sS[h * kClsLp + tt] = tt < L ? v : -__builtin_inff();
-            }
-        }
-        for (int e = tid; e < 16 * kClsLp; e += 512)  // rows the score tiles do not cover
-            if (e % kClsLp >= (L + 15) / 16 * 16) sS[e] = -__builtin_inff();
-        __syncthreads();
-        {  // softmax of head h = tid / 32 over its tokens; w = p rstd (hi, lo), alpha = sum p a
-            const int h = tid >> 5, part = tid & 31;
-            float sv[kClsLp / 32];
-            float m = -__builtin_inff();
-#pragma unroll
-            for (int i = 0; i < kClsLp / 32; i++) {
-                sv[i] = sS[h * kClsLp + part + 32 * i];
-                m = fmaxf(m, sv[i]);
-            }
-#pragma unroll
-            for (int o = 16; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 32));
-            float sum = 0.f;
-#pragma unroll
-            for (int i = 0; i < kClsLp / 32; i++) {
-                sv[i] = h < H && part + 32 * i < L ? __builtin_amdgcn_exp2f(sv[i] - m) : 0.f;
-                sum += sv[i];
-            }
-#pragma unroll
-            for (int o = 16; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, 32);
-            const float inv = h < H ? 1.0f / sum : 0.f;
-            float al = 0.f;
-#pragma unroll
-            for (int i = 0; i < kClsLp / 32; i++) {
-                const int t = part + 32 * i;
-                const float pn = sv[i] * inv;
-                const float2 st = sRS[t];
-                const float w = pn * st.x;
-                al = __builtin_fmaf(pn, st.y, al);
-                const _Float16 hi = (_Float16)w;
-                sWt[h * C::TS + t] = hi;
-                sWt[(16 + h) * C::TS + t] = (_Float16)(w - (float)hi);
-            }
-#pragma unroll
-            for (int o = 16; o >= 1; o >>= 1) al += __shfl_xor(al, o, 32);
-            if (part == 0 && h < H) alpha[b * H + h] = al;
-        }
-        __syncthreads();
-        // z: D[h = 4g + e][c = c0 + l15] = sum_t w[h][t] x_t[c] (A = w rows, B = x columns read
-        // transposed: lane 4q + p of a 16-lane group addresses row q, columns 4p..4p+3 of a 4 x 16
-        // block and receives column l15 of its 4 rows; two blocks give the 8 tokens of the operand)
+        // softmax state of head hs = tid / 32 (every thread of the head's 32 holds it)
+        const int hs = tid >> 5, part = tid & 31;
+        const float sig = hs < H ? qsb[b * 32 + hs] : 0.f, bet = hs < H ? qsb[b * 32 + 16 + hs] : 0.f;
+        float m = -__builtin_inff(), l = 0.f, al = 0.f;
         f32x4 zacc[CT];
 #pragma unroll
         for (int i = 0; i < CT; i++) zacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-        for (int tc = 0; tc * 32 < L; tc++) {
-            for (int e = tid; e < 32 * (W / 8); e += 512) {
-                const int r = e / (W / 8), c8 = e % (W / 8);
-                const int t = tc * 32 + r < L ? tc * 32 + r : L - 1;  // (rows >= L carry weight 0)
-                *(f16x8*)(sX + r * C::XS + c8 * 8) = *(const f16x8*)(x + (b * L + t) * (int64_t)W + c8 * 8);
-            }
-            __syncthreads();
-            const f16x8 ah = *(const f16x8*)(sWt + l15 * C::TS + tc * 32 + g * 8);
-            const f16x8 al = *(const f16x8*)(sWt + (16 + l15) * C::TS + tc * 32 + g * 8);
+        for (int ch = 0; ch < nch; ch++) {
+            __syncthreads();  // the previous chunk's readers of sX / sWt / sRS / sH are done
 #pragma unroll
-            for (int i = 0; i < CT; i++) {
-                const int c0 = (wid + 8 * i) * 16;
-                const _Float16* a0 = sX + (8 * g + (l15 >> 2)) * C::XS + c0 + 4 * (l15 & 3);
-                const trh4 r0 = __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) trh4*)a0);
-                const trh4 r1 =
-                    __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) trh4*)(a0 + 4 * C::XS));
-                const uint2 u0 = __builtin_bit_cast(uint2, r0), u1 = __builtin_bit_cast(uint2, r1);
-                const f16x8 bf = __builtin_bit_cast(f16x8, make_uint4(u0.x, u0.y, u1.x, u1.y));
-                zacc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bf, zacc[i], 0, 0, 0);
-                zacc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bf, zacc[i], 0, 0, 0);
+            for (int v = 0; v < XV; v++) {
+                const int e = tid + 512 * v, r = e / (W / 8), c8 = e % (W / 8);
+                *(f16x8*)(sX + r * C::XS + c8 * 8) = xr[v];
+            }
+            if (tid < 32) sRS[tid] = ch * 32 + tid < L ? rs[b * L + ch * 32 + tid] : make_float2(0.f, 0.f);
+            if (ch + 1 < nch) fetch(ch + 1);
+            __syncthreads();
+            {  // partial scores: tile wid & 1 (tokens 16 (wid & 1) ..), K quarter wid >> 1
+                const int tile = wid & 1, kq = wid >> 1;
+                f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int k = 0; k < KQ; k++) {
+                    const int c = (kq * KQ + k) * 32 + g * 8;
+                    const f16x8 xf = *(const f16x8*)(sX + (tile * 16 + l15) * C::XS + c);
+                    const f16x8 uh = *(const f16x8*)(sU + l15 * C::US + c);
+                    const f16x8 ul = *(const f16x8*)(sU + (16 + l15) * C::US + c);
+                    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(uh, xf, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ul, xf, acc, 0, 0, 0);
+                }
+#pragma unroll
+                for (int e = 0; e < 4; e++) sP[(wid * 16 + 4 * g + e) * 16 + l15] = acc[e];
             }
             __syncthreads();
+            {  // online softmax of head hs over the chunk's token part
+                const int t = ch * 32 + part, tile = part >> 4, tl = part & 15;
+                float raw = 0.f;
+#pragma unroll
+                for (int kq = 0; kq < 4; kq++) raw += sP[((2 * kq + tile) * 16 + hs) * 16 + tl];
+                const float2 st = sRS[part];
+                const float sc = hs < H && t < L ? (st.x * raw + st.y * sig + bet) * scale_log2 : -__builtin_inff();
+                float cm = sc;
+#pragma unroll
+                for (int o = 16; o >= 1; o >>= 1) cm = fmaxf(cm, __shfl_xor(cm, o, 32));
+                const float mn = fmaxf(m, cm);
+                const float f = hs < H ? __builtin_amdgcn_exp2f(m - mn) : 1.f;  // (m = -inf: 0)
+                const float p = hs < H && t < L ? __builtin_amdgcn_exp2f(sc - mn) : 0.f;
+                float ps = p, pa = p * st.y;
+#pragma unroll
+                for (int o = 16; o >= 1; o >>= 1) {
+                    ps += __shfl_xor(ps, o, 32);
+                    pa += __shfl_xor(pa, o, 32);
+                }
+                l = __builtin_fmaf(l, f, ps);
+                al = __builtin_fmaf(al, f, pa);
+                m = hs < H ? mn : m;
+                const float w = p * st.x;
+                const _Float16 hi = (_Float16)w;
+                sWt[hs * C::TS + part] = hi;
+                sWt[(16 + hs) * C::TS + part] = (_Float16)(w - (float)hi);
+                if (part == 0) sH[hs] = f;
+            }
+            __syncthreads();
+            {  // z: rescale, then + w^T x (hi, lo)
+                float fr[4];
+#pragma unroll
+                for (int e = 0; e < 4; e++) fr[e] = sH[4 * g + e];
+                const f16x8 ah = *(const f16x8*)(sWt + l15 * C::TS + g * 8);
+                const f16x8 alo = *(const f16x8*)(sWt + (16 + l15) * C::TS + g * 8);
+#pragma unroll
+                for (int i = 0; i < CT; i++) {
+                    const int c0 = (wid + 8 * i) * 16;
+                    const _Float16* a0 = sX + (8 * g + (l15 >> 2)) * C::XS + c0 + 4 * (l15 & 3);
+                    const trh4 r0 = __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) trh4*)a0);
+                    const trh4 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4f16(
+                        (__attribute__((address_space(3))) trh4*)(a0 + 4 * C::XS));
+                    const uint2 u0 = __builtin_bit_cast(uint2, r0), u1 = __builtin_bit_cast(uint2, r1);
+                    const f16x8 bf = __builtin_bit_cast(f16x8, make_uint4(u0.x, u0.y, u1.x, u1.y));
+#pragma unroll
+                    for (int e = 0; e < 4; e++) zacc[i][e] *= fr[e];
+                    zacc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bf, zacc[i], 0, 0, 0);
+                    zacc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, bf, zacc[i], 0, 0, 0);
+                }
+            }
         }
+        __syncthreads();
+        if (part == 0) sH[16 + hs] = hs < H ? 1.0f / l : 0.f;
+        if (part == 0 && hs < H) alpha[b * H + hs] = al / l;
+        __syncthreads();
+        float inv[4];
+#pragma unroll
+        for (int e = 0; e < 4; e++) inv[e] = sH[16 + 4 * g + e];
 #pragma unroll
         for (int i = 0; i < CT; i++) {
             const int c0 = (wid + 8 * i) * 16;
 #pragma unroll
             for (int e = 0; e < 4; e++) {
                 const int h = 4 * g + e;
-                if (h < H) z[(b * H + h) * (int64_t)W + c0 + l15] = zacc[i][e];
+                if (h < H) z[(b * H + h) * (int64_t)W + c0 + l15] = zacc[i][e] * inv[e];
             }
         }
     }
