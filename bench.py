@@ -353,7 +353,12 @@ def msmt17_leg(model, dev, rank, world, batch, dataset="msmt17"):
                                              "frac": round(max(fl_e, hb) / tr, 4)}},
             "roofline": {"embed": {"bound": "mfma", "achieved": round(embed_flop / te / 1e12, 1),
                                    "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
-                                   "frac": round(embed_flop / te / 1e12 / PEAK_F16_TFLOPS, 4)}}}
+                                   "frac": round(embed_flop / te / 1e12 / PEAK_F16_TFLOPS, 4),
+                                   # the reference's work per pass (SURVEY.md §8d, 37.90 GFLOP); this
+                                   # encoder executes 34.6: the last block runs for the CLS row only and
+                                   # forms no K / V
+                                   "flop_basis": "reference-equivalent 37.90 GFLOP/pass (executed 34.6)",
+                                   "executed_TFLOPs": round(embed_flop * 34.6 / 37.90 / te / 1e12, 1)}}}
 
 
 def rerank_leg(dev, cpu=True, threads=1):
