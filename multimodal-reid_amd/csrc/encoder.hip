@@ -433,8 +433,12 @@ static int run_block_cls(const reidmi_block_weights& bw, char* ws, const Plan& P
     // same statistics); gathered into the padded per-sequence buffer the Q GEMM reads
     hipLaunchKernelGGL(gather_rowstat_kernel, dim3(ceil_div(nseq, 256)), dim3(256), 0, s, st, nseq, L, sc);
     RM_LAUNCHED();
-    const char* kv_env = getenv("REIDMI_CLS_KV");  // (read per call: tests switch it in-process)
-    const bool kv_path = kv_env != nullptr && kv_env[0] == '1';
+    // the reassociated path covers widths 768 / 1024 (64-wide heads), L <= 224 and scratch that
+    // fits the K buffer of the other path (L * W * 2 bytes per image); anything else (and
+    // REIDMI_CLS_KV=1, read per call: tests switch it in-process) takes the K / V path
+    const char* kv_env = getenv("REIDMI_CLS_KV");
+    const bool kv_path = (kv_env != nullptr && kv_env[0] == '1') || !(W == 768 || W == 1024) || L > 224 ||
+                         cls_attn_nokv_ws_bytes(nseq, W) > nseq * L * W * 2;
     EpiArgs qa{};
     qa.bias = bw.qkv_b;
     qa.rowstat = sc;
@@ -444,9 +448,7 @@ static int run_block_cls(const reidmi_block_weights& bw, char* ws, const Plan& P
     qa.heads = H;
     qa.lpad = 1;
     if (!kv_path) {
-        // (P.k, nseq * L * W * 2 bytes, the K buffer of the other path, holds its scratch)
         if ((rc = gemm_f16(EPI_QKV, x, ldc, bw.qkv_w, W, nseq, W, W, qa, s))) return rc;
-        RM_REQUIRE(cls_attn_nokv_ws_bytes(nseq, W) <= nseq * L * W * 2, "run_block_cls: scratch");
         if ((rc = cls_attn_nokv(x, st, ws + P.q, bw.qkv_w, bw.qkv_s, bw.qkv_b, nseq, L, H, W, ws + P.k, o, s)))
             return rc;
     } else {  // K and V for every token, then the single-query kernel
