@@ -317,9 +317,9 @@ def test_vit_cls_path_and_tta(vit_b16):
     imgs = torch.from_numpy(syn.images(3, seed=0))
     _, x12, xp = m.encode_image(imgs)
     c12, cp = m.encode_cls(imgs)
-    # CLS path: last block computes K/V for all tokens but Q/attention/MLP for the CLS row
-    # only, with a dedicated single-query attention (fp32 dot products, different summation
-    # order than the MFMA tile): equal to the full path up to fp32 rounding.
+    # CLS path: the last block's Q / attention / MLP for the CLS row only, its attention
+    # reassociated through the folded in_proj (no K / V: cls_attn_nokv) with fp32-exact
+    # products: equal to the full path up to the fp16 roundings of K / V it skips.
     assert _cos(c12.cpu().numpy(), x12[:, 0].cpu().numpy()).min() >= 0.999999
     assert _cos(cp.cpu().numpy(), xp[:, 0].cpu().numpy()).min() >= 0.999999
     assert (c12 - x12[:, 0]).abs().max() < 5e-3 and (cp - xp[:, 0]).abs().max() < 5e-3
