@@ -191,7 +191,9 @@ __global__ void rows_f16_to_f32_kernel(const _Float16* __restrict__ x, int64_t r
 // value -1 (= 0 before Normalize(0.5,0.5)), crop at (top i, left j).
 // One workgroup per (image, patch row py): the P source rows of all 3 channels that the
 // row's gw patches read (shifted by the TTA offset; rows outside the image = -1) are staged
-// in LDS as fp32 by coalesced 16-byte loads, then the gw * kpad outputs are written as
+// in LDS as fp16 (the output precision: fp32 inputs round once, here instead of at the store;
+// 12 KB per workgroup at 256 x 128, so 8 workgroups share a CU) by coalesced 16-byte loads,
+// then the gw * kpad outputs are written as
 // 16-byte chunks (consecutive threads -> consecutive chunks).  The stride-S overlap (each
 // pixel in up to 2x2 patches) is served from LDS, so HBM sees each image once.
 // PT: the patch size as a compile-time constant (16: ViT-B/16, 14: ViT-L/14; 0 = runtime).
@@ -199,7 +201,7 @@ template <typename TI, int PT>
 __global__ __launch_bounds__(256) void im2col_kernel(const TI* __restrict__ img, int H, int Wd, int P_, int S,
                                                      int gh, int gw, int kpad, const int32_t* __restrict__ tta,
                                                      _Float16* __restrict__ col) {
-    extern __shared__ float srow[];  // [3][P][Wd]
+    extern __shared__ _Float16 srow[];  // [3][P][Wd]
     const int P = PT > 0 ? PT : P_;
     const int b = blockIdx.x / gh, py = blockIdx.x - (blockIdx.x / gh) * gh;
     const bool aug = tta != nullptr;
@@ -211,19 +213,21 @@ __global__ __launch_bounds__(256) void im2col_kernel(const TI* __restrict__ img,
     for (int e = threadIdx.x; e < 3 * P * vpr; e += blockDim.x) {
         const int cr = e / vpr, xv = e - cr * vpr;  // cr = c * P + ky
         const int c = cr / P, y = y0 + (cr - c * P);
-        float* d = srow + cr * Wd + xv * V;
+        _Float16* d = srow + cr * Wd + xv * V;
         if (y >= 0 && y < H) {
             const uint4 raw = *(const uint4*)(im + ((int64_t)c * H + y) * Wd + xv * V);
             if constexpr (sizeof(TI) == 2) {
-                const f16x8 v = __builtin_bit_cast(f16x8, raw);
-#pragma unroll
-                for (int u = 0; u < 8; u++) d[u] = (float)v[u];
-            } else {
                 *(uint4*)d = raw;
+            } else {
+                const float4 f = __builtin_bit_cast(float4, raw);
+                d[0] = (_Float16)f.x;
+                d[1] = (_Float16)f.y;
+                d[2] = (_Float16)f.z;
+                d[3] = (_Float16)f.w;
             }
         } else {
 #pragma unroll
-            for (int u = 0; u < V; u++) d[u] = -1.0f;
+            for (int u = 0; u < V; u++) d[u] = (_Float16)-1.0f;
         }
     }
     __syncthreads();
@@ -245,7 +249,7 @@ __global__ __launch_bounds__(256) void im2col_kernel(const TI* __restrict__ img,
                     inb = x >= 0 && x < Wd;
                     x = Wd - 1 - x;
                 }
-                v = inb ? srow[(c * P + ky) * Wd + x] : -1.0f;
+                v = inb ? (float)srow[(c * P + ky) * Wd + x] : -1.0f;
             }
             o[u] = (_Float16)v;
         }
@@ -536,7 +540,7 @@ REIDMI_API int reidmi_vit_forward(const reidmi_vit_weights* w, const void* image
     RM_REQUIRE(B * w->grid_h < (1ll << 31) && Wimg % 8 == 0, "vit: im2col needs B * grid_h < 2^31 and width % 8 == 0");
     {
         const dim3 g((unsigned)(B * w->grid_h)), t(256);
-        const size_t lds = (size_t)3 * w->patch * Wimg * sizeof(float);
+        const size_t lds = (size_t)3 * w->patch * Wimg * sizeof(_Float16);
         RM_REQUIRE(lds <= 64 * 1024, "vit: image too wide for the im2col row stage");
 #define RM_IM2COL(TI, PT)                                                                                      \
     hipLaunchKernelGGL((im2col_kernel<TI, PT>), g, t, lds, s, (const TI*)images, H, Wimg, w->patch, w->stride, \
