@@ -56,7 +56,8 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const TX* x, int64_t row
                                                         const float* __restrict__ beta, float eps,
                                                         float* __restrict__ y32, int64_t ldy32,
                                                         _Float16* __restrict__ y16, int64_t ldy16,
-                                                        _Float16* yh, int64_t ldyh, float2* __restrict__ st) {
+                                                        _Float16* yh, int64_t ldyh, float2* __restrict__ st,
+                                                        float2* __restrict__ sto) {
     const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= rows) return;
     const int lane = threadIdx.x & 63;
@@ -99,30 +100,47 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const TX* x, int64_t row
         if (yh) {  // may alias x (in-place ln_pre): the whole row is in registers already
             f16x4 h = {(_Float16)o.x, (_Float16)o.y, (_Float16)o.z, (_Float16)o.w};
             ((f16x4*)(yh + r * ldyh))[f] = h;
+            if (sto) v[i] = make_float4((float)h[0], (float)h[1], (float)h[2], (float)h[3]);
         }
+    }
+    if (sto) {  // statistics of the fp16 row just written (the next LayerNorm's, folded into a GEMM):
+        // the same lane layout and summation order as the st pass over yh, so bit-identical to it
+        float s2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < NV; i++) s2 += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+        const float mean2 = wave_sum(s2) * invW;
+        float ss2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < NV; i++) {
+            const float a = v[i].x - mean2, b = v[i].y - mean2, c = v[i].z - mean2, d = v[i].w - mean2;
+            ss2 += (a * a + b * b) + (c * c + d * d);
+        }
+        const float rstd2 = __builtin_amdgcn_rsqf(wave_sum(ss2) * invW + eps);
+        if (lane == 0) sto[r] = make_float2(rstd2, -mean2 * rstd2);
     }
 }
 
 template <typename TX>
 int layernorm(const TX* x, int64_t rows, int64_t ldx, const int32_t* row_idx, int64_t W, const float* g,
               const float* b, float eps, float* y32, int64_t ldy32, _Float16* y16, int64_t ldy16, hipStream_t s,
-              _Float16* yh = nullptr, int64_t ldyh = 0, float2* st = nullptr) {
+              _Float16* yh = nullptr, int64_t ldyh = 0, float2* st = nullptr, float2* sto = nullptr) {
     if (rows == 0) return OK;
     RM_REQUIRE(ldx % 4 == 0 && (!y32 || ldy32 % 4 == 0) && (!y16 || ldy16 % 4 == 0) && (!yh || ldyh % 4 == 0),
                "layernorm: strides");
+    RM_REQUIRE(!sto || (yh && !st), "layernorm: output statistics need the fp16 output");
     dim3 grid(ceil_div(rows, 4));
     switch (W) {
         case 512:
             hipLaunchKernelGGL((layernorm_kernel<2, TX>), grid, dim3(256), 0, s, x, rows, ldx, row_idx, g, b, eps, y32,
-                               ldy32, y16, ldy16, yh, ldyh, st);
+                               ldy32, y16, ldy16, yh, ldyh, st, sto);
             break;
         case 768:
             hipLaunchKernelGGL((layernorm_kernel<3, TX>), grid, dim3(256), 0, s, x, rows, ldx, row_idx, g, b, eps, y32,
-                               ldy32, y16, ldy16, yh, ldyh, st);
+                               ldy32, y16, ldy16, yh, ldyh, st, sto);
             break;
         case 1024:
             hipLaunchKernelGGL((layernorm_kernel<4, TX>), grid, dim3(256), 0, s, x, rows, ldx, row_idx, g, b, eps, y32,
-                               ldy32, y16, ldy16, yh, ldyh, st);
+                               ldy32, y16, ldy16, yh, ldyh, st, sto);
             break;
         default:
             return fail(EINVAL_, "layernorm: width must be 512, 768 or 1024");
@@ -351,13 +369,24 @@ static Plan plan(int64_t nseq, int L, int W, int lp, int64_t extra_rows) {
     return p;
 }
 
+// Where a block's ln_1 statistics come from: a pass over x (row_stats), the partials the
+// previous block's c_proj epilogue wrote (x_pst), or already at P.st (ln_pre wrote them).
+enum XStats { XS_ROWS = 0, XS_PARTIALS = 1, XS_READY = 2 };
+
+static int ln1_stats(XStats xs, char* ws, const Plan& P, int64_t M, int W, hipStream_t s) {
+    float2* st = (float2*)(ws + P.st);
+    if (xs == XS_READY) return OK;
+    if (xs == XS_PARTIALS) return row_stats_from_partials((const float2*)(ws + P.pst), M, W, st, s);
+    return row_stats((const _Float16*)(ws + P.x), M, W, W, st, s);
+}
+
 // One ResidualAttentionBlock on the fp16 residual stream x [nseq*L][W].  ln_1 / ln_2 are
 // folded into the QKV / c_fc GEMMs (fp16 operands: x itself and W diag(gamma)); only the
 // per-row statistics are computed here (row_stats), never the normalised activations.
-// x_pst: the partials at P.pst describe x as it is now (written by the previous block's
-// c_proj epilogue and not overwritten since), so ln_1's statistics are combined from them.
+// xs: where ln_1's statistics come from (XStats); XS_PARTIALS when the partials at P.pst
+// describe x as it is now (written by the previous block's c_proj epilogue, not overwritten since).
 static int run_block(const reidmi_block_weights& bw, char* ws, const Plan& P, int64_t nseq, int L, int W, int H,
-                     bool causal, bool x_pst, hipStream_t s) {
+                     bool causal, XStats xs, hipStream_t s) {
     const int64_t M = nseq * L;
     float2* pst = (float2*)(ws + P.pst);
     _Float16* x = (_Float16*)(ws + P.x);
@@ -366,7 +395,7 @@ static int run_block(const reidmi_block_weights& bw, char* ws, const Plan& P, in
     float2* st = (float2*)(ws + P.st);
     int rc;
     // ln_1 (custom_clip_model.py:27)
-    if ((rc = x_pst ? row_stats_from_partials(pst, M, W, st, s) : row_stats(x, M, W, W, st, s))) return rc;
+    if ((rc = ln1_stats(xs, ws, P, M, W, s))) return rc;
     {
         EpiArgs ea{};
         ea.bias = bw.qkv_b;
@@ -422,7 +451,7 @@ __global__ void gather_rowstat_kernel(const float2* __restrict__ st, int64_t nse
 // row 0 up to that rounding and the fp16 roundings of K / V it skips (tests/test_gpu_encoder.py
 // bounds the difference).
 static int run_block_cls(const reidmi_block_weights& bw, char* ws, const Plan& P, int64_t nseq, int L, int W, int H,
-                         bool x_pst, hipStream_t s) {
+                         XStats xs, hipStream_t s) {
     const int64_t M = nseq * L;
     _Float16* x = (_Float16*)(ws + P.x);
     _Float16* o = (_Float16*)(ws + P.o);
@@ -431,8 +460,7 @@ static int run_block_cls(const reidmi_block_weights& bw, char* ws, const Plan& P
     float2* sc = (float2*)(ws + P.st_cls);
     const int64_t ldc = (int64_t)L * W;  // CLS row of each sequence
     int rc;
-    if ((rc = x_pst ? row_stats_from_partials((const float2*)(ws + P.pst), M, W, st, s) : row_stats(x, M, W, W, st, s)))
-        return rc;
+    if ((rc = ln1_stats(xs, ws, P, M, W, s))) return rc;
     // the CLS rows' ln_1 statistics are rows b*L of st (so Q, K and V of a CLS row use the
     // same statistics); gathered into the padded per-sequence buffer the Q GEMM reads
     hipLaunchKernelGGL(gather_rowstat_kernel, dim3(ceil_div(nseq, 256)), dim3(256), 0, s, st, nseq, L, sc);
@@ -569,7 +597,9 @@ REIDMI_API int reidmi_vit_forward(const reidmi_vit_weights* w, const void* image
     hipLaunchKernelGGL(cls_rows_kernel, dim3(ceil_div(ce, 256)), dim3(256), 0, s, x, B, L, W, w->class_emb,
                        w->pos_emb, NP, w->n_ctx, w->vpt);
     RM_LAUNCHED();
-    if ((rc = layernorm(x, M, W, nullptr, W, w->ln_pre_w, w->ln_pre_b, 1e-5f, nullptr, 0, nullptr, 0, s, x, W)))
+    // in place; also writes the statistics of its output rows, block 0's ln_1 (XS_READY)
+    if ((rc = layernorm(x, M, W, nullptr, W, w->ln_pre_w, w->ln_pre_b, 1e-5f, nullptr, 0, nullptr, 0, s, x, W, nullptr,
+                        (float2*)(ws + P.st))))
         return rc;
     // resblocks[:11] then resblocks[11] (custom_clip_model.py:91-92)
     for (int i = 0; i < 12; i++) {
@@ -580,11 +610,11 @@ REIDMI_API int reidmi_vit_forward(const reidmi_vit_weights* w, const void* image
                                L - w->n_ctx, w->n_ctx, bw.prompt);
             RM_LAUNCHED();
         }
-        // x's partials are current unless this is block 0 (x from ln_pre) or prompt rows
-        // were just overwritten (IVLP)
-        const bool x_pst = i > 0 && !(bw.prompt && w->n_ctx > 0);
-        if (i == 11 && !full) rc = run_block_cls(bw, ws, P, B, L, W, w->heads, x_pst, s);
-        else rc = run_block(bw, ws, P, B, L, W, w->heads, false, x_pst, s);
+        // x's partials are current unless this is block 0 (ln_pre wrote x and its statistics)
+        // or prompt rows were just overwritten (IVLP)
+        const XStats xs = i == 0 ? XS_READY : (bw.prompt && w->n_ctx > 0) ? XS_ROWS : XS_PARTIALS;
+        if (i == 11 && !full) rc = run_block_cls(bw, ws, P, B, L, W, w->heads, xs, s);
+        else rc = run_block(bw, ws, P, B, L, W, w->heads, false, xs, s);
         if (rc) return rc;
         if (i == 10 && out_x11) {  // resblocks[:11] output (fp16 stream -> fp32)
             const int64_t r11 = full ? M : B;
@@ -642,8 +672,8 @@ REIDMI_API int reidmi_text_forward(const reidmi_text_weights* w, const int64_t* 
                                w->n_ctx, bw.prompt);
             RM_LAUNCHED();
         }
-        const bool x_pst = i > 0 && !(bw.prompt && w->n_ctx > 0);
-        if ((rc = run_block(bw, ws, P, N, L, W, w->heads, true, x_pst, s))) return rc;
+        const XStats xs = i > 0 && !(bw.prompt && w->n_ctx > 0) ? XS_PARTIALS : XS_ROWS;
+        if ((rc = run_block(bw, ws, P, N, L, W, w->heads, true, xs, s))) return rc;
     }
     hipLaunchKernelGGL(eot_rows_kernel, dim3(ceil_div(N, 256)), dim3(256), 0, s, tokens, N, L, Lt, rows);
     RM_LAUNCHED();
