@@ -185,7 +185,8 @@ def test_layernorm(gpu, W):
     assert (y16.float().cpu() - ref).abs().max() < 1e-3 * ref.abs().max()
 
 
-@pytest.mark.parametrize("L,causal", [(211, False), (213, False), (77, True), (50, False), (256, True), (128, False)])
+@pytest.mark.parametrize("L,causal", [(211, False), (213, False), (77, True), (50, False), (256, True), (128, False),
+                                      (193, False), (208, False), (209, False), (224, False)])
 def test_mhsa(gpu, L, causal):
     lib = _lib()
     nseq, H = 3, 4
