@@ -249,8 +249,25 @@ __global__ __launch_bounds__(256) void im2col_kernel(const TI* __restrict__ img,
         }
     }
     __syncthreads();
-    const int kch = kpad / 8, PP = P * P;
+    // PT > 0: kpad is the packed (3 P^2 + 63) / 64 * 64 (checked at launch), a compile-time chunk count
+    const int kch = PT > 0 ? (3 * PT * PT + 63) / 64 * 8 : kpad / 8, PP = P * P;
     _Float16* out = col + ((int64_t)b * gh * gw + (int64_t)py * gw) * kpad;
+    if (PT % 8 == 0 && PT > 0 && !aug && S % 4 == 0) {
+        // plain view, P % 8 == 0: a chunk's 8 k share (c, ky) and read 8 consecutive staged
+        // pixels, 8-byte aligned (row stride Wd % 8 == 0, px * S * 2 bytes with S % 4 == 0)
+        for (int e = threadIdx.x; e < gw * kch; e += blockDim.x) {
+            const int px = e / kch, kc = e - px * kch, k0 = kc * 8;
+            uint4 v = make_uint4(0u, 0u, 0u, 0u);
+            if (k0 < 3 * PP) {
+                const int c = k0 / PP, rem = k0 - c * PP, ky = rem / P, kx0 = rem - ky * P;
+                const _Float16* src = srow + (c * P + ky) * Wd + px * S + kx0;
+                const uint2 lo = *(const uint2*)src, hi = *(const uint2*)(src + 4);
+                v = make_uint4(lo.x, lo.y, hi.x, hi.y);
+            }
+            *(uint4*)(out + (int64_t)px * kpad + kc * 8) = v;
+        }
+        return;
+    }
     for (int e = threadIdx.x; e < gw * kch; e += blockDim.x) {
         const int px = e / kch, kc = e - px * kch;
         f16x8 o;
@@ -573,13 +590,15 @@ REIDMI_API int reidmi_vit_forward(const reidmi_vit_weights* w, const void* image
 #define RM_IM2COL(TI, PT)                                                                                      \
     hipLaunchKernelGGL((im2col_kernel<TI, PT>), g, t, lds, s, (const TI*)images, H, Wimg, w->patch, w->stride, \
                        w->grid_h, w->grid_w, w->kpad, tta, col)
+        // the compile-time patch sizes assume the packed kpad (pack.hip)
+        const int pt = w->kpad == (3 * w->patch * w->patch + 63) / 64 * 64 ? w->patch : 0;
         if (images_f16) {
-            if (w->patch == 16) RM_IM2COL(_Float16, 16);
-            else if (w->patch == 14) RM_IM2COL(_Float16, 14);
+            if (pt == 16) RM_IM2COL(_Float16, 16);
+            else if (pt == 14) RM_IM2COL(_Float16, 14);
             else RM_IM2COL(_Float16, 0);
         } else {
-            if (w->patch == 16) RM_IM2COL(float, 16);
-            else if (w->patch == 14) RM_IM2COL(float, 14);
+            if (pt == 16) RM_IM2COL(float, 16);
+            else if (pt == 14) RM_IM2COL(float, 14);
             else RM_IM2COL(float, 0);
         }
 #undef RM_IM2COL
