@@ -327,17 +327,24 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
             return ea.pos + (1 + (uint32_t)m % (uint32_t)ea.npatch) * (int64_t)N + ncol + cq;
         };
         auto store_batch = [&](int i0) {
+            const int q = lane >> 4;
 #pragma unroll
             for (int ii = 0; ii < NB; ii++) {
                 const int64_t m = mrow + (i0 + ii) * 16 + (lane & 15);
-                if (m >= M) continue;
-                // patch rows of the fp16 residual stream
-                const uint32_t img = (uint32_t)m / (uint32_t)ea.npatch, p = (uint32_t)m - img * (uint32_t)ea.npatch;
-                _Float16* d = (_Float16*)ea.out + ((int64_t)img * ea.seq + 1 + p) * ea.ldc + ncol + cq;
+                // patch rows of the fp16 residual stream; 16-byte stores after the fp16 path's
+                // v_permlane16_swap pairing (lane group q: 8 columns of fragment 2jp + (q & 1))
+                const uint32_t mc = (uint32_t)(m < M ? m : M - 1);
+                const uint32_t img = mc / (uint32_t)ea.npatch, p = mc - img * (uint32_t)ea.npatch;
+                _Float16* d = (_Float16*)ea.out + ((int64_t)img * ea.seq + 1 + p) * ea.ldc + ncol;
 #pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const f32x4 v = acc[i0 + ii][j];
-                    *(f16x4*)(d + j * 16) = f16x4{(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
+                for (int jp = 0; jp < 2; jp++) {
+                    const f32x4 a = acc[i0 + ii][2 * jp], c = acc[i0 + ii][2 * jp + 1];
+                    const auto lo = __builtin_amdgcn_permlane16_swap(cvt_pk_f16(a[0], a[1]), cvt_pk_f16(c[0], c[1]),
+                                                                     false, false);
+                    const auto hi = __builtin_amdgcn_permlane16_swap(cvt_pk_f16(a[2], a[3]), cvt_pk_f16(c[2], c[3]),
+                                                                     false, false);
+                    if (m < M)
+                        *(uint4*)(d + (2 * jp + (q & 1)) * 16 + (q >> 1) * 8) = make_uint4(lo[0], hi[0], lo[1], hi[1]);
                 }
             }
         };
