@@ -228,6 +228,46 @@ __global__ __launch_bounds__(256) void im2col_kernel(const TI* __restrict__ img,
     const TI* im = img + (int64_t)b * 3 * H * Wd;
     constexpr int V = 16 / sizeof(TI);  // elements per 16-byte load (Wd % V == 0, checked at launch)
     const int vpr = Wd / V;             // loads per source row
+    // fast: P % 8 == 0 and S % 4 == 0, so a col chunk is 8 consecutive staged pixels of one row at
+    // an 8-byte aligned offset; the TTA view is then staged flipped and shifted (srow[cr][x'] = the
+    // pixel the crop shows at column x': image column Wd - 1 - (x' + tj - 10), or -1 outside), and
+    // both views read the stage the same way
+    const bool fast = PT % 8 == 0 && PT > 0 && S % 4 == 0;
+    if (fast && aug) {
+        for (int e = threadIdx.x; e < 3 * P * vpr; e += blockDim.x) {
+            const int cr = e / vpr, xv = e - cr * vpr;
+            const int c = cr / P, y = y0 + (cr - c * P);
+            _Float16 v[V];
+            if (y >= 0 && y < H) {
+                const uint4 raw = *(const uint4*)(im + ((int64_t)c * H + y) * Wd + xv * V);
+                if constexpr (sizeof(TI) == 2) {
+                    const f16x8 h = __builtin_bit_cast(f16x8, raw);
+#pragma unroll
+                    for (int u = 0; u < V; u++) v[u] = h[u];
+                } else {
+                    const float4 f = __builtin_bit_cast(float4, raw);
+                    v[0] = (_Float16)f.x;
+                    v[1] = (_Float16)f.y;
+                    v[2] = (_Float16)f.z;
+                    v[3] = (_Float16)f.w;
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < V; u++) v[u] = (_Float16)-1.0f;
+            }
+#pragma unroll
+            for (int u = 0; u < V; u++) {
+                const int xp = Wd - 1 - (xv * V + u) - tj + 10;  // the crop column showing image column xv*V+u
+                if (xp >= 0 && xp < Wd) srow[cr * Wd + xp] = v[u];
+            }
+        }
+        // crop columns whose source lies outside the image (the Pad): -1
+        const int nl = tj < 10 ? 10 - tj : 0, nr = tj > 10 ? tj - 10 : 0;
+        for (int e = threadIdx.x; e < 3 * P * (nl + nr); e += blockDim.x) {
+            const int cr = e / (nl + nr), u = e - cr * (nl + nr);
+            srow[cr * Wd + (u < nl ? u : Wd - nr + (u - nl))] = (_Float16)-1.0f;
+        }
+    } else {
     for (int e = threadIdx.x; e < 3 * P * vpr; e += blockDim.x) {
         const int cr = e / vpr, xv = e - cr * vpr;  // cr = c * P + ky
         const int c = cr / P, y = y0 + (cr - c * P);
@@ -248,13 +288,14 @@ __global__ __launch_bounds__(256) void im2col_kernel(const TI* __restrict__ img,
             for (int u = 0; u < V; u++) d[u] = (_Float16)-1.0f;
         }
     }
+    }
     __syncthreads();
     // PT > 0: kpad is the packed (3 P^2 + 63) / 64 * 64 (checked at launch), a compile-time chunk count
     const int kch = PT > 0 ? (3 * PT * PT + 63) / 64 * 8 : kpad / 8, PP = P * P;
     _Float16* out = col + ((int64_t)b * gh * gw + (int64_t)py * gw) * kpad;
-    if (PT % 8 == 0 && PT > 0 && !aug && S % 4 == 0) {
-        // plain view, P % 8 == 0: a chunk's 8 k share (c, ky) and read 8 consecutive staged
-        // pixels, 8-byte aligned (row stride Wd % 8 == 0, px * S * 2 bytes with S % 4 == 0)
+    if (fast) {
+        // a chunk's 8 k share (c, ky) and read 8 consecutive staged pixels, 8-byte aligned (row
+        // stride Wd % 8 == 0, px * S * 2 bytes with S % 4 == 0)
         for (int e = threadIdx.x; e < gw * kch; e += blockDim.x) {
             const int px = e / kch, kc = e - px * kch, k0 = kc * 8;
             uint4 v = make_uint4(0u, 0u, 0u, 0u);
