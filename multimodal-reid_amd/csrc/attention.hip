@@ -1430,19 +1430,22 @@ template <int W>
 __global__ __launch_bounds__(256) void cls_o_kernel(const float* __restrict__ z, const float* __restrict__ alpha,
                                                     const _Float16* __restrict__ wv, const float* __restrict__ sv,
                                                     const float* __restrict__ bv, int64_t nseq, _Float16* __restrict__ o) {
-    constexpr int H = W / 64, NT = W / 16, KS = W / 32;
+    constexpr int H = W / 64, KS = W / 32;
     const int lane = threadIdx.x & 63, l15 = lane & 15, g = lane >> 4;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t b0 = (int64_t)blockIdx.x * kClsImg;
     const int64_t img = b0 + l15 < nseq ? b0 + l15 : nseq - 1;  // (images past nseq: not stored)
-    for (int nt = wid; nt < NT; nt += 4) {
-        const int n0 = nt * 16, h = n0 / 64;
-        const _Float16* wr = wv + (int64_t)(n0 + l15) * W + g * 8;
+    // a wave per head: its 4 N-tiles share the head's z fragment (loaded and split into fp16 hi / lo
+    // once per K-step) and run 4 independent MFMA chains; each output's chain is unchanged
+    for (int h = wid; h < H; h += 4) {
+        const _Float16* wr = wv + (int64_t)(64 * h + l15) * W + g * 8;
         const float* zr = z + (img * H + h) * (int64_t)W + g * 8;
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
+        f32x4 acc[4] = {};
+#pragma unroll 2
         for (int ks = 0; ks < KS; ks++) {
-            const f16x8 a = *(const f16x8*)(wr + ks * 32);
+            f16x8 a[4];
+#pragma unroll
+            for (int t = 0; t < 4; t++) a[t] = *(const f16x8*)(wr + (int64_t)t * 16 * W + ks * 32);
             const float4 z0 = *(const float4*)(zr + ks * 32), z1 = *(const float4*)(zr + ks * 32 + 4);
             const float zv[8] = {z0.x, z0.y, z0.z, z0.w, z1.x, z1.y, z1.z, z1.w};
             f16x8 bh, bl;
@@ -1451,18 +1454,25 @@ __global__ __launch_bounds__(256) void cls_o_kernel(const float* __restrict__ z,
                 bh[e] = (_Float16)zv[e];
                 bl[e] = (_Float16)(zv[e] - (float)bh[e]);
             }
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bh, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bl, acc, 0, 0, 0);
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[t], bh, acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[t], bl, acc[t], 0, 0, 0);
+            }
         }
         if (b0 + l15 < nseq) {
             const float al = alpha[img * H + h];
-            _Float16 r[4];
 #pragma unroll
-            for (int e = 0; e < 4; e++) {
-                const int n = n0 + 4 * g + e;
-                r[e] = (_Float16)(acc[e] + al * sv[n] + bv[n]);
+            for (int t = 0; t < 4; t++) {
+                const int n0 = 64 * h + 16 * t;
+                _Float16 r[4];
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    const int n = n0 + 4 * g + e;
+                    r[e] = (_Float16)(acc[t][e] + al * sv[n] + bv[n]);
+                }
+                *(uint2*)(o + img * W + n0 + 4 * g) = __builtin_bit_cast(uint2, r);
             }
-            *(uint2*)(o + img * W + n0 + 4 * g) = __builtin_bit_cast(uint2, r);
         }
     }
 }
