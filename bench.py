@@ -18,10 +18,12 @@ sharded k-reciprocal re-rank + CMC/mAP, wall seconds max over ranks); "rerank" =
 Duke-size re-rank on rank 0 with the C port timed on the full config; "text" = the --mm
 zero-shot classifier's text side at Market size (750 x 56 token rows, TF/s); "backend" /
 "preprocess" = retrieval-kernel and transform rooflines; "jpeg" = the loaders' JPEG decode of
-a Market split of files on the device (and + transform), Pillow timed beside it; "cpu_baseline".
+a Market split of files on the device (and + transform), Pillow timed beside it; "files_to_map" =
+the same Market eval from 19 281 host JPEG buffers through get_loader -> inference ->
+get_cmc_map (N = 1); "cpu_baseline".
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B (default 20480)] [--backend nccl|gloo]
-                    [--no-cpu-baseline] [--no-rerank] [--no-msmt17] [--no-text] [--no-jpeg]
+                    [--no-cpu-baseline] [--no-rerank] [--no-msmt17] [--no-text] [--no-jpeg] [--no-files]
 
 `--gpus N` under torchrun (WORLD_SIZE set) must equal the world size; without torchrun,
 bench.py starts the N rank processes itself (launch_ranks) and relays rank 0's line.
@@ -565,6 +567,77 @@ def jpeg_leg(dev, n=19281, reps=5, unique=2048, cpu=True, n_cpu=2000):
     return line
 
 
+def market_jpeg_files(wl, dev, quality=90, threads=16):
+    """The Market split as 128x64 4:2:0 JPEG files in host memory: identity-structured crops
+    (IdentityCrops at the raw crop size, the headline's labels and seeds) rounded to uint8 and
+    Pillow-encoded on `threads` host threads.  Returns (query files, gallery files)."""
+    import concurrent.futures
+    import io
+
+    from PIL import Image
+    sp = syn.DATASET_SPLITS["market1501"]
+    ic = IdentityCrops(sp["num_ids"], sp["num_cams"], 5, dev, height=128, width=64, noise=0.3)
+
+    def u8(x):
+        return ((x.float() + 1) * 127.5).round_().clamp_(0, 255).to(torch.uint8).permute(0, 2, 3, 1).contiguous().cpu().numpy()
+
+    q = u8(ic(wl.q_pids, wl.q_cams, 0, wl.Q))
+    ic.seed = 6
+    g = u8(ic(wl.g_pids, wl.g_cams, 0, wl.G))
+    del ic
+
+    def enc(a):
+        b = io.BytesIO()
+        Image.fromarray(a).save(b, "JPEG", quality=quality, subsampling=2)
+        return b.getvalue()
+
+    with concurrent.futures.ThreadPoolExecutor(threads) as ex:
+        return list(ex.map(enc, q)), list(ex.map(enc, g))
+
+
+def files_leg(wl, dev, batch=4096, reps=2):
+    """VERDICT r5 Next #4: Market from 19 281 host JPEG buffers to mAP through the drop-in surface
+    — loader.get_loader (native threaded gather into pinned buffers + header parse on a host
+    thread; H2D + reidmi_jpeg_decode + reidmi_preprocess_u8 on a side stream, one batch ahead)
+    -> zero_shot_learning.inference (both TTA passes; the augmented view applied in im2col) for
+    gallery and query -> get_cmc_map (L2-normalise, exact distance, CMC/mAP).  Timed end to end
+    (best of `reps` after one warm-up run), beside the HBM-resident headline step."""
+    import types
+
+    from multimodal_reid_amd import loader
+    t = time.perf_counter()
+    qf, gf = market_jpeg_files(wl, dev)
+    t_gen = time.perf_counter() - t
+    ds = types.SimpleNamespace(query=[(f, int(p), int(c), 0, k) for k, (f, p, c) in enumerate(zip(qf, wl.q_pids, wl.q_cams))],
+                               gallery=[(f, int(p), int(c), 0, k) for k, (f, p, c) in enumerate(zip(gf, wl.g_pids, wl.g_cams))])
+
+    def run():
+        lg, lq, lga, lqa = loader.get_loader(ds, batch, 256, 128, "vit", tta_seed=1)
+        g_emb, g_pid, g_cam, _ = zsl.inference(wl.model, None, None, None, lg, lga, False, "vit")
+        q_emb, q_pid, q_cam, _ = zsl.inference(wl.model, None, None, None, lq, lqa, False, "vit")
+        cmc, mAP = zsl.get_cmc_map(g_emb, q_emb, g_pid, q_pid, g_cam, q_cam)
+        torch.cuda.synchronize()
+        for ld in (lg, lq):
+            ld.pipe.close()
+        return cmc, mAP
+
+    run()
+    walls = []
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        cmc, mAP = run()
+        walls.append(time.perf_counter() - t)
+    n = wl.Q + wl.G
+    fb = sum(map(len, qf)) + sum(map(len, gf))
+    w = min(walls)
+    return {"config": f"Market-1501 {wl.Q}q x {wl.G}g as {n} host JPEG buffers (128x64 4:2:0 q90, {fb / n:.0f} B avg, "
+                      "identity-structured crops) -> get_loader (batch %d) -> inference (2 passes) -> get_cmc_map" % batch,
+            "wall_s": round(w, 4), "walls_s": [round(v, 4) for v in walls], "imgs_per_s": round(n / w, 1),
+            "mAP": round(float(mAP), 6), "rank1": round(float(cmc[0]), 6), "file_bytes": fb,
+            "files_generated_s": round(t_gen, 2)}
+
+
 def text_leg(dev, n_cls=750, n_tpl=56, reps=3, cpu=True, threads=1, n_cpu=32):
     """the --mm zero-shot classifier's text side at Market size
     (zero_shot_learning.py:37-49): n_cls identities x n_tpl augmented templates = 42 000 token
@@ -771,6 +844,7 @@ def _parse(argv=None):
     ap.add_argument("--no-jpeg", action="store_true")
     ap.add_argument("--no-backend", action="store_true")
     ap.add_argument("--no-preprocess", action="store_true")
+    ap.add_argument("--no-files", action="store_true")
     return ap.parse_args(argv)
 
 
@@ -879,6 +953,9 @@ def main():
         cpu = not a.no_cpu_baseline and world == 1
         if not a.no_jpeg:
             line["jpeg"] = jpeg_leg(dev, cpu=cpu)
+        if not a.no_files and world == 1:
+            line["files_to_map"] = files_leg(wl, dev)
+            line["files_to_map"]["hbm_resident_step_s"] = round(elapsed / a.steps, 4)
         threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
         if not a.no_rerank:
             line["rerank"] = rerank_leg(dev, cpu=cpu, threads=threads)

@@ -545,6 +545,25 @@ int reidmi_jpeg_plan(const uint8_t* files, const int64_t* offsets, int64_t B, vo
 int reidmi_jpeg_decode(const uint8_t* files, const void* plan, const int64_t* info, int64_t B, void* ws,
                        int64_t ws_bytes, uint8_t* pix, int32_t* err, void* stream);
 
+/* ---------------------------------------------------------------- loader file reads (§8f) */
+
+/* The file side of reidDataset.__getitem__ (data_prepare.py:89 `Image.open(path)` in 4
+ * DataLoader workers, data_prepare.py:275-283): one batch of encoded files gathered into ONE
+ * caller-owned (pinned) host buffer by `nthreads` host threads (<= 0: up to 16), byte ranges
+ * split evenly over the threads.  HOST only, no GPU.
+ *
+ * reidmi_files_size: sizes[i] = byte size of paths[i] (UTF-8 / file-system encoded, NUL-ended),
+ *   or -1 where it cannot be opened.
+ * reidmi_files_read: dst[offsets[i] .. offsets[i+1]) = the contents of paths[i]; status[i] = 0,
+ *   1 (cannot open / read error) or 2 (the size differs from offsets[i+1] - offsets[i]).
+ * reidmi_bytes_gather: dst[offsets[i] .. offsets[i+1]) = srcs[i][0 .. offsets[i+1] - offsets[i])
+ *   (in-memory files, e.g. Python bytes objects).
+ * Each returns an error only for bad arguments; per-file problems go to sizes / status. */
+int reidmi_files_size(const char* const* paths, int64_t n, int64_t* sizes, int nthreads);
+int reidmi_files_read(const char* const* paths, int64_t n, const int64_t* offsets, uint8_t* dst, int32_t* status,
+                      int nthreads);
+int reidmi_bytes_gather(const void* const* srcs, int64_t n, const int64_t* offsets, uint8_t* dst, int nthreads);
+
 #ifdef __cplusplus
 }
 #endif

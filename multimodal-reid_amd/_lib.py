@@ -85,6 +85,9 @@ SIGNATURES = {
     "reidmi_preprocess_lds_size": [_i32, _i32, _i32, _i32, _vp],
     "reidmi_jpeg_plan": [_vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp],
     "reidmi_jpeg_decode": [_vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp],
+    "reidmi_files_size": [_vp, _i64, _vp, _i32],
+    "reidmi_files_read": [_vp, _i64, _vp, _vp, _vp, _i32],
+    "reidmi_bytes_gather": [_vp, _i64, _vp, _vp, _i32],
     "reidmi_comm_unique_id": [_vp],
     "reidmi_comm_init": [_vp, _i32, _i32, _vp, _i32],
     "reidmi_comm_destroy": [_vp],

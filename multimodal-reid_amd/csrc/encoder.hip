@@ -527,8 +527,8 @@ static int run_block_cls(const reidmi_block_weights& bw, char* ws, const Plan& P
     // fits the K buffer of the other path (L * W * 2 bytes per image); anything else (and
     // REIDMI_CLS_KV=1, read per call: tests switch it in-process) takes the K / V path
     const char* kv_env = getenv("REIDMI_CLS_KV");
-    const bool kv_path = (kv_env != nullptr && kv_env[0] == '1') || !(W == 768 || W == 1024) || L > 224 ||
-                         cls_attn_nokv_ws_bytes(nseq, W) > nseq * L * W * 2;
+    const bool kv_path = (kv_env != nullptr && kv_env[0] == '1') || !(W == 768 || W == 1024) || H * 64 != W ||
+                         L > 224 || cls_attn_nokv_ws_bytes(nseq, W) > nseq * L * W * 2;
     EpiArgs qa{};
     qa.bias = bw.qkv_b;
     qa.rowstat = sc;

@@ -559,3 +559,109 @@ REIDMI_API int reidmi_jpeg_decode(const uint8_t* files, const void* plan, const 
     RM_LAUNCHED();
     return OK;
 }
+
+// ------------------------------------------------------------------ host: the loader's file reads
+// reidDataset.__getitem__ opens one file per item in 4 DataLoader worker processes
+// (data_prepare.py:87-89, 275-283); here one batch of files lands in one caller-owned pinned
+// buffer (the H2D copy source of the decode) from up to 16 host threads, each taking a
+// contiguous range of items holding ~1/nt of the bytes.
+
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+namespace {
+
+int loader_threads(int nthreads, int64_t n, int64_t bytes) {
+    const int64_t hw = std::max<int64_t>(1, (int64_t)std::thread::hardware_concurrency());
+    int64_t nt = nthreads > 0 ? nthreads : std::min<int64_t>(16, hw);
+    nt = std::min<int64_t>({nt, std::max<int64_t>(1, n), std::max<int64_t>(1, bytes >> 20)});   // >= 1 MiB each
+    return (int)std::max<int64_t>(1, nt);
+}
+
+// items [first[t], first[t + 1]) for thread t: equal shares of the bytes (offsets is the prefix sum)
+template <class F>
+void over_items(const int64_t* offsets, int64_t n, int nt, F&& f) {
+    if (nt <= 1 || n <= 1) {
+        f((int64_t)0, n);
+        return;
+    }
+    std::vector<int64_t> first((size_t)nt + 1, n);
+    first[0] = 0;
+    const int64_t total = offsets[n] - offsets[0];
+    for (int t = 1; t < nt; ++t) {
+        const int64_t target = offsets[0] + total * t / nt;
+        first[(size_t)t] = std::lower_bound(offsets, offsets + n, target) - offsets;
+        first[(size_t)t] = std::max(first[(size_t)t], first[(size_t)t - 1]);
+    }
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t) th.emplace_back([&, t] { f(first[(size_t)t], first[(size_t)t + 1]); });
+    for (auto& x : th) x.join();
+}
+
+}  // namespace
+
+REIDMI_API int reidmi_files_size(const char* const* paths, int64_t n, int64_t* sizes, int nthreads) {
+    RM_REQUIRE(n >= 0 && (n == 0 || (paths && sizes)), "reidmi_files_size: bad arguments");
+    std::vector<int64_t> idx((size_t)n + 1);
+    for (int64_t i = 0; i <= n; ++i) idx[(size_t)i] = i;   // equal item counts per thread
+    over_items(idx.data(), n, loader_threads(nthreads, n, n << 20), [&](int64_t a, int64_t b) {
+        for (int64_t i = a; i < b; ++i) {
+            struct stat sb;
+            sizes[i] = (paths[i] != nullptr && stat(paths[i], &sb) == 0 && S_ISREG(sb.st_mode)) ? (int64_t)sb.st_size : -1;
+        }
+    });
+    return OK;
+}
+
+REIDMI_API int reidmi_files_read(const char* const* paths, int64_t n, const int64_t* offsets, uint8_t* dst,
+                                 int32_t* status, int nthreads) {
+    RM_REQUIRE(n >= 0 && (n == 0 || (paths && offsets && status && (dst || offsets[n] == offsets[0]))),
+               "reidmi_files_read: bad arguments");
+    for (int64_t i = 0; i < n; ++i)
+        RM_REQUIRE(offsets[i + 1] >= offsets[i] && offsets[i] >= 0, "reidmi_files_read: offsets must be non-decreasing from >= 0");
+    over_items(offsets, n, loader_threads(nthreads, n, offsets[n] - offsets[0]), [&](int64_t a, int64_t b) {
+        for (int64_t i = a; i < b; ++i) {
+            const int64_t want = offsets[i + 1] - offsets[i];
+            const int fd = paths[i] ? open(paths[i], O_RDONLY | O_CLOEXEC) : -1;
+            if (fd < 0) {
+                status[i] = 1;
+                continue;
+            }
+            int64_t got = 0;
+            int32_t st = 0;
+            while (got < want) {
+                const ssize_t r = pread(fd, dst + offsets[i] + got, (size_t)(want - got), (off_t)got);
+                if (r < 0) {
+                    st = 1;
+                    break;
+                }
+                if (r == 0) break;
+                got += r;
+            }
+            if (st == 0 && got != want) st = 2;
+            if (st == 0) {   // a longer file than its stated size is a size mismatch too
+                uint8_t extra;
+                if (pread(fd, &extra, 1, (off_t)want) == 1) st = 2;
+            }
+            close(fd);
+            status[i] = st;
+        }
+    });
+    return OK;
+}
+
+REIDMI_API int reidmi_bytes_gather(const void* const* srcs, int64_t n, const int64_t* offsets, uint8_t* dst,
+                                   int nthreads) {
+    RM_REQUIRE(n >= 0 && (n == 0 || (srcs && offsets && (dst || offsets[n] == offsets[0]))),
+               "reidmi_bytes_gather: bad arguments");
+    for (int64_t i = 0; i < n; ++i) {
+        RM_REQUIRE(offsets[i + 1] >= offsets[i] && offsets[i] >= 0, "reidmi_bytes_gather: offsets must be non-decreasing from >= 0");
+        RM_REQUIRE(srcs[i] != nullptr || offsets[i + 1] == offsets[i], "reidmi_bytes_gather: null source");
+    }
+    over_items(offsets, n, loader_threads(nthreads, n, offsets[n] - offsets[0]), [&](int64_t a, int64_t b) {
+        for (int64_t i = a; i < b; ++i)
+            if (offsets[i + 1] > offsets[i]) memcpy(dst + offsets[i], srcs[i], (size_t)(offsets[i + 1] - offsets[i]));
+    });
+    return OK;
+}

@@ -159,6 +159,9 @@ struct BitReader {
                     loaded += 32 - bits;
                     bits = 32;
                 }
+                // each stuffed pair takes two window bytes for 8 bits: from a short window
+                // (e.g. 5 bits + FF 00 FF 00 = 21) the byte loop tops it up to >= 32
+                if (!marker && bits < 32) bytewise = true;
             }
             if (!bytewise) {
                 fetch();

@@ -21,6 +21,7 @@ batch `preprocess` builds from PIL images — bit-exact with Pillow's decoder.
 """
 import ctypes
 import os
+import sys
 import warnings
 
 import numpy as np
@@ -103,20 +104,67 @@ class EvalTransform:
         return preprocess(images, self.h, self.w, self.model_type, self.dtype, device)
 
 
-def read_files(files):
-    """Concatenate JPEG files (paths or bytes objects): (uint8 buffer, int64 offsets [B+1])."""
-    blobs = []
-    for f in files:
-        if isinstance(f, bytes):
-            blobs.append(f)
-        elif isinstance(f, (bytearray, memoryview)):
-            blobs.append(bytes(f))
-        else:
-            with open(os.fspath(f), "rb") as fh:
-                blobs.append(fh.read())
-    offsets = np.zeros(len(blobs) + 1, np.int64)
-    offsets[1:] = np.cumsum(np.fromiter(map(len, blobs), np.int64, len(blobs)))
-    return np.frombuffer(b"".join(blobs), np.uint8), offsets   # read-only view of one joined copy
+# CPython lays a bytes object's data (NUL-terminated) right after its header: the first byte
+# sits at id(b) + sys.getsizeof(b"") - 1.  Reading 19k pointers that way costs ~1 ms where a
+# ctypes array of c_char_p costs ~5-10 ms; `_bytes_pointers` checks the layout on the batch's
+# first object and uses the ctypes route where it does not hold.
+_BYTES_DATA = sys.getsizeof(b"") - 1
+
+
+def _bytes_pointers(blobs):
+    n = len(blobs)
+    p = np.fromiter(map(id, blobs), np.int64, n) + _BYTES_DATA
+    if n and ctypes.cast(ctypes.c_char_p(blobs[0]), ctypes.c_void_p).value != int(p[0]):
+        arr = (ctypes.c_char_p * n)(*blobs)
+        p = np.frombuffer(ctypes.cast(arr, ctypes.POINTER(ctypes.c_int64 * n)).contents, np.int64).copy()
+        return p, arr
+    return p, blobs
+
+
+def read_files(files, out=None, nthreads=0):
+    """Gather a batch of JPEG files (paths, or in-memory bytes-like objects) into ONE host
+    buffer: (uint8 array, int64 offsets [B+1]).  Paths are read by reidmi_files_read, bytes
+    copied by reidmi_bytes_gather — both on up to 16 host threads (`nthreads`, 0 = default),
+    the file side of data_prepare.py:89's `Image.open(path)` in 4 DataLoader workers.  `out`:
+    a preallocated uint8 array (e.g. a pinned tensor's numpy view), used when large enough.
+    A path that cannot be read raises OSError (as open() would)."""
+    files = list(files)
+    n = len(files)
+    kinds = {isinstance(f, (bytes, bytearray, memoryview)) for f in files}
+    if len(kinds) > 1:  # mixed batch: read the paths here, then gather everything as bytes
+        files = [f if isinstance(f, (bytes, bytearray, memoryview)) else open(os.fspath(f), "rb").read()
+                 for f in files]
+        kinds = {True}
+    offsets = np.zeros(n + 1, np.int64)
+    vp = ctypes.c_void_p
+    if kinds == {True}:
+        blobs = [f if isinstance(f, bytes) else bytes(f) for f in files]
+        offsets[1:] = np.cumsum(np.fromiter(map(len, blobs), np.int64, n))
+        total = int(offsets[-1])
+        buf = out[:total] if out is not None and out.size >= total else np.empty(total, np.uint8)
+        ptrs, keep = _bytes_pointers(blobs)
+        _lib.call("reidmi_bytes_gather", ptrs.ctypes.data_as(vp), n, offsets.ctypes.data_as(vp),
+                  buf.ctypes.data_as(vp), int(nthreads))
+        del keep
+        return buf, offsets
+    paths = [os.fsencode(os.fspath(f)) for f in files]
+    ptrs, keep = _bytes_pointers(paths)
+    sizes = np.empty(n, np.int64)
+    _lib.call("reidmi_files_size", ptrs.ctypes.data_as(vp), n, sizes.ctypes.data_as(vp), int(nthreads))
+    if n and (sizes < 0).any():
+        i = int(np.argmax(sizes < 0))
+        raise FileNotFoundError(f"cannot open {os.fsdecode(paths[i])} ({int((sizes < 0).sum())} of {n} files)")
+    offsets[1:] = np.cumsum(sizes)
+    total = int(offsets[-1])
+    buf = out[:total] if out is not None and out.size >= total else np.empty(total, np.uint8)
+    status = np.zeros(n, np.int32)
+    _lib.call("reidmi_files_read", ptrs.ctypes.data_as(vp), n, offsets.ctypes.data_as(vp), buf.ctypes.data_as(vp),
+              status.ctypes.data_as(vp), int(nthreads))
+    del keep
+    if status.any():
+        i = int(np.argmax(status != 0))
+        raise OSError(f"reading {os.fsdecode(paths[i])} failed ({'changed size' if status[i] == 2 else 'read error'})")
+    return buf, offsets
 
 
 def _to_device(a, device):
@@ -136,8 +184,9 @@ class JpegBatch:
     """Host side of a JPEG batch: the file bytes, the decode plan (reidmi_jpeg_plan) and the
     per-image status / (offset, h, w) of the decoded layout.  Host only: needs no GPU."""
 
-    def __init__(self, files, buffer=None):
-        # buffer: (uint8 bytes, int64 offsets [B+1]) already joined by read_files (files unused)
+    def __init__(self, files, buffer=None, plan_out=None):
+        # buffer: (uint8 bytes, int64 offsets [B+1]) already joined by read_files (files unused);
+        # plan_out: a uint8 array the plan is written into when it fits (the loader's pinned slot)
         self.buf, self.offsets = read_files(files) if buffer is None else buffer
         B = len(self.offsets) - 1
         self.B = B
@@ -149,7 +198,11 @@ class JpegBatch:
                self.info.ctypes.data_as(ctypes.c_void_p))
         # one parse when the tables fit the first guess (a dataset has a handful of distinct ones)
         cap = 4096 + B * 256 + 64 * 1536
-        self.plan = np.zeros(cap, np.uint8)
+        if plan_out is not None and plan_out.size >= cap:
+            cap = plan_out.size
+            self.plan = plan_out
+        else:
+            self.plan = np.zeros(cap, np.uint8)
         _lib.call("reidmi_jpeg_plan", *args, self.plan.ctypes.data_as(ctypes.c_void_p), cap, *out)
         if int(self.info[0]) > cap:
             self.plan = np.zeros(int(self.info[0]), np.uint8)
@@ -212,6 +265,13 @@ def preprocess_jpeg(files, height=256, width=128, model_type="vit", dtype=torch.
     _lib.call("reidmi_preprocess_u8", _lib.ptr(pix), _lib.ptr(meta), B, jb.max_h, jb.max_w, height, width, mean_c,
               std_c, 0 if dtype == torch.float32 else 1, _lib.ptr(out), _lib.stream(device))
     return out
+
+
+def get_loader(dataset, batch_size, image_height, image_width, model_type, **kw):
+    """data_prepare.py:256-284 on the device for an already-listed dataset (loader.get_loader):
+    (loader_gallery, loader_query, loader_gallery_augmented, loader_query_augmented)."""
+    from .loader import get_loader as _get_loader
+    return _get_loader(dataset, batch_size, image_height, image_width, model_type, **kw)
 
 
 def tta_offsets(n, generator=None):

@@ -18,6 +18,7 @@ import torch
 
 from . import _lib
 from .evaluate import R1_mAP_eval
+from .loader import TtaView
 
 
 def _vis(model):
@@ -25,16 +26,14 @@ def _vis(model):
 
 
 def embed_pair(model, images, images_aug=None, tta=None, zeroshot_weights=None, multimodal=False, out=None):
-    """Feature rows for one batch: plain pass + augmented pass (either an augmented image
-    batch or on-the-fly ``tta`` crop offsets applied to ``images``), fused epilogue."""
+    """Feature rows for one batch: plain pass + augmented pass (an augmented image batch, or
+    on-the-fly ``tta`` crop offsets applied to ``images_aug`` when given, else to ``images``),
+    fused epilogue."""
     vis = _vis(model)
     B = images.shape[0]
     W, E = vis.width, vis.out_dim
     a12, ap = vis.encode_cls(images)
-    if images_aug is not None:
-        b12, bp = vis.encode_cls(images_aug)
-    else:
-        b12, bp = vis.encode_cls(images, tta=tta)
+    b12, bp = vis.encode_cls(images if images_aug is None else images_aug, tta=tta)
     st = _lib.stream(vis.device)
     if multimodal:
         zs = zeroshot_weights.to(vis.device, torch.float32).contiguous()
@@ -54,13 +53,19 @@ def embed_pair(model, images, images_aug=None, tta=None, zeroshot_weights=None, 
 def inference(model, bottleneck, bottleneck_proj, zeroshot_weights, loader, loader_augment, multimodal,
               model_type):
     """zero_shot_learning.py:61-134.  Loaders yield (images, target, cams, seqs, indices);
-    the i-th batches of the two loaders hold the same images (shuffle=False)."""
+    the i-th batches of the two loaders hold the same images (shuffle=False).  An augmented
+    batch may be a loader.TtaView (the device loaders of loader.get_loader): its flip / pad /
+    crop then run inside the encoder's im2col."""
     if model_type != "vit":
         raise NotImplementedError("libreidmi implements the ViT tower (north-star path) only")
     embeddings, targets, camera_ids, sequence_ids = [], [], [], []
     with torch.no_grad():
         for (images, target, cams, seqs, _), (images_aug, *_rest) in zip(loader, loader_augment):
-            embeddings.append(embed_pair(model, images, images_aug, None, zeroshot_weights, multimodal))
+            if isinstance(images_aug, TtaView):
+                emb = embed_pair(model, images, images_aug.images, images_aug.offsets, zeroshot_weights, multimodal)
+            else:
+                emb = embed_pair(model, images, images_aug, None, zeroshot_weights, multimodal)
+            embeddings.append(emb)
             targets.append(torch.as_tensor(target))
             camera_ids.append(torch.as_tensor(cams))
             sequence_ids.append(torch.as_tensor(seqs))

@@ -30,6 +30,60 @@ def _save(arr, **kw):
     return b.getvalue()
 
 
+def _dht(tc_th, lengths, symbols):
+    """A DHT segment: BITS from the code-length counts, HUFFVAL in canonical order."""
+    body = bytes([tc_th]) + bytes(lengths[1:17]) + bytes(symbols)
+    return b"\xff\xc4" + (2 + len(body)).to_bytes(2, "big") + body
+
+
+def _stuff(bits):
+    """Entropy-coded segment from a '0'/'1' string (padded with 1s), 0xFF stuffed as FF 00."""
+    bits += "1" * (-len(bits) % 8)
+    out = bytearray()
+    for i in range(0, len(bits), 8):
+        out.append(int(bits[i:i + 8], 2))
+        if out[-1] == 0xFF:
+            out.append(0)
+    return bytes(out)
+
+
+def stuffed_window_cases():
+    """Hand-built grayscale baseline files whose entropy data puts two stuffed pairs
+    (FF 00 FF 00) in one 4-byte refill window while the bit window holds only 5 bits, followed
+    by a 16-bit AC code and 10 extra bits (ADVICE r5: the word path of BitReader::refill used to
+    return with 21 bits, and the extra bits read zeros).  Custom tables: DC category 0 = '0',
+    category c = '1' + 15 zeros; AC codes of every length 2..16 on a '0 1...1 0' ladder, EOB =
+    '00', run/size 0x0A = '0' + 15 ones.  Variants shift the window state with the DC category
+    (bits left 5 / 1 / 9) and with a second FF 00 pair right after the first window."""
+    dqt = b"\xff\xdb\x00\x43\x00" + bytes([1] * 64)
+    ac_len = [0] * 17
+    for L in range(2, 16):
+        ac_len[L] = 1
+    ac_len[16] = 3
+    # EOB, 13 fillers (lengths 3..15), then the three 16-bit codes: A, B = '0' + 15 ones (0x0A), C
+    ac_sym = [0x00] + list(range(0x11, 0x1B)) + [0x31, 0x32, 0x33] + [0x21, 0x0A, 0x22]
+    ac_b = "0" + "1" * 15
+    out = []
+    for name, cat, extra, tail, second in (("ffff-b5", 11, "01111111111", "1111111111", False),
+                                           ("ffff-b1", 15, "011111111111111", "1111111111", False),
+                                           ("ffff-b9", 7, "0111111", "1111111110", False),
+                                           ("ffff-b5-twice", 11, "01111111111", "1111111111", True)):
+        dc_len = [0] * 17
+        dc_len[1], dc_len[16] = 1, 1
+        blocks = 8
+        bits = "1" + "0" * 15 + extra + ac_b + tail   # block 0: DC category `cat`, one AC coefficient
+        if second:   # a second coefficient with the same 16-bit code: FF 00 FF 00 once more
+            bits += ac_b + "1" * 10
+        bits += "00" + "000" * (blocks - 1)           # EOB; blocks 1..: DC diff 0, EOB
+        sof = b"\xff\xc0\x00\x0b\x08\x00\x08" + (8 * blocks).to_bytes(2, "big") + b"\x01\x01\x11\x00"
+        sos = b"\xff\xda\x00\x08\x01\x01\x00\x00\x3f\x00"
+        f = (b"\xff\xd8" + dqt + sof + _dht(0x00, dc_len, [0, cat]) + _dht(0x10, ac_len, ac_sym) + sos
+             + _stuff(bits) + b"\xff\xd9")
+        assert b"\xff\x00\xff\x00" in f
+        out.append((name, f))
+    return out
+
+
 def parity_cases():
     """Edge geometry (1 px, narrow chroma that libjpeg-turbo replicates instead of filtering,
     partial MCUs), every Pillow subsampling, low / high quality, restart intervals, optimised
@@ -54,7 +108,7 @@ def parity_cases():
                                   .astype(np.uint8).repeat(3, 2), quality=100, subsampling=0)))
     out.append(("gray", _gray(37, 29, 7, quality=85)))
     out.append(("gray-rst", _gray(128, 64, 8, quality=60, restart_marker_blocks=2)))
-    return out
+    return out + stuffed_window_cases()
 
 
 # ------------------------------------------------------------------ CPU: host plan
