@@ -37,7 +37,7 @@ def _items(n, seed, tmp_path=None):
 @pytest.fixture(scope="module")
 def vit(gpu):
     from multimodal_reid_amd import model
-    return model.VisionTransformer(syn.vit_state_dict("ViT-B/16", layers=2, seed=3))
+    return model.VisionTransformer(syn.vit_state_dict("ViT-B/16", seed=3))  # resblocks[:12] run: 12 layers
 
 
 @pytest.mark.parametrize("source", ["bytes", "paths"])
