@@ -45,6 +45,13 @@ int reidmi_qkv_attention_f16(const void* x, int64_t ldx, const void* wq, int64_t
 int reidmi_gemm_f16_w4(const void* A, int64_t lda, const void* W, int64_t ldw, int64_t M, int64_t N, int64_t K,
                        const float* bias, void* out, int64_t ldc, int nostore, void* stream);
 
+/* The round-robin vision attention kernel (mhsa_rr_kernel: 8 waves walk (head, 32-query block)
+ * units over three LDS slots) for non-causal 205 <= L <= 212 with V^T rows of 212 elements:
+ * bit-identical to reidmi_mhsa_f16 (which takes V^T rows of reidmi_attn_lpad(L)), measured no
+ * faster, so only the tools library has it. */
+int reidmi_mhsa_f16_rr(const void* q, const void* k, const void* vt, void* o, int64_t nseq, int L, int H,
+                       void* stream);
+
 int reidmi_gemm_f16_qkv(const void* A, int64_t lda, const void* W, int64_t ldw, int64_t nseq, int L, int H,
                         const float* bias, const void* rowstat, const float* colsum, void* q, void* k, void* vt,
                         int lpad, void* stream);

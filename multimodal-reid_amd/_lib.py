@@ -104,6 +104,7 @@ TOOLS_SIGNATURES = {
                                  _vp],
     "reidmi_gemm_f16_w4": [_vp, _i64, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _i64, _i32, _vp],
     "reidmi_gemm_f16_qkv": [_vp, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp],
+    "reidmi_mhsa_f16_rr": [_vp, _vp, _vp, _vp, _i64, _i32, _i32, _vp],
 }
 # entry points with struct arguments are typed in model.py (reidmi_vit_*, reidmi_text_*)
 STRUCT_ENTRY_POINTS = ("reidmi_vit_workspace_bytes", "reidmi_vit_forward", "reidmi_text_workspace_bytes",

@@ -167,6 +167,9 @@ constexpr int kAttnPipeStores = 4;
 #ifndef ATTN_PIPE
 #define ATTN_PIPE 1
 #endif
+#if !defined(REIDMI_TOOLS) && ATTN_PIPE != 1
+#error "attention.hip: ATTN_PIPE variants build only with -DREIDMI_TOOLS (never into libreidmi.so)"
+#endif
 
 template <int I, int N, typename F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -221,7 +224,7 @@ __device__ uint64_t g_attn_stamps[256 * 8 * 8 * 8];
 
 // mid(): called once in the P.V phase (after block NKB/2's MFMAs), after(): right after the
 // last P.V MFMA, before the O stores — the caller's prefetch for the next head goes there.
-template <int NKB, typename Mid, typename After>
+template <int NKB, int VS_ = NKB * 32 + 4, typename Mid, typename After>
 __device__ __forceinline__ void attn_block_pipe(const _Float16* sK, const _Float16* sV, const f16x8 (&qf)[4], int qi,
                                                 int L, int64_t bh, int H, _Float16* __restrict__ o, float scale_log2,
                                                 Mid&& mid, After&& after
@@ -230,7 +233,7 @@ __device__ __forceinline__ void attn_block_pipe(const _Float16* sK, const _Float
                                                 uint64_t* stamp
 #endif
 ) {
-    constexpr int VS = NKB * 32 + 4;  // vt_stride(LP)
+    constexpr int VS = VS_;  // V^T row stride in LDS (mhsa_pipe_kernel: vt_stride(LP); mhsa_rr_kernel: 212)
     const int lane = threadIdx.x & 63;
     const int hh = lane >> 5, ql = lane & 31;
     // K fragment bases (one per 16-wide k-step; the key block is an immediate: the swizzle
@@ -683,6 +686,179 @@ __global__ __launch_bounds__(NKB * 64) void mhsa_pipe_kernel(const _Float16* __r
     }
 }
 
+// ----------------------------------------------------------- round-robin units (round 6)
+// Built only into the tools library (libreidmi_tools.so, REIDMI_TOOLS): bit-exact with
+// mhsa_pipe_kernel and measured no faster (profiles/r06/attn_rr_ab.txt), so the
+// product library does not ship it.
+// mhsa_pipe_kernel runs one (sequence, head) at a time on ceil(L/32) = 7 waves, and 7 waves on
+// a CU's 4 SIMDs leave three SIMDs with two waves and one with one: a head's time follows the
+// busiest SIMD (2 units of 32 queries), 8/7 of the balanced 7/4 (the round-5
+// length scan).  Here 8 waves walk the workgroup's (head, 32-query block) UNITS round-robin:
+// round r gives wave w unit u = 8r + w of the workgroup's sequence (local head j = u / NKB,
+// block u % NKB; global head blockIdx.x + j * gridDim.x), so every SIMD runs two units per
+// round and a round completes 8/7 heads.  A round touches at most two heads; three LDS slots
+// hold them and the head the next round adds, slot j % 3 — K [VS][64] (rows < L written,
+// XOR-swizzled as in mhsa_pipe_kernel) + V^T [64][VS] with VS = 212 for L in 205..212 (the
+// caller's V^T rows; 212 = 4 mod 8 keeps the P.V reads conflict-free): 3 x 54 272 B + 64 B of read
+// overhang = 162 880 B.  The reads past a slot's K rows or V^T columns are the masked keys of
+// attn_block_pipe (scores replaced by -inf, V^T zeroed in registers), as in mhsa_pipe_kernel.
+// Loads of the head the next round adds (wave-uniform schedule): its slot's previous head either
+// finished before this round — the older waves issue its K at the round's start and its V^T after
+// their P.V (as mhsa_pipe_kernel's prefetch) — or its last unit is this round's unit 8r (wave 0's;
+// once every 7 rounds, when the next round adds two heads): wave 0 then issues the new head's K
+// after its own S phase (mid) and its V^T after its own P.V (after), so the slot is refilled
+// right behind its last reader.  One barrier per round; each wave's own loads are retired by
+// vmcnt(kAttnPipeStores) in front of it (its O stores stay in flight).  Same arithmetic as
+// mhsa_pipe_kernel (attn_block_pipe): bit-identical outputs.
+#ifdef REIDMI_TOOLS
+constexpr int kRrWaves = 8, kRrSlots = 3;
+constexpr int kRrVS = 212, kRrLmin = 205;  // V^T rows of kRrVS for L in [kRrLmin, kRrVS]
+
+template <int NKB, int VS>
+__global__ __launch_bounds__(kRrWaves * 64, 1) void mhsa_rr_kernel(const _Float16* __restrict__ q,
+                                                                 const _Float16* __restrict__ k,
+                                                                 const _Float16* __restrict__ vt,
+                                                                 _Float16* __restrict__ o, int L, int H,
+                                                                 int64_t nbh, float scale_log2) {
+    constexpr int NW = kRrWaves, NS = kRrSlots;
+    constexpr int KR = VS;                              // K rows per slot (>= L)
+    constexpr int SLOT = KR * 64 + 64 * VS;             // halves
+    constexpr int KPIECES = (KR + 7) / 8;               // 1-KiB pieces of 8 K rows (rows >= L skipped)
+    constexpr int VBYTES = 64 * VS * 2;                 // V^T blob: its HBM row stride == VS
+    constexpr int VPIECES = (VBYTES + 1023) / 1024;     // the last may be partial
+    constexpr int VLAST = (VBYTES - (VPIECES - 1) * 1024) / 16;
+    static_assert(VS % 8 == 4 && VBYTES % 16 == 0, "V^T row stride: 2 mod 4 dwords");
+    static_assert(NKB >= 7, "8 consecutive units must span at most two heads (three slots)");
+    extern __shared__ __attribute__((aligned(16))) _Float16 lds[];
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int hh = lane >> 5, ql = lane & 31;
+    const int G = (int)gridDim.x, b0 = (int)blockIdx.x;
+    // this workgroup's heads j = 0 .. nh-1 are the global heads b0 + j * G (nbh < 2^31: the caller)
+    const int nh = (int)((nbh - b0 + G - 1) / G);
+    if (nh <= 0) return;
+    const int U = nh * NKB, R = (U + NW - 1) / NW;
+    auto head_k = [&](int j) { return k + ((int64_t)b0 + (int64_t)j * G) * L * 64; };
+    auto head_v = [&](int j) { return vt + ((int64_t)b0 + (int64_t)j * G) * 64 * VS; };
+    auto slot = [&](int j) { return lds + (j % NS) * SLOT; };
+
+    auto issue_k = [&](const _Float16* kh, _Float16* sK, int first, int step) {
+#pragma unroll 1
+        for (int pc = first; pc < KPIECES; pc += step) {
+            const int r = 8 * pc + (lane >> 3);
+            const int kc = (lane & 7) ^ ((r >> 1) & 7);
+            if (r < L)
+                __builtin_amdgcn_global_load_lds(kh + r * 64 + kc * 8, (lds_ptr_t)(sK + pc * 512), 16, 0, 0);
+        }
+    };
+    auto issue_v = [&](const _Float16* vh, _Float16* sV, int first, int step) {
+#pragma unroll 1
+        for (int pc = first; pc < VPIECES; pc += step)
+            if (pc + 1 < VPIECES || lane < VLAST)  // never read or write past the blob
+                __builtin_amdgcn_global_load_lds(vh + pc * 512 + lane * 8, (lds_ptr_t)(sV + pc * 512), 16, 0, 0);
+    };
+    // Q rows of unit u's queries (rows >= L read row L-1: finite, never stored); inline-asm
+    // loads retired by the round's counted wait, every use ordered after it by pin()
+    auto q_row = [&](int u) {
+        const int j = u / NKB;
+        const int qi = (u - j * NKB) * 32 + ql;
+        return q + (((int64_t)b0 + (int64_t)j * G) * L + (qi < L ? qi : L - 1)) * 64 + hh * 8;
+    };
+    auto load_q = [&](const _Float16* qh, f16x8* qf) {
+        asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(qf[0]) : "v"(qh) : "memory");
+        asm volatile("global_load_dwordx4 %0, %1, off offset:32" : "=v"(qf[1]) : "v"(qh) : "memory");
+        asm volatile("global_load_dwordx4 %0, %1, off offset:64" : "=v"(qf[2]) : "v"(qh) : "memory");
+        asm volatile("global_load_dwordx4 %0, %1, off offset:96" : "=v"(qf[3]) : "v"(qh) : "memory");
+    };
+    auto pin = [&](f16x8* qf) { asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3])); };
+
+    // prologue: the heads of round 0, and each wave's first Q
+    int loaded = (NW - 1) / NKB < nh - 1 ? (NW - 1) / NKB : nh - 1;  // last head whose loads are issued
+    for (int j = 0; j <= loaded; j++) {
+        issue_k(head_k(j), slot(j), wid, NW);
+        issue_v(head_v(j), slot(j) + KR * 64, wid, NW);
+    }
+    f16x8 qf[4];
+    if (wid < U) load_q(q_row(wid), qf);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    pin(qf);
+    __builtin_amdgcn_s_barrier();
+    const bool older = wid < 4;
+    for (int r = 0; r < R; r++) {
+        const int u = r * NW + wid, un = u + NW;
+        // this round's heads: issued in earlier rounds by the schedule below; one it cannot cover
+        // is loaded here with everyone waiting (never taken for NKB = 7 and 8 waves: kept so any
+        // shape stays correct)
+        {
+            const int need = (r * NW + NW - 1 < U ? r * NW + NW - 1 : U - 1) / NKB;
+            if (loaded < need) {
+                for (int j = loaded + 1; j <= need; j++) {
+                    issue_k(head_k(j), slot(j), wid, NW);
+                    issue_v(head_v(j), slot(j) + KR * 64, wid, NW);
+                }
+                loaded = need;
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+            }
+        }
+        // the head(s) the next round adds: pa (its slot's head finished before this round) and
+        // pb (its slot's head ends with this round's unit r * NW, wave 0's); wave-uniform
+        int pa = -1, pb = -1;
+        if ((r + 1) * NW < U) {
+            const int need = ((r + 1) * NW + NW - 1 < U ? (r + 1) * NW + NW - 1 : U - 1) / NKB;
+            while (loaded < need) {
+                const int c = loaded + 1, prev_end = (c - NS) * NKB + NKB - 1;
+                if ((c < NS || prev_end < r * NW) && pa < 0) {
+                    pa = c;
+                } else if (prev_end == r * NW && pb < 0) {
+                    pb = c;
+                } else {
+                    break;
+                }
+                loaded = c;
+            }
+        }
+        // pa's loads are shared by the older waves (waves 1-3 when wave 0 carries pb's)
+        const int w0 = pb >= 0 ? 1 : 0, nws = 4 - w0;
+        const bool share_a = pa >= 0 && older && wid >= w0;
+        const bool carry_b = pb >= 0 && wid == 0;
+        const _Float16* ka = share_a ? head_k(pa) : k;
+        const _Float16* va = share_a ? head_v(pa) : vt;
+        _Float16* sa = slot(share_a ? pa : 0);
+        const _Float16* kb = carry_b ? head_k(pb) : k;
+        const _Float16* vb = carry_b ? head_v(pb) : vt;
+        _Float16* sb = slot(carry_b ? pb : 0);
+        const _Float16* qn_row = q_row(un < U ? un : 0);
+        f16x8 qn[4];
+        if (share_a) issue_k(ka, sa, wid - w0, nws);
+        if (un < U && older) load_q(qn_row, qn);
+        if (u < U) {
+            const int j = u / NKB;
+            const _Float16* sK = slot(j);
+            attn_block_pipe<NKB, VS>(
+                sK, sK + KR * 64, qf, (u - j * NKB) * 32 + ql, L, (int64_t)b0 + (int64_t)j * G, H, o, scale_log2,
+                [&] {
+                    if (un < U && !older) load_q(qn_row, qn);
+                    if (carry_b) issue_k(kb, sb, 0, 1);  // after this wave's S phase: its K is no longer read
+                },
+                [&] {
+                    if (share_a) issue_v(va, sa + KR * 64, wid - w0, nws);
+                    if (carry_b) issue_v(vb, sb + KR * 64, 0, 1);  // after its P.V: its V^T is no longer read
+                });
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kAttnPipeStores) : "memory");
+        } else {  // no unit this round (the last round only; no next-round loads then)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();
+        if (un < U) {
+            pin(qn);
+#pragma unroll
+            for (int ks = 0; ks < 4; ks++) qf[ks] = qn[ks];
+        }
+    }
+}
+#endif  // REIDMI_TOOLS (round-robin vision attention)
+
 // ======================================================== fused QKV GEMM + attention
 // Built only into the tools library (libreidmi_tools.so, REIDMI_TOOLS): bit-exact with the
 // two-kernel block and measured slower, so the product library does not ship it.
@@ -1058,6 +1234,28 @@ static int launch_mhsa_pipe(const void* q, const void* k, const void* vt, void* 
     RM_LAUNCHED();
     return OK;
 }
+
+#ifdef REIDMI_TOOLS
+static int launch_mhsa_rr(const void* q, const void* k, const void* vt, void* o, int64_t nseq, int L, int H,
+                          hipStream_t s) {
+    constexpr int NKB = 7, VS = kRrVS;
+    // three slots + the overhang of the last slot's masked V^T reads (< 32 halves)
+    constexpr size_t lds = (size_t)kRrSlots * (VS * 64 + 64 * VS) * 2 + 64;
+    static_assert(lds <= 160 * 1024, "three slots must fit the CU's LDS");
+    auto kern = mhsa_rr_kernel<NKB, VS>;
+    static bool attr = false;
+    if (!attr) {
+        RM_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        attr = true;
+    }
+    const int64_t nbh = nseq * H;  // < 2^31 (mhsa)
+    const int64_t grid = nbh < num_cu() ? nbh : num_cu();  // one workgroup per CU (LDS)
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kRrWaves * 64), lds, s, (const _Float16*)q,
+                       (const _Float16*)k, (const _Float16*)vt, (_Float16*)o, L, H, nbh, 0.125f * 1.4426950408889634f);
+    RM_LAUNCHED();
+    return OK;
+}
+#endif  // REIDMI_TOOLS
 
 template <int NKB, bool CAUSAL>
 static int launch_mhsa(const void* q, const void* k, const void* vt, void* o, int64_t nseq, int L, int H,
@@ -1619,3 +1817,14 @@ REIDMI_API int reidmi_mhsa_f16(const void* q, const void* k, const void* vt, voi
                                 int causal, void* stream) {
     return mhsa(q, k, vt, o, nseq, L, H, causal != 0, (hipStream_t)stream);
 }
+
+#ifdef REIDMI_TOOLS
+// mhsa_rr_kernel (8 waves on round-robin (head, 32-query block) units, three LDS slots) for
+// non-causal L in 205..212 with V^T rows of 212: the round-6 A/B of the product's two-stage
+// kernel, bit-identical to it (tests/test_gpu_encoder.py, tools/attn_rr_ab.py).
+REIDMI_API int reidmi_mhsa_f16_rr(const void* q, const void* k, const void* vt, void* o, int64_t nseq, int L, int H,
+                                  void* stream) {
+    RM_REQUIRE(L >= kRrLmin && L <= kRrVS && nseq * H < (1ll << 31), "reidmi_mhsa_f16_rr: 205 <= L <= 212");
+    return launch_mhsa_rr(q, k, vt, o, nseq, L, H, (hipStream_t)stream);
+}
+#endif

@@ -212,6 +212,36 @@ def test_mhsa(gpu, L, causal):
     assert (got - ref).abs().max() < 5e-3  # fp16 P and O (bf16 needed 3e-2)
 
 
+@pytest.mark.parametrize("L,nseq,H", [(211, 300, 12), (211, 1, 12), (211, 21, 12), (211, 23, 12), (205, 40, 12),
+                                      (208, 3, 4), (209, 100, 12), (212, 64, 16)])
+def test_mhsa_rr_bitexact_vs_two_stage_kernel(gpu, L, nseq, H):
+    """The round-robin vision kernel of the tools library (mhsa_rr_kernel: 8 waves walk (head,
+    32-query block) units over three LDS slots, V^T rows of 212; reidmi_mhsa_f16_rr — round 6's
+    A/B, measured no faster) against the product's two-stage kernel (reidmi_mhsa_f16,
+    V^T rows of reidmi_attn_lpad(L)): the same bits for every output.  Head counts below, at and
+    above one per CU and workgroup sequences of 1-15 heads, so every load path of its schedule
+    runs (the prologue's two heads, the shared prefetch, wave 0's refill of a slot its own last
+    unit just read, idle waves in a partial last round); NaN in every V^T padding column."""
+    from multimodal_reid_amd import _lib as L_
+    lp = L_.load().reidmi_attn_lpad(L)
+    g = torch.Generator(device="cuda").manual_seed(L * 7 + nseq)
+    n = nseq * H
+    q = (torch.randn(n, L, 64, generator=g, device="cuda") * 2).half()
+    k = (torch.randn(n, L, 64, generator=g, device="cuda") * 2).half()
+    v = torch.randn(n, L, 64, generator=g, device="cuda").half()
+    vt_rr = torch.full((n, 64, 212), float("nan"), dtype=torch.float16, device="cuda")
+    vt_rr[:, :, :L] = v.transpose(1, 2)
+    vt = torch.full((n, 64, lp), float("nan"), dtype=torch.float16, device="cuda")
+    vt[:, :, :L] = v.transpose(1, 2)
+    o_rr = torch.full((nseq * L, H * 64), float("nan"), dtype=torch.float16, device="cuda")
+    o = torch.full((nseq * L, H * 64), float("nan"), dtype=torch.float16, device="cuda")
+    L_.call_tools("reidmi_mhsa_f16_rr", L_.ptr(q), L_.ptr(k), L_.ptr(vt_rr), L_.ptr(o_rr), nseq, L, H, L_.stream())
+    L_.call("reidmi_mhsa_f16", L_.ptr(q), L_.ptr(k), L_.ptr(vt), L_.ptr(o), nseq, L, H, 0, L_.stream())
+    torch.cuda.synchronize()
+    assert torch.isfinite(o).all()
+    assert torch.equal(o_rr.view(torch.int16), o.view(torch.int16))
+
+
 @pytest.mark.parametrize("M,N,K", [(3000, 768, 3072), (513, 2304, 768), (256, 256, 128)])
 def test_gemm_w4_prototype_bitexact(gpu, M, N, K):
     """The one-wave-per-SIMD GEMM prototype of the tools library gives the shipped
