@@ -138,7 +138,7 @@ def read_files(files, out=None, nthreads=0):
     offsets = np.zeros(n + 1, np.int64)
     vp = ctypes.c_void_p
     if kinds == {True}:
-        blobs = [f if isinstance(f, bytes) else bytes(f) for f in files]
+        blobs = [f if type(f) is bytes else bytes(f) for f in files]  # exact bytes: the layout _bytes_pointers reads
         offsets[1:] = np.cumsum(np.fromiter(map(len, blobs), np.int64, n))
         total = int(offsets[-1])
         buf = out[:total] if out is not None and out.size >= total else np.empty(total, np.uint8)
