@@ -845,6 +845,7 @@ def _parse(argv=None):
     ap.add_argument("--no-backend", action="store_true")
     ap.add_argument("--no-preprocess", action="store_true")
     ap.add_argument("--no-files", action="store_true")
+    ap.add_argument("--files-batch", type=int, default=4096)  # the files_to_map leg's get_loader batch
     return ap.parse_args(argv)
 
 
@@ -954,7 +955,7 @@ def main():
         if not a.no_jpeg:
             line["jpeg"] = jpeg_leg(dev, cpu=cpu)
         if not a.no_files and world == 1:
-            line["files_to_map"] = files_leg(wl, dev)
+            line["files_to_map"] = files_leg(wl, dev, batch=a.files_batch)
             line["files_to_map"]["hbm_resident_step_s"] = round(elapsed / a.steps, 4)
         threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
         if not a.no_rerank:

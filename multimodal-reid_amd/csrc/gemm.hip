@@ -43,6 +43,9 @@ constexpr int GB_M = 128, GB_N = 128, GB_K = 64;
 #ifndef GEMM_VAR_NOSTORE
 #define GEMM_VAR_NOSTORE 0
 #endif
+#ifndef GEMM_VAR_GELU1  // timing-only (wrong results): QuickGELU with one transcendental per element
+#define GEMM_VAR_GELU1 0   // (VERDICT r5 lever (b): the ceiling of any single-transcendental form)
+#endif
 #ifndef GEMM_VAR_NOGELU
 #define GEMM_VAR_NOGELU 0
 #endif
@@ -86,7 +89,7 @@ constexpr int GB_M = 128, GB_N = 128, GB_K = 64;
 // any value but the shipped one is refused outside a tools / variant build (-DREIDMI_TOOLS:
 // libreidmi_tools.so, tools/build_variant.py), so none can enter libreidmi.so.
 #if !defined(REIDMI_TOOLS) &&                                                                              \
-    (GEMM_VAR_NOSTORE != 0 || GEMM_VAR_NOGELU != 0 || GEMM_VAR_NOPSTAT != 0 || GEMM_VAR_NORESLOAD != 0 ||   \
+    (GEMM_VAR_NOSTORE != 0 || GEMM_VAR_NOGELU != 0 || GEMM_VAR_GELU1 != 0 || GEMM_VAR_NOPSTAT != 0 || GEMM_VAR_NORESLOAD != 0 ||   \
      GEMM_VAR_STAGGER != 0 || GEMM_VAR_DIAG_LOAD0 != 0 || GEMM_VAR_RPRE != 1 || GEMM_VAR_FB2 != 1 ||       \
      GEMM_VAR_STAG_SHIFT != 0 || GEMM_VAR_STAG_MASK != 1 || GEMM_VAR_STAG_SLP != 127 || GEMM_VAR_NODMA != 0 || \
      GEMM_VAR_ASAME != 0 || GEMM_VAR_NOWAIT != 0)
@@ -108,7 +111,11 @@ __device__ __forceinline__ uint32_t cvt_pk_f16(float a, float b) {
 __device__ __forceinline__ f32x2v quick_gelu2(f32x2v x) {
     const f32x2v y = x * -2.4554669595930157f;
     const f32x2v d = f32x2v{__builtin_amdgcn_exp2f(y.x), __builtin_amdgcn_exp2f(y.y)} + 1.0f;
+#if GEMM_VAR_GELU1
+    return x * (2.0f - d);  // one packed FMA in place of the two v_rcp_f32: any one-transcendental form costs more
+#else
     return x * f32x2v{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+#endif
 }
 
 __device__ __forceinline__ f32x4 mfma16(const f16x8& w, const f16x8& a, const f32x4& c) {
