@@ -595,7 +595,7 @@ def market_jpeg_files(wl, dev, quality=90, threads=16):
         return list(ex.map(enc, q)), list(ex.map(enc, g))
 
 
-def files_leg(wl, dev, batch=4096, reps=2):
+def files_leg(wl, dev, batch=8192, reps=2):
     """VERDICT r5 Next #4: Market from 19 281 host JPEG buffers to mAP through the drop-in surface
     — loader.get_loader (native threaded gather into pinned buffers + header parse on a host
     thread; H2D + reidmi_jpeg_decode + reidmi_preprocess_u8 on a side stream, one batch ahead)
@@ -845,7 +845,7 @@ def _parse(argv=None):
     ap.add_argument("--no-backend", action="store_true")
     ap.add_argument("--no-preprocess", action="store_true")
     ap.add_argument("--no-files", action="store_true")
-    ap.add_argument("--files-batch", type=int, default=4096)  # the files_to_map leg's get_loader batch
+    ap.add_argument("--files-batch", type=int, default=8192)  # files_to_map get_loader batch (profiles/r06/files_batch_sweep.txt)
     return ap.parse_args(argv)
 
 
