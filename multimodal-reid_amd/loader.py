@@ -92,9 +92,18 @@ class _Pipeline:
     """The shared source of a plain / augmented loader pair (see the module docstring)."""
 
     def __init__(self, items, batch_size, image_height, image_width, model_type, dtype, device, host_threads,
-                 depth, tta_seed):
+                 depth, tta_seed, shard=None):
         if dtype not in (torch.float32, torch.float16):
             raise ValueError("dtype must be torch.float32 or torch.float16")
+        items = list(items)
+        # RandomCrop offsets of every item, drawn once for the whole list (the reference draws them
+        # unseeded in the workers, data_prepare.py:266-267), so a shard's items get the offsets
+        # they get in one process
+        tta = tta_offsets(len(items), tta_seed)
+        if shard is not None:  # this rank's contiguous shard of the list (distributed.shard)
+            from .distributed import shard as _shard
+            lo, hi = _shard(len(items), *shard)
+            items, tta = items[lo:hi], tta[lo:hi]
         self.files, (self.pids, self.cams, self.seqs, self.idxs) = _items(items)
         self.N = len(self.files)
         self.bs = int(batch_size)
@@ -113,9 +122,7 @@ class _Pipeline:
         self.host = {}      # batch -> future of the host stage
         self.ready = {}     # batch -> [images, event, slot, jpeg batch, status checked] on the side stream
                             # (or the exception its host stage raised)
-        # RandomCrop offsets of every item, drawn once (the reference draws them unseeded in the
-        # workers, data_prepare.py:266-267), on the device for the encoder's im2col
-        self.tta = torch.from_numpy(tta_offsets(self.N, tta_seed)).to(self.device)
+        self.tta = torch.from_numpy(np.ascontiguousarray(tta)).to(self.device)  # for the encoder's im2col
 
     def rows(self, k):
         return k * self.bs, min(self.N, (k + 1) * self.bs)
@@ -247,23 +254,25 @@ class DeviceLoader:
 
 
 def loader_pair(items, batch_size, image_height=256, image_width=128, model_type="vit", dtype=torch.float16,
-                device=None, host_threads=0, depth=2, tta_seed=0):
+                device=None, host_threads=0, depth=2, tta_seed=0, shard=None):
     """(plain loader, augmented loader) over one item list, sharing one decode pipeline."""
     p = _Pipeline(items, batch_size, image_height, image_width, model_type, dtype, device, host_threads, depth,
-                  tta_seed)
+                  tta_seed, shard)
     return DeviceLoader(p, False), DeviceLoader(p, True)
 
 
 def get_loader(dataset, batch_size, image_height, image_width, model_type, dtype=torch.float16, device=None,
-               host_threads=0, depth=2, tta_seed=0):
+               host_threads=0, depth=2, tta_seed=0, shard=None):
     """data_prepare.py:256-284 for an already-listed dataset (`dataset.query`, `dataset.gallery`):
     returns (loader_gallery, loader_query, loader_gallery_augmented, loader_query_augmented),
     the reference's order.  `tta_seed` seeds the augmented views' RandomCrop offsets (gallery
-    and query draw from seeds tta_seed and tta_seed + 1)."""
+    and query draw from seeds tta_seed and tta_seed + 1).  `shard=(rank, world)`: each loader
+    walks this rank's contiguous shard of its list (one process per GPU; the items keep the
+    offsets they have in one process) — feed the shards to get_cmc_map(..., sharded=True)."""
     if model_type != "vit":
         raise NotImplementedError("libreidmi implements the ViT tower (north-star path) only")
     g, ga = loader_pair(dataset.gallery, batch_size, image_height, image_width, model_type, dtype, device,
-                        host_threads, depth, tta_seed)
+                        host_threads, depth, tta_seed, shard)
     q, qa = loader_pair(dataset.query, batch_size, image_height, image_width, model_type, dtype, device,
-                        host_threads, depth, None if tta_seed is None else tta_seed + 1)
+                        host_threads, depth, None if tta_seed is None else tta_seed + 1, shard)
     return g, q, ga, qa

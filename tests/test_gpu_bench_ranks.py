@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 QUICK = ["--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--no-rerank", "--no-msmt17", "--no-text",
-         "--no-jpeg", "--no-backend", "--no-preprocess"]
+         "--no-jpeg", "--no-backend", "--no-preprocess", "--no-files"]
 
 
 def _bench(*args):
