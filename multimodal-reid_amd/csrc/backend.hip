@@ -163,8 +163,8 @@ __global__ __launch_bounds__(256) void distmat_f32_kernel(
 #define DM2_BAND 4
 #endif
 #if !defined(REIDMI_TOOLS) && (DM2_BK_ != 16 || DM2_MINWG_ != 4 || DM2_BAND != 4 || defined(RS_STATS) || \
-                               defined(RS_SINGLE_PASS))
-#error "backend.hip: DM2_* / RS_* variants build only with -DREIDMI_TOOLS (never into libreidmi.so)"
+                               defined(RS_SINGLE_PASS) || defined(EV_STAMPS) || defined(EV_PREFETCH))
+#error "backend.hip: DM2_* / RS_* / EV_* variants build only with -DREIDMI_TOOLS (never into libreidmi.so)"
 #endif
 constexpr int DM2_BK = DM2_BK_, DM2_LD = DM_BM + 1;
 constexpr int DM2_F4 = DM2_BK / 4;            // float4 per operand row and K-step
@@ -1322,6 +1322,9 @@ __global__ void ev_pack_kernel(const int64_t* __restrict__ gp, int64_t G, int64_
 // than EVW_MAXP positives or EVW_MAXJ junk items are left to eval_rows_kernel (valid = 2).
 // Per-phase cycle stamps: profiles/r02/eval_rows_phase_stamps.txt (-DEV_STAMPS build).
 constexpr int EVW_MAXP = 512, EVW_MAXJ = 256, EVW_T = 1024;
+#ifndef EV_PREFETCH
+#define EV_PREFETCH 0
+#endif
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void eval_rows_wg_kernel(
     const float* __restrict__ dist, int64_t G, int64_t ld, const int64_t* __restrict__ qp,
@@ -1336,7 +1339,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
     __shared__ int s_m, s_nj, s_ns;
     __shared__ double tvals[AP_STACK];
     __shared__ int tops[AP_STACK];
-    __shared__ int2 bucket[EVW_T];  // [S[t], S[t+1]): the positives whose bucket is t
+    // bucket t: {bits of the first positive in it (+inf when none), S[t] | 1 << 16 when it holds
+    // two or more}; entry T = {+inf, m} closes the table (S[T] = m)
+    __shared__ int2 bucket[EVW_T + 1];
+    __shared__ int trash[256];  // one histogram slot per thread for the items not binned
     const int tid = threadIdx.x, lane = tid & 63;
 #ifdef EV_STAMPS
     const uint64_t t0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
@@ -1348,6 +1354,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
     const uint64_t below = (1ull << lane) - 1;
     int* sidx = (int*)bucket;  // same-pid gallery indices of pass 1 (the bucket table comes later)
     constexpr int SCAP = EVW_MAXP + EVW_MAXJ;
+    // the distance pass's layout (16-byte loads after a scalar head) and its first chunk,
+    // loaded now so its latency hides behind the label pass and the sort
+    const int head = (int)(((16 - ((uintptr_t)row & 15)) & 15) >> 2);  // scalar items before 16-B alignment
+    const int h = head < G ? head : (int)G;
+    const int nv = (int)((G - h) >> 2);  // float4 groups (G < 2^31)
+    const float4* r4 = (const float4*)(row + h);
+    constexpr int U2 = 4;
+    float4 v[U2];
+    auto load_chunk = [&](int g0) {  // past the row's end: reload its last group, not binned
+#pragma unroll
+        for (int u = 0; u < U2; u++) {
+            const int g = g0 + u * 256 + tid;
+            v[u] = r4[g < nv ? g : nv - 1];
+        }
+    };
+#if EV_PREFETCH
+    if (nv > 0) load_chunk(0);
+#endif
     if (tid == 0) { s_m = 0; s_nj = 0; s_ns = 0; }
     __syncthreads();
     // ---- pass 1: labels -> indices of the gallery items with the query's pid (ballot
@@ -1465,7 +1489,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
     // bucket table narrows each item's candidates: t(x) = clamp(floor((x - v_0) * T /
     // (v_last - v_0)), 0, T-1) is monotone in x (the same float operations for every x), so
     // positives in buckets below t(x) are all smaller, those above all larger, and only the
-    // positives of bucket t(x) (usually none or one) need the exact (value, index) compare.
+    // positives of bucket t(x) need the exact (value, index) compare.  The table entry carries
+    // the bucket's first positive value: with at most one positive in the bucket and no tie
+    // with it, b = S[t] + (v_first < x) — branch-free, one 8-byte LDS read per item; buckets
+    // of two or more positives and exact ties take the (value, index) walk, per wave only when
+    // some lane needs it.
     const float lv = pv[m - 1];
     const int li = pi[m - 1];
     const float v0 = pv[0];
@@ -1476,83 +1504,87 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
     float scale = (float)T / (lv - v0);
     if (!(scale <= 3.0e38f)) scale = 0.0f;
     const float c0 = -v0 * scale, tmax = (float)(T - 1);
-    auto bucket_of = [&](float x) {  // med3 clamps to [0, T-1], so truncation is the floor
+    auto bucket_of = [&](float x) {  // med3 clamps to [0, T-1] (NaN to 0 or T-1), truncation floors
         return (int)__builtin_amdgcn_fmed3f(__builtin_fmaf(x, scale, c0), 0.0f, tmax);
     };
-    for (int t = tid; t < T; t += 256) {  // S[t] = #{k : t(pv_k) < t}
-        int lo = 0, hi = m;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (bucket_of(pv[mid]) < t) lo = mid + 1; else hi = mid;
+    constexpr int MULTI = 1 << 16;
+    for (int t = tid; t <= T; t += 256) {  // S[t] = #{k : t(pv_k) < t}; n_t positives in bucket t
+        int lo = m, n = 0;
+        if (t < T) {
+            lo = 0;
+            int hi = m;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (bucket_of(pv[mid]) < t) lo = mid + 1; else hi = mid;
+            }
+            int lo2 = lo, hi2 = m;
+            while (lo2 < hi2) {
+                const int mid = (lo2 + hi2) >> 1;
+                if (bucket_of(pv[mid]) <= t) lo2 = mid + 1; else hi2 = mid;
+            }
+            n = lo2 - lo;
         }
-        int lo2 = lo, hi2 = m;
-        while (lo2 < hi2) {
-            const int mid = (lo2 + hi2) >> 1;
-            if (bucket_of(pv[mid]) <= t) lo2 = mid + 1; else hi2 = mid;
-        }
-        bucket[t] = make_int2(lo, lo2);
+        bucket[t] = make_int2(n > 0 ? __float_as_int(pv[lo]) : 0x7f800000, lo | (n > 1 ? MULTI : 0));
     }
     __syncthreads();
 #ifdef EV_STAMPS
     t2 = __builtin_amdgcn_s_memtime();
 #endif
+    // b for an item of bucket t with entry e: the exact (value, index) walk over the bucket
+    auto walk = [&](int t, int2 e, float v, int j) {
+        int b = e.y & 0xFFFF;
+        const int end = bucket[t + 1].y & 0xFFFF;
+        while (b < end && key_less(pv[b], pi[b], v, j)) b++;
+        return b;
+    };
     auto bin = [&](float v, int j) {
         // after the last positive (b = m, not needed); NaN sorts last (np.argsort):
         // key_less(lv, li, v, j) || v != v, with the NaN test folded into !(v <= lv)
         if (!(v <= lv) || (v == lv && j > li)) return;
-        const int2 se = bucket[bucket_of(v)];
-        int b = se.x;
-        while (b < se.y && key_less(pv[b], pi[b], v, j)) b++;
-        atomicAdd(&hist[b], 1);
+        const int t = bucket_of(v);
+        atomicAdd(&hist[walk(t, bucket[t], v, j)], 1);
     };
-    const int head = (int)(((16 - ((uintptr_t)row & 15)) & 15) >> 2);  // scalar items before 16-B alignment
-    const int h = head < G ? head : (int)G;
     if (tid < h) bin(row[tid], tid);
-    const int64_t nv = (G - h) >> 2;  // float4 groups
-    const float4* r4 = (const float4*)(row + h);
-    constexpr int U2 = 4;
-    for (int64_t g0 = 0; g0 < nv; g0 += 256 * U2) {
-        float4 v[U2];
+    int* const mytrash = &trash[tid];
+    for (int g0 = 0; g0 < nv; g0 += 256 * U2) {
+        if (!EV_PREFETCH || g0 > 0) load_chunk(g0);
 #pragma unroll
         for (int u = 0; u < U2; u++) {
-            const int64_t g = g0 + u * 256 + tid;
-            v[u] = g < nv ? r4[g] : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-        // 8 items at a time: their bucket indices first, then the 8 bucket-table reads issued
-        // together (one LDS round trip per 8 items, not one per item), then the rare exact
-        // compares and the histogram adds
+            const int g = g0 + u * 256 + tid;
+            const float x[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+            int tb[4];
+            bool ok[4];
 #pragma unroll
-        for (int hu = 0; hu < U2; hu += 2) {
-            float x[8];
-            int jj[8], tb[8];
-            bool ok[8];
-#pragma unroll
-            for (int k = 0; k < 8; k++) {
-                const int u = hu + (k >> 2);
-                const int64_t g = g0 + u * 256 + tid;
-                x[k] = (k & 3) == 0 ? v[u].x : (k & 3) == 1 ? v[u].y : (k & 3) == 2 ? v[u].z : v[u].w;
-                jj[k] = h + (int)g * 4 + (k & 3);
+            for (int k = 0; k < 4; k++) {
                 // items after the last positive are not needed (b = m); NaN sorts last
                 // (np.argsort) and fails x <= lv.  An item tied with the last positive's value
-                // but after it (x == lv, j > li) is binned: the exact compares give it b = m,
-                // a count in hist[m] that no rank reads
-                ok[k] = g < nv && x[k] <= lv;
-                tb[k] = ok[k] ? bucket_of(x[k]) : 0;
+                // but after it (x == lv, j > li) is binned: it gets b = m, a count in hist[m]
+                // that no rank reads
+                ok[k] = (g < nv) & (x[k] <= lv);
+                tb[k] = bucket_of(x[k]);
             }
-            int2 se[8];
+            int2 se[4];
 #pragma unroll
-            for (int k = 0; k < 8; k++) se[k] = bucket[tb[k]];
+            for (int k = 0; k < 4; k++) se[k] = bucket[tb[k]];
+            int b[4];
+            bool sl[4], slow = false;
 #pragma unroll
-            for (int k = 0; k < 8; k++) {
-                if (ok[k]) {
-                    int b = se[k].x;
-                    while (b < se[k].y && key_less(pv[b], pi[b], x[k], jj[k])) b++;
-                    atomicAdd(&hist[b], 1);
-                }
+            for (int k = 0; k < 4; k++) {
+                const float vf = __int_as_float(se[k].x);
+                b[k] = (se[k].y & 0xFFFF) + (vf < x[k] ? 1 : 0);
+                sl[k] = ok[k] & ((se[k].y >= MULTI) | (vf == x[k]));
+                slow = slow | sl[k];
             }
+            if (__ballot(slow)) {
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+                    if (sl[k]) b[k] = walk(tb[k], se[k], x[k], h + g * 4 + k);
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) atomicAdd(ok[k] ? &hist[b[k]] : mytrash, 1);
         }
     }
-    for (int64_t j = h + nv * 4 + tid; j < G; j += 256) bin(row[j], (int)j);
+    for (int64_t j = h + (int64_t)nv * 4 + tid; j < G; j += 256) bin(row[j], (int)j);
     __syncthreads();
 #ifdef EV_STAMPS
     t3 = __builtin_amdgcn_s_memtime();

@@ -211,6 +211,33 @@ def test_eval_many_positives_and_junk_vs_oracle(gpu, G, pid_shift, pid_scale):
         assert np.array_equal(a.astype(b.dtype), b)
 
 
+@pytest.mark.parametrize("steps", [0, 16, 1024])
+def test_eval_bucket_paths_vs_oracle(gpu, steps):
+    """The main kernel's bucket binning (every query within its LDS lists): 1..300 positives
+    per query, distances continuous (steps 0) or quantised to 1/16 or 1/1024 (items tied with
+    positives, several positives per bucket: the exact (value, index) walk), with negative
+    values and +-inf mixed in.  Bit-exact against the oracle.  (NaN distances are outside the
+    contract: the oracle's comparator, like the kernel's, does not order them.)"""
+    r = np.random.default_rng(100 + steps)
+    Q, G = 48, 5003
+    gp = r.integers(1, 60, G).astype(np.int64)
+    gc = r.integers(0, 4, G).astype(np.int64)
+    gp[:300], gc[:300] = 77, np.arange(300) % 4     # query 0's identity: ~225 positives
+    qp = np.concatenate([[77], r.integers(1, 60, Q - 1)]).astype(np.int64)
+    qc = r.integers(0, 4, Q).astype(np.int64)
+    dist = (r.random((Q, G)) * 4 - 1).astype(np.float32)
+    if steps:
+        dist = (np.round(dist * steps) / steps).astype(np.float32)
+    dist[1::5, r.integers(0, G, 40)] = np.inf
+    dist[2::5, r.integers(0, G, 40)] = -np.inf
+    dist[3::5, r.integers(0, G, 40)] = dist[3::5, :1]  # more exact ties with a row's first item
+    dist[4] = 0.5                                    # one row of equal values: every compare a tie
+    rows = _eval_rows_np(dist, qp, gp, qc, gc)
+    ref = oracle.eval_rows(dist, qp, gp, qc, gc)
+    for a, b in zip(rows, ref):
+        assert np.array_equal(a.astype(b.dtype), b)
+
+
 @pytest.mark.parametrize("G,pid_shift", [(6007, 0), (9001, -(1 << 40))])
 def test_eval_beyond_lds_lists_vs_oracle(gpu, G, pid_shift):
     """Queries with more positives than the large-list kernel's LDS holds (> 2048) are

@@ -1,5 +1,6 @@
 """In-process A/B of reidmi_eval_rows across library builds (tools/build_variant.py) on Market-
-and MSMT17-size random distance matrices with synthetic labels; interleaved rounds, outputs
+and MSMT17-size random distance matrices with synthetic labels, and Market-size distances of
+identity-clustered features; interleaved rounds, outputs
 checked bit-identical across the builds.
 
     python tools/eval_ab.py LIB.so[,LIB2.so,...] [ROUNDS]"""
@@ -18,16 +19,26 @@ from multimodal_reid_amd import _lib as L, synthetic as syn  # noqa: E402
 from lib_ab import open_lib  # noqa: E402
 
 
+def clustered_distances(qp, gp, dev, dim=256, noise=2.2):
+    """Euclidean distances of L2-normalised identity-clustered features (positives near the
+    top of each row, as in the bench's Market step) instead of uniform random ones."""
+    from multimodal_reid_amd import evaluate
+    qf, gf = syn.features(qp, gp, dim=dim, seed=0, noise=noise)
+    qn = evaluate.l2_normalize_device(torch.from_numpy(qf).to(dev))
+    gn = evaluate.l2_normalize_device(torch.from_numpy(gf).to(dev))
+    return evaluate.euclidean_distance_device(qn, gn)
+
+
 def main():
     libs = [(os.path.basename(p), open_lib(p)) for p in sys.argv[1].split(",")]
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 3
     dev = torch.device("cuda")
     cases = []
-    for name in ("market1501", "msmt17"):
-        sp = syn.DATASET_SPLITS[name]
+    for name in ("market1501", "msmt17", "market1501-clustered"):
+        sp = syn.DATASET_SPLITS[name.split("-")[0]]
         Q, G = sp["num_query"], sp["num_gallery"]
         qp, gp, qc, gc = syn.labels(Q, G, sp["num_ids"], sp["num_cams"], seed=0, junk_frac=0.02)
-        d = torch.rand(Q, G, device=dev)
+        d = torch.rand(Q, G, device=dev) if "-" not in name else clustered_distances(qp, gp, dev)
         lab = [torch.from_numpy(a).to(dev) for a in (qp, gp, qc, gc)]
         cases.append((name, Q, G, d, lab))
     for r in range(rounds):

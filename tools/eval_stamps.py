@@ -1,5 +1,6 @@
 """Per-phase cycle stamps of eval_rows_wg_kernel (diagnostic build: tools/build_variant.py
-stamps backend.hip -DEV_STAMPS=1), Market-size random distances.  Phases: P1 label pass,
+stamps backend.hip -DEV_STAMPS=1), Market-size random distances (or, with a third argument
+"clustered", distances of identity-clustered features).  Phases: P1 label pass,
 P2 gather + sort + bucket table, P3 distance pass, P4 ranks + AP; start time spread."""
 import os
 import sys
@@ -21,7 +22,11 @@ dev = torch.device("cuda")
 sp = syn.DATASET_SPLITS[name]
 Q, G = sp["num_query"], sp["num_gallery"]
 qp, gp, qc, gc = syn.labels(Q, G, sp["num_ids"], sp["num_cams"], seed=0, junk_frac=0.02)
-d = torch.rand(Q, G, device=dev)
+if len(sys.argv) > 3 and sys.argv[3] == "clustered":
+    from eval_ab import clustered_distances  # noqa: E402
+    d = clustered_distances(qp, gp, dev)
+else:
+    d = torch.rand(Q, G, device=dev)
 lab = [torch.from_numpy(a).to(dev) for a in (qp, gp, qc, gc)]
 valid = torch.empty(Q, device=dev, dtype=torch.int32)
 first = torch.empty(Q, device=dev, dtype=torch.int64)
