@@ -188,7 +188,8 @@ def test_eval_market_scale_rows_vs_oracle(gpu):
 
 
 @pytest.mark.parametrize("G,pid_shift,pid_scale", [(3001, 0, 1), (4099, 0, 1), (3001, -(1 << 40), 1),
-                                                   (2053, (1 << 62) - 9, 1), (3001, 0, 100003), (4099, -5, 1 << 40)])
+                                                   (2053, (1 << 62) - 9, 1), (3001, 0, 100003), (4099, -5, 1 << 40),
+                                                   (3001, 5, 1800), (3001, 5, 7000)])  # wide 16-bit key ranges
 def test_eval_many_positives_and_junk_vs_oracle(gpu, G, pid_shift, pid_scale):
     """Queries whose positives (> 512) or junk items (> 256) exceed the main kernel's LDS
     lists go to the large-list kernel; ragged row starts (ld = G) exercise the 16-byte
