@@ -50,8 +50,9 @@ int reidmi_distmat_f32(const float* q, int64_t Q, int64_t ldq, const float* g, i
  * out[i*ldo+j] = (||q_i||^2 + ||g_j||^2) - 2 fp16(q_i).fp16(g_j), the dot products on the fp16
  * MFMA GEMM (fp32 accumulation), the squared norms exact fp32.  Not bit-exact with the
  * reference (reidmi_distmat_f32 is); |error| <= 2^-8 ||q_i|| ||g_j|| per entry (fp16-range rows).
- * ws: reidmi_distmat_f16_workspace_bytes(Q, G, D) bytes (fp16 copies padded to the GEMM tile
- * and the Q x round_up(G, 256) fp32 products). */
+ * The GEMM's epilogue writes the distances straight into out (no product buffer).
+ * ws: reidmi_distmat_f16_workspace_bytes(Q, G, D) bytes (fp16 copies padded to the GEMM tile,
+ * the squared norms). */
 int64_t reidmi_distmat_f16_workspace_bytes(int64_t Q, int64_t G, int64_t D);
 int reidmi_distmat_f16(const float* q, int64_t Q, int64_t ldq, const float* g, int64_t G, int64_t ldg, int64_t D,
                        float* out, int64_t ldo, void* ws, int64_t ws_bytes, void* stream);

@@ -16,15 +16,17 @@
 namespace reidmi {
 
 // --------------------------------------------------------------------------- norms
-// 256 rows per 256-thread workgroup, one row's fmaf chain per thread (k ascending, the
-// distance kernel's arithmetic).  With 16-byte rows the row segments are staged through LDS
-// 32 columns at a time by coalesced float4 loads (the next segment in flight while the
-// current one is summed), instead of 256 threads each walking its own row (uncoalesced).
-constexpr int RSQ_K = 32;
-__global__ __launch_bounds__(256) void row_sqnorm_kernel(const float* __restrict__ x, int64_t n, int64_t d,
-                                                         int64_t ld, float* __restrict__ out) {
-    __shared__ float tile[256][RSQ_K + 1];
-    const int64_t r0 = (int64_t)blockIdx.x * 256, i = r0 + threadIdx.x;
+// R rows per R-thread workgroup, one row's fmaf chain per thread (k ascending, the distance
+// kernel's arithmetic).  With 16-byte rows the row segments are staged through LDS 32 columns
+// at a time by coalesced float4 loads (the next segment in flight while the current one is
+// summed), instead of each thread walking its own row (uncoalesced).  R = 64: a Market gallery
+// (15 913 rows) is 249 workgroups, not 63 on 256 CUs (rows_sqnorm_launch).
+constexpr int RSQ_K = 32, RSQ_R = 64;
+template <int R>
+__global__ __launch_bounds__(R) void row_sqnorm_kernel(const float* __restrict__ x, int64_t n, int64_t d, int64_t ld,
+                                                       float* __restrict__ out) {
+    __shared__ float tile[R][RSQ_K + 1];
+    const int64_t r0 = (int64_t)blockIdx.x * R, i = r0 + threadIdx.x;
     if ((ld & 3) != 0 || ((uintptr_t)x & 15) != 0 || d < RSQ_K) {  // uniform
         if (i >= n) return;
         const float* r = x + i * ld;
@@ -33,13 +35,13 @@ __global__ __launch_bounds__(256) void row_sqnorm_kernel(const float* __restrict
         out[i] = acc;
         return;
     }
-    // float4 f = threadIdx.x + 256 u of a segment: row f / 8, columns 4 (f % 8) .. + 3
-    constexpr int U = 256 * RSQ_K / 4 / 256;
+    // float4 f = threadIdx.x + R u of a segment: row f / 8, columns 4 (f % 8) .. + 3
+    constexpr int U = RSQ_K / 4;
     float4 v[U];
     auto load = [&](int64_t k0) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const int f = threadIdx.x + 256 * u, row = f >> 3, c = (f & 7) * 4;
+            const int f = threadIdx.x + R * u, row = f >> 3, c = (f & 7) * 4;
             const int64_t gi = r0 + row < n ? r0 + row : n - 1;
             v[u] = *(const float4*)(x + gi * ld + k0 + c);
         }
@@ -50,7 +52,7 @@ __global__ __launch_bounds__(256) void row_sqnorm_kernel(const float* __restrict
     for (int64_t kt = 0; kt < nk; kt++) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const int f = threadIdx.x + 256 * u, row = f >> 3, c = (f & 7) * 4;
+            const int f = threadIdx.x + R * u, row = f >> 3, c = (f & 7) * 4;
             tile[row][c] = v[u].x;
             tile[row][c + 1] = v[u].y;
             tile[row][c + 2] = v[u].z;
@@ -66,6 +68,11 @@ __global__ __launch_bounds__(256) void row_sqnorm_kernel(const float* __restrict
     const float* r = x + i * ld;
     for (int64_t k = nk * RSQ_K; k < d; k++) acc = __builtin_fmaf(r[k], r[k], acc);
     out[i] = acc;
+}
+
+static void rows_sqnorm_launch(const float* x, int64_t n, int64_t d, int64_t ld, float* out, hipStream_t s) {
+    hipLaunchKernelGGL(row_sqnorm_kernel<RSQ_R>, dim3((unsigned)ceil_div(n, RSQ_R)), dim3(RSQ_R), 0, s, x, n, d, ld,
+                       out);
 }
 
 // y = x / max(sqrt(ss), 1e-12): one workgroup per row, coalesced.
@@ -301,7 +308,7 @@ static bool dm2_ok(const float* q, int64_t ldq, const float* g, int64_t ldg, int
 int distmat_self_launch(const float* x, int64_t N, int64_t ldx, int64_t D, float* out, int64_t ldo, float* ws,
                         hipStream_t s) {
     RM_REQUIRE(N > 0 && D > 0 && ldx >= D && ldo >= N && ws != nullptr, "distmat_self: bad shape");
-    hipLaunchKernelGGL(row_sqnorm_kernel, dim3(ceil_div(N, 256)), dim3(256), 0, s, x, N, D, ldx, ws);
+    rows_sqnorm_launch(x, N, D, ldx, ws, s);
     RM_LAUNCHED();
     if (!dm2_ok(x, ldx, x, ldx, D)) {
         dim3 grid(ceil_div(N, DM_BN), ceil_div(N, DM_BM));
@@ -1892,7 +1899,7 @@ using namespace reidmi;
 REIDMI_API int reidmi_row_sqnorm_f32(const float* x, int64_t n, int64_t d, int64_t ldx, float* out, void* stream) {
     RM_REQUIRE(n >= 0 && d >= 0 && ldx >= d, "row_sqnorm: bad shape");
     if (n == 0) return OK;
-    hipLaunchKernelGGL(row_sqnorm_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, (hipStream_t)stream, x, n, d, ldx, out);
+    rows_sqnorm_launch(x, n, d, ldx, out, (hipStream_t)stream);
     RM_LAUNCHED();
     return OK;
 }
@@ -1902,7 +1909,7 @@ REIDMI_API int reidmi_l2norm_f32(const float* x, int64_t n, int64_t d, int64_t l
     RM_REQUIRE(n >= 0 && d > 0 && ldx >= d && ldy >= d && ws != nullptr, "l2norm: bad shape or workspace");
     if (n == 0) return OK;
     hipStream_t s = (hipStream_t)stream;
-    hipLaunchKernelGGL(row_sqnorm_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, s, x, n, d, ldx, ws);
+    rows_sqnorm_launch(x, n, d, ldx, ws, s);
     RM_LAUNCHED();
     hipLaunchKernelGGL(row_scale_kernel, dim3((unsigned)n), dim3(256), 0, s, x, ws, d, ldx, y, ldy);
     RM_LAUNCHED();
@@ -1918,9 +1925,9 @@ int reidmi::distmat_impl(bool cosine, const float* q, int64_t Q, int64_t ldq, co
     hipStream_t s = (hipStream_t)stream;
     float* qq = ws;
     float* gg = ws + Q;
-    hipLaunchKernelGGL(row_sqnorm_kernel, dim3(ceil_div(Q, 256)), dim3(256), 0, s, q, Q, D, ldq, qq);
+    rows_sqnorm_launch(q, Q, D, ldq, qq, s);
     RM_LAUNCHED();
-    hipLaunchKernelGGL(row_sqnorm_kernel, dim3(ceil_div(G, 256)), dim3(256), 0, s, g, G, D, ldg, gg);
+    rows_sqnorm_launch(g, G, D, ldg, gg, s);
     RM_LAUNCHED();
     dim3 grid(ceil_div(G, DM_BN), ceil_div(Q, DM_BM));
     RM_REQUIRE(grid.y <= 65535, "distmat: too many query rows for one launch");

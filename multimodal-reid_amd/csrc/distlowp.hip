@@ -14,25 +14,17 @@ extern "C" int reidmi_row_sqnorm_f32(const float* x, int64_t n, int64_t d, int64
 namespace reidmi {
 
 __global__ __launch_bounds__(256) void rows_to_f16_kernel(const float* __restrict__ src, int64_t rows, int64_t cols,
-                                                          int64_t lds, int64_t rows_pad, _Float16* __restrict__ dst,
-                                                          int64_t ldd) {
-    // fp32 [rows][cols] -> fp16 [rows_pad][ldd]; padding rows and columns are zero
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= rows_pad * ldd) return;
-    const int64_t r = t / ldd, c = t - r * ldd;
-    dst[t] = (r < rows && c < cols) ? (_Float16)src[r * lds + c] : (_Float16)0.0f;
-}
-
-__global__ __launch_bounds__(256) void dist_finish_kernel(const float* __restrict__ dot, int64_t ldt,
-                                                          const float* __restrict__ qq, const float* __restrict__ gg,
-                                                          int64_t Q, int64_t G, float* __restrict__ out, int64_t ldo) {
-    const int64_t i = blockIdx.y;
-    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < G; j += (int64_t)gridDim.x * blockDim.x)
-        out[i * ldo + j] = (qq[i] + gg[j]) - 2.0f * dot[i * ldt + j];
+                                                          int64_t lds, _Float16* __restrict__ dst, int64_t ldd) {
+    // fp32 [rows][cols] -> fp16 [gridDim.x][ldd], one workgroup per destination row; padding
+    // rows and columns are zero
+    const int64_t r = blockIdx.x;
+    const float* s = src + r * lds;
+    _Float16* d = dst + r * ldd;
+    for (int64_t c = threadIdx.x; c < ldd; c += 256) d[c] = (r < rows && c < cols) ? (_Float16)s[c] : (_Float16)0.0f;
 }
 
 struct LowpPlan {
-    int64_t Dp, Gp, qh, gh, qq, gg, dot, total;
+    int64_t Dp, Gp, qh, gh, qq, gg, total;
 };
 
 static LowpPlan lowp_plan(int64_t Q, int64_t G, int64_t D) {
@@ -45,7 +37,6 @@ static LowpPlan lowp_plan(int64_t Q, int64_t G, int64_t D) {
     p.gh = o; o = al(o + p.Gp * p.Dp * 2);
     p.qq = o; o = al(o + Q * 4);
     p.gg = o; o = al(o + G * 4);
-    p.dot = o; o = al(o + Q * p.Gp * 4);
     p.total = o;
     return p;
 }
@@ -66,32 +57,28 @@ REIDMI_API int reidmi_distmat_f16(const float* q, int64_t Q, int64_t ldq, const 
     RM_REQUIRE(ws != nullptr && ws_bytes >= p.total, "distmat_f16: workspace smaller than reidmi_distmat_f16_workspace_bytes");
     if (Q == 0 || G == 0) return OK;
     RM_REQUIRE(q && g && out, "distmat_f16: null operand");
+    RM_REQUIRE(p.Gp < (1ll << 31), "distmat_f16: too many rows");
     hipStream_t s = (hipStream_t)stream;
     char* w = (char*)ws;
     _Float16* qh = (_Float16*)(w + p.qh);
     _Float16* gh = (_Float16*)(w + p.gh);
     float* qq = (float*)(w + p.qq);
     float* gg = (float*)(w + p.gg);
-    float* dot = (float*)(w + p.dot);
-    hipLaunchKernelGGL(rows_to_f16_kernel, dim3(ceil_div(Q * p.Dp, 256)), dim3(256), 0, s, q, Q, D, ldq, Q, qh, p.Dp);
+    hipLaunchKernelGGL(rows_to_f16_kernel, dim3((unsigned)Q), dim3(256), 0, s, q, Q, D, ldq, qh, p.Dp);
     RM_LAUNCHED();
-    hipLaunchKernelGGL(rows_to_f16_kernel, dim3(ceil_div(p.Gp * p.Dp, 256)), dim3(256), 0, s, g, G, D, ldg, p.Gp, gh,
-                       p.Dp);
+    hipLaunchKernelGGL(rows_to_f16_kernel, dim3((unsigned)p.Gp), dim3(256), 0, s, g, G, D, ldg, gh, p.Dp);
     RM_LAUNCHED();
     int rc;
     // exact fp32 squared norms (backend.hip's fmaf chain over k)
     if ((rc = reidmi_row_sqnorm_f32(q, Q, D, ldq, qq, stream))) return rc;
     if ((rc = reidmi_row_sqnorm_f32(g, G, D, ldg, gg, stream))) return rc;
+    // the products and the distance in one pass: the GEMM's epilogue writes
+    // (||q_i||^2 + ||g_j||^2) - 2 q.g straight into out (no Q x G product buffer)
     EpiArgs ea{};
-    ea.out = dot;
-    ea.ldc = p.Gp;
-    if ((rc = gemm_f16(EPI_F32, qh, p.Dp, gh, p.Dp, Q, p.Gp, p.Dp, ea, s))) return rc;
-    const int64_t bx = std::min<int64_t>(ceil_div(G, 256), 64);
-    for (int64_t r0 = 0; r0 < Q; r0 += 65535) {
-        const int64_t nr = std::min<int64_t>(Q - r0, 65535);
-        hipLaunchKernelGGL(dist_finish_kernel, dim3((unsigned)bx, (unsigned)nr), dim3(256), 0, s, dot + r0 * p.Gp, p.Gp,
-                           qq + r0, gg, nr, G, out + r0 * ldo, ldo);
-        RM_LAUNCHED();
-    }
-    return OK;
+    ea.out = out;
+    ea.ldc = ldo;
+    ea.dist_rsq = qq;
+    ea.dist_csq = gg;
+    ea.dist_n = G;
+    return gemm_f16(EPI_F32, qh, p.Dp, gh, p.Dp, Q, p.Gp, p.Dp, ea, s);
 }

@@ -9,7 +9,8 @@
 //   EPI_GELU_H16  out fp16 = QuickGELU(acc + bias)            (mlp.c_fc + gelu, :14-16,52-54)
 //   EPI_QKV       q,k -> [B,H,L,64] fp16, v -> [B,H,64,Lp]    (attn.in_proj + head split)
 //   EPI_PATCH     x[b*L+1+p] = acc + pos[1+p]  fp16           (conv1 + pos-embed, :78-86)
-//   EPI_F32       out fp32 = acc + bias                       (proj / text_projection)
+//   EPI_F32       out fp32 = acc + bias                       (proj / text_projection), or with
+//                 dist_rsq the Euclidean distance (rsq_m + csq_n) - 2 acc (distlowp.hip)
 //   EPI_RESID_F16 x fp16 += acc + bias (fp32 sum, one rounding) (out_proj / c_proj + residual, :27-28)
 //   EPI_RRHI      out fp32 = hi(i, j), the upper bound of the exact distance of items i, j from their
 //                 fp16 product (the k-reciprocal re-rank's pre-filter, rerank.hip): only the bound
@@ -89,6 +90,11 @@ struct EpiArgs {
     int* sv_cnt;
     int2* sv_list;
     int sv_cap;
+    // EPI_F32 distance form (dist_rsq non-null): out[m][n] = (dist_rsq[m] + dist_csq[n]) - 2 acc
+    // for n < dist_n (columns past it are not written; out may be any fp32 row pitch >= dist_n)
+    const float* dist_rsq;
+    const float* dist_csq;
+    int64_t dist_n;
 };
 
 // hi(i, j) = fl(dt + e), dt = fl(fma(-2, dot, s_i + s_j)),

@@ -427,6 +427,40 @@ __device__ __forceinline__ void epilogue_tile(const EpiArgs& ea, f32x4 (&acc)[NI
         return;
     }
     if constexpr (EPI == EPI_F32) {
+        if (ea.dist_rsq != nullptr) {  // Euclidean distance: the same fp32 operations as a separate pass
+            const int64_t n = ea.dist_n;
+            float sj[4][4];
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    const int64_t c = ncol + j * 16 + cq + e;
+                    sj[j][e] = ea.dist_csq[c < n ? c : n - 1];
+                }
+            const bool vec = (ea.ldc & 3) == 0 && ((uintptr_t)ea.out & 15) == 0;
+#pragma unroll
+            for (int i = 0; i < NI; i++) {
+                const int64_t m = mrow + i * 16 + (lane & 15);
+                if (m >= M) continue;
+                const float si = ea.dist_rsq[m];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int64_t c0 = ncol + j * 16 + cq;
+                    float h[4];
+#pragma unroll
+                    for (int e = 0; e < 4; e++) h[e] = (si + sj[j][e]) - 2.0f * acc[i][j][e];
+                    float* o = (float*)ea.out + m * ea.ldc + c0;
+                    if (vec && c0 + 3 < n) {
+                        *(float4*)o = make_float4(h[0], h[1], h[2], h[3]);
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 4; e++)
+                            if (c0 + e < n) o[e] = h[e];
+                    }
+                }
+            }
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < NI; i++) {
             const int64_t m = mrow + i * 16 + (lane & 15);
@@ -1142,6 +1176,8 @@ __global__ __launch_bounds__(512, 2) void gemm_persistent_kernel(const _Float16*
                 issue_w(buf ^ 1, 0, p1);
                 deferred = m0 + G2_M <= M;
                 if constexpr (EPI == EPI_QKV) deferred = deferred && (n0 + ea.n_off) / (ea.heads * 64) != 2;
+                // the distance form's masked / unaligned stores vary in number: not deferred
+                if constexpr (EPI == EPI_F32) deferred = deferred && ea.dist_rsq == nullptr;
             }
         }
         // residual epilogue: its row reads go out before the bias arithmetic (after the next
@@ -1292,6 +1328,9 @@ int gemm_f16(int epi, const void* A, int64_t lda, const void* W, int64_t ldw, in
     RM_REQUIRE((ea.rowstat == nullptr) == (ea.colsum == nullptr), "gemm: rowstat and colsum go together");
     RM_REQUIRE(ea.rowstat == nullptr || ea.bias != nullptr, "gemm: a folded LayerNorm needs the folded bias");
     RM_REQUIRE(epi != EPI_RESID_F16 || ea.rowstat == nullptr, "gemm: the residual epilogue takes no folded LayerNorm");
+    RM_REQUIRE(ea.dist_rsq == nullptr || (epi == EPI_F32 && ea.dist_csq != nullptr && ea.dist_n > 0 &&
+                                          ea.dist_n <= N && ea.ldc >= ea.dist_n && ea.bias == nullptr),
+               "gemm: the distance form needs EPI_F32, both norm vectors, 0 < dist_n <= N, ldc >= dist_n, no bias");
     if (M == 0) return OK;
     hipEvent_t ev_b = nullptr;
     if (prof::enabled) {

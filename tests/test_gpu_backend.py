@@ -76,6 +76,36 @@ def test_distmat_f16_mode_bound(gpu, Q, G, D):
         ev.euclidean_distance_device(qd, gd, precision="bf16")
 
 
+@pytest.mark.parametrize("Q,G,D,pad", [(37, 259, 768, 0), (130, 1001, 1280, 3), (3000, 6007, 1280, 0)])
+def test_distmat_f16_fused_equals_products_pass(gpu, Q, G, D, pad):
+    """The fp16 mode's distances come out of the GEMM's epilogue: bit-identical to the plain
+    fp32 products of the same GEMM (reidmi_gemm_f16, EPI_F32) finished as (||q||^2 + ||g||^2)
+    - 2 dot in fp32 (the separate pass the epilogue replaced), for unaligned row pitches, ragged
+    columns, partial tiles and the persistent tile (3000 x 6007); columns past G untouched."""
+    from multimodal_reid_amd import _lib
+    r = np.random.default_rng(Q + G)
+    q = torch.from_numpy(r.standard_normal((Q, D)).astype(np.float32)).cuda()
+    g = torch.from_numpy(r.standard_normal((G, D)).astype(np.float32)).cuda()
+    out = torch.full((Q, G + pad), float("nan"), device="cuda")
+    ws = torch.empty(_lib.load().reidmi_distmat_f16_workspace_bytes(Q, G, D), device="cuda", dtype=torch.uint8)
+    _lib.call("reidmi_distmat_f16", _lib.ptr(q), Q, D, _lib.ptr(g), G, D, D, _lib.ptr(out), G + pad, _lib.ptr(ws),
+              ws.numel(), _lib.stream())
+    Dp, Gp = (D + 63) // 64 * 64, (G + 255) // 256 * 256
+    qh = torch.zeros(Q, Dp, dtype=torch.float16, device="cuda")
+    gh = torch.zeros(Gp, Dp, dtype=torch.float16, device="cuda")
+    qh[:, :D], gh[:G, :D] = q.half(), g.half()
+    dot = torch.empty(Q, Gp, device="cuda")
+    _lib.call("reidmi_gemm_f16", 5, _lib.ptr(qh), Dp, _lib.ptr(gh), Dp, Q, Gp, Dp, None, None, None, _lib.ptr(dot),
+              Gp, _lib.stream())
+    qq, gg = torch.empty(Q, device="cuda"), torch.empty(G, device="cuda")
+    _lib.call("reidmi_row_sqnorm_f32", _lib.ptr(q), Q, D, D, _lib.ptr(qq), _lib.stream())
+    _lib.call("reidmi_row_sqnorm_f32", _lib.ptr(g), G, D, D, _lib.ptr(gg), _lib.stream())
+    ref = (qq[:, None] + gg[None, :]) - 2.0 * dot[:, :G]
+    assert torch.equal(out[:, :G].contiguous().view(torch.int32), ref.view(torch.int32))
+    if pad:
+        assert bool(torch.isnan(out[:, G:]).all())
+
+
 def test_distmat_f16_mode_ranking(gpu):
     """mAP / rank-1 through the reduced-precision mode against the exact one on identity-clustered
     features of 800 q x 6000 g (normalised, as R1_mAP_eval feeds the distance): the retrieval
