@@ -66,6 +66,20 @@ def _items(items):
     return files, [np.asarray(c, np.int64) for c in cols]
 
 
+def _shard_items(items, tta_seed, shard):
+    """(items, RandomCrop offsets) of this rank's contiguous shard (distributed.shard) of the
+    list, or of all of it (shard None).  The offsets are drawn once for the whole list (the
+    reference draws them unseeded in the workers, data_prepare.py:266-267), so a shard's items
+    get the offsets they get in one process."""
+    items = list(items)
+    tta = tta_offsets(len(items), tta_seed)
+    if shard is not None:
+        from .distributed import shard as _shard
+        lo, hi = _shard(len(items), *shard)
+        items, tta = items[lo:hi], tta[lo:hi]
+    return items, tta
+
+
 class _Slot:
     """Pinned host staging of one batch in flight: file bytes, plan, meta, device status."""
 
@@ -95,15 +109,7 @@ class _Pipeline:
                  depth, tta_seed, shard=None):
         if dtype not in (torch.float32, torch.float16):
             raise ValueError("dtype must be torch.float32 or torch.float16")
-        items = list(items)
-        # RandomCrop offsets of every item, drawn once for the whole list (the reference draws them
-        # unseeded in the workers, data_prepare.py:266-267), so a shard's items get the offsets
-        # they get in one process
-        tta = tta_offsets(len(items), tta_seed)
-        if shard is not None:  # this rank's contiguous shard of the list (distributed.shard)
-            from .distributed import shard as _shard
-            lo, hi = _shard(len(items), *shard)
-            items, tta = items[lo:hi], tta[lo:hi]
+        items, tta = _shard_items(items, tta_seed, shard)
         self.files, (self.pids, self.cams, self.seqs, self.idxs) = _items(items)
         self.N = len(self.files)
         self.bs = int(batch_size)

@@ -57,3 +57,20 @@ def test_loader_item_lists():
     assert files == ["a", "b", "c"]
     assert p.tolist() == [3, -1, 0] and c.tolist() == [1, 2, 5] and s.tolist() == [7, 8, 0] and i.tolist() == [70, 71, 2]
     assert all(a.dtype == np.int64 for a in (p, c, s, i))
+
+
+def test_shard_items_keep_one_process_offsets():
+    """get_loader(..., shard=(rank, world)): the ranks' contiguous shards cover the list in
+    order, and every item keeps the RandomCrop offsets it has in one process."""
+    from multimodal_reid_amd import data_prepare, loader
+    items = [(b"x%d" % k, k % 7, k % 3, 0, k) for k in range(103)]
+    full, off = loader._shard_items(items, 9, None)
+    assert full == items and np.array_equal(off, data_prepare.tta_offsets(103, 9))
+    for world in (2, 3, 8):
+        got_items, got_off = [], []
+        for rank in range(world):
+            it, o = loader._shard_items(items, 9, (rank, world))
+            assert len(it) == len(o)
+            got_items += it
+            got_off.append(o)
+        assert got_items == items and np.array_equal(np.concatenate(got_off), off)
