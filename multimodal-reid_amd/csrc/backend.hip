@@ -1264,11 +1264,23 @@ __global__ __launch_bounds__(1024) void ev_prep1_kernel(const int64_t* __restric
                                                         int32_t* __restrict__ overflow) {
     __shared__ uint64_t slo[16], shi[16];
     const int tid = threadIdx.x;
+    // 8 loads in flight per thread (a past-the-end item re-reads the last label: no effect on
+    // min / max)
+    constexpr int U = 8;
     uint64_t lo = ~0ull, hi = 0;
-    for (int64_t j = tid; j < G; j += 1024) {
-        const uint64_t o = ord64(gp[j]);
-        lo = o < lo ? o : lo;
-        hi = o > hi ? o : hi;
+    for (int64_t j0 = 0; j0 < G; j0 += 1024 * U) {
+        int64_t v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int64_t j = j0 + u * 1024 + tid;
+            v[u] = gp[j < G ? j : G - 1];
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint64_t o = ord64(v[u]);
+            lo = o < lo ? o : lo;
+            hi = o > hi ? o : hi;
+        }
     }
     for (int off = 32; off > 0; off >>= 1) {
         const uint64_t a = __shfl_xor(lo, off, 64), b = __shfl_xor(hi, off, 64);
@@ -1286,7 +1298,19 @@ __global__ __launch_bounds__(1024) void ev_prep1_kernel(const int64_t* __restric
     if (tid == 0) { mm[0] = lo; mm[1] = hi; mm[2] = 0ull; mm[3] = 0ull; *overflow = 0; }
     const int64_t plo = unord64(lo), phi = unord64(hi);
     if ((uint64_t)(phi - plo) >= 0xFFFFull) return;  // wide pid range: the int64 path
-    for (int64_t j = tid; j < G8; j += 1024) pk[j] = j < G ? (uint16_t)(gp[j] - plo) : (uint16_t)0xFFFF;
+    for (int64_t j0 = 0; j0 < G8; j0 += 1024 * U) {
+        int64_t v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int64_t j = j0 + u * 1024 + tid;
+            v[u] = gp[j < G ? j : G - 1];
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int64_t j = j0 + u * 1024 + tid;
+            if (j < G8) pk[j] = j < G ? (uint16_t)(v[u] - plo) : (uint16_t)0xFFFF;
+        }
+    }
 }
 
 __global__ __launch_bounds__(256) void ev_minmax_kernel(const int64_t* __restrict__ gp, int64_t G,
