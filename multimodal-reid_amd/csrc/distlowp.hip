@@ -7,8 +7,6 @@
 #include "common.h"
 #include "gemm.h"
 
-#include <algorithm>
-
 extern "C" int reidmi_row_sqnorm_f32(const float* x, int64_t n, int64_t d, int64_t ldx, float* out, void* stream);
 
 namespace reidmi {
@@ -57,7 +55,7 @@ REIDMI_API int reidmi_distmat_f16(const float* q, int64_t Q, int64_t ldq, const 
     RM_REQUIRE(ws != nullptr && ws_bytes >= p.total, "distmat_f16: workspace smaller than reidmi_distmat_f16_workspace_bytes");
     if (Q == 0 || G == 0) return OK;
     RM_REQUIRE(q && g && out, "distmat_f16: null operand");
-    RM_REQUIRE(p.Gp < (1ll << 31), "distmat_f16: too many rows");
+    RM_REQUIRE(Q < (1ll << 31) && p.Gp < (1ll << 31), "distmat_f16: too many rows");
     hipStream_t s = (hipStream_t)stream;
     char* w = (char*)ws;
     _Float16* qh = (_Float16*)(w + p.qh);
