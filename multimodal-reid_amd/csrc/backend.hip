@@ -170,7 +170,7 @@ __global__ __launch_bounds__(256) void distmat_f32_kernel(
 #define DM2_BAND 4
 #endif
 #if !defined(REIDMI_TOOLS) && (DM2_BK_ != 16 || DM2_MINWG_ != 4 || DM2_BAND != 4 || defined(RS_STATS) || \
-                               defined(RS_SINGLE_PASS) || defined(EV_STAMPS) || defined(EV_PREFETCH))
+                               defined(RS_SINGLE_PASS) || defined(EV_STAMPS) || defined(EV_PREFETCH) || defined(EV_U1))
 #error "backend.hip: DM2_* / RS_* / EV_* variants build only with -DREIDMI_TOOLS (never into libreidmi.so)"
 #endif
 constexpr int DM2_BK = DM2_BK_, DM2_LD = DM_BM + 1;
@@ -1356,6 +1356,9 @@ constexpr int EVW_MAXP = 512, EVW_MAXJ = 256, EVW_T = 1024;
 #ifndef EV_PREFETCH
 #define EV_PREFETCH 0
 #endif
+#ifndef EV_U1  // 16-byte label loads in flight per thread in the label pass
+#define EV_U1 8
+#endif
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void eval_rows_wg_kernel(
     const float* __restrict__ dist, int64_t G, int64_t ld, const int64_t* __restrict__ qp,
@@ -1420,7 +1423,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
     if ((uint64_t)(phi - plo) < 0xFFFFull) {  // packed uint16 labels, 8 per 16-byte load
         if (qpid >= plo && qpid <= phi) {
             const uint16_t key = (uint16_t)(qpid - plo);
-            constexpr int U1 = 4, CH = 2048 * U1;
+            constexpr int U1 = EV_U1, CH = 2048 * U1;
             const int64_t nch = (G + CH - 1) / CH;
             const int64_t c0 = (q * 37) % nch;
             const int64_t n8 = (G + 7) / 8;
